@@ -1,0 +1,153 @@
+"""ctypes binding of oracle/liboracle.so -- TEST INFRASTRUCTURE ONLY.
+
+The clean-room CPU restatement (oracle/dc_oracle.c) is the checker for the parity
+tests, for __graft_entry__.smoke() and for bench.py's cpu_baseline leg. The product
+(data_compression_amd/) never imports this module.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+u8p = C.POINTER(C.c_uint8)
+u32p = C.POINTER(C.c_uint32)
+u64p = C.POINTER(C.c_uint64)
+ip = C.POINTER(C.c_int)
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE, "liboracle.so"], check=True)
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(HERE, "liboracle.so")
+        if not os.path.exists(path):
+            build()
+        L = C.CDLL(path)
+        L.orc_histogram_bytes.argtypes = [u8p, C.c_uint64, u64p]
+        L.orc_huffman_lengths.argtypes = [C.c_int, u64p, C.c_int, ip]
+        L.orc_huffman_lengths.restype = C.c_int
+        L.orc_canonical.argtypes = [C.c_int, ip, C.c_int, ip, u32p]
+        L.orc_bitcodes.argtypes = [ip, u32p, C.c_int, u32p, u8p]
+        L.orc_bitcodes.restype = C.c_int
+        L.orc_huff_pack.argtypes = [u8p, C.c_uint64, u32p, u8p, u8p, C.c_uint64, C.c_uint32, u64p]
+        L.orc_huff_pack.restype = C.c_uint64
+        L.orc_huff_unpack.argtypes = [u8p, C.c_uint64, C.c_uint64, C.c_int, ip, u32p, C.c_int, u8p]
+        L.orc_huff_unpack.restype = C.c_int
+        L.orc_base64url.argtypes = [u8p, C.c_uint64, C.c_char_p]
+        L.orc_base64url.restype = C.c_uint64
+        for f in ("orc_nybble_compress", "orc_nybble_decompress"):
+            getattr(L, f).argtypes = [u8p, C.c_uint64, u8p, C.c_int]
+            getattr(L, f).restype = C.c_uint64
+        for f in ("orc_small_compress", "orc_small_decompress"):
+            getattr(L, f).argtypes = [u8p, C.c_uint64, u8p]
+            getattr(L, f).restype = C.c_uint64
+        _LIB = L
+    return _LIB
+
+
+def _p(a, t):
+    return a.ctypes.data_as(t)
+
+
+def histogram(x: np.ndarray) -> np.ndarray:
+    x = np.ascontiguousarray(x, dtype=np.uint8)
+    h = np.zeros(256, dtype=np.uint64)
+    lib().orc_histogram_bytes(_p(x, u8p), x.size, _p(h, u64p))
+    return h
+
+
+def huffman_lengths(freq, n_ary: int, max_leaf: int = 258) -> np.ndarray:
+    f = np.zeros(max_leaf + 1, dtype=np.uint64)
+    f[: len(freq)] = np.asarray(freq, dtype=np.uint64)
+    out = np.zeros(max_leaf + 1, dtype=np.int32)
+    lib().orc_huffman_lengths(max_leaf, _p(f, u64p), n_ary, _p(out, ip))
+    return out
+
+
+def canonical(lengths, n_ary: int, max_sym: int = 258, size: int | None = None):
+    size = size or (max_sym + 1)
+    L = np.zeros(size, dtype=np.int32)
+    L[: len(lengths)] = lengths
+    el = np.zeros(size, dtype=np.int32)
+    ev = np.zeros(size, dtype=np.uint32)
+    lib().orc_canonical(max_sym, _p(L, ip), n_ary, _p(el, ip), _p(ev, u32p))
+    return el, ev
+
+
+def bitcodes(enc_len, enc_val, n_ary):
+    el = np.ascontiguousarray(enc_len, dtype=np.int32)
+    ev = np.ascontiguousarray(enc_val, dtype=np.uint32)
+    code = np.zeros(256, dtype=np.uint32)
+    nb = np.zeros(256, dtype=np.uint8)
+    mx = lib().orc_bitcodes(_p(el, ip), _p(ev, u32p), n_ary, _p(code, u32p), _p(nb, u8p))
+    return code, nb, mx
+
+
+def huff_pack(x, code, nbits, bit_base=0, sync_syms=0):
+    x = np.ascontiguousarray(x, dtype=np.uint8)
+    total = int((nbits[x].astype(np.uint64)).sum()) if x.size else 0
+    out = np.zeros((total + (bit_base & 7) + 7) // 8 + 8, dtype=np.uint8)
+    nidx = (x.size + sync_syms - 1) // sync_syms if sync_syms else 0
+    idx = np.zeros(max(nidx, 1), dtype=np.uint64)
+    bits = lib().orc_huff_pack(_p(x, u8p), x.size, _p(code, u32p), _p(nbits, u8p), _p(out, u8p),
+                               bit_base, sync_syms, _p(idx, u64p) if sync_syms else None)
+    if bits == 2**64 - 1:
+        raise ValueError("byte without a code")
+    nbytes = ((bit_base & 7) + bits + 7) // 8
+    return out[:nbytes], int(bits), idx[:nidx]
+
+
+def huff_unpack(payload, bits, n_out, enc_len, enc_val, n_ary, max_sym=258):
+    payload = np.ascontiguousarray(payload, dtype=np.uint8)
+    el = np.ascontiguousarray(enc_len, dtype=np.int32)
+    ev = np.ascontiguousarray(enc_val, dtype=np.uint32)
+    out = np.zeros(max(n_out, 1), dtype=np.uint8)
+    rc = lib().orc_huff_unpack(_p(payload, u8p), bits, n_out, max_sym, _p(el, ip), _p(ev, u32p),
+                               n_ary, _p(out, u8p))
+    if rc != 0:
+        raise ValueError("bad stream")
+    return out[:n_out]
+
+
+def base64url(payload, bits) -> bytes:
+    payload = np.ascontiguousarray(payload, dtype=np.uint8)
+    out = C.create_string_buffer((bits + 5) // 6 + 1)
+    n = lib().orc_base64url(_p(payload, u8p), bits, out)
+    return out.raw[:n]
+
+
+def nybble_compress(x: bytes, modify: bool) -> bytes:
+    a = np.frombuffer(x, dtype=np.uint8).copy() if len(x) else np.zeros(1, np.uint8)
+    out = np.zeros(len(x) + 8, dtype=np.uint8)
+    n = lib().orc_nybble_compress(_p(a, u8p), len(x), _p(out, u8p), int(modify))
+    return out[:n].tobytes()
+
+
+def nybble_decompress(c: bytes, modify: bool) -> bytes:
+    a = np.frombuffer(c, dtype=np.uint8).copy() if len(c) else np.zeros(1, np.uint8)
+    out = np.zeros(2 * len(c) + 8, dtype=np.uint8)
+    n = lib().orc_nybble_decompress(_p(a, u8p), len(c), _p(out, u8p), int(modify))
+    return out[:n].tobytes()
+
+
+def small_compress(x: bytes) -> bytes:
+    a = np.frombuffer(x, dtype=np.uint8).copy() if len(x) else np.zeros(1, np.uint8)
+    out = np.zeros(len(x) + 8, dtype=np.uint8)
+    n = lib().orc_small_compress(_p(a, u8p), len(x), _p(out, u8p))
+    return out[:n].tobytes()
+
+
+def small_decompress(c: bytes) -> bytes:
+    a = np.frombuffer(c, dtype=np.uint8).copy() if len(c) else np.zeros(1, np.uint8)
+    out = np.zeros(2 * len(c) + 8, dtype=np.uint8)
+    n = lib().orc_small_decompress(_p(a, u8p), len(c), _p(out, u8p))
+    return out[:n].tobytes()
