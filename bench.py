@@ -1,0 +1,225 @@
+"""Headline benchmark: GB/s encode+decode on a 1 GiB byte stream per MI355X, % HBM roofline.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--cfg C2] [--nary 2] [--size BYTES]
+    torchrun --nproc-per-node N bench.py --gpus N ...          (driver launches N>1 so)
+
+Workload (BASELINE.json metric / configs[1] generator at the metric's 1 GiB): a 1 GiB
+enwik-like synthetic byte stream per GPU, binary (n=2) Huffman. One step = the whole
+codec on that stream, inputs resident in HBM:
+    encode = histogram -> [RCCL all-reduce of the 256-bin histogram] -> code table ->
+             per-block bit plan -> [RCCL all-gather of per-rank bit counts] -> pack at the
+             rank's global bit offset (+ sync index)
+    decode = parallel decode of the rank's shard back to bytes
+value = total uncompressed bytes of all ranks / step time (GB/s, 1e9), "scaling": "weak".
+The round trip is verified (decoded == input) after the timed region.
+
+roofline: dominant kernel, algorithmic bytes per launch / its mean HIP-event duration on
+the codec's stream, against 8.0 TB/s. cpu_baseline: the oracle (single-threaded C
+restatement) on a bounded sample of the same stream, rank 0, N=1 only.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK = 8.0e12          # MI355X HBM3E spec, bytes/s (MI355X_MICROARCH.md)
+METRIC = "GB/s encode+decode on 1 GiB byte stream at 1/2/4/8 MI355X; % HBM roofline"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--cfg", default="C2")
+    ap.add_argument("--nary", type=int, default=2)
+    ap.add_argument("--size", type=int, default=1 << 30, help="bytes per GPU")
+    ap.add_argument("--sync", type=int, default=0, help="sync-index granularity (0 = default)")
+    ap.add_argument("--cpu-sample", type=int, default=256 << 20)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--profile-steps", type=int, default=5)
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from data_compression_amd import synth
+    from data_compression_amd.device import Codec
+
+    n = a.size
+    x = synth.device_text(a.cfg, n, seed=0xC2 + 7919 * rank, device=dev)
+    torch.cuda.synchronize()
+    c = Codec(local)   # launches on torch's current stream
+    S = a.sync or c.default_sync(n)
+    nsync = (n + S - 1) // S
+
+    hist = torch.empty(256, dtype=torch.int64, device=dev)
+    tab = torch.empty(c.table_bytes, dtype=torch.uint8, device=dev)
+    total = torch.empty(1, dtype=torch.int64, device=dev)
+    allt = torch.empty(world, dtype=torch.int64, device=dev)
+    words = torch.empty(c.words_needed(2**40, 32 * n) + 8, dtype=torch.int32, device=dev)
+    sync = torch.empty(nsync, dtype=torch.int64, device=dev)
+    out = torch.empty(n, dtype=torch.uint8, device=dev)
+    state = {}
+
+    def encode():
+        c.hist(x, out=hist)
+        if world > 1:
+            dist.all_reduce(hist)
+        c.table(hist, a.nary, out=tab)
+        c.plan(tab, total=total)
+        base = 0
+        if world > 1:
+            dist.all_gather_into_tensor(allt, total)
+            base = int(allt[:rank].sum().item()) if rank else 0
+        c.pack_async(x, tab, base, words, sync, S)
+        state["base"] = base
+
+    def decode():
+        c.decode(words, state["base"], sync, S, n, tab, out)
+
+    def step():
+        encode()
+        decode()
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+    ms_step = el / a.steps * 1e3
+
+    # ---- correctness of the measured configuration (outside the timed region) ----------
+    st = c.pack_status(tab)
+    ok = st == 0 and c.decode_status() == 0 and bool(torch.equal(out, x))
+    bits = int(total.item())
+    if world > 1:
+        okt = torch.tensor([1 if ok else 0], device=dev)
+        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+        ok = bool(okt.item())
+
+    # ---- encode / decode split and per-kernel HIP-event durations ------------------------
+    def timed(fn, k):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(k):
+            fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t) / k * 1e3
+
+    enc_ms = timed(encode, a.profile_steps)
+    dec_ms = timed(decode, a.profile_steps)
+    c.timing(True)
+    for _ in range(a.profile_steps):
+        step()
+    kt = c.timings()
+    c.timing(False)
+    per = {}
+    for name, ms in kt:
+        per.setdefault(name, []).append(ms)
+    payload = (bits + 7) // 8
+    sync_bytes = nsync * 8
+    alg = {"hist_blocks": n, "huff_pack": n + payload + sync_bytes, "huff_decode": payload + sync_bytes + n}
+    kernels = {}
+    for name, v in per.items():
+        m = float(np.mean(v))
+        e = {"ms": round(m, 4), "launches_per_step": len(v) // a.profile_steps}
+        if name in alg:
+            e["GBps"] = round(alg[name] / (m * 1e-3) / 1e9, 1)
+        kernels[name] = e
+    dom = max(per, key=lambda k: float(np.sum(per[k])))
+    dom_ms = float(np.mean(per[dom]))
+    dom_bytes = alg.get(dom, n)
+    achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
+
+    value = world * n / (ms_step * 1e-3) / 1e9
+    res = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "GB/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(ms_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic",
+        "config": {"workload": f"{a.cfg} enwik-like text, {n >> 20} MiB per GPU, n={a.nary} Huffman "
+                               "encode+decode (configs[1] generator at the metric's 1 GiB)",
+                   "bytes_per_gpu": n, "n_ary": a.nary, "sync_syms": S,
+                   "parallelism": f"shard{world}" if world > 1 else "single"},
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK / 1e9,
+                     "unit": "GB/s", "frac": round(achieved * 1e9 / HBM_PEAK, 4), "traffic": None,
+                     "alg_bytes_per_launch": dom_bytes, "mean_ms": round(dom_ms, 4)},
+        "encode_GBps": round(n / (enc_ms * 1e-3) / 1e9, 2),
+        "decode_GBps": round(n / (dec_ms * 1e-3) / 1e9, 2),
+        "ratio": round(payload / n, 4),
+        "kernels": kernels,
+        "roundtrip_ok": ok,
+    }
+    if rank == 0 and world == 1 and not a.no_cpu:
+        res["cpu_baseline"] = cpu_baseline(x, a)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(x, a):
+    """Oracle (single-threaded C restatement, oracle/dc_oracle.c) on a bounded sample."""
+    from oracle import oracle as orc
+    m = min(a.cpu_sample, x.numel())
+    s = x[:m].cpu().numpy()
+    t0 = time.perf_counter()
+    h = orc.histogram(s)
+    L = orc.huffman_lengths(h, a.nary)
+    el, ev = orc.canonical(L, a.nary)
+    code, nb, _ = orc.bitcodes(el, ev, a.nary)
+    payload, bits, _ = orc.huff_pack(s, code, nb, sync_syms=4096)
+    t1 = time.perf_counter()
+    back = orc.huff_unpack(payload, bits, m, el, ev, a.nary)
+    t2 = time.perf_counter()
+    assert np.array_equal(back, s)
+    try:
+        cpu = open("/proc/cpuinfo").read().split("model name")[1].split("\n")[0].strip(": \t")
+    except Exception:
+        cpu = "unknown"
+    return {"value": round(m / (t2 - t0) / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": f"first {m >> 20} MiB of the rank-0 stream; encode {t1 - t0:.2f} s + decode "
+                      f"{t2 - t1:.2f} s; {cpu}; nproc={os.cpu_count()}"}
+
+
+if __name__ == "__main__":
+    main()

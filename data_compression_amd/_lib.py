@@ -1,0 +1,114 @@
+"""Loading of the in-tree native libraries (data_compression_amd/lib/*.so).
+
+The libraries link the HIP runtime by soname (libamdhip64.so.7). PyTorch-ROCm ships its
+own copy; importing torch first makes every later dlopen resolve to that one copy, so
+the kernels and torch share one runtime (device memory, streams, RCCL). Nothing here
+falls back to Python or CPU compute: a missing library raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+try:  # one HIP runtime per process: torch's, when torch is present
+    import torch  # noqa: F401
+except Exception:  # pragma: no cover - torch is optional for the C-ABI itself
+    torch = None
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+LIBDIR = os.path.join(PKG, "lib")
+
+_cache: dict[str, C.CDLL] = {}
+
+vp = C.c_void_p
+u8p = C.POINTER(C.c_uint8)
+u64 = C.c_uint64
+u32 = C.c_uint32
+i32 = C.c_int
+
+
+class DcError(RuntimeError):
+    NAMES = {-1: "DC_E_ARG", -2: "DC_E_HIP", -3: "DC_E_CODE_TOO_LONG", -4: "DC_E_NOCODE",
+             -5: "DC_E_STATE", -6: "DC_E_CAPACITY", -7: "DC_E_STREAM"}
+
+    def __init__(self, fn, rc):
+        super().__init__(f"{fn} failed: {self.NAMES.get(rc, rc)}")
+        self.rc = rc
+
+
+def check(fn, rc):
+    if rc != 0:
+        raise DcError(fn, rc)
+    return rc
+
+
+def lib_path(name: str) -> str:
+    return os.path.join(LIBDIR, name)
+
+
+def load(name: str) -> C.CDLL:
+    if name in _cache:
+        return _cache[name]
+    path = lib_path(name)
+    if not os.path.exists(path):
+        raise RuntimeError(f"{path} is missing: run `python -m data_compression_amd.build` "
+                           "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+    lib = C.CDLL(path)
+    if name == "libdc_core.so":
+        _declare_core(lib)
+    _cache[name] = lib
+    return lib
+
+
+def core() -> C.CDLL:
+    return load("libdc_core.so")
+
+
+def _declare_core(L):
+    P = vp
+    sig = {
+        "dc_ctx_create": ([C.POINTER(vp), i32, vp], i32),
+        "dc_ctx_destroy": ([vp], None),
+        "dc_ctx_sync": ([vp], i32),
+        "dc_ctx_stream": ([vp], vp),
+        "dc_ctx_set_timing": ([vp, i32], i32),
+        "dc_ctx_timings": ([vp, C.POINTER(C.c_char_p), C.POINTER(C.c_float), i32], i32),
+        "dc_version": ([], C.c_char_p),
+        "dc_dtable_size": ([], C.c_size_t),
+        "dc_malloc": ([C.POINTER(vp), C.c_size_t], i32),
+        "dc_free": ([vp], i32),
+        "dc_memcpy_h2d": ([vp, vp, vp, C.c_size_t], i32),
+        "dc_memcpy_d2h": ([vp, vp, vp, C.c_size_t], i32),
+        "dc_memset": ([vp, vp, i32, C.c_size_t], i32),
+        "dc_huff_hist": ([vp, P, u64, P], i32),
+        "dc_huff_table": ([vp, P, i32, i32, P], i32),
+        "dc_huff_table_freq": ([vp, P, i32, i32, P], i32),
+        "dc_huff_table_lengths": ([vp, P, i32, i32, P], i32),
+        "dc_huff_table_status": ([vp, P, C.POINTER(C.c_int32)], i32),
+        "dc_huff_plan": ([vp, P, P], i32),
+        "dc_huff_pack": ([vp, P, u64, P, u64, P, u64, P, u32], i32),
+        "dc_huff_words_needed": ([u64, u64], u64),
+        "dc_huff_pack_async": ([vp, P, u64, P, u64, P, u64, P, u32], i32),
+        "dc_huff_pack_status": ([vp, P], i32),
+        "dc_huff_decode": ([vp, P, u64, u64, P, u32, u64, P, P], i32),
+        "dc_huff_decode_status": ([vp], i32),
+        "dc_huff_base64url": ([vp, P, u64, u64, P], i32),
+        "dc_huff_default_sync": ([u64], u32),
+        "dc_nyb_compress": ([vp, P, u64, i32, P, C.POINTER(u64)], i32),
+        "dc_nyb_decompress": ([vp, P, u64, i32, P, C.POINTER(u64)], i32),
+        "dc_small_compress": ([vp, P, u64, P, C.POINTER(u64)], i32),
+        "dc_small_decompress": ([vp, P, u64, P, C.POINTER(u64)], i32),
+        "dc_host_ctx": ([], vp),
+        "dc_huff_compress_bound": ([u64, u32], u64),
+        "dc_huff_compress_host": ([u8p, u64, i32, C.POINTER(C.c_int32), i32, u32, u8p, u64, C.POINTER(u64)], i32),
+        "dc_huff_decompress_host": ([u8p, u64, u8p, u64, C.POINTER(u64)], i32),
+        "dc_huff_container_info": ([u8p, u64, C.POINTER(u64), C.POINTER(i32), C.POINTER(u64)], i32),
+        "dc_nyb_compress_host": ([u8p, u64, i32, u8p, u64, C.POINTER(u64)], i32),
+        "dc_nyb_decompress_host": ([u8p, u64, i32, u8p, u64, C.POINTER(u64)], i32),
+        "dc_small_compress_host": ([u8p, u64, u8p, u64, C.POINTER(u64)], i32),
+        "dc_small_decompress_host": ([u8p, u64, u8p, u64, C.POINTER(u64)], i32),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res

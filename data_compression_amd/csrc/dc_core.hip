@@ -1,0 +1,1441 @@
+// dc_core.hip -- gfx950 (MI355X) kernels + the device-resident extended C-ABI (dc_gpu.h).
+//
+// Hot path: byte histogram (H1) -> n-ary Huffman lengths (H2-H5) ->
+// canonical n-ary codes (H6) -> bit packing (H7) -> decode (H8); nybble codec (N1-N7);
+// small front-end (small_compression.c:507-665). Everything here is integer/byte work
+// and HBM-bound: no MFMA. Design notes and the roofline per kernel: DESIGN.md.
+//
+// Built by data_compression_amd/build.py:
+//   hipcc --offload-arch=gfx950 -O3 -fPIC -shared -> data_compression_amd/lib/libdc_core.so
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+#include <stdlib.h>
+
+#include "dc_gpu.h"
+
+#define DC_VERSION "dc-mi355x 0.1 (gfx950)"
+
+// ------------------------------------------------------------------------------------
+// small device helpers
+// ------------------------------------------------------------------------------------
+static __device__ __forceinline__ uint32_t bswap32(uint32_t v) { return __builtin_bswap32(v); }
+
+// 256-thread exclusive scan (u32). `scratch` holds >= 4 u32. Returns the prefix and
+// the total through *total. Contains two __syncthreads().
+static __device__ __forceinline__ uint32_t wg_scan_excl_u32(uint32_t v, uint32_t *scratch,
+                                                            uint32_t *total)
+{
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    if (lane == 63) scratch[wid] = x;
+    __syncthreads();
+    uint32_t base = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        uint32_t s = scratch[w];
+        base += (w < wid) ? s : 0u;
+        tot += s;
+    }
+    __syncthreads();
+    *total = tot;
+    return base + x - v;
+}
+
+// ------------------------------------------------------------------------------------
+// (H1) byte histogram per 32 KiB block.  n_ary_huffman.c:461-493
+// LDS layout: dword (bin*64 + lane) holds four 8-bit counters, one per wave of the
+// workgroup. Every lane owns its own dword column, so one ds_add_u32 per input byte is
+// bank-conflict free (bank = lane mod 32) whatever the byte distribution, and skewed
+// text (' ' and 'e' in most lanes) does not serialise. A lane sees 128 bytes per block,
+// so an 8-bit counter cannot overflow. Reduction reads and clears with a rotated column
+// index so it is conflict free as well.
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_hist_blocks(const uint8_t *__restrict__ in, uint64_t n,
+                                                     uint64_t nblocks, uint16_t *__restrict__ bh)
+{
+    __shared__ uint32_t cnt[256 * 64];
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const uint32_t inc = 1u << (8 * wv);
+    for (int i = t; i < 256 * 64; i += 256) cnt[i] = 0u;
+    __syncthreads();
+    for (uint64_t b = blockIdx.x; b < nblocks; b += gridDim.x) {
+        const uint64_t base = b * (uint64_t)DC_BLOCK_BYTES;
+        if (base + DC_BLOCK_BYTES <= n) {
+            const uint4 *p = reinterpret_cast<const uint4 *>(in + base) + t;
+            uint4 v[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] = p[k * 256];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const uint32_t w4[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        atomicAdd(&cnt[((w4[j] >> (8 * q)) & 255u) * 64 + lane], inc);
+                }
+            }
+        } else {
+            const uint64_t end = n;
+            for (uint64_t i = base + t; i < end; i += 256) atomicAdd(&cnt[in[i] * 64 + lane], inc);
+        }
+        __syncthreads();
+        uint32_t acc = 0;
+#pragma unroll 8
+        for (int j = 0; j < 64; ++j) {
+            const int idx = t * 64 + ((j + t) & 63);
+            const uint32_t d = cnt[idx];
+            cnt[idx] = 0u;
+            acc += (d & 0x00FF00FFu) + ((d >> 8) & 0x00FF00FFu);
+        }
+        bh[b * 256 + t] = (uint16_t)((acc & 0xFFFFu) + (acc >> 16));
+        __syncthreads();
+    }
+}
+
+// partial sums of the block histograms: partials[g][256]
+__global__ __launch_bounds__(256) void k_hist_reduce(const uint16_t *__restrict__ bh, uint64_t nblocks,
+                                                     uint64_t *__restrict__ partials)
+{
+    const int t = threadIdx.x;
+    const uint64_t per = (nblocks + gridDim.x - 1) / gridDim.x;
+    const uint64_t b0 = (uint64_t)blockIdx.x * per;
+    const uint64_t b1 = (b0 + per < nblocks) ? b0 + per : nblocks;
+    uint64_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+    uint64_t b = b0;
+    for (; b + 4 <= b1; b += 4) {
+        a0 += bh[(b + 0) * 256 + t];
+        a1 += bh[(b + 1) * 256 + t];
+        a2 += bh[(b + 2) * 256 + t];
+        a3 += bh[(b + 3) * 256 + t];
+    }
+    for (; b < b1; ++b) a0 += bh[b * 256 + t];
+    partials[(uint64_t)blockIdx.x * 256 + t] = a0 + a1 + a2 + a3;
+}
+
+__global__ __launch_bounds__(256) void k_hist_final(const uint64_t *__restrict__ partials, int G,
+                                                    uint64_t *__restrict__ hist)
+{
+    const int t = threadIdx.x;
+    uint64_t a = 0;
+    for (int g = 0; g < G; ++g) a += partials[(uint64_t)g * 256 + t];
+    hist[t] = a;
+}
+
+// ------------------------------------------------------------------------------------
+// (H2-H6) code table: n-ary Huffman lengths + canonical n-ary codes + packed bit codes
+// + decode tables. One workgroup.
+//   * merge order: the reference re-sorts its active list with a stable bubble sort
+//     before every merge (n_ary_huffman.c:672-731, :962-1002); that order is ascending
+//     (count, node_index) with dummy leaves at max_leaf_value+1.. (count 1, :921-929)
+//     and internal nodes numbered in creation order. Here: bitonic sort of the packed
+//     keys (count<<11 | index) in LDS, then the two-queue merge (internal nodes are
+//     created with non-decreasing counts, so a FIFO keeps them sorted).
+//   * dummy count: (n-1) - ((k-1) % (n-1)), C remainder (:900-903), incl. its phantom
+//     leaf for n = 2.
+//   * canonical values (:1540-1568) with the reference's index-M quirks (:1336, :1421).
+// ------------------------------------------------------------------------------------
+#define TBL_SORT_MAX 2048
+#define TBL_NODES 4096
+
+__global__ __launch_bounds__(256) void k_huff_table(const uint64_t *__restrict__ freq, int freq_is_hist256,
+                                                    const int32_t *__restrict__ lens_in, int M, int nary,
+                                                    dc_dtable *__restrict__ T)
+{
+    __shared__ uint64_t s_key[TBL_SORT_MAX];
+    __shared__ uint64_t s_q2[TBL_SORT_MAX];
+    __shared__ int16_t s_parent[TBL_NODES];
+    __shared__ int32_t s_len[DC_MAX_SYMS];
+    __shared__ uint32_t s_cnt[DC_MAX_DIGITS + 2];
+    __shared__ uint32_t s_startv[DC_MAX_DIGITS + 2];
+    __shared__ uint32_t s_starti[DC_MAX_DIGITS + 2];
+    __shared__ uint32_t s_code[256];
+    __shared__ uint32_t s_nb[256];
+    __shared__ int s_k, s_min, s_max, s_maxbits, s_bad;
+
+    const int t = threadIdx.x;
+    const int leaves = M + 1;
+    int w = 0;
+    while ((1 << w) < nary) ++w;
+
+    if (t == 0) { s_k = 0; s_min = 300; s_max = 0; s_maxbits = 0; s_bad = 0; }
+    __syncthreads();
+
+    if (lens_in == nullptr) {
+        for (int i = t; i < leaves; i += 256) {
+            const uint64_t f = freq_is_hist256 ? (i < 256 ? freq[i] : 0ull) : freq[i];
+            if (f) {
+                const int slot = atomicAdd(&s_k, 1);
+                s_key[slot] = (f << 11) | (uint64_t)i;
+                if (f >> 53) s_bad = 1;
+            }
+        }
+        __syncthreads();
+        const int k = s_k;
+        const int dummies = (nary - 1) - ((k - 1) % (nary - 1));
+        const int items = k + dummies;
+        int P = 1;
+        while (P < items) P <<= 1;
+        for (int i = k + t; i < P; i += 256)
+            s_key[i] = (i < items) ? ((1ull << 11) | (uint64_t)(leaves + (i - k))) : ~0ull;
+        for (int i = t; i < TBL_NODES; i += 256) s_parent[i] = 0;
+        __syncthreads();
+        // bitonic sort, ascending
+        for (int size = 2; size <= P; size <<= 1) {
+            for (int stride = size >> 1; stride > 0; stride >>= 1) {
+                for (int i = t; i < (P >> 1); i += 256) {
+                    const int lo = 2 * stride * (i / stride) + (i % stride);
+                    const int hi = lo + stride;
+                    const bool asc = ((lo & size) == 0);
+                    const uint64_t a = s_key[lo], b = s_key[hi];
+                    if ((a > b) == asc) { s_key[lo] = b; s_key[hi] = a; }
+                }
+                __syncthreads();
+            }
+        }
+        if (t == 0) {
+            int h1 = 0, h2 = 0, t2 = 0, active = items;
+            const int first_internal = leaves + dummies;
+            int next = first_internal;
+            uint64_t head1 = (items > 0) ? s_key[0] : ~0ull;
+            while (active > 1) {
+                uint64_t sum = 0;
+                for (int q = 0; q < nary; ++q) {
+                    const uint64_t c1 = (h1 < items) ? (head1 >> 11) : ~0ull;
+                    const uint64_t c2 = (h2 < t2) ? s_q2[h2] : ~0ull;
+                    int idx;
+                    if (h1 < items && (h2 == t2 || c1 <= c2)) {
+                        idx = (int)(head1 & 2047u);
+                        sum += c1;
+                        ++h1;
+                        head1 = (h1 < items) ? s_key[h1] : ~0ull;
+                    } else {
+                        idx = first_internal + h2;
+                        sum += c2;
+                        ++h2;
+                    }
+                    if (idx < TBL_NODES) s_parent[idx] = (int16_t)next;
+                }
+                s_q2[t2++] = sum;
+                ++next;
+                active -= nary - 1;
+            }
+            if (next >= TBL_NODES) s_bad = 1;
+        }
+        __syncthreads();
+        // depth = number of parent hops to the root (n_ary_huffman.c:1069-1076)
+        for (int i = t; i < leaves; i += 256) {
+            int d = 0, c = i;
+            while (s_parent[c] != 0 && d < TBL_NODES) { ++d; c = s_parent[c]; }
+            s_len[i] = d;
+        }
+    } else {
+        for (int i = t; i < leaves; i += 256) s_len[i] = lens_in[i];
+    }
+    for (int L = t; L < DC_MAX_DIGITS + 2; L += 256) s_cnt[L] = 0;
+    __syncthreads();
+
+    // canonical codes: min/max over i < M, assignment over i <= M
+    for (int i = t; i < M; i += 256) {
+        const int L = s_len[i];
+        atomicMax(&s_max, L);
+        if (L > 0) atomicMin(&s_min, L);
+    }
+    __syncthreads();
+    const int minL = s_min, maxL = s_max;
+    if (maxL > DC_MAX_DIGITS) {
+        if (t == 0) s_bad = 1;
+    }
+    for (int i = t; i < leaves; i += 256) {
+        const int L = s_len[i];
+        if (L >= minL && L <= maxL && L <= DC_MAX_DIGITS) atomicAdd(&s_cnt[L], 1u);
+    }
+    __syncthreads();
+    if (t == 0) {
+        uint32_t code = 0, acc = 0;   // reference: int arithmetic, wraps mod 2^32
+        for (int L = 0; L <= DC_MAX_DIGITS; ++L) {
+            s_starti[L] = acc;
+            if (L >= minL && L <= maxL) {
+                s_startv[L] = code;
+                code = (code + s_cnt[L]) * (uint32_t)nary;
+                acc += s_cnt[L];
+            } else {
+                s_startv[L] = 0;
+            }
+        }
+    }
+    for (int s = t; s < 256; s += 256) { s_code[s] = 0; s_nb[s] = 0; }
+    __syncthreads();
+    for (int i = t; i < leaves; i += 256) {
+        const int L = s_len[i];
+        T->lengths[i] = L;
+        if (L >= minL && L <= maxL && L <= DC_MAX_DIGITS) {
+            uint32_t rank = 0;
+            for (int j = 0; j < i; ++j) rank += (s_len[j] == L);
+            const uint32_t val = s_startv[L] + rank;
+            T->enc_len[i] = L;
+            T->enc_val[i] = val;
+            T->syms[s_starti[L] + rank] = (uint16_t)i;
+            if (i < 256) {
+                // L base-n digits of val, MSB-first, w bits each
+                if ((long long)L * w <= 32) {
+                    uint64_t v = val, packed = 0;
+                    for (int d = 0; d < L; ++d) {
+                        packed |= (v % (uint64_t)nary) << (w * d);
+                        v /= (uint64_t)nary;
+                    }
+                    s_code[i] = (uint32_t)packed;
+                    s_nb[i] = (uint32_t)(L * w);
+                    atomicMax(&s_maxbits, L * w);
+                } else {
+                    atomicMax(&s_maxbits, 33);
+                }
+            }
+            if (i == M) T->last_written = 1;
+        } else {
+            if (i < M) { T->enc_len[i] = 0; T->enc_val[i] = 0; }
+            else { T->last_written = 0; T->enc_len[i] = 0; T->enc_val[i] = 0; }
+        }
+    }
+    for (int i = leaves + t; i < DC_MAX_SYMS; i += 256) {
+        T->lengths[i] = 0; T->enc_len[i] = 0; T->enc_val[i] = 0;
+    }
+    for (int L = t; L <= DC_MAX_DIGITS; L += 256) {
+        const bool in = (L >= minL && L <= maxL);
+        T->first[L] = in ? s_startv[L] : 0u;
+        T->count[L] = in ? s_cnt[L] : 0u;
+        T->start[L] = s_starti[L];
+    }
+    for (int e = t; e < (1 << DC_LUT_BITS); e += 256) T->lut[e] = 0;
+    __syncthreads();
+    T->code[t] = s_code[t];
+    T->nbits[t] = s_nb[t];
+    // first-level decode table: every 12-bit window whose prefix is a code of <= 12 bits
+    for (int s = 0; s < 256; ++s) {
+        const uint32_t nb = s_nb[s];
+        if (nb == 0 || nb > DC_LUT_BITS) continue;
+        const uint32_t span = 1u << (DC_LUT_BITS - nb);
+        const uint32_t base = s_code[s] << (DC_LUT_BITS - nb);
+        for (uint32_t j = t; j < span; j += 256) T->lut[base + j] = (uint16_t)(s | (nb << 8));
+    }
+    if (t == 0) {
+        T->n_ary = nary;
+        T->w = w;
+        T->max_symbol_value = M;
+        T->max_bits = s_maxbits;
+        T->min_len = minL;
+        T->max_len = maxL;
+        T->status = s_bad ? DC_E_ARG : (s_maxbits > 32 ? DC_E_CODE_TOO_LONG : DC_OK);
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// (H7) encode plan: bits per 32 KiB block = sum_s h_b[s] * nbits[s] (the reference's
+// own payload formula, n_ary_huffman.c:2485), then an exclusive scan over blocks.
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_block_bits(const uint16_t *__restrict__ bh, uint64_t nblocks,
+                                                    const dc_dtable *__restrict__ T,
+                                                    uint64_t *__restrict__ bits, int *__restrict__ err)
+{
+    const int lane = threadIdx.x & 63;
+    const uint64_t b = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (b >= nblocks) return;
+    const uint2 h = *reinterpret_cast<const uint2 *>(bh + b * 256 + lane * 4);
+    const uint32_t c[4] = {h.x & 0xFFFFu, h.x >> 16, h.y & 0xFFFFu, h.y >> 16};
+    uint64_t acc = 0;
+    int missing = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t nb = T->nbits[lane * 4 + j];
+        acc += (uint64_t)c[j] * nb;
+        missing |= (c[j] != 0 && nb == 0);
+    }
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) acc += __shfl_xor(acc, d, 64);
+    if (__any(missing) && lane == 0) atomicOr(err, 1);
+    if (lane == 0) bits[b] = acc;
+}
+
+// single-workgroup exclusive scan; off[b] relative, off[nblocks] = total
+__global__ __launch_bounds__(1024) void k_block_scan(uint64_t *__restrict__ bits_off, uint64_t nblocks,
+                                                     uint64_t *__restrict__ d_total)
+{
+    __shared__ uint64_t s[1024];
+    const int t = threadIdx.x;
+    const uint64_t per = (nblocks + 1023) / 1024;
+    const uint64_t b0 = (uint64_t)t * per;
+    const uint64_t b1 = (b0 + per < nblocks) ? b0 + per : nblocks;
+    uint64_t sum = 0;
+    for (uint64_t b = b0; b < b1; ++b) sum += bits_off[b];
+    s[t] = sum;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {
+        const uint64_t y = (t >= d) ? s[t - d] : 0ull;
+        __syncthreads();
+        s[t] += y;
+        __syncthreads();
+    }
+    uint64_t run = s[t] - sum;
+    for (uint64_t b = b0; b < b1; ++b) {
+        const uint64_t v = bits_off[b];
+        bits_off[b] = run;
+        run += v;
+    }
+    if (t == 1023) {
+        bits_off[nblocks] = s[1023];
+        *d_total = s[1023];
+    }
+}
+
+// zero every word that two blocks share (the words holding a block start) before
+// k_huff_pack OR-merges into them
+__global__ void k_zero_bounds(const uint64_t *__restrict__ off, uint64_t nblocks, uint64_t bit_base,
+                              uint32_t *__restrict__ words, uint64_t words_cap, int *__restrict__ err)
+{
+    const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b > nblocks || err[0] != 0) return;
+    if (((bit_base & 31) + off[nblocks] + 31) / 32 > words_cap) {
+        if (b == 0) err[2] = 1;
+        return;
+    }
+    const uint64_t abs = bit_base + off[b];
+    if (b == nblocks && (abs & 31) == 0) return;
+    words[(abs >> 5) - (bit_base >> 5)] = 0u;
+}
+
+// ------------------------------------------------------------------------------------
+// (H7) pack. One workgroup per 32 KiB block (grid-stride), 8 tiles of 4 KiB; a lane
+// codes 16 bytes (one 16-B load). Per tile: LDS table lookups -> workgroup scan of bit
+// counts -> each lane writes its bits into an LDS staging area of 32-bit words
+// (ds_or_b32 only for the words it shares with a neighbour lane) -> coalesced dword
+// stores of the complete words; the partial last word is carried to the next tile.
+// Only the two words a block shares with its neighbour blocks are OR-ed into HBM with
+// global atomics. The stream is MSB-first: staged words are byte-swapped on store.
+// ------------------------------------------------------------------------------------
+#define PACK_TILE 4096
+#define PACK_STAGE (PACK_TILE + 64)
+
+__global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ in, uint64_t n,
+                                                   const dc_dtable *__restrict__ T,
+                                                   const uint64_t *__restrict__ block_off, uint64_t bit_base,
+                                                   uint32_t *__restrict__ out, uint64_t *__restrict__ sync,
+                                                   uint32_t sync_syms, uint64_t nblocks, uint64_t words_cap,
+                                                   const int *__restrict__ err)
+{
+    __shared__ uint2 s_tab[256];
+    __shared__ uint32_t s_stage[PACK_STAGE];
+    __shared__ uint32_t s_scan[4];
+    const int t = threadIdx.x;
+    // device-side guards (no host round trip): a byte without a code (plan error) or an
+    // output buffer smaller than the planned stream -> write nothing
+    if (err[0] != 0 || ((bit_base & 31) + block_off[nblocks] + 31) / 32 > words_cap) return;
+    s_tab[t] = make_uint2(T->code[t], T->nbits[t]);
+    const uint64_t word_base = bit_base >> 5;
+    __syncthreads();
+
+    for (uint64_t b = blockIdx.x; b < nblocks; b += gridDim.x) {
+        const uint64_t blk_start = b * (uint64_t)DC_BLOCK_BYTES;
+        const uint64_t blk_end = (blk_start + DC_BLOCK_BYTES < n) ? blk_start + DC_BLOCK_BYTES : n;
+        const uint64_t blk_abs = bit_base + block_off[b];
+        const uint64_t blk_first_word = blk_abs >> 5;
+        uint64_t tile_abs = blk_abs;
+        if (t == 0) s_stage[0] = 0u;
+        __syncthreads();
+        for (uint64_t tile = blk_start; tile < blk_end; tile += PACK_TILE) {
+            const uint64_t p = tile + (uint64_t)t * 16;
+            const int cnt = (p + 16 <= blk_end) ? 16 : (p < blk_end ? (int)(blk_end - p) : 0);
+            uint32_t bytes4[4] = {0u, 0u, 0u, 0u};
+            if (cnt == 16) {
+                const uint4 v = *reinterpret_cast<const uint4 *>(in + p);
+                bytes4[0] = v.x; bytes4[1] = v.y; bytes4[2] = v.z; bytes4[3] = v.w;
+            } else {
+                for (int i = 0; i < cnt; ++i) bytes4[i >> 2] |= (uint32_t)in[p + i] << (8 * (i & 3));
+            }
+            uint32_t code[16], nb[16];
+            uint32_t T_bits = 0;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const uint2 e = s_tab[(bytes4[i >> 2] >> (8 * (i & 3))) & 255u];
+                code[i] = e.x;
+                nb[i] = (i < cnt) ? e.y : 0u;
+                T_bits += nb[i];
+            }
+            uint32_t tile_bits;
+            const uint32_t pre = wg_scan_excl_u32(T_bits, s_scan, &tile_bits);
+            const uint64_t TB = tile_abs >> 5;
+            const uint64_t As = tile_abs + pre;
+            const uint64_t Ae = As + T_bits;
+            if (sync != nullptr && cnt > 0 && (p & (uint64_t)(sync_syms - 1)) == 0)
+                sync[p / sync_syms] = As;
+            const uint32_t ws = (uint32_t)((As >> 5) - TB);
+            if (ws != 0) s_stage[ws] = 0u;
+            if (t == 255) {
+                const uint32_t we = (uint32_t)((Ae >> 5) - TB);
+                if (we != 0) s_stage[we] = 0u;
+            }
+            __syncthreads();
+            if (T_bits > 0) {
+                uint64_t acc = 0;
+                uint32_t nacc = (uint32_t)(As & 31);
+                uint32_t wi = ws;
+                bool first = true;
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    if (nb[i]) {
+                        acc = (acc << nb[i]) | code[i];
+                        nacc += nb[i];
+                        if (nacc >= 32) {
+                            nacc -= 32;
+                            const uint32_t word = (uint32_t)(acc >> nacc);
+                            if (first) atomicOr(&s_stage[wi], word);
+                            else s_stage[wi] = word;
+                            first = false;
+                            ++wi;
+                        }
+                    }
+                }
+                if (nacc > 0) atomicOr(&s_stage[wi], (uint32_t)(acc << (32 - nacc)));
+            }
+            __syncthreads();
+            const uint64_t tile_end_abs = tile_abs + tile_bits;
+            const uint32_t nfull = (uint32_t)((tile_end_abs >> 5) - TB);
+            for (uint32_t i = t; i < nfull; i += 256) {
+                const uint32_t v = bswap32(s_stage[i]);
+                const uint64_t gw = TB + i;
+                if (gw == blk_first_word) atomicOr(&out[gw - word_base], v);
+                else out[gw - word_base] = v;
+            }
+            __syncthreads();
+            if (t == 0) s_stage[0] = (tile_end_abs & 31) ? s_stage[nfull] : 0u;
+            tile_abs = tile_end_abs;
+            __syncthreads();
+        }
+        if (t == 0 && (tile_abs & 31)) atomicOr(&out[(tile_abs >> 5) - word_base], bswap32(s_stage[0]));
+        __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// (H8) decode. One lane per sync chunk (sync_syms symbols): 64-bit MSB-first window,
+// 12-bit LDS lookup table, digit-by-digit canonical fallback for longer codes; output
+// gathered 16 bytes per lane and stored with one 16-B store.
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_huff_decode(const uint32_t *__restrict__ in, uint64_t bit_base,
+                                                     const uint64_t *__restrict__ sync, uint32_t S,
+                                                     uint64_t n, const dc_dtable *__restrict__ T,
+                                                     uint8_t *__restrict__ out, int *__restrict__ err)
+{
+    __shared__ uint16_t s_lut[1 << DC_LUT_BITS];
+    __shared__ uint32_t s_first[DC_MAX_DIGITS + 1], s_count[DC_MAX_DIGITS + 1], s_start[DC_MAX_DIGITS + 1];
+    __shared__ uint16_t s_syms[DC_MAX_SYMS];
+    const int t = threadIdx.x;
+    {
+        const uint4 *src = reinterpret_cast<const uint4 *>(T->lut);
+        uint4 *dst = reinterpret_cast<uint4 *>(s_lut);
+        for (int i = t; i < (1 << DC_LUT_BITS) / 8; i += 256) dst[i] = src[i];
+        for (int L = t; L <= DC_MAX_DIGITS; L += 256) {
+            s_first[L] = T->first[L]; s_count[L] = T->count[L]; s_start[L] = T->start[L];
+        }
+        for (int i = t; i < DC_MAX_SYMS; i += 256) s_syms[i] = T->syms[i];
+    }
+    const int nary = T->n_ary, w = T->w;
+    __syncthreads();
+
+    const uint64_t c = (uint64_t)blockIdx.x * 256 + t;
+    const uint64_t sym0 = c * S;
+    if (sym0 >= n) return;
+    const uint64_t cnt = (n - sym0 < S) ? (n - sym0) : S;
+    const uint64_t rel = sync[c] - ((bit_base >> 5) << 5);
+    const uint32_t *wp = in + (rel >> 5);
+    const uint32_t sh = (uint32_t)(rel & 31);
+    uint64_t win = (((uint64_t)bswap32(wp[0]) << 32) | bswap32(wp[1])) << sh;
+    int wbits = 64 - (int)sh;
+    wp += 2;
+    int bad = 0;
+    uint8_t *o = out + sym0;
+    for (uint64_t g = 0; g < cnt; g += 16) {
+        uint32_t ob[4] = {0u, 0u, 0u, 0u};
+        const int m = (cnt - g >= 16) ? 16 : (int)(cnt - g);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            if (k < m) {
+                if (wbits < 32) {
+                    win |= (uint64_t)bswap32(*wp++) << (32 - wbits);
+                    wbits += 32;
+                }
+                const uint32_t e = s_lut[win >> (64 - DC_LUT_BITS)];
+                uint32_t sym, nbt;
+                if (e != 0) {
+                    sym = e & 255u;
+                    nbt = e >> 8;
+                } else {
+                    // long code: canonical decode one base-n digit at a time
+                    uint64_t x = win;
+                    uint32_t v = 0;
+                    int L = 0;
+                    sym = 0;
+                    nbt = 0;
+                    while (true) {
+                        const uint32_t digit = (uint32_t)(x >> (64 - w));
+                        x <<= w;
+                        v = v * (uint32_t)nary + digit;
+                        ++L;
+                        if (L * w > 32 || L > DC_MAX_DIGITS) { bad = 1; nbt = (uint32_t)w; break; }
+                        if (s_count[L] && v - s_first[L] < s_count[L]) {
+                            sym = s_syms[s_start[L] + (v - s_first[L])];
+                            nbt = (uint32_t)(L * w);
+                            break;
+                        }
+                    }
+                }
+                win <<= nbt;
+                wbits -= (int)nbt;
+                ob[k >> 2] |= (sym & 255u) << (8 * (k & 3));
+            }
+        }
+        if (m == 16) {
+            *reinterpret_cast<uint4 *>(o + g) = make_uint4(ob[0], ob[1], ob[2], ob[3]);
+        } else {
+            for (int k = 0; k < m; ++k) o[g + k] = (uint8_t)(ob[k >> 2] >> (8 * (k & 3)));
+        }
+    }
+    if (bad) atomicOr(err, 1);
+}
+
+// base64url rendering of a bit range (int2digit alphabet, n_ary_huffman.c:371-378)
+__global__ void k_base64url(const uint32_t *__restrict__ words, uint64_t bit_base, uint64_t bits,
+                            char *__restrict__ text)
+{
+    const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t nchar = (bits + 5) / 6;
+    if (c >= nchar) return;
+    const char tbl[65] = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789-_";
+    const uint64_t rel0 = (bit_base & 31) + c * 6;
+    const uint64_t wi = rel0 >> 5;
+    const uint64_t pair = ((uint64_t)bswap32(words[wi]) << 32) |
+                          (((rel0 & 31) > 26) ? bswap32(words[wi + 1]) : 0u);
+    uint32_t v = (uint32_t)((pair << (rel0 & 31)) >> 58);
+    const uint64_t valid = bits - c * 6;
+    if (valid < 6) v &= (0x3Fu << (6 - valid)) & 0x3Fu;
+    text[c] = tbl[v];
+}
+
+// ------------------------------------------------------------------------------------
+// Byte-stream codecs with a 2-state transducer: nybble static encode/decode
+// (nybble_compression.c:734-1038 with modify=false) and the small front-end
+// (small_compression.c:582-665) plus its inverse. Each element (input byte) maps the
+// state s in {0,1} to a next state and an output byte count; composition is associative,
+// so tiles of 4096 elements are summarised, scanned, and re-walked to write.
+//   nybble encode, state = "a hit nybble is pending" (nybble_offset, :908-996):
+//       hit : s -> 1-s, emits s bytes ; miss : s -> 0, emits 1+s bytes ; tail: +s
+//   nybble decode, state = "start at the low nybble" (nybble_offset, :753-795)
+//   small encode / decode: stateless counts
+// ------------------------------------------------------------------------------------
+enum { M_NYB_ENC = 0, M_NYB_DEC = 1, M_SMALL_ENC = 2, M_SMALL_DEC = 3 };
+#define FSM_TILE 4096
+
+struct Fsm {
+    uint32_t c0, c1;   // bytes emitted when entering in state 0 / 1
+    uint32_t s0, s1;   // exit state when entering in state 0 / 1
+};
+static __device__ __forceinline__ Fsm fsm_id() { Fsm f; f.c0 = 0; f.c1 = 0; f.s0 = 0; f.s1 = 1; return f; }
+static __device__ __forceinline__ Fsm fsm_then(const Fsm &a, const Fsm &b)
+{
+    Fsm r;
+    r.c0 = a.c0 + (a.s0 ? b.c1 : b.c0);
+    r.s0 = a.s0 ? b.s1 : b.s0;
+    r.c1 = a.c1 + (a.s1 ? b.c1 : b.c0);
+    r.s1 = a.s1 ? b.s1 : b.s0;
+    return r;
+}
+
+__constant__ uint8_t c_static_rank[256];   // " etaoins" -> 0..7, else 0xFF (initialize_dictionary)
+
+static __device__ __forceinline__ bool is_lower(uint32_t b) { return b >= 'a' && b <= 'z'; }
+
+// element j of mode M: transducer entry
+template <int M>
+static __device__ __forceinline__ Fsm elem_fsm(const uint8_t *__restrict__ in, uint64_t len, uint64_t j)
+{
+    Fsm f;
+    if (M == M_NYB_ENC) {                // byte i = j+1
+        const uint32_t x = in[j + 1];
+        if (c_static_rank[x] != 0xFF) { f.c0 = 0; f.c1 = 1; f.s0 = 1; f.s1 = 0; }
+        else { f.c0 = 1; f.c1 = 2; f.s0 = 0; f.s1 = 0; }
+    } else if (M == M_NYB_DEC) {         // compressed byte k = j+2
+        const uint32_t b = in[j + 2];
+        const uint32_t h = b >> 4, l = b & 15;
+        if (h & 8) { f.c0 = 2; f.s0 = (l & 8) ? 0 : 1; }
+        else { f.c0 = 1; f.s0 = 0; }
+        f.c1 = 1;
+        f.s1 = (l & 8) ? 0 : 1;
+    } else if (M == M_SMALL_ENC) {       // byte i = j+1
+        const uint64_t i = j + 1;
+        const uint32_t x = in[i];
+        const bool second = (i >= 2) && in[i - 1] == ' ' && is_lower(x);
+        f.c0 = f.c1 = second ? 0 : 1;
+        f.s0 = f.s1 = 0;
+    } else {                             // small decode, byte k = j+2
+        const uint32_t b = in[j + 2];
+        f.c0 = f.c1 = (b >= 0x80) ? 2 : 1;
+        f.s0 = f.s1 = 0;
+    }
+    (void)len;
+    return f;
+}
+
+template <int M>
+__global__ __launch_bounds__(256) void k_fsm_tiles(const uint8_t *__restrict__ in, uint64_t len,
+                                                   uint64_t nelem, uint4 *__restrict__ summ)
+{
+    __shared__ uint4 s_f[256];
+    const int t = threadIdx.x;
+    const uint64_t j0 = (uint64_t)blockIdx.x * FSM_TILE + (uint64_t)t * 16;
+    Fsm f = fsm_id();
+    for (int k = 0; k < 16; ++k) {
+        const uint64_t j = j0 + k;
+        if (j < nelem) f = fsm_then(f, elem_fsm<M>(in, len, j));
+    }
+    s_f[t] = make_uint4(f.c0, f.c1, f.s0, f.s1);
+    __syncthreads();
+    for (int stride = 128; stride > 0; stride >>= 1) {
+        const bool act = t < stride;
+        Fsm r = fsm_id();
+        if (act) {
+            const uint4 a = s_f[2 * t], b = s_f[2 * t + 1];
+            Fsm fa, fb;
+            fa.c0 = a.x; fa.c1 = a.y; fa.s0 = a.z; fa.s1 = a.w;
+            fb.c0 = b.x; fb.c1 = b.y; fb.s0 = b.z; fb.s1 = b.w;
+            r = fsm_then(fa, fb);
+        }
+        __syncthreads();
+        if (act) s_f[t] = make_uint4(r.c0, r.c1, r.s0, r.s1);
+        __syncthreads();
+    }
+    if (t == 0) summ[blockIdx.x] = s_f[0];
+}
+
+// single workgroup: tile entry (offset, state) from the summaries; meta[0] = total count,
+// meta[1] = final state (starting from state 0)
+__global__ __launch_bounds__(1024) void k_fsm_scan(const uint4 *__restrict__ summ, uint64_t ntiles,
+                                                   uint64_t *__restrict__ entry, uint64_t *__restrict__ meta)
+{
+    __shared__ uint64_t s_c0[1024], s_c1[1024];
+    __shared__ uint32_t s_s0[1024], s_s1[1024];
+    const int t = threadIdx.x;
+    const uint64_t per = (ntiles + 1023) / 1024;
+    const uint64_t a0 = (uint64_t)t * per;
+    const uint64_t a1 = (a0 + per < ntiles) ? a0 + per : ntiles;
+    uint64_t c0 = 0, c1 = 0;
+    uint32_t s0 = 0, s1 = 1;
+    for (uint64_t k = a0; k < a1; ++k) {
+        const uint4 b = summ[k];
+        const uint64_t n0 = c0 + (s0 ? b.y : b.x), n1 = c1 + (s1 ? b.y : b.x);
+        const uint32_t m0 = s0 ? b.w : b.z, m1 = s1 ? b.w : b.z;
+        c0 = n0; c1 = n1; s0 = m0; s1 = m1;
+    }
+    s_c0[t] = c0; s_c1[t] = c1; s_s0[t] = s0; s_s1[t] = s1;
+    __syncthreads();
+    // inclusive Hillis-Steele over compositions (left operand = earlier)
+    for (int d = 1; d < 1024; d <<= 1) {
+        uint64_t pc0 = 0, pc1 = 0;
+        uint32_t ps0 = 0, ps1 = 1;
+        const bool has = t >= d;
+        if (has) { pc0 = s_c0[t - d]; pc1 = s_c1[t - d]; ps0 = s_s0[t - d]; ps1 = s_s1[t - d]; }
+        const uint64_t mc0 = s_c0[t], mc1 = s_c1[t];
+        const uint32_t ms0 = s_s0[t], ms1 = s_s1[t];
+        __syncthreads();
+        if (has) {
+            s_c0[t] = pc0 + (ps0 ? mc1 : mc0);
+            s_s0[t] = ps0 ? ms1 : ms0;
+            s_c1[t] = pc1 + (ps1 ? mc1 : mc0);
+            s_s1[t] = ps1 ? ms1 : ms0;
+        }
+        __syncthreads();
+    }
+    // exclusive prefix applied to the initial state 0
+    uint64_t off = 0;
+    uint32_t st = 0;
+    if (t > 0) { off = s_c0[t - 1]; st = s_s0[t - 1]; }
+    for (uint64_t k = a0; k < a1; ++k) {
+        entry[k] = (off << 1) | st;
+        const uint4 b = summ[k];
+        off += st ? b.y : b.x;
+        st = st ? b.w : b.z;
+    }
+    if (t == 1023) { meta[0] = s_c0[1023]; meta[1] = s_s0[1023]; }
+}
+
+// Re-walk each tile with its entry state and write the output bytes.
+//   layout: nybble/small encode: out[0] = type, out[1] = x[0], body at out[2..];
+//           decoders: out[0] = in[1], body at out[1..]. Encoders fall back to
+//           LITERAL (' ' + raw, :1018-1037) when the stream is not shorter than n.
+template <int M>
+__global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ in, uint64_t len, uint64_t nelem,
+                                                   const uint64_t *__restrict__ entry,
+                                                   const uint64_t *__restrict__ meta, uint8_t *__restrict__ out)
+{
+    __shared__ uint4 s_f[256];
+    __shared__ uint64_t s_base[256];
+    __shared__ uint32_t s_st[256];
+    const int t = threadIdx.x;
+    const bool enc = (M == M_NYB_ENC || M == M_SMALL_ENC);
+    const uint64_t body = (M == M_NYB_ENC) ? meta[0] + meta[1] : meta[0];
+    const uint64_t total = enc ? 2 + body : 1 + body;
+    const bool literal = enc && total >= len;
+    if (literal) {
+        // copy x -> out[1..len], one grid-stride pass
+        for (uint64_t i = (uint64_t)blockIdx.x * 256 + t; i < len; i += (uint64_t)gridDim.x * 256)
+            out[1 + i] = in[i];
+        if (blockIdx.x == 0 && t == 0) out[0] = ' ';
+        return;
+    }
+    if (blockIdx.x == 0 && t == 0) {
+        if (M == M_NYB_ENC) { out[0] = 0xAF; out[1] = in[0]; }
+        else if (M == M_SMALL_ENC) { out[0] = 8; out[1] = in[0]; }
+        else { out[0] = in[1]; }
+    }
+    const uint64_t j0 = (uint64_t)blockIdx.x * FSM_TILE + (uint64_t)t * 16;
+    Fsm f = fsm_id();
+    for (int k = 0; k < 16; ++k) {
+        const uint64_t j = j0 + k;
+        if (j < nelem) f = fsm_then(f, elem_fsm<M>(in, len, j));
+    }
+    // workgroup exclusive scan of compositions (Hillis-Steele on the 256 thread maps)
+    s_f[t] = make_uint4(f.c0, f.c1, f.s0, f.s1);
+    __syncthreads();
+    for (int d = 1; d < 256; d <<= 1) {
+        uint4 p = make_uint4(0, 0, 0, 1);
+        const bool has = t >= d;
+        if (has) p = s_f[t - d];
+        const uint4 me = s_f[t];
+        __syncthreads();
+        if (has) {
+            Fsm fa, fb;
+            fa.c0 = p.x; fa.c1 = p.y; fa.s0 = p.z; fa.s1 = p.w;
+            fb.c0 = me.x; fb.c1 = me.y; fb.s0 = me.z; fb.s1 = me.w;
+            const Fsm r = fsm_then(fa, fb);
+            s_f[t] = make_uint4(r.c0, r.c1, r.s0, r.s1);
+        }
+        __syncthreads();
+    }
+    const uint64_t e = entry[blockIdx.x];
+    uint64_t o = e >> 1;
+    uint32_t s = (uint32_t)(e & 1);
+    if (t > 0) {
+        const uint4 p = s_f[t - 1];
+        o += s ? p.y : p.x;
+        s = s ? p.w : p.z;
+    }
+    (void)s_base; (void)s_st;
+    const uint64_t head = enc ? 2 : 1;
+    o += head;
+    for (int k = 0; k < 16; ++k) {
+        const uint64_t j = j0 + k;
+        if (j >= nelem) break;
+        if (M == M_NYB_ENC) {
+            const uint64_t i = j + 1;
+            const uint32_t x = in[i];
+            const uint32_t r = c_static_rank[x];
+            if (r != 0xFF) {
+                if (s == 1) {
+                    const uint32_t rp = c_static_rank[in[i - 1]];
+                    out[o++] = (uint8_t)(((8u | rp) << 4) | (8u | r));
+                    s = 0;
+                } else {
+                    s = 1;
+                    if (i == len - 1) out[o] = (uint8_t)x;   // odd tail (:1000-1009)
+                }
+            } else {
+                if (s == 1) { out[o++] = in[i - 1]; out[o++] = (uint8_t)x; }
+                else out[o++] = (uint8_t)x;
+                s = 0;
+            }
+        } else if (M == M_NYB_DEC) {
+            const uint64_t kk = j + 2;
+            const uint32_t b = in[kk];
+            const uint32_t h = b >> 4, l = b & 15;
+            const uint32_t nxt = (kk + 1 < len) ? (uint32_t)(in[kk + 1] >> 4) : 0u;
+            const uint8_t *tbl = (const uint8_t *)" etaoins";
+            if (s == 0) {
+                if (h & 8) {
+                    out[o++] = tbl[h & 7];
+                    if (l & 8) { out[o++] = tbl[l & 7]; s = 0; }
+                    else { out[o++] = (uint8_t)(((l & 7) << 4) + nxt); s = 1; }
+                } else {
+                    out[o++] = (uint8_t)b;
+                    s = 0;
+                }
+            } else {
+                if (l & 8) { out[o++] = tbl[l & 7]; s = 0; }
+                else { out[o++] = (uint8_t)(((l & 7) << 4) + nxt); s = 1; }
+            }
+        } else if (M == M_SMALL_ENC) {
+            const uint64_t i = j + 1;
+            const uint32_t x = in[i];
+            const bool second = (i >= 2) && in[i - 1] == ' ' && is_lower(x);
+            if (!second) {
+                if (x == ' ' && i + 1 < len && is_lower(in[i + 1])) out[o++] = (uint8_t)(0x80 + in[i + 1]);
+                else out[o++] = (uint8_t)x;
+            }
+        } else {
+            const uint32_t b = in[j + 2];
+            if (b >= 0x80) { out[o++] = ' '; out[o++] = (uint8_t)(b - 0x80); }
+            else out[o++] = (uint8_t)b;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// Adaptive (modify=true) nybble codec: the context/move-to-front state depends on the
+// whole history (N4), so a single stream is walked by one lane; the 16x8
+// MTF lists live in LDS. Same algorithm as nybble_compression.c:643-1038.
+// ------------------------------------------------------------------------------------
+static __device__ __forceinline__ void mtf_touch(uint8_t *list, uint8_t v)
+{
+    uint8_t carry = v;
+    for (int p = 0; p < 8; ++p) {
+        const uint8_t old = list[p];
+        list[p] = carry;
+        carry = old;
+        if (carry == v) break;
+    }
+}
+
+__global__ void k_nyb_seq(const uint8_t *__restrict__ in, uint64_t len, int enc, int modify,
+                          uint8_t *__restrict__ out, uint64_t *__restrict__ meta)
+{
+    __shared__ uint8_t lists[16][8];
+    if (threadIdx.x != 0) return;
+    const uint8_t init[8] = {' ', 'e', 't', 'a', 'o', 'i', 'n', 's'};
+    for (int c = 0; c < 16; ++c)
+        for (int r = 0; r < 8; ++r) lists[c][r] = init[r];
+    uint64_t o = 0;
+    if (enc) {
+        out[o++] = 0xAF;
+        out[o++] = in[0];
+        int half = 0;
+        for (uint64_t i = 1; i < len; ++i) {
+            const uint8_t xp = in[i - 1], x = in[i];
+            const int c = (xp >> 3) & 15;
+            int r = -1;
+            for (int q = 0; q < 8; ++q) if (lists[c][q] == x) { r = q; break; }
+            if (r < 0) {
+                if (!half) out[o++] = x;
+                else { out[o] = xp; out[o + 1] = x; o += 2; half = 0; }
+            } else {
+                const uint8_t nyb = (uint8_t)(8 | r);
+                if (!half) { out[o] = (uint8_t)(nyb << 4); half = 1; }
+                else { out[o] = (uint8_t)(out[o] | nyb); ++o; half = 0; }
+            }
+            if (modify) mtf_touch(lists[c], x);
+        }
+        if (half) out[o++] = in[len - 1];
+        if (o >= len) {   // LITERAL fallback
+            out[0] = ' ';
+            for (uint64_t i = 0; i < len; ++i) out[1 + i] = in[i];
+            o = len + 1;
+        }
+    } else {
+        out[o++] = in[1];
+        uint64_t pos = 2;
+        int off = 0;
+        while (pos < len) {
+            const uint8_t b = in[pos];
+            int nyb, nxt;
+            if (off == 0) { nyb = b >> 4; nxt = b & 15; }
+            else { nyb = b & 15; nxt = (pos + 1 < len) ? (in[pos + 1] >> 4) : 0; }
+            const int c = (out[o - 1] >> 3) & 15;
+            int used;
+            if (nyb & 8) { out[o] = lists[c][nyb & 7]; used = 1; }
+            else { out[o] = (uint8_t)(((nyb & 7) << 4) + nxt); used = 2; }
+            if (modify) mtf_touch(lists[c], out[o]);
+            ++o;
+            off += used;
+            if (off >= 2) { ++pos; off -= 2; }
+        }
+    }
+    meta[0] = o;
+}
+
+// =====================================================================================
+// host side
+// =====================================================================================
+#define DC_MAX_EVENTS 64
+
+struct dc_ctx {
+    int device;
+    hipStream_t stream;
+    bool own_stream;
+    // workspace
+    uint16_t *d_bh;         size_t bh_cap;        // block histograms (u16 x 256 per block)
+    uint64_t *d_partials;                         // 1024 x 256
+    uint64_t *d_off;        size_t off_cap;       // nblocks + 1
+    int *d_err;                                   // [0] plan, [1] decode
+    uint64_t *d_meta;                             // small device scalars
+    uint4 *d_summ;          size_t summ_cap;
+    uint64_t *d_entry;      size_t entry_cap;
+    uint64_t *h_pinned;                           // pinned host scalars
+    const uint8_t *hist_in; uint64_t hist_n;      // identity of the last dc_huff_hist input
+    bool plan_ok;
+    // timing
+    int timing;
+    int nev;
+    hipEvent_t ev0[DC_MAX_EVENTS], ev1[DC_MAX_EVENTS];
+    const char *evname[DC_MAX_EVENTS];
+    bool events_made;
+};
+
+#define HIPCHK(x) do { if ((x) != hipSuccess) return DC_E_HIP; } while (0)
+
+static int ensure(void **p, size_t *cap, size_t bytes)
+{
+    if (*cap >= bytes && *p) return DC_OK;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    size_t want = bytes < 4096 ? 4096 : bytes;
+    if (hipMalloc(p, want) != hipSuccess) { *p = nullptr; return DC_E_HIP; }
+    *cap = want;
+    return DC_OK;
+}
+
+static void t_begin(dc_ctx *c, const char *name, int *slot)
+{
+    *slot = -1;
+    if (!c->timing || c->nev >= DC_MAX_EVENTS) return;
+    *slot = c->nev++;
+    c->evname[*slot] = name;
+    (void)hipEventRecord(c->ev0[*slot], c->stream);
+}
+static void t_end(dc_ctx *c, int slot)
+{
+    if (slot >= 0) (void)hipEventRecord(c->ev1[slot], c->stream);
+}
+
+#define LAUNCH(ctx, name, kern, grid, block, ...) do {                         \
+        int _slot; t_begin(ctx, name, &_slot);                                  \
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(block), 0, ctx->stream, __VA_ARGS__); \
+        if (hipGetLastError() != hipSuccess) return DC_E_HIP;                   \
+        t_end(ctx, _slot);                                                      \
+    } while (0)
+
+static int g_rank_uploaded = -1;
+
+extern "C" {
+
+const char *dc_version(void) { return DC_VERSION; }
+size_t dc_dtable_size(void) { return sizeof(dc_dtable); }
+
+int dc_ctx_create(dc_ctx **out, int device, void *stream)
+{
+    if (!out) return DC_E_ARG;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || device >= ndev) return DC_E_HIP;
+    HIPCHK(hipSetDevice(device));
+    dc_ctx *c = (dc_ctx *)calloc(1, sizeof(dc_ctx));
+    if (!c) return DC_E_ARG;
+    c->device = device;
+    if (stream) { c->stream = (hipStream_t)stream; c->own_stream = false; }
+    else {
+        if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) { free(c); return DC_E_HIP; }
+        c->own_stream = true;
+    }
+    if (hipMalloc((void **)&c->d_partials, 1024 * 256 * sizeof(uint64_t)) != hipSuccess ||
+        hipMalloc((void **)&c->d_err, 16 * sizeof(int)) != hipSuccess ||
+        hipMalloc((void **)&c->d_meta, 16 * sizeof(uint64_t)) != hipSuccess ||
+        hipHostMalloc((void **)&c->h_pinned, 16 * sizeof(uint64_t), 0) != hipSuccess) {
+        free(c);
+        return DC_E_HIP;
+    }
+    if (g_rank_uploaded != device) {
+        uint8_t rank[256];
+        memset(rank, 0xFF, sizeof(rank));
+        const char *t = " etaoins";
+        for (int r = 0; r < 8; ++r) rank[(uint8_t)t[r]] = (uint8_t)r;
+        if (hipMemcpyToSymbol(HIP_SYMBOL(c_static_rank), rank, 256) != hipSuccess) { free(c); return DC_E_HIP; }
+        g_rank_uploaded = device;
+    }
+    *out = c;
+    return DC_OK;
+}
+
+void dc_ctx_destroy(dc_ctx *c)
+{
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    if (c->d_bh) (void)hipFree(c->d_bh);
+    if (c->d_partials) (void)hipFree(c->d_partials);
+    if (c->d_off) (void)hipFree(c->d_off);
+    if (c->d_err) (void)hipFree(c->d_err);
+    if (c->d_meta) (void)hipFree(c->d_meta);
+    if (c->d_summ) (void)hipFree(c->d_summ);
+    if (c->d_entry) (void)hipFree(c->d_entry);
+    if (c->h_pinned) (void)hipHostFree(c->h_pinned);
+    if (c->events_made)
+        for (int i = 0; i < DC_MAX_EVENTS; ++i) { (void)hipEventDestroy(c->ev0[i]); (void)hipEventDestroy(c->ev1[i]); }
+    if (c->own_stream) (void)hipStreamDestroy(c->stream);
+    free(c);
+}
+
+int dc_ctx_sync(dc_ctx *c) { return (c && hipStreamSynchronize(c->stream) == hipSuccess) ? DC_OK : DC_E_HIP; }
+void *dc_ctx_stream(dc_ctx *c) { return c ? (void *)c->stream : nullptr; }
+
+int dc_ctx_set_timing(dc_ctx *c, int enable)
+{
+    if (!c) return DC_E_ARG;
+    if (enable && !c->events_made) {
+        for (int i = 0; i < DC_MAX_EVENTS; ++i) {
+            HIPCHK(hipEventCreate(&c->ev0[i]));
+            HIPCHK(hipEventCreate(&c->ev1[i]));
+        }
+        c->events_made = true;
+    }
+    c->timing = enable;
+    c->nev = 0;
+    return DC_OK;
+}
+
+int dc_ctx_timings(dc_ctx *c, const char **names, float *ms, int max)
+{
+    if (!c) return DC_E_ARG;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    int n = c->nev < max ? c->nev : max;
+    for (int i = 0; i < n; ++i) {
+        names[i] = c->evname[i];
+        float v = 0.f;
+        HIPCHK(hipEventElapsedTime(&v, c->ev0[i], c->ev1[i]));
+        ms[i] = v;
+    }
+    return n;
+}
+
+int dc_malloc(void **p, size_t bytes) { return hipMalloc(p, bytes ? bytes : 1) == hipSuccess ? DC_OK : DC_E_HIP; }
+int dc_free(void *p) { return hipFree(p) == hipSuccess ? DC_OK : DC_E_HIP; }
+int dc_memcpy_h2d(dc_ctx *c, void *d, const void *h, size_t bytes)
+{
+    if (!bytes) return DC_OK;
+    HIPCHK(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return DC_OK;
+}
+int dc_memcpy_d2h(dc_ctx *c, void *h, const void *d, size_t bytes)
+{
+    if (!bytes) return DC_OK;
+    HIPCHK(hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return DC_OK;
+}
+int dc_memset(dc_ctx *c, void *d, int v, size_t bytes)
+{
+    if (!bytes) return DC_OK;
+    HIPCHK(hipMemsetAsync(d, v, bytes, c->stream));
+    return DC_OK;
+}
+
+// ---- Huffman -----------------------------------------------------------------------
+static uint64_t nblocks_of(uint64_t n) { return (n + DC_BLOCK_BYTES - 1) / DC_BLOCK_BYTES; }
+
+int dc_huff_hist(dc_ctx *c, const uint8_t *d_in, uint64_t n, uint64_t *d_hist)
+{
+    if (!c || !d_hist || (n && !d_in)) return DC_E_ARG;
+    if (((uintptr_t)d_in) & 15) return DC_E_ARG;
+    const uint64_t nb = nblocks_of(n);
+    if (ensure((void **)&c->d_bh, &c->bh_cap, (nb ? nb : 1) * 256 * sizeof(uint16_t))) return DC_E_HIP;
+    c->hist_in = d_in;
+    c->hist_n = n;
+    c->plan_ok = false;
+    if (nb == 0) {
+        HIPCHK(hipMemsetAsync(d_hist, 0, 256 * sizeof(uint64_t), c->stream));
+        return DC_OK;
+    }
+    const uint64_t grid = nb < 2048 ? nb : 2048;
+    LAUNCH(c, "hist_blocks", k_hist_blocks, grid, 256, d_in, n, nb, c->d_bh);
+    const int G = (int)(nb < 512 ? nb : 512);
+    LAUNCH(c, "hist_reduce", k_hist_reduce, G, 256, (const uint16_t *)c->d_bh, nb, c->d_partials);
+    LAUNCH(c, "hist_final", k_hist_final, 1, 256, (const uint64_t *)c->d_partials, G, d_hist);
+    return DC_OK;
+}
+
+static int table_common(dc_ctx *c, const uint64_t *d_freq, int is_hist, const int32_t *d_len, int M,
+                        int nary, dc_dtable *d_table)
+{
+    if (!c || !d_table || M < 0 || M >= DC_MAX_SYMS || nary < 2 || nary > 256) return DC_E_ARG;
+    LAUNCH(c, "huff_table", k_huff_table, 1, 256, d_freq, is_hist, d_len, M, nary, d_table);
+    return DC_OK;
+}
+
+int dc_huff_table(dc_ctx *c, const uint64_t *d_hist, int M, int nary, dc_dtable *d_table)
+{
+    if (!d_hist) return DC_E_ARG;
+    return table_common(c, d_hist, 1, nullptr, M, nary, d_table);
+}
+int dc_huff_table_freq(dc_ctx *c, const uint64_t *d_freq, int M, int nary, dc_dtable *d_table)
+{
+    if (!d_freq) return DC_E_ARG;
+    return table_common(c, d_freq, 0, nullptr, M, nary, d_table);
+}
+int dc_huff_table_lengths(dc_ctx *c, const int32_t *d_len, int M, int nary, dc_dtable *d_table)
+{
+    if (!d_len) return DC_E_ARG;
+    return table_common(c, nullptr, 0, d_len, M, nary, d_table);
+}
+
+int dc_huff_table_status(dc_ctx *c, const dc_dtable *d_table, int32_t *max_bits)
+{
+    int32_t v[2];
+    HIPCHK(hipMemcpyAsync(v, &d_table->max_bits, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(v + 1, &d_table->status, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (max_bits) *max_bits = v[0];
+    return v[1];
+}
+
+int dc_huff_plan(dc_ctx *c, const dc_dtable *d_table, uint64_t *d_total_bits)
+{
+    if (!c || !d_table || !d_total_bits) return DC_E_ARG;
+    if (!c->hist_in && c->hist_n) return DC_E_STATE;
+    const uint64_t nb = nblocks_of(c->hist_n);
+    if (ensure((void **)&c->d_off, &c->off_cap, (nb + 1) * sizeof(uint64_t))) return DC_E_HIP;
+    HIPCHK(hipMemsetAsync(c->d_err, 0, 16 * sizeof(int), c->stream));
+    if (nb == 0) {
+        HIPCHK(hipMemsetAsync(c->d_off, 0, sizeof(uint64_t), c->stream));
+        HIPCHK(hipMemsetAsync(d_total_bits, 0, sizeof(uint64_t), c->stream));
+        c->plan_ok = true;
+        return DC_OK;
+    }
+    LAUNCH(c, "block_bits", k_block_bits, (nb + 3) / 4, 256, (const uint16_t *)c->d_bh, nb, d_table, c->d_off,
+           c->d_err);
+    LAUNCH(c, "block_scan", k_block_scan, 1, 1024, c->d_off, nb, d_total_bits);
+    c->plan_ok = true;
+    return DC_OK;
+}
+
+uint64_t dc_huff_words_needed(uint64_t bit_base, uint64_t total_bits)
+{
+    return (((bit_base & 31) + total_bits + 31) >> 5) + 4;   // + slack for the decoder's look-ahead
+}
+
+int dc_huff_pack_async(dc_ctx *c, const uint8_t *d_in, uint64_t n, const dc_dtable *d_table, uint64_t bit_base,
+                       uint32_t *d_words, uint64_t words_cap, uint64_t *d_sync, uint32_t sync_syms)
+{
+    if (!c || !d_table || !d_words) return DC_E_ARG;
+    if (d_in != c->hist_in || n != c->hist_n || !c->plan_ok) return DC_E_STATE;
+    if (d_sync && (sync_syms < 16 || (sync_syms & (sync_syms - 1)))) return DC_E_ARG;
+    const uint64_t nb = nblocks_of(n);
+    if (nb == 0) return DC_OK;
+    LAUNCH(c, "zero_bounds", k_zero_bounds, (nb + 1 + 255) / 256, 256, (const uint64_t *)c->d_off, nb, bit_base,
+           d_words, words_cap, c->d_err);
+    const uint64_t grid = nb < 4096 ? nb : 4096;
+    LAUNCH(c, "huff_pack", k_huff_pack, grid, 256, d_in, n, d_table, (const uint64_t *)c->d_off, bit_base, d_words,
+           d_sync, sync_syms, nb, words_cap, (const int *)c->d_err);
+    return DC_OK;
+}
+
+int dc_huff_pack_status(dc_ctx *c, const dc_dtable *d_table)
+{
+    int v[3] = {0, 0, 0};
+    HIPCHK(hipMemcpyAsync(v, c->d_err, 3 * sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (v[0]) {
+        const int st = dc_huff_table_status(c, d_table, nullptr);
+        return st ? st : DC_E_NOCODE;
+    }
+    return v[2] ? DC_E_CAPACITY : DC_OK;
+}
+
+int dc_huff_pack(dc_ctx *c, const uint8_t *d_in, uint64_t n, const dc_dtable *d_table, uint64_t bit_base,
+                 uint32_t *d_words, uint64_t words_cap, uint64_t *d_sync, uint32_t sync_syms)
+{
+    if (!c || !d_table || !d_words) return DC_E_ARG;
+    if (d_in != c->hist_in || n != c->hist_n || !c->plan_ok) return DC_E_STATE;
+    if (d_sync && (sync_syms < 16 || (sync_syms & (sync_syms - 1)))) return DC_E_ARG;
+    // plan errors (a byte without a code) are checked here: host read of one int
+    int err = 0;
+    HIPCHK(hipMemcpyAsync(c->h_pinned, c->d_err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(c->h_pinned + 1, c->d_off + nblocks_of(n), sizeof(uint64_t), hipMemcpyDeviceToHost,
+                          c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    err = *(int *)c->h_pinned;
+    if (err) {
+        const int st = dc_huff_table_status(c, d_table, nullptr);
+        return st ? st : DC_E_NOCODE;
+    }
+    const uint64_t total = c->h_pinned[1];
+    if (dc_huff_words_needed(bit_base, total) > words_cap) return DC_E_CAPACITY;
+    return dc_huff_pack_async(c, d_in, n, d_table, bit_base, d_words, words_cap, d_sync, sync_syms);
+}
+
+uint32_t dc_huff_default_sync(uint64_t n)
+{
+    uint32_t S = 64;
+    while (S < (1u << 16) && (n >> 19) > S) S <<= 1;
+    return S;
+}
+
+int dc_huff_decode(dc_ctx *c, const uint32_t *d_words, uint64_t bit_base, uint64_t words, const uint64_t *d_sync,
+                   uint32_t S, uint64_t n, const dc_dtable *d_table, uint8_t *d_out)
+{
+    if (!c || !d_table || (n && (!d_words || !d_sync || !d_out))) return DC_E_ARG;
+    if (S < 16 || (S & (S - 1))) return DC_E_ARG;
+    if (((uintptr_t)d_out) & 15) return DC_E_ARG;
+    (void)words;
+    if (n == 0) return DC_OK;
+    const uint64_t nchunks = (n + S - 1) / S;
+    HIPCHK(hipMemsetAsync(c->d_err + 1, 0, sizeof(int), c->stream));
+    LAUNCH(c, "huff_decode", k_huff_decode, (nchunks + 255) / 256, 256, d_words, bit_base, d_sync, S, n, d_table,
+           d_out, c->d_err + 1);
+    return DC_OK;
+}
+
+int dc_huff_decode_status(dc_ctx *c)
+{
+    int v = 0;
+    HIPCHK(hipMemcpyAsync(&v, c->d_err + 1, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return v ? DC_E_STREAM : DC_OK;
+}
+
+int dc_huff_base64url(dc_ctx *c, const uint32_t *d_words, uint64_t bit_base, uint64_t bits, char *d_text)
+{
+    if (!c || (bits && (!d_words || !d_text))) return DC_E_ARG;
+    const uint64_t nchar = (bits + 5) / 6;
+    if (nchar == 0) return DC_OK;
+    LAUNCH(c, "base64url", k_base64url, (nchar + 255) / 256, 256, d_words, bit_base, bits, d_text);
+    return DC_OK;
+}
+
+}  // extern "C"
+
+// ---- byte-stream transducer codecs --------------------------------------------------
+template <int M>
+static int fsm_run(dc_ctx *c, const uint8_t *d_in, uint64_t len, uint64_t nelem, uint8_t *d_out, uint64_t *h_len,
+                   const char *name)
+{
+    const uint64_t ntiles = (nelem + FSM_TILE - 1) / FSM_TILE;
+    const uint64_t nt = ntiles ? ntiles : 1;
+    if (ensure((void **)&c->d_summ, &c->summ_cap, nt * sizeof(uint4))) return DC_E_HIP;
+    if (ensure((void **)&c->d_entry, &c->entry_cap, nt * sizeof(uint64_t))) return DC_E_HIP;
+    if (ntiles == 0) {
+        HIPCHK(hipMemsetAsync(c->d_meta, 0, 2 * sizeof(uint64_t), c->stream));
+        HIPCHK(hipMemsetAsync(c->d_entry, 0, sizeof(uint64_t), c->stream));
+    } else {
+        LAUNCH(c, name, k_fsm_tiles<M>, ntiles, 256, d_in, len, nelem, c->d_summ);
+        LAUNCH(c, "fsm_scan", k_fsm_scan, 1, 1024, (const uint4 *)c->d_summ, ntiles, c->d_entry, c->d_meta);
+    }
+    const uint64_t wgrid = ntiles ? ntiles : 1;
+    LAUNCH(c, "fsm_write", k_fsm_write<M>, wgrid, 256, d_in, len, nelem, (const uint64_t *)c->d_entry,
+           (const uint64_t *)c->d_meta, d_out);
+    HIPCHK(hipMemcpyAsync(c->h_pinned, c->d_meta, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    const bool enc = (M == M_NYB_ENC || M == M_SMALL_ENC);
+    const uint64_t body = (M == M_NYB_ENC) ? c->h_pinned[0] + c->h_pinned[1] : c->h_pinned[0];
+    uint64_t total = enc ? 2 + body : 1 + body;
+    if (enc && total >= len) total = len + 1;
+    *h_len = total;
+    return DC_OK;
+}
+
+static int read_byte(dc_ctx *c, const uint8_t *d, uint8_t *v)
+{
+    HIPCHK(hipMemcpyAsync(c->h_pinned, d, 1, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    *v = *(uint8_t *)c->h_pinned;
+    return DC_OK;
+}
+
+static int write_byte(dc_ctx *c, uint8_t *d, uint8_t v)
+{
+    HIPCHK(hipMemsetAsync(d, v, 1, c->stream));
+    return DC_OK;
+}
+
+// decoder type dispatch shared by nybble and small (:744, :799, :806)
+static int copy_typed(dc_ctx *c, const uint8_t *d_in, uint64_t m, uint8_t type, uint8_t *d_out, uint64_t *h_len,
+                      bool *handled)
+{
+    *handled = true;
+    if (type == ' ') {
+        if (m > 1) HIPCHK(hipMemcpyAsync(d_out, d_in + 1, m - 1, hipMemcpyDeviceToDevice, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        *h_len = m - 1;
+        return DC_OK;
+    }
+    *handled = false;
+    return DC_OK;
+}
+
+extern "C" {
+
+int dc_nyb_compress(dc_ctx *c, const uint8_t *d_in, uint64_t n, int modify, uint8_t *d_out, uint64_t *h_len)
+{
+    if (!c || !d_out || !h_len || (n && !d_in)) return DC_E_ARG;
+    if (n == 0) { int r = write_byte(c, d_out, ' '); if (r) return r; HIPCHK(hipStreamSynchronize(c->stream)); *h_len = 1; return DC_OK; }
+    if (!modify) return fsm_run<M_NYB_ENC>(c, d_in, n, n - 1, d_out, h_len, "nyb_enc_tiles");
+    LAUNCH(c, "nyb_seq_enc", k_nyb_seq, 1, 64, d_in, n, 1, 1, d_out, c->d_meta);
+    HIPCHK(hipMemcpyAsync(c->h_pinned, c->d_meta, sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    *h_len = c->h_pinned[0];
+    return DC_OK;
+}
+
+int dc_nyb_decompress(dc_ctx *c, const uint8_t *d_in, uint64_t m, int modify, uint8_t *d_out, uint64_t *h_len)
+{
+    if (!c || !d_out || !h_len || (m && !d_in)) return DC_E_ARG;
+    if (m == 0) { *h_len = 0; return DC_OK; }
+    uint8_t type = 0;
+    int r = read_byte(c, d_in, &type);
+    if (r) return r;
+    if (type == 0xAF) {
+        if (m < 2) { *h_len = 0; return DC_OK; }
+        if (!modify) return fsm_run<M_NYB_DEC>(c, d_in, m, m - 2, d_out, h_len, "nyb_dec_tiles");
+        LAUNCH(c, "nyb_seq_dec", k_nyb_seq, 1, 64, d_in, m, 0, 1, d_out, c->d_meta);
+        HIPCHK(hipMemcpyAsync(c->h_pinned, c->d_meta, sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        *h_len = c->h_pinned[0];
+        return DC_OK;
+    }
+    bool handled = false;
+    r = copy_typed(c, d_in, m, type, d_out, h_len, &handled);
+    if (r || handled) return r;
+    HIPCHK(hipMemcpyAsync(d_out, d_in, m, hipMemcpyDeviceToDevice, c->stream));   // unknown type (:806-812)
+    HIPCHK(hipStreamSynchronize(c->stream));
+    *h_len = m;
+    return DC_OK;
+}
+
+int dc_small_compress(dc_ctx *c, const uint8_t *d_in, uint64_t n, uint8_t *d_out, uint64_t *h_len)
+{
+    if (!c || !d_out || !h_len || (n && !d_in)) return DC_E_ARG;
+    if (n == 0) { int r = write_byte(c, d_out, ' '); if (r) return r; HIPCHK(hipStreamSynchronize(c->stream)); *h_len = 1; return DC_OK; }
+    return fsm_run<M_SMALL_ENC>(c, d_in, n, n - 1, d_out, h_len, "small_enc_tiles");
+}
+
+int dc_small_decompress(dc_ctx *c, const uint8_t *d_in, uint64_t m, uint8_t *d_out, uint64_t *h_len)
+{
+    if (!c || !d_out || !h_len || (m && !d_in)) return DC_E_ARG;
+    if (m == 0) { *h_len = 0; return DC_OK; }
+    uint8_t type = 0;
+    int r = read_byte(c, d_in, &type);
+    if (r) return r;
+    if (type == 8) {
+        if (m < 2) { *h_len = 0; return DC_OK; }
+        return fsm_run<M_SMALL_DEC>(c, d_in, m, m - 2, d_out, h_len, "small_dec_tiles");
+    }
+    bool handled = false;
+    r = copy_typed(c, d_in, m, type, d_out, h_len, &handled);
+    if (r || handled) return r;
+    *h_len = 0;   // "invalid compressed data": empty output (small_compression.c:497-499)
+    return DC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,182 @@
+"""Device-resident pipelines on torch tensors (HBM) over libdc_core.so.
+
+`Codec` owns one dc_ctx bound to a HIP stream (torch's current stream by default, so
+torch.cuda events and synchronisation see the kernels). Stages map 1:1 onto dc_gpu.h:
+
+    hist = c.hist(x)                      # H1  histogram()             n_ary_huffman.c:461
+    tab  = c.table(hist, n_ary)           # H2-H6 huffman()+convert()   :1161, :1382
+    bits = c.plan(tab)                    # per-block bit counts + scan (:2485 formula)
+    c.pack(x, tab, bit_base, words, sync, S)          # H7 encode (build-defined v1)
+    c.decode(words, bit_base, sync, S, n, tab, out)   # H8 decode
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from ._lib import DcError, check, core
+
+try:
+    import torch
+except Exception:  # pragma: no cover
+    torch = None
+
+
+def _ptr(t) -> int:
+    if t is None:
+        return None
+    if isinstance(t, int):
+        return t
+    return t.data_ptr()
+
+
+class Codec:
+    _host_default = None
+
+    def __init__(self, device: int = 0, stream=None, own_stream: bool = False):
+        self.L = core()
+        self.ctx = C.c_void_p()
+        if own_stream:
+            handle = None
+        elif stream is not None:
+            handle = stream if isinstance(stream, int) else stream.cuda_stream
+        elif torch is not None and torch.cuda.is_available():
+            handle = torch.cuda.current_stream(device).cuda_stream
+        else:
+            handle = None
+        check("dc_ctx_create", self.L.dc_ctx_create(C.byref(self.ctx), device, handle))
+        self.device = device
+        self.table_bytes = int(self.L.dc_dtable_size())
+
+    @classmethod
+    def host_default(cls):
+        if cls._host_default is None:
+            cls._host_default = cls(own_stream=True)
+        return cls._host_default
+
+    def close(self):
+        if self.ctx:
+            self.L.dc_ctx_destroy(self.ctx)
+            self.ctx = C.c_void_p()
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- helpers --------------------------------------------------------------------
+    def sync(self):
+        check("dc_ctx_sync", self.L.dc_ctx_sync(self.ctx))
+
+    def timing(self, enable: bool):
+        check("dc_ctx_set_timing", self.L.dc_ctx_set_timing(self.ctx, int(enable)))
+
+    def timings(self, max_n: int = 64):
+        names = (C.c_char_p * max_n)()
+        ms = (C.c_float * max_n)()
+        n = self.L.dc_ctx_timings(self.ctx, names, ms, max_n)
+        if n < 0:
+            raise DcError("dc_ctx_timings", n)
+        return [(names[i].decode(), float(ms[i])) for i in range(n)]
+
+    def _t(self, nbytes, dtype=None):
+        return torch.empty(nbytes, dtype=dtype or torch.uint8, device=f"cuda:{self.device}")
+
+    # ---- Huffman stages ---------------------------------------------------------------
+    def hist(self, x, out=None):
+        out = out if out is not None else self._t(256, torch.int64)
+        check("dc_huff_hist", self.L.dc_huff_hist(self.ctx, _ptr(x), x.numel(), _ptr(out)))
+        return out
+
+    def table(self, hist, n_ary: int, max_symbol_value: int = 258, out=None):
+        out = out if out is not None else self._t(self.table_bytes)
+        check("dc_huff_table", self.L.dc_huff_table(self.ctx, _ptr(hist), max_symbol_value, n_ary, _ptr(out)))
+        return out
+
+    def table_freq(self, freq, n_ary: int, max_symbol_value: int, out=None):
+        out = out if out is not None else self._t(self.table_bytes)
+        check("dc_huff_table_freq",
+              self.L.dc_huff_table_freq(self.ctx, _ptr(freq), max_symbol_value, n_ary, _ptr(out)))
+        return out
+
+    def table_lengths(self, lengths, n_ary: int, max_symbol_value: int = 258, out=None):
+        out = out if out is not None else self._t(self.table_bytes)
+        check("dc_huff_table_lengths",
+              self.L.dc_huff_table_lengths(self.ctx, _ptr(lengths), max_symbol_value, n_ary, _ptr(out)))
+        return out
+
+    def table_status(self, tab):
+        mb = C.c_int32(0)
+        st = self.L.dc_huff_table_status(self.ctx, _ptr(tab), C.byref(mb))
+        return st, mb.value
+
+    def plan(self, tab, total=None):
+        total = total if total is not None else self._t(1, torch.int64)
+        check("dc_huff_plan", self.L.dc_huff_plan(self.ctx, _ptr(tab), _ptr(total)))
+        return total
+
+    def words_needed(self, bit_base: int, total_bits: int) -> int:
+        return int(self.L.dc_huff_words_needed(bit_base, total_bits))
+
+    def pack(self, x, tab, bit_base, words, sync, sync_syms):
+        check("dc_huff_pack", self.L.dc_huff_pack(self.ctx, _ptr(x), x.numel(), _ptr(tab), bit_base, _ptr(words),
+                                                  words.numel(), _ptr(sync), sync_syms if sync is not None else 0))
+
+    def pack_async(self, x, tab, bit_base, words, sync, sync_syms):
+        check("dc_huff_pack_async",
+              self.L.dc_huff_pack_async(self.ctx, _ptr(x), x.numel(), _ptr(tab), bit_base, _ptr(words),
+                                        words.numel(), _ptr(sync), sync_syms if sync is not None else 0))
+
+    def pack_status(self, tab):
+        return int(self.L.dc_huff_pack_status(self.ctx, _ptr(tab)))
+
+    def decode(self, words, bit_base, sync, sync_syms, n, tab, out):
+        check("dc_huff_decode", self.L.dc_huff_decode(self.ctx, _ptr(words), bit_base, words.numel(), _ptr(sync),
+                                                      sync_syms, n, _ptr(tab), _ptr(out)))
+
+    def decode_status(self):
+        return int(self.L.dc_huff_decode_status(self.ctx))
+
+    def default_sync(self, n: int) -> int:
+        return int(self.L.dc_huff_default_sync(n))
+
+    def encode(self, x, n_ary: int = 2, sync_syms: int | None = None, bit_base: int = 0):
+        """hist -> table -> plan -> pack on one device. Returns dict of device tensors."""
+        n = x.numel()
+        S = sync_syms or self.default_sync(n)
+        hist = self.hist(x)
+        tab = self.table(hist, n_ary)
+        total = self.plan(tab)
+        bits = int(total.item())
+        words = self._t(self.words_needed(bit_base, bits), torch.int32)
+        sync = self._t(max(1, (n + S - 1) // S), torch.int64)
+        self.pack(x, tab, bit_base, words, sync, S)
+        return {"hist": hist, "table": tab, "bits": bits, "words": words, "sync": sync, "S": S,
+                "bit_base": bit_base, "n": n}
+
+    def decode_into(self, enc, out):
+        self.decode(enc["words"], enc["bit_base"], enc["sync"], enc["S"], enc["n"], enc["table"], out)
+
+    # ---- host helpers -------------------------------------------------------------------
+    def histogram_host(self, x: np.ndarray, max_symbol_value: int = 258) -> np.ndarray:
+        from ._lib import vp
+        n = x.size
+        d_in = C.c_void_p()
+        d_h = C.c_void_p()
+        check("dc_malloc", self.L.dc_malloc(C.byref(d_in), n + 64))
+        check("dc_malloc", self.L.dc_malloc(C.byref(d_h), 256 * 8))
+        try:
+            if n:
+                check("h2d", self.L.dc_memcpy_h2d(self.ctx, d_in, x.ctypes.data_as(vp), n))
+            check("dc_huff_hist", self.L.dc_huff_hist(self.ctx, d_in, n, d_h))
+            h = np.zeros(256, dtype=np.uint64)
+            check("d2h", self.L.dc_memcpy_d2h(self.ctx, h.ctypes.data_as(vp), d_h, 256 * 8))
+        finally:
+            self.L.dc_free(d_in)
+            self.L.dc_free(d_h)
+        out = np.zeros(max_symbol_value + 1, dtype=np.int64)
+        k = min(256, max_symbol_value + 1)
+        out[:k] = h[:k].astype(np.int64)
+        return out

@@ -78,18 +78,19 @@ def _zipf_weights(k, s=1.0):
     return 1.0 / np.arange(1, k + 1, dtype=np.float64) ** s
 
 
-def english_like(n: int, seed: int = 0xC1) -> np.ndarray:
-    rng = np.random.default_rng(seed)
+def _english_vocab():
     words = [w + " " for w in _WORDS] + [w + ", " for w in _WORDS[:20]] + [
         w + ". " for w in _WORDS[:20]] + [w.capitalize() + " " for w in _WORDS[:30]] + ["\n"]
     wts = list(_zipf_weights(len(_WORDS), 0.9)) + list(_zipf_weights(20) * 0.05) + list(
         _zipf_weights(20) * 0.05) + list(_zipf_weights(30) * 0.05) + [0.02]
-    arr, lens, p = _vocab_arrays(words, wts)
-    return _emit_tokens(n, rng, arr, lens, p)
+    return _vocab_arrays(words, wts)
 
 
-def enwik_like(n: int, seed: int = 0xC2) -> np.ndarray:
-    rng = np.random.default_rng(seed)
+def english_like(n: int, seed: int = 0xC1) -> np.ndarray:
+    return _emit_tokens(n, np.random.default_rng(seed), *_english_vocab())
+
+
+def _enwik_vocab():
     toks = [w + " " for w in _WORDS] + [w.capitalize() + " " for w in _WORDS[:60]]
     wts = list(_zipf_weights(len(_WORDS), 1.0)) + list(_zipf_weights(60) * 0.15)
     toks += _MARKUP
@@ -104,8 +105,11 @@ def enwik_like(n: int, seed: int = 0xC2) -> np.ndarray:
     wts += [2e-4] * len(rare)
     toks += ["\t"]
     wts += [1e-3]
-    arr, lens, p = _vocab_arrays(toks, wts)
-    return _emit_tokens(n, rng, arr, lens, p)
+    return _vocab_arrays(toks, wts)
+
+
+def enwik_like(n: int, seed: int = 0xC2) -> np.ndarray:
+    return _emit_tokens(n, np.random.default_rng(seed), *_enwik_vocab())
 
 
 def uniform_bytes(n: int, seed: int = 0xC3, lo: int = 1, hi: int = 255) -> np.ndarray:
@@ -131,8 +135,7 @@ def zipf_bytes(n: int, seed: int = 0xC4, s: float = 1.0) -> np.ndarray:
     return out
 
 
-def log_like(n: int, seed: int = 0xC5) -> np.ndarray:
-    rng = np.random.default_rng(seed)
+def _log_vocab():
     toks = [w + " " for w in _WORDS]
     wts = list(_zipf_weights(len(_WORDS), 1.0))
     stamps = ["2025-08-0%dT%02d:%02d:%02dZ " % (d, h, m, s)
@@ -140,8 +143,11 @@ def log_like(n: int, seed: int = 0xC5) -> np.ndarray:
     hosts = ["host%02d app[%d]: " % (h, 1000 + 37 * h) for h in range(16)]
     toks += ["\n" + t for t in stamps] + hosts + ["error ", "warn ", "info ", "debug "]
     wts += [0.6 / len(stamps)] * len(stamps) + [0.6 / len(hosts)] * len(hosts) + [0.05] * 4
-    arr, lens, p = _vocab_arrays(toks, wts)
-    return _emit_tokens(n, rng, arr, lens, p)
+    return _vocab_arrays(toks, wts)
+
+
+def log_like(n: int, seed: int = 0xC5) -> np.ndarray:
+    return _emit_tokens(n, np.random.default_rng(seed), *_log_vocab())
 
 
 GENERATORS = {
@@ -151,3 +157,44 @@ GENERATORS = {
     "C4": zipf_bytes,
     "C5": log_like,
 }
+
+
+_VOCAB = {"C1": _english_vocab, "C2": _enwik_vocab, "C5": _log_vocab}
+
+
+def device_text(cfg: str, n: int, seed: int, device):
+    """Same token vocabulary and probabilities as the numpy generator of `cfg`, sampled
+    on the GPU with torch (different random stream; used for the full-size bench inputs,
+    where numpy would need tens of seconds per GiB)."""
+    import torch
+
+    if cfg == "C3":
+        g = torch.Generator(device=device).manual_seed(seed)
+        return torch.randint(1, 256, (n,), generator=g, device=device, dtype=torch.int32).to(torch.uint8)
+    if cfg == "C4":
+        p = _zipf_weights(255, 1.0)
+        perm = np.random.default_rng(0xC4).permutation(255).astype(np.uint8) + 1
+        cdf = torch.from_numpy(np.cumsum(p / p.sum())).to(device)
+        g = torch.Generator(device=device).manual_seed(seed)
+        u = torch.rand(n, generator=g, device=device, dtype=torch.float64)
+        idx = torch.clamp(torch.searchsorted(cdf, u), max=254)
+        return torch.from_numpy(perm).to(device)[idx]
+    arr, lens, p = _VOCAB[cfg]()
+    tok = torch.from_numpy(arr).to(device)
+    tlen = torch.from_numpy(lens).to(device)
+    cdf = torch.from_numpy(np.cumsum(p)).to(device)
+    g = torch.Generator(device=device).manual_seed(seed)
+    avg = float((lens * p).sum())
+    col = torch.arange(arr.shape[1], device=device)[None, :]
+    out = torch.empty(n, dtype=torch.uint8, device=device)
+    filled = 0
+    while filled < n:
+        want = min(n - filled, 64 << 20)
+        ntok = int(want / avg * 1.05) + 64
+        u = torch.rand(ntok, generator=g, device=device, dtype=torch.float64)
+        ids = torch.clamp(torch.searchsorted(cdf, u), max=len(lens) - 1)
+        chunk = tok[ids][col < tlen[ids][:, None]]
+        take = min(chunk.numel(), n - filled)
+        out[filled : filled + take] = chunk[:take]
+        filled += take
+    return out

@@ -1,0 +1,145 @@
+/*
+ * dc_gpu.h -- device-resident extended API of libdc_core.so (MI355X / gfx950).
+ *
+ * This is the API the drop-in shims (dc_huffman.h, dc_nybble.h), bench.py and the
+ * multi-GPU driver are built on. All pointers named d_* are device pointers (HBM);
+ * every call is asynchronous on the context's HIP stream unless it says otherwise.
+ * Every function returns 0 (DC_OK) or a negative DC_E_* status; none of them prints.
+ *
+ * Reference interfaces these stages replace (file:line in carycode/data_compression):
+ *   dc_huff_hist          histogram()                          n_ary_huffman.c:461-493
+ *   dc_huff_table*        huffman() + convert_lengths_to_encode_table()
+ *                                                              n_ary_huffman.c:1161-1208, :1382-1612
+ *   dc_huff_plan/pack     represent_items_with_codes() (stub)  n_ary_huffman.c:1621-1678
+ *   dc_huff_decode        decompress() data block (missing)     n_ary_huffman.c:2014-2094
+ *   dc_nyb_*              compress_bytestring/decompress_bytestring
+ *                                                              nybble_compression.c:734-1038
+ * The Huffman bitstream layout is build-defined (DESIGN.md "Huffman bitstream v1").
+ */
+#ifndef DC_GPU_H
+#define DC_GPU_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+    DC_OK = 0,
+    DC_E_ARG = -1,           /* bad argument */
+    DC_E_HIP = -2,           /* a HIP runtime call failed (no device, launch failure, ...) */
+    DC_E_CODE_TOO_LONG = -3, /* a byte's packed code exceeds 32 bits */
+    DC_E_NOCODE = -4,        /* the input holds a byte that has no code */
+    DC_E_STATE = -5,         /* stage called out of order (e.g. pack before hist of that input) */
+    DC_E_CAPACITY = -6,      /* output buffer too small */
+    DC_E_STREAM = -7         /* corrupt compressed stream */
+};
+
+#define DC_BLOCK_BYTES 32768u   /* encoder block: one histogram + one bit offset each */
+#define DC_LUT_BITS 12          /* decoder first-level lookup table: 2^12 entries */
+#define DC_MAX_SYMS 1024        /* max_symbol_value + 1 supported by the table kernel */
+#define DC_MAX_DIGITS 128       /* longest code length (in base-n digits) handled */
+
+typedef struct dc_ctx dc_ctx;
+
+/* Device-resident code table, written by the table kernels (layout is ABI). */
+typedef struct dc_dtable {
+    uint32_t code[256];             /* packed MSB-first code bits of byte s           */
+    uint32_t nbits[256];            /* its bit length (0: byte has no code)           */
+    uint16_t lut[1 << DC_LUT_BITS]; /* next 12 bits -> sym | nbits<<8 ; 0 = long code */
+    uint32_t first[DC_MAX_DIGITS + 1]; /* canonical first value per digit length      */
+    uint32_t count[DC_MAX_DIGITS + 1];
+    uint32_t start[DC_MAX_DIGITS + 1];
+    uint16_t syms[DC_MAX_SYMS];     /* symbols sorted by (length, value)               */
+    int32_t lengths[DC_MAX_SYMS];   /* Huffman lengths in digits (huffman())          */
+    int32_t enc_len[DC_MAX_SYMS];   /* convert_lengths_to_encode_table() outputs      */
+    uint32_t enc_val[DC_MAX_SYMS];
+    int32_t n_ary, w, max_symbol_value, max_bits;
+    int32_t min_len, max_len, status, last_written; /* last_written: index M assigned */
+} dc_dtable;
+
+/* ---- context ------------------------------------------------------------------------ */
+/* stream: a hipStream_t to launch on (e.g. torch's current stream), or NULL for a
+ * context-owned non-blocking stream. Fails with DC_E_HIP when no HIP device is usable. */
+int dc_ctx_create(dc_ctx **out, int device, void *stream);
+void dc_ctx_destroy(dc_ctx *ctx);
+int dc_ctx_sync(dc_ctx *ctx);
+void *dc_ctx_stream(dc_ctx *ctx);
+/* Per-stage HIP-event timing (on the stream the kernels run on). enable=1 starts
+ * recording; dc_ctx_timings() synchronises and returns up to max stages. */
+int dc_ctx_set_timing(dc_ctx *ctx, int enable);
+int dc_ctx_timings(dc_ctx *ctx, const char **names, float *ms, int max);
+const char *dc_version(void);
+size_t dc_dtable_size(void);
+
+/* ---- device memory helpers (plain hipMalloc/hipMemcpy wrappers for ctypes users) --- */
+int dc_malloc(void **d_ptr, size_t bytes);
+int dc_free(void *d_ptr);
+int dc_memcpy_h2d(dc_ctx *ctx, void *d_dst, const void *h_src, size_t bytes);
+int dc_memcpy_d2h(dc_ctx *ctx, void *h_dst, const void *d_src, size_t bytes);
+int dc_memset(dc_ctx *ctx, void *d_dst, int value, size_t bytes);
+
+/* ---- Huffman, device-resident stages ------------------------------------------------- */
+/* (1) byte histogram of d_in[0..n) -> d_hist[256] (u64). Keeps per-block histograms in
+ *     the context for dc_huff_plan on the SAME (d_in, n). */
+int dc_huff_hist(dc_ctx *ctx, const uint8_t *d_in, uint64_t n, uint64_t *d_hist);
+/* (2a) table from byte histogram d_hist[256]; symbols 256..max_symbol_value count 0. */
+int dc_huff_table(dc_ctx *ctx, const uint64_t *d_hist, int max_symbol_value, int n_ary,
+                  dc_dtable *d_table);
+/* (2b) table from an arbitrary frequency array d_freq[max_symbol_value+1] (u64). */
+int dc_huff_table_freq(dc_ctx *ctx, const uint64_t *d_freq, int max_symbol_value, int n_ary,
+                       dc_dtable *d_table);
+/* (2c) table from given lengths d_lengths[max_symbol_value+1] (skips the merge). */
+int dc_huff_table_lengths(dc_ctx *ctx, const int32_t *d_lengths, int max_symbol_value,
+                          int n_ary, dc_dtable *d_table);
+/* (3) per-block bit counts + exclusive scan for the input of the last dc_huff_hist;
+ *     writes the payload bit count to *d_total_bits (device u64). */
+int dc_huff_plan(dc_ctx *ctx, const dc_dtable *d_table, uint64_t *d_total_bits);
+/* (4) pack at global bit offset bit_base into d_words (word 0 = stream word bit_base/32,
+ *     MSB-first bytes). Capacity: dc_huff_words_needed(). d_sync[c] = absolute bit offset
+ *     of symbol c*sync_syms (sync_syms: power of two >= 16, or 0 for no index). */
+int dc_huff_pack(dc_ctx *ctx, const uint8_t *d_in, uint64_t n, const dc_dtable *d_table,
+                 uint64_t bit_base, uint32_t *d_words, uint64_t words_cap, uint64_t *d_sync,
+                 uint32_t sync_syms);
+uint64_t dc_huff_words_needed(uint64_t bit_base, uint64_t total_bits);
+/* (4') the same without any host round trip (graph/timing friendly): a byte without a
+ *     code or words_cap too small makes the kernels write nothing; read the outcome with
+ *     dc_huff_pack_status() (synchronising). */
+int dc_huff_pack_async(dc_ctx *ctx, const uint8_t *d_in, uint64_t n, const dc_dtable *d_table,
+                       uint64_t bit_base, uint32_t *d_words, uint64_t words_cap, uint64_t *d_sync,
+                       uint32_t sync_syms);
+int dc_huff_pack_status(dc_ctx *ctx, const dc_dtable *d_table);
+/* Status word written by the table / plan kernels (host-synchronising read). */
+int dc_huff_table_status(dc_ctx *ctx, const dc_dtable *d_table, int32_t *max_bits);
+/* (5) decode n symbols. d_words/bit_base as for pack; d_sync from pack. */
+int dc_huff_decode(dc_ctx *ctx, const uint32_t *d_words, uint64_t bit_base, uint64_t words,
+                   const uint64_t *d_sync, uint32_t sync_syms, uint64_t n,
+                   const dc_dtable *d_table, uint8_t *d_out);
+/* status of the last dc_huff_decode on this context (synchronising): 0 or DC_E_STREAM */
+int dc_huff_decode_status(dc_ctx *ctx);
+/* base64url text (6 bits per char, MSB-first) of bits [bit_base, bit_base+bits) */
+int dc_huff_base64url(dc_ctx *ctx, const uint32_t *d_words, uint64_t bit_base, uint64_t bits,
+                      char *d_text);
+/* recommended sync granularity for n symbols (keeps >= 2^18 chunks in flight) */
+uint32_t dc_huff_default_sync(uint64_t n);
+
+/* ---- nybble codec (nybble_compression.c), device-resident ---------------------------- */
+/* Full reference byte stream (header, packed nybbles, LITERAL fallback) of d_in[0..n).
+ * d_out capacity >= n + 2. *h_out_len receives the length (host, synchronising). */
+int dc_nyb_compress(dc_ctx *ctx, const uint8_t *d_in, uint64_t n, int modify, uint8_t *d_out,
+                    uint64_t *h_out_len);
+/* Decode m compressed bytes; d_out capacity >= 2*m. *h_out_len as above. */
+int dc_nyb_decompress(dc_ctx *ctx, const uint8_t *d_in, uint64_t m, int modify, uint8_t *d_out,
+                      uint64_t *h_out_len);
+
+/* ---- small front-end (small_compression.c:507-665), device-resident ----------------- */
+int dc_small_compress(dc_ctx *ctx, const uint8_t *d_in, uint64_t n, uint8_t *d_out,
+                      uint64_t *h_out_len);
+int dc_small_decompress(dc_ctx *ctx, const uint8_t *d_in, uint64_t m, uint8_t *d_out,
+                        uint64_t *h_out_len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,62 @@
+/*
+ * dc_huffman.h -- drop-in replacement for the public functions of n_ary_huffman.c
+ * (carycode/data_compression @ 2025-08-08), exported by libdc_huffman.so with the
+ * reference's own names, argument meanings and array conventions. All compute runs in
+ * gfx950 HIP kernels (libdc_core.so); see INTEGRATION.md for the one-line link change.
+ *
+ * Reference interface replaced                         | reference file:line
+ * ---------------------------------------------------- | ---------------------------
+ * histogram                                            | n_ary_huffman.c:461-493
+ * huffman                                              | n_ary_huffman.c:1161-1208
+ * convert_lengths_to_encode_table                      | n_ary_huffman.c:1382-1612
+ * represent_items_with_codes                           | n_ary_huffman.c:1621-1678
+ * dc_huff_compress  (same parameters as static compress)   | n_ary_huffman.c:1688-1815
+ * dc_huff_decompress (same parameters as static decompress) | n_ary_huffman.c:2014-2094
+ *
+ * Semantics and the deliberate differences (all documented in DESIGN.md §Boundary):
+ *  - histogram counts bytes up to the first NUL into h[0..max_symbol_value] (bytes above
+ *    max_symbol_value are ignored; the reference writes out of bounds there) and prints
+ *    nothing (the reference prints one diagnostic per byte > 126, :485-487).
+ *  - huffman and convert_lengths_to_encode_table reproduce the reference built with
+ *    -DNDEBUG (as shipped, n=2 aborts at :908): the phantom dummy leaf, the index
+ *    max_symbol_value quirks, 32-bit wrap of code values. max_symbol_value < 1024.
+ *  - represent_items_with_codes (an assert(0) stub in the reference, :1661) writes the
+ *    base64url rendering (6 bits per character, int2digit alphabet :371-378) of the
+ *    build-defined bitstream (DESIGN.md "Huffman bitstream v1") starting at
+ *    compressed_text[start] and returns the characters written, or -1 when a byte has no
+ *    code, a code exceeds 32 bits, or the text would not fit in bufsize+1 bytes.
+ *  - compress/decompress are `static` in the reference; the same-parameter functions
+ *    are exported as dc_huff_compress/dc_huff_decompress and use the binary "DCH1"
+ *    container (dc_host.h) instead of the reference's always-raw netstring block.
+ *  - On a HIP failure (no GPU) the void functions abort with a message, as the
+ *    reference's asserts do; they never fall back to CPU compute.
+ */
+#ifndef DC_HUFFMAN_H
+#define DC_HUFFMAN_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+void histogram(const char *text, const int max_symbol_value, int h[]);
+void huffman(const int max_leaf_value, const int symbol_frequencies[],
+             const int compressed_symbols, int lengths[]);
+void convert_lengths_to_encode_table(const int max_symbol_value, const int canonical_lengths[],
+                                     const int compressed_symbols, int encode_length_table[],
+                                     unsigned int encode_value_table[]);
+int represent_items_with_codes(const int max_symbol_value, int canonical_lengths[],
+                               const int compressed_symbols, const int bufsize,
+                               const int original_length, char original_text[], int start,
+                               char compressed_text[]);
+/* returns bytes written, or a negative DC_E_* status */
+int dc_huff_compress(const int max_symbol_value, int canonical_lengths[],
+                     const int compressed_symbols, const int bufsize, const int original_length,
+                     char original_text[], char compressed_text[]);
+/* returns the decompressed length, or a negative DC_E_* status */
+int dc_huff_decompress(const int max_compressed_size, const char compressed_text[],
+                       const int max_decompressed_size, char decompressed_text[]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

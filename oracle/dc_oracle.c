@@ -166,19 +166,24 @@ uint64_t orc_huff_pack(const uint8_t *x, uint64_t n, const uint32_t code[256],
                        const uint8_t nbits[256], uint8_t *out, uint64_t bit_base,
                        uint32_t sync_syms, uint64_t *idx)
 {
-    uint64_t pos = bit_base & 7;       /* bit position inside out[] */
+    /* MSB-first: pending bits sit right-aligned in acc; whole bytes are flushed */
+    uint64_t acc = 0, o = 0, total = 0;
+    unsigned nacc = (unsigned)(bit_base & 7);     /* leading bits of out[0] stay zero */
     for (uint64_t i = 0; i < n; i++) {
         if (idx && sync_syms && (i % sync_syms) == 0)
-            idx[i / sync_syms] = (bit_base & ~(uint64_t)7) + pos;
-        const int nb = nbits[x[i]];
+            idx[i / sync_syms] = (bit_base & ~(uint64_t)7) + o * 8 + nacc;
+        const unsigned nb = nbits[x[i]];
         if (nb == 0) return UINT64_MAX;
-        const uint32_t c = code[x[i]];
-        for (int b = nb - 1; b >= 0; b--) {
-            if ((c >> b) & 1u) out[pos >> 3] |= (uint8_t)(0x80u >> (pos & 7));
-            pos++;
+        acc = (acc << nb) | code[x[i]];
+        nacc += nb;
+        total += nb;
+        while (nacc >= 8) {
+            nacc -= 8;
+            out[o++] = (uint8_t)(acc >> nacc);
         }
     }
-    return pos - (bit_base & 7);
+    if (nacc) out[o] = (uint8_t)(acc << (8 - nacc));
+    return total;
 }
 
 int orc_huff_unpack(const uint8_t *in, uint64_t in_bits, uint64_t n_out,
@@ -214,11 +219,11 @@ int orc_huff_unpack(const uint8_t *in, uint64_t in_bits, uint64_t n_out,
         int L = 0, found = -1;
         while (found < 0) {
             if (pos + (uint64_t)w > in_bits || L >= MAXL) return -1;
-            uint64_t digit = 0;
-            for (int b = 0; b < w; b++) {
-                digit = (digit << 1) | ((in[pos >> 3] >> (7 - (pos & 7))) & 1u);
-                pos++;
-            }
+            const uint64_t byte = pos >> 3;
+            const unsigned two = ((unsigned)in[byte] << 8) |
+                                 ((byte + 1 < (in_bits + 7) / 8) ? in[byte + 1] : 0u);
+            const uint64_t digit = (two >> (16 - (pos & 7) - (unsigned)w)) & ((1u << w) - 1u);
+            pos += (uint64_t)w;
             if (digit >= (uint64_t)n_ary) return -1;
             v = v * (uint64_t)n_ary + digit;
             L++;
