@@ -68,6 +68,7 @@ def _declare_core(L):
     P = vp
     sig = {
         "dc_ctx_create": ([C.POINTER(vp), i32, vp], i32),
+        "dc_ctx_create_owned": ([C.POINTER(vp), i32], i32),
         "dc_ctx_destroy": ([vp], None),
         "dc_ctx_sync": ([vp], i32),
         "dc_ctx_stream": ([vp], vp),
@@ -90,6 +91,8 @@ def _declare_core(L):
         "dc_huff_words_needed": ([u64, u64], u64),
         "dc_huff_pack_async": ([vp, P, u64, P, u64, P, u64, P, u32], i32),
         "dc_huff_pack_status": ([vp, P], i32),
+        "dc_huff_plan_offsets": ([vp, P, u64, C.POINTER(u64)], i32),
+        "dc_huff_block_hist": ([vp, P, u64], i32),
         "dc_huff_decode": ([vp, P, u64, u64, P, u32, u64, P, P], i32),
         "dc_huff_decode_status": ([vp], i32),
         "dc_huff_base64url": ([vp, P, u64, u64, P], i32),

@@ -1034,7 +1034,12 @@ extern "C" {
 const char *dc_version(void) { return DC_VERSION; }
 size_t dc_dtable_size(void) { return sizeof(dc_dtable); }
 
-int dc_ctx_create(dc_ctx **out, int device, void *stream)
+static int ctx_create(dc_ctx **out, int device, void *stream, bool own);
+
+int dc_ctx_create(dc_ctx **out, int device, void *stream) { return ctx_create(out, device, stream, false); }
+int dc_ctx_create_owned(dc_ctx **out, int device) { return ctx_create(out, device, nullptr, true); }
+
+static int ctx_create(dc_ctx **out, int device, void *stream, bool own)
 {
     if (!out) return DC_E_ARG;
     *out = nullptr;
@@ -1044,7 +1049,7 @@ int dc_ctx_create(dc_ctx **out, int device, void *stream)
     dc_ctx *c = (dc_ctx *)calloc(1, sizeof(dc_ctx));
     if (!c) return DC_E_ARG;
     c->device = device;
-    if (stream) { c->stream = (hipStream_t)stream; c->own_stream = false; }
+    if (!own) { c->stream = (hipStream_t)stream; c->own_stream = false; }   // NULL = default stream
     else {
         if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) { free(c); return DC_E_HIP; }
         c->own_stream = true;
@@ -1217,6 +1222,29 @@ int dc_huff_plan(dc_ctx *c, const dc_dtable *d_table, uint64_t *d_total_bits)
            c->d_err);
     LAUNCH(c, "block_scan", k_block_scan, 1, 1024, c->d_off, nb, d_total_bits);
     c->plan_ok = true;
+    return DC_OK;
+}
+
+int dc_huff_plan_offsets(dc_ctx *c, uint64_t *h_off, uint64_t max_entries, uint64_t *h_n)
+{
+    if (!c || !c->plan_ok) return DC_E_STATE;
+    const uint64_t nb = nblocks_of(c->hist_n) + 1;
+    const uint64_t k = nb < max_entries ? nb : max_entries;
+    if (h_n) *h_n = nb;
+    if (k) {
+        HIPCHK(hipMemcpyAsync(h_off, c->d_off, k * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+    }
+    return DC_OK;
+}
+
+int dc_huff_block_hist(dc_ctx *c, uint16_t *h_bh, uint64_t max_entries)
+{
+    if (!c || !c->hist_n) return DC_E_STATE;
+    const uint64_t nb = nblocks_of(c->hist_n) * 256;
+    const uint64_t k = nb < max_entries ? nb : max_entries;
+    HIPCHK(hipMemcpyAsync(h_bh, c->d_bh, k * sizeof(uint16_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
     return DC_OK;
 }
 

@@ -44,7 +44,7 @@ int state(HostState **s)
         int dev = 0;
         const char *e = getenv("DC_DEVICE");
         if (e) dev = atoi(e);
-        int r = dc_ctx_create(&st.ctx, dev, nullptr);
+        int r = dc_ctx_create_owned(&st.ctx, dev);
         if (r) return r;
     }
     *s = &st;

@@ -38,14 +38,16 @@ class Codec:
         self.L = core()
         self.ctx = C.c_void_p()
         if own_stream:
-            handle = None
-        elif stream is not None:
-            handle = stream if isinstance(stream, int) else stream.cuda_stream
-        elif torch is not None and torch.cuda.is_available():
-            handle = torch.cuda.current_stream(device).cuda_stream
+            check("dc_ctx_create_owned", self.L.dc_ctx_create_owned(C.byref(self.ctx), device))
         else:
-            handle = None
-        check("dc_ctx_create", self.L.dc_ctx_create(C.byref(self.ctx), device, handle))
+            # torch's current stream (its default stream has handle 0 = the HIP NULL stream)
+            if stream is not None:
+                handle = stream if isinstance(stream, int) else stream.cuda_stream
+            elif torch is not None and torch.cuda.is_available():
+                handle = torch.cuda.current_stream(device).cuda_stream
+            else:
+                handle = 0
+            check("dc_ctx_create", self.L.dc_ctx_create(C.byref(self.ctx), device, handle or None))
         self.device = device
         self.table_bytes = int(self.L.dc_dtable_size())
 

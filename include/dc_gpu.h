@@ -60,9 +60,11 @@ typedef struct dc_dtable {
 } dc_dtable;
 
 /* ---- context ------------------------------------------------------------------------ */
-/* stream: a hipStream_t to launch on (e.g. torch's current stream), or NULL for a
- * context-owned non-blocking stream. Fails with DC_E_HIP when no HIP device is usable. */
+/* stream: the hipStream_t to launch on (e.g. torch's current stream); NULL is the
+ * default (legacy) stream. dc_ctx_create_owned makes a private non-blocking stream.
+ * Both fail with DC_E_HIP when no HIP device is usable. */
 int dc_ctx_create(dc_ctx **out, int device, void *stream);
+int dc_ctx_create_owned(dc_ctx **out, int device);
 void dc_ctx_destroy(dc_ctx *ctx);
 int dc_ctx_sync(dc_ctx *ctx);
 void *dc_ctx_stream(dc_ctx *ctx);
@@ -103,6 +105,10 @@ int dc_huff_pack(dc_ctx *ctx, const uint8_t *d_in, uint64_t n, const dc_dtable *
                  uint64_t bit_base, uint32_t *d_words, uint64_t words_cap, uint64_t *d_sync,
                  uint32_t sync_syms);
 uint64_t dc_huff_words_needed(uint64_t bit_base, uint64_t total_bits);
+/* inspection (synchronising): the plan's exclusive per-block bit offsets (nblocks+1
+ * entries, last = total) and the per-block u16 histograms of the last dc_huff_hist */
+int dc_huff_plan_offsets(dc_ctx *ctx, uint64_t *h_off, uint64_t max_entries, uint64_t *h_n);
+int dc_huff_block_hist(dc_ctx *ctx, uint16_t *h_bh, uint64_t max_entries);
 /* (4') the same without any host round trip (graph/timing friendly): a byte without a
  *     code or words_cap too small makes the kernels write nothing; read the outcome with
  *     dc_huff_pack_status() (synchronising). */
