@@ -100,9 +100,10 @@ __global__ __launch_bounds__(256) void k_hist_blocks(const uint8_t *__restrict__
     }
 }
 
-// partial sums of the block histograms: partials[g][256]
+// sum of the block histograms: each workgroup sums a range of blocks per bin and adds
+// it into hist[256] (zeroed by the host launcher) with one u64 atomic per bin
 __global__ __launch_bounds__(256) void k_hist_reduce(const uint16_t *__restrict__ bh, uint64_t nblocks,
-                                                     uint64_t *__restrict__ partials)
+                                                     uint64_t *__restrict__ hist)
 {
     const int t = threadIdx.x;
     const uint64_t per = (nblocks + gridDim.x - 1) / gridDim.x;
@@ -117,16 +118,8 @@ __global__ __launch_bounds__(256) void k_hist_reduce(const uint16_t *__restrict_
         a3 += bh[(b + 3) * 256 + t];
     }
     for (; b < b1; ++b) a0 += bh[b * 256 + t];
-    partials[(uint64_t)blockIdx.x * 256 + t] = a0 + a1 + a2 + a3;
-}
-
-__global__ __launch_bounds__(256) void k_hist_final(const uint64_t *__restrict__ partials, int G,
-                                                    uint64_t *__restrict__ hist)
-{
-    const int t = threadIdx.x;
-    uint64_t a = 0;
-    for (int g = 0; g < G; ++g) a += partials[(uint64_t)g * 256 + t];
-    hist[t] = a;
+    const uint64_t sum = a0 + a1 + a2 + a3;
+    if (sum) atomicAdd((unsigned long long *)&hist[t], (unsigned long long)sum);
 }
 
 // ------------------------------------------------------------------------------------
@@ -313,6 +306,16 @@ __global__ __launch_bounds__(256) void k_huff_table(const uint64_t *__restrict__
         T->count[L] = in ? s_cnt[L] : 0u;
         T->start[L] = s_starti[L];
     }
+    // left-justified canonical limits per BIT length b (power-of-two n): codes of digit
+    // length <= floor(b/w) are exactly the 32-bit windows below lim[b]
+    if (t <= 32) {
+        const int Ld = t / w;
+        uint64_t lim;
+        if (Ld < minL) lim = 0;
+        else if (Ld >= maxL || Ld * w > 32) lim = 1ull << 32;
+        else lim = ((uint64_t)s_startv[Ld] + s_cnt[Ld]) << (32 - Ld * w);
+        T->lim[t] = lim;
+    }
     for (int e = t; e < (1 << DC_LUT_BITS); e += 256) T->lut[e] = 0;
     __syncthreads();
     T->code[t] = s_code[t];
@@ -373,7 +376,15 @@ __global__ __launch_bounds__(1024) void k_block_scan(uint64_t *__restrict__ bits
     const uint64_t b0 = (uint64_t)t * per;
     const uint64_t b1 = (b0 + per < nblocks) ? b0 + per : nblocks;
     uint64_t sum = 0;
-    for (uint64_t b = b0; b < b1; ++b) sum += bits_off[b];
+    uint64_t b = b0;
+    for (; b + 8 <= b1; b += 8) {   // 8 independent loads in flight per lane
+        uint64_t v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = bits_off[b + k];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) sum += v[k];
+    }
+    for (; b < b1; ++b) sum += bits_off[b];
     s[t] = sum;
     __syncthreads();
     for (int d = 1; d < 1024; d <<= 1) {
@@ -383,7 +394,15 @@ __global__ __launch_bounds__(1024) void k_block_scan(uint64_t *__restrict__ bits
         __syncthreads();
     }
     uint64_t run = s[t] - sum;
-    for (uint64_t b = b0; b < b1; ++b) {
+    b = b0;
+    for (; b + 8 <= b1; b += 8) {
+        uint64_t v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = bits_off[b + k];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { bits_off[b + k] = run; run += v[k]; }
+    }
+    for (; b < b1; ++b) {
         const uint64_t v = bits_off[b];
         bits_off[b] = run;
         run += v;
@@ -523,10 +542,37 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
 }
 
 // ------------------------------------------------------------------------------------
-// (H8) decode. One lane per sync chunk (sync_syms symbols): 64-bit MSB-first window,
-// 12-bit LDS lookup table, digit-by-digit canonical fallback for longer codes; output
-// gathered 16 bytes per lane and stored with one 16-B store.
+// (H8) decode. One lane per sync chunk (sync_syms symbols, output bytes [c*S, c*S+S)).
+//  * input: a per-lane register FIFO of 8 words fed by 32-byte prefetches issued one FIFO
+//    ahead, so a refill never waits on a dependent HBM load (the v1 kernel stalled on a
+//    global load at nearly every symbol step because some lane of the wave refilled);
+//  * 64-bit MSB-first window; first-level LDS table on the next 12 bits;
+//  * codes > 12 bits, n a power of two: canonical limit compare against the left-justified
+//    per-length limits (wave-uniform, LDS broadcast) -> O(1) length, one LDS symbol read;
+//    other n: canonical decode one base-n digit at a time;
+//  * output gathered 16 bytes per lane -> one 16-B store.
 // ------------------------------------------------------------------------------------
+struct Fifo {
+    uint32_t q0, q1, q2, q3, q4, q5, q6, q7;
+    uint4 n0, n1;
+    const uint4 *gp;
+    int qn;
+    __device__ __forceinline__ uint32_t pop()
+    {
+        const uint32_t v = q0;
+        q0 = q1; q1 = q2; q2 = q3; q3 = q4; q4 = q5; q5 = q6; q6 = q7;
+        if (--qn == 0) {
+            q0 = n0.x; q1 = n0.y; q2 = n0.z; q3 = n0.w;
+            q4 = n1.x; q5 = n1.y; q6 = n1.z; q7 = n1.w;
+            n0 = gp[0];
+            n1 = gp[1];
+            gp += 2;
+            qn = 8;
+        }
+        return bswap32(v);
+    }
+};
+
 __global__ __launch_bounds__(256) void k_huff_decode(const uint32_t *__restrict__ in, uint64_t bit_base,
                                                      const uint64_t *__restrict__ sync, uint32_t S,
                                                      uint64_t n, const dc_dtable *__restrict__ T,
@@ -546,6 +592,7 @@ __global__ __launch_bounds__(256) void k_huff_decode(const uint32_t *__restrict_
         for (int i = t; i < DC_MAX_SYMS; i += 256) s_syms[i] = T->syms[i];
     }
     const int nary = T->n_ary, w = T->w;
+    const bool pow2 = (nary & (nary - 1)) == 0;
     __syncthreads();
 
     const uint64_t c = (uint64_t)blockIdx.x * 256 + t;
@@ -553,21 +600,37 @@ __global__ __launch_bounds__(256) void k_huff_decode(const uint32_t *__restrict_
     if (sym0 >= n) return;
     const uint64_t cnt = (n - sym0 < S) ? (n - sym0) : S;
     const uint64_t rel = sync[c] - ((bit_base >> 5) << 5);
-    const uint32_t *wp = in + (rel >> 5);
+    const uint64_t w0 = rel >> 5;
+    const uint4 *g = reinterpret_cast<const uint4 *>(in + (w0 & ~3ull));
+    Fifo f;
+    {
+        const uint4 a0 = g[0], a1 = g[1];
+        f.q0 = a0.x; f.q1 = a0.y; f.q2 = a0.z; f.q3 = a0.w;
+        f.q4 = a1.x; f.q5 = a1.y; f.q6 = a1.z; f.q7 = a1.w;
+        f.n0 = g[2];
+        f.n1 = g[3];
+        f.gp = g + 4;
+        f.qn = 8;
+        for (int k = (int)(w0 & 3); k > 0; --k) {   // drop the words before the chunk start
+            f.q0 = f.q1; f.q1 = f.q2; f.q2 = f.q3; f.q3 = f.q4; f.q4 = f.q5; f.q5 = f.q6; f.q6 = f.q7;
+            --f.qn;
+        }
+    }
     const uint32_t sh = (uint32_t)(rel & 31);
-    uint64_t win = (((uint64_t)bswap32(wp[0]) << 32) | bswap32(wp[1])) << sh;
+    const uint32_t hi = f.pop();
+    const uint32_t lo = f.pop();
+    uint64_t win = (((uint64_t)hi << 32) | lo) << sh;
     int wbits = 64 - (int)sh;
-    wp += 2;
     int bad = 0;
     uint8_t *o = out + sym0;
-    for (uint64_t g = 0; g < cnt; g += 16) {
+    for (uint64_t gsym = 0; gsym < cnt; gsym += 16) {
         uint32_t ob[4] = {0u, 0u, 0u, 0u};
-        const int m = (cnt - g >= 16) ? 16 : (int)(cnt - g);
+        const int m = (cnt - gsym >= 16) ? 16 : (int)(cnt - gsym);
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
             if (k < m) {
                 if (wbits < 32) {
-                    win |= (uint64_t)bswap32(*wp++) << (32 - wbits);
+                    win |= (uint64_t)f.pop() << (32 - wbits);
                     wbits += 32;
                 }
                 const uint32_t e = s_lut[win >> (64 - DC_LUT_BITS)];
@@ -575,8 +638,18 @@ __global__ __launch_bounds__(256) void k_huff_decode(const uint32_t *__restrict_
                 if (e != 0) {
                     sym = e & 255u;
                     nbt = e >> 8;
+                } else if (pow2) {
+                    // smallest bit length b > 12 whose left-justified limit exceeds the window
+                    const uint64_t top = win >> 32;
+                    uint32_t b = DC_LUT_BITS + 1;
+#pragma unroll
+                    for (int bb = DC_LUT_BITS + 1; bb <= 32; ++bb) b += (top >= T->lim[bb]) ? 1u : 0u;
+                    if (b > 32) { bad = 1; b = 32; }
+                    const uint32_t L = b / (uint32_t)w;
+                    const uint32_t v = (uint32_t)(top >> (32 - b));
+                    sym = s_syms[(s_start[L] + (v - s_first[L])) & (DC_MAX_SYMS - 1)];
+                    nbt = b;
                 } else {
-                    // long code: canonical decode one base-n digit at a time
                     uint64_t x = win;
                     uint32_t v = 0;
                     int L = 0;
@@ -601,9 +674,9 @@ __global__ __launch_bounds__(256) void k_huff_decode(const uint32_t *__restrict_
             }
         }
         if (m == 16) {
-            *reinterpret_cast<uint4 *>(o + g) = make_uint4(ob[0], ob[1], ob[2], ob[3]);
+            *reinterpret_cast<uint4 *>(o + gsym) = make_uint4(ob[0], ob[1], ob[2], ob[3]);
         } else {
-            for (int k = 0; k < m; ++k) o[g + k] = (uint8_t)(ob[k >> 2] >> (8 * (k & 3)));
+            for (int k = 0; k < m; ++k) o[gsym + k] = (uint8_t)(ob[k >> 2] >> (8 * (k & 3)));
         }
     }
     if (bad) atomicOr(err, 1);
@@ -1165,9 +1238,9 @@ int dc_huff_hist(dc_ctx *c, const uint8_t *d_in, uint64_t n, uint64_t *d_hist)
     }
     const uint64_t grid = nb < 2048 ? nb : 2048;
     LAUNCH(c, "hist_blocks", k_hist_blocks, grid, 256, d_in, n, nb, c->d_bh);
-    const int G = (int)(nb < 512 ? nb : 512);
-    LAUNCH(c, "hist_reduce", k_hist_reduce, G, 256, (const uint16_t *)c->d_bh, nb, c->d_partials);
-    LAUNCH(c, "hist_final", k_hist_final, 1, 256, (const uint64_t *)c->d_partials, G, d_hist);
+    const int G = (int)(nb < 256 ? nb : 256);
+    HIPCHK(hipMemsetAsync(d_hist, 0, 256 * sizeof(uint64_t), c->stream));
+    LAUNCH(c, "hist_reduce", k_hist_reduce, G, 256, (const uint16_t *)c->d_bh, nb, d_hist);
     return DC_OK;
 }
 
@@ -1250,7 +1323,7 @@ int dc_huff_block_hist(dc_ctx *c, uint16_t *h_bh, uint64_t max_entries)
 
 uint64_t dc_huff_words_needed(uint64_t bit_base, uint64_t total_bits)
 {
-    return (((bit_base & 31) + total_bits + 31) >> 5) + 4;   // + slack for the decoder's look-ahead
+    return (((bit_base & 31) + total_bits + 31) >> 5) + 24;   // + slack: the decoder prefetches 64 B ahead
 }
 
 int dc_huff_pack_async(dc_ctx *c, const uint8_t *d_in, uint64_t n, const dc_dtable *d_table, uint64_t bit_base,

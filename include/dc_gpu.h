@@ -51,6 +51,7 @@ typedef struct dc_dtable {
     uint32_t first[DC_MAX_DIGITS + 1]; /* canonical first value per digit length      */
     uint32_t count[DC_MAX_DIGITS + 1];
     uint32_t start[DC_MAX_DIGITS + 1];
+    uint64_t lim[33];               /* left-justified limit per bit length (n = 2^w)  */
     uint16_t syms[DC_MAX_SYMS];     /* symbols sorted by (length, value)               */
     int32_t lengths[DC_MAX_SYMS];   /* Huffman lengths in digits (huffman())          */
     int32_t enc_len[DC_MAX_SYMS];   /* convert_lengths_to_encode_table() outputs      */

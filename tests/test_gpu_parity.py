@@ -201,7 +201,7 @@ def test_decode_of_oracle_stream(torch_cuda, codec):
         L, el, ev, code, nb, mx = _oracle_encode(x, n_ary)
         S = 128
         payload, bits, idx = orc.huff_pack(x, code, nb, sync_syms=S)
-        words = np.zeros((len(payload) + 3) // 4 + 8, np.uint32)
+        words = np.zeros((len(payload) + 3) // 4 + 32, np.uint32)
         words.view(np.uint8)[: len(payload)] = payload
         lens = torch.from_numpy(L.astype(np.int32)).cuda()
         tab = codec.table_lengths(lens, n_ary)
