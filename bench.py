@@ -69,14 +69,14 @@ def main():
     torch.cuda.synchronize()
     c = Codec(local)   # launches on torch's current stream
     S = a.sync or c.default_sync(n)
-    nsync = (n + S - 1) // S
+    ngroups, nchunks = c.sync_sizes(n, S)
 
     hist = torch.empty(256, dtype=torch.int64, device=dev)
     tab = torch.empty(c.table_bytes, dtype=torch.uint8, device=dev)
     total = torch.empty(1, dtype=torch.int64, device=dev)
     allt = torch.empty(world, dtype=torch.int64, device=dev)
     words = torch.empty(c.words_needed(2**40, 32 * n) + 8, dtype=torch.int32, device=dev)
-    sync = torch.empty(nsync, dtype=torch.int64, device=dev)
+    sync = c.alloc_sync(n, S)
     out = torch.empty(n, dtype=torch.uint8, device=dev)
     state = {}
 
@@ -148,7 +148,7 @@ def main():
     for name, ms in kt:
         per.setdefault(name, []).append(ms)
     payload = (bits + 7) // 8
-    sync_bytes = nsync * 8
+    sync_bytes = ngroups * 8 + nchunks * 2
     alg = {"hist_blocks": n, "huff_pack": n + payload + sync_bytes, "huff_decode": payload + sync_bytes + n}
     kernels = {}
     for name, v in per.items():

@@ -87,13 +87,15 @@ def _declare_core(L):
         "dc_huff_table_lengths": ([vp, P, i32, i32, P], i32),
         "dc_huff_table_status": ([vp, P, C.POINTER(C.c_int32)], i32),
         "dc_huff_plan": ([vp, P, P], i32),
-        "dc_huff_pack": ([vp, P, u64, P, u64, P, u64, P, u32], i32),
+        "dc_huff_pack": ([vp, P, u64, P, u64, P, u64, P, P, u32], i32),
+        "dc_huff_sync_chunks": ([u64, u32], u64),
+        "dc_huff_sync_groups": ([u64, u32], u64),
         "dc_huff_words_needed": ([u64, u64], u64),
-        "dc_huff_pack_async": ([vp, P, u64, P, u64, P, u64, P, u32], i32),
+        "dc_huff_pack_async": ([vp, P, u64, P, u64, P, u64, P, P, u32], i32),
         "dc_huff_pack_status": ([vp, P], i32),
         "dc_huff_plan_offsets": ([vp, P, u64, C.POINTER(u64)], i32),
         "dc_huff_block_hist": ([vp, P, u64], i32),
-        "dc_huff_decode": ([vp, P, u64, u64, P, u32, u64, P, P], i32),
+        "dc_huff_decode": ([vp, P, u64, u64, P, P, u32, u64, P, P], i32),
         "dc_huff_decode_status": ([vp], i32),
         "dc_huff_base64url": ([vp, P, u64, u64, P], i32),
         "dc_huff_default_sync": ([u64], u32),

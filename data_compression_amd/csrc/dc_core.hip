@@ -16,6 +16,7 @@
 #include "dc_gpu.h"
 
 #define DC_VERSION "dc-mi355x 0.1 (gfx950)"
+#define DC_SYNC_GROUP 64
 
 // ------------------------------------------------------------------------------------
 // small device helpers
@@ -444,8 +445,9 @@ __global__ void k_zero_bounds(const uint64_t *__restrict__ off, uint64_t nblocks
 __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ in, uint64_t n,
                                                    const dc_dtable *__restrict__ T,
                                                    const uint64_t *__restrict__ block_off, uint64_t bit_base,
-                                                   uint32_t *__restrict__ out, uint64_t *__restrict__ sync,
-                                                   uint32_t sync_syms, uint64_t nblocks, uint64_t words_cap,
+                                                   uint32_t *__restrict__ out, uint64_t *__restrict__ sync_base,
+                                                   uint16_t *__restrict__ sync_len, uint32_t sync_syms,
+                                                   uint64_t nblocks, uint64_t words_cap,
                                                    const int *__restrict__ err)
 {
     __shared__ uint2 s_tab[256];
@@ -491,8 +493,16 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
             const uint64_t TB = tile_abs >> 5;
             const uint64_t As = tile_abs + pre;
             const uint64_t Ae = As + T_bits;
-            if (sync != nullptr && cnt > 0 && (p & (uint64_t)(sync_syms - 1)) == 0)
-                sync[p / sync_syms] = As;
+            if (sync_len != nullptr) {
+                // chunk = sync_syms symbols = sync_syms/16 consecutive lanes of one wave
+                uint32_t cb = T_bits;
+                for (uint32_t d = 1; d < (sync_syms >> 4); d <<= 1) cb += __shfl_xor(cb, (int)d, 64);
+                if (cnt > 0 && (p & (uint64_t)(sync_syms - 1)) == 0) {
+                    sync_len[p / sync_syms] = (uint16_t)cb;
+                    if ((p & ((uint64_t)sync_syms * DC_SYNC_GROUP - 1)) == 0)
+                        sync_base[p / ((uint64_t)sync_syms * DC_SYNC_GROUP)] = As;
+                }
+            }
             const uint32_t ws = (uint32_t)((As >> 5) - TB);
             if (ws != 0) s_stage[ws] = 0u;
             if (t == 255) {
@@ -542,87 +552,43 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
 }
 
 // ------------------------------------------------------------------------------------
-// (H8) decode. One lane per sync chunk (sync_syms symbols, output bytes [c*S, c*S+S)).
-//  * input: a per-lane register FIFO of 8 words fed by 32-byte prefetches issued one FIFO
-//    ahead, so a refill never waits on a dependent HBM load (the v1 kernel stalled on a
-//    global load at nearly every symbol step because some lane of the wave refilled);
-//  * 64-bit MSB-first window; first-level LDS table on the next 12 bits;
-//  * codes > 12 bits, n a power of two: canonical limit compare against the left-justified
-//    per-length limits (wave-uniform, LDS broadcast) -> O(1) length, one LDS symbol read;
-//    other n: canonical decode one base-n digit at a time;
-//  * output gathered 16 bytes per lane -> one 16-B store.
+// (H8) decode. The stream is cut into chunks of S symbols (sync index: u16 bit length per
+// chunk, u64 absolute bit offset per group of 64 chunks). One wave decodes one group,
+// one lane per chunk:
+//  1. lanes read the 64 chunk lengths (one coalesced 128-B load) and prefix-sum them;
+//  2. the wave copies the group's whole compressed span (contiguous) into its private LDS
+//     staging area with 16-B loads, 1 KiB per wave-instruction, then waits once;
+//  3. each lane decodes its chunk from LDS: 64-bit MSB-first window refilled from the
+//     staged words, 12-bit first-level LDS table, canonical limit compare for longer
+//     codes (n a power of two) or a base-n digit walk (other n);
+//  4. 16 decoded bytes per lane -> one 16-B store.
+// A group whose span exceeds the staging area is decoded straight from HBM (fallback).
+// Persistent grid: each workgroup loads the tables once and walks groups grid-stride.
 // ------------------------------------------------------------------------------------
-struct Fifo {
-    uint32_t q0, q1, q2, q3, q4, q5, q6, q7;
-    uint4 n0, n1;
-    const uint4 *gp;
-    int qn;
-    __device__ __forceinline__ uint32_t pop()
-    {
-        const uint32_t v = q0;
-        q0 = q1; q1 = q2; q2 = q3; q3 = q4; q4 = q5; q5 = q6; q6 = q7;
-        if (--qn == 0) {
-            q0 = n0.x; q1 = n0.y; q2 = n0.z; q3 = n0.w;
-            q4 = n1.x; q5 = n1.y; q6 = n1.z; q7 = n1.w;
-            n0 = gp[0];
-            n1 = gp[1];
-            gp += 2;
-            qn = 8;
-        }
-        return bswap32(v);
-    }
+#define DEC_WAVES 4
+#define DEC_STAGE_WORDS 2560   /* 10 KiB per wave */
+
+struct LdsWords {
+    const uint32_t *p;
+    __device__ __forceinline__ uint32_t next() { return bswap32(*p++); }
 };
 
-__global__ __launch_bounds__(256) void k_huff_decode(const uint32_t *__restrict__ in, uint64_t bit_base,
-                                                     const uint64_t *__restrict__ sync, uint32_t S,
-                                                     uint64_t n, const dc_dtable *__restrict__ T,
-                                                     uint8_t *__restrict__ out, int *__restrict__ err)
-{
-    __shared__ uint16_t s_lut[1 << DC_LUT_BITS];
-    __shared__ uint32_t s_first[DC_MAX_DIGITS + 1], s_count[DC_MAX_DIGITS + 1], s_start[DC_MAX_DIGITS + 1];
-    __shared__ uint16_t s_syms[DC_MAX_SYMS];
-    const int t = threadIdx.x;
-    {
-        const uint4 *src = reinterpret_cast<const uint4 *>(T->lut);
-        uint4 *dst = reinterpret_cast<uint4 *>(s_lut);
-        for (int i = t; i < (1 << DC_LUT_BITS) / 8; i += 256) dst[i] = src[i];
-        for (int L = t; L <= DC_MAX_DIGITS; L += 256) {
-            s_first[L] = T->first[L]; s_count[L] = T->count[L]; s_start[L] = T->start[L];
-        }
-        for (int i = t; i < DC_MAX_SYMS; i += 256) s_syms[i] = T->syms[i];
-    }
-    const int nary = T->n_ary, w = T->w;
-    const bool pow2 = (nary & (nary - 1)) == 0;
-    __syncthreads();
+struct HbmWords {
+    const uint32_t *p;
+    __device__ __forceinline__ uint32_t next() { return bswap32(*p++); }
+};
 
-    const uint64_t c = (uint64_t)blockIdx.x * 256 + t;
-    const uint64_t sym0 = c * S;
-    if (sym0 >= n) return;
-    const uint64_t cnt = (n - sym0 < S) ? (n - sym0) : S;
-    const uint64_t rel = sync[c] - ((bit_base >> 5) << 5);
-    const uint64_t w0 = rel >> 5;
-    const uint4 *g = reinterpret_cast<const uint4 *>(in + (w0 & ~3ull));
-    Fifo f;
-    {
-        const uint4 a0 = g[0], a1 = g[1];
-        f.q0 = a0.x; f.q1 = a0.y; f.q2 = a0.z; f.q3 = a0.w;
-        f.q4 = a1.x; f.q5 = a1.y; f.q6 = a1.z; f.q7 = a1.w;
-        f.n0 = g[2];
-        f.n1 = g[3];
-        f.gp = g + 4;
-        f.qn = 8;
-        for (int k = (int)(w0 & 3); k > 0; --k) {   // drop the words before the chunk start
-            f.q0 = f.q1; f.q1 = f.q2; f.q2 = f.q3; f.q3 = f.q4; f.q4 = f.q5; f.q5 = f.q6; f.q6 = f.q7;
-            --f.qn;
-        }
-    }
-    const uint32_t sh = (uint32_t)(rel & 31);
-    const uint32_t hi = f.pop();
-    const uint32_t lo = f.pop();
+template <class R>
+static __device__ __forceinline__ void decode_chunk(R rd, uint32_t sh, uint64_t cnt, uint8_t *__restrict__ o,
+                                                    const uint16_t *s_lut, const uint32_t *s_first,
+                                                    const uint32_t *s_count, const uint32_t *s_start,
+                                                    const uint16_t *s_syms, const dc_dtable *__restrict__ T,
+                                                    int nary, int w, bool pow2, int &bad)
+{
+    const uint32_t hi = rd.next();
+    const uint32_t lo = rd.next();
     uint64_t win = (((uint64_t)hi << 32) | lo) << sh;
     int wbits = 64 - (int)sh;
-    int bad = 0;
-    uint8_t *o = out + sym0;
     for (uint64_t gsym = 0; gsym < cnt; gsym += 16) {
         uint32_t ob[4] = {0u, 0u, 0u, 0u};
         const int m = (cnt - gsym >= 16) ? 16 : (int)(cnt - gsym);
@@ -630,7 +596,7 @@ __global__ __launch_bounds__(256) void k_huff_decode(const uint32_t *__restrict_
         for (int k = 0; k < 16; ++k) {
             if (k < m) {
                 if (wbits < 32) {
-                    win |= (uint64_t)f.pop() << (32 - wbits);
+                    win |= (uint64_t)rd.next() << (32 - wbits);
                     wbits += 32;
                 }
                 const uint32_t e = s_lut[win >> (64 - DC_LUT_BITS)];
@@ -677,6 +643,76 @@ __global__ __launch_bounds__(256) void k_huff_decode(const uint32_t *__restrict_
             *reinterpret_cast<uint4 *>(o + gsym) = make_uint4(ob[0], ob[1], ob[2], ob[3]);
         } else {
             for (int k = 0; k < m; ++k) o[gsym + k] = (uint8_t)(ob[k >> 2] >> (8 * (k & 3)));
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_huff_decode(const uint32_t *__restrict__ in, uint64_t bit_base,
+                                                     const uint64_t *__restrict__ sync_base,
+                                                     const uint16_t *__restrict__ sync_len, uint32_t S,
+                                                     uint64_t n, const dc_dtable *__restrict__ T,
+                                                     uint8_t *__restrict__ out, int *__restrict__ err)
+{
+    __shared__ uint16_t s_lut[1 << DC_LUT_BITS];
+    __shared__ uint32_t s_first[DC_MAX_DIGITS + 1], s_count[DC_MAX_DIGITS + 1], s_start[DC_MAX_DIGITS + 1];
+    __shared__ uint16_t s_syms[DC_MAX_SYMS];
+    __shared__ __attribute__((aligned(16))) uint32_t s_stage[DEC_WAVES][DEC_STAGE_WORDS];
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    {
+        const uint4 *src = reinterpret_cast<const uint4 *>(T->lut);
+        uint4 *dst = reinterpret_cast<uint4 *>(s_lut);
+        for (int i = t; i < (1 << DC_LUT_BITS) / 8; i += 256) dst[i] = src[i];
+        for (int L = t; L <= DC_MAX_DIGITS; L += 256) {
+            s_first[L] = T->first[L]; s_count[L] = T->count[L]; s_start[L] = T->start[L];
+        }
+        for (int i = t; i < DC_MAX_SYMS; i += 256) s_syms[i] = T->syms[i];
+    }
+    const int nary = T->n_ary, w = T->w;
+    const bool pow2 = (nary & (nary - 1)) == 0;
+    __syncthreads();
+
+    const uint64_t nchunks = (n + S - 1) / S;
+    const uint64_t ngroups = (nchunks + DC_SYNC_GROUP - 1) / DC_SYNC_GROUP;
+    const uint64_t word_base = bit_base >> 5;
+    uint32_t *stage = s_stage[wv];
+    int bad = 0;
+    for (uint64_t g = (uint64_t)blockIdx.x * DEC_WAVES + wv; g < ngroups; g += (uint64_t)gridDim.x * DEC_WAVES) {
+        const uint64_t c = g * DC_SYNC_GROUP + lane;
+        const bool valid = c < nchunks;
+        const uint32_t len = valid ? sync_len[c] : 0u;
+        uint32_t incl = len;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(incl, d, 64);
+            if (lane >= d) incl += y;
+        }
+        const uint32_t span_bits = __shfl(incl, 63, 64);
+        const uint32_t off = incl - len;
+        const uint64_t rel0 = sync_base[g] - (word_base << 5);   // group start, bits from in[0]
+        const uint64_t w0 = (rel0 >> 5) & ~3ull;                  // 16-B aligned staging origin
+        const uint32_t lead = (uint32_t)(rel0 - (w0 << 5));        // bits before the group start
+        const uint32_t nwords = (lead + span_bits + 31) / 32 + 2;  // + window look-ahead
+        const uint64_t sym0 = c * S;
+        const uint64_t cnt = valid ? ((n - sym0 < S) ? (n - sym0) : S) : 0;
+        const uint32_t pos = lead + off;                           // lane start, bits into staging
+        if (nwords <= DEC_STAGE_WORDS) {
+            const uint4 *src = reinterpret_cast<const uint4 *>(in + w0);
+            uint4 *dst = reinterpret_cast<uint4 *>(stage);
+            const uint32_t nvec = (nwords + 3) / 4;
+            for (uint32_t i = lane; i < nvec; i += 64) dst[i] = src[i];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (valid) {
+                LdsWords rd{stage + (pos >> 5)};
+                decode_chunk(rd, pos & 31, cnt, out + sym0, s_lut, s_first, s_count, s_start, s_syms, T, nary, w,
+                             pow2, bad);
+            }
+            __builtin_amdgcn_wave_barrier();   // staging reused by the next group
+        } else if (valid) {
+            HbmWords rd{in + w0 + (pos >> 5)};
+            decode_chunk(rd, pos & 31, cnt, out + sym0, s_lut, s_first, s_count, s_start, s_syms, T, nary, w,
+                         pow2, bad);
         }
     }
     if (bad) atomicOr(err, 1);
@@ -1326,19 +1362,26 @@ uint64_t dc_huff_words_needed(uint64_t bit_base, uint64_t total_bits)
     return (((bit_base & 31) + total_bits + 31) >> 5) + 24;   // + slack: the decoder prefetches 64 B ahead
 }
 
+static bool sync_ok(uint32_t S) { return S >= 16 && S <= DC_SYNC_MAX && (S & (S - 1)) == 0; }
+
+uint64_t dc_huff_sync_chunks(uint64_t n, uint32_t S) { return S ? (n + S - 1) / S : 0; }
+uint64_t dc_huff_sync_groups(uint64_t n, uint32_t S) { return (dc_huff_sync_chunks(n, S) + DC_SYNC_GROUP - 1) / DC_SYNC_GROUP; }
+
 int dc_huff_pack_async(dc_ctx *c, const uint8_t *d_in, uint64_t n, const dc_dtable *d_table, uint64_t bit_base,
-                       uint32_t *d_words, uint64_t words_cap, uint64_t *d_sync, uint32_t sync_syms)
+                       uint32_t *d_words, uint64_t words_cap, uint64_t *d_sync_base, uint16_t *d_sync_len,
+                       uint32_t sync_syms)
 {
     if (!c || !d_table || !d_words) return DC_E_ARG;
     if (d_in != c->hist_in || n != c->hist_n || !c->plan_ok) return DC_E_STATE;
-    if (d_sync && (sync_syms < 16 || (sync_syms & (sync_syms - 1)))) return DC_E_ARG;
+    if ((d_sync_base != nullptr) != (d_sync_len != nullptr)) return DC_E_ARG;
+    if (d_sync_len && !sync_ok(sync_syms)) return DC_E_ARG;
     const uint64_t nb = nblocks_of(n);
     if (nb == 0) return DC_OK;
     LAUNCH(c, "zero_bounds", k_zero_bounds, (nb + 1 + 255) / 256, 256, (const uint64_t *)c->d_off, nb, bit_base,
            d_words, words_cap, c->d_err);
     const uint64_t grid = nb < 4096 ? nb : 4096;
     LAUNCH(c, "huff_pack", k_huff_pack, grid, 256, d_in, n, d_table, (const uint64_t *)c->d_off, bit_base, d_words,
-           d_sync, sync_syms, nb, words_cap, (const int *)c->d_err);
+           d_sync_base, d_sync_len, sync_syms, nb, words_cap, (const int *)c->d_err);
     return DC_OK;
 }
 
@@ -1355,11 +1398,13 @@ int dc_huff_pack_status(dc_ctx *c, const dc_dtable *d_table)
 }
 
 int dc_huff_pack(dc_ctx *c, const uint8_t *d_in, uint64_t n, const dc_dtable *d_table, uint64_t bit_base,
-                 uint32_t *d_words, uint64_t words_cap, uint64_t *d_sync, uint32_t sync_syms)
+                 uint32_t *d_words, uint64_t words_cap, uint64_t *d_sync_base, uint16_t *d_sync_len,
+                 uint32_t sync_syms)
 {
     if (!c || !d_table || !d_words) return DC_E_ARG;
     if (d_in != c->hist_in || n != c->hist_n || !c->plan_ok) return DC_E_STATE;
-    if (d_sync && (sync_syms < 16 || (sync_syms & (sync_syms - 1)))) return DC_E_ARG;
+    if ((d_sync_base != nullptr) != (d_sync_len != nullptr)) return DC_E_ARG;
+    if (d_sync_len && !sync_ok(sync_syms)) return DC_E_ARG;
     // plan errors (a byte without a code) are checked here: host read of one int
     int err = 0;
     HIPCHK(hipMemcpyAsync(c->h_pinned, c->d_err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
@@ -1373,27 +1418,30 @@ int dc_huff_pack(dc_ctx *c, const uint8_t *d_in, uint64_t n, const dc_dtable *d_
     }
     const uint64_t total = c->h_pinned[1];
     if (dc_huff_words_needed(bit_base, total) > words_cap) return DC_E_CAPACITY;
-    return dc_huff_pack_async(c, d_in, n, d_table, bit_base, d_words, words_cap, d_sync, sync_syms);
+    return dc_huff_pack_async(c, d_in, n, d_table, bit_base, d_words, words_cap, d_sync_base, d_sync_len, sync_syms);
 }
 
 uint32_t dc_huff_default_sync(uint64_t n)
 {
-    uint32_t S = 64;
-    while (S < (1u << 16) && (n >> 19) > S) S <<= 1;
-    return S;
+    (void)n;
+    return 128;   // 1.6 % index overhead; a wave's 64 chunks fit its 10 KiB LDS stage below ~9 bits/symbol
 }
 
-int dc_huff_decode(dc_ctx *c, const uint32_t *d_words, uint64_t bit_base, uint64_t words, const uint64_t *d_sync,
-                   uint32_t S, uint64_t n, const dc_dtable *d_table, uint8_t *d_out)
+int dc_huff_decode(dc_ctx *c, const uint32_t *d_words, uint64_t bit_base, uint64_t words,
+                   const uint64_t *d_sync_base, const uint16_t *d_sync_len, uint32_t S, uint64_t n,
+                   const dc_dtable *d_table, uint8_t *d_out)
 {
-    if (!c || !d_table || (n && (!d_words || !d_sync || !d_out))) return DC_E_ARG;
-    if (S < 16 || (S & (S - 1))) return DC_E_ARG;
+    if (!c || !d_table || (n && (!d_words || !d_sync_base || !d_sync_len || !d_out))) return DC_E_ARG;
+    if (!sync_ok(S)) return DC_E_ARG;
     if (((uintptr_t)d_out) & 15) return DC_E_ARG;
+    if (((uintptr_t)d_words) & 15) return DC_E_ARG;
     (void)words;
     if (n == 0) return DC_OK;
-    const uint64_t nchunks = (n + S - 1) / S;
+    const uint64_t groups = dc_huff_sync_groups(n, S);
     HIPCHK(hipMemsetAsync(c->d_err + 1, 0, sizeof(int), c->stream));
-    LAUNCH(c, "huff_decode", k_huff_decode, (nchunks + 255) / 256, 256, d_words, bit_base, d_sync, S, n, d_table,
+    const uint64_t wgs = (groups + DEC_WAVES - 1) / DEC_WAVES;
+    const uint64_t grid = wgs < 256 * 3 ? wgs : 256 * 3;   // persistent: 3 workgroups per CU (LDS)
+    LAUNCH(c, "huff_decode", k_huff_decode, grid, 256, d_words, bit_base, d_sync_base, d_sync_len, S, n, d_table,
            d_out, c->d_err + 1);
     return DC_OK;
 }

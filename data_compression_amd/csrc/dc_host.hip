@@ -65,6 +65,12 @@ inline uint64_t get64(const uint8_t *p) { uint64_t v; memcpy(&v, p, 8); return v
 
 extern "C" {
 
+// sync index in the container: u64 group bases, then u16 chunk bit lengths
+static uint64_t index_bytes(uint64_t n, uint32_t S)
+{
+    return dc_huff_sync_groups(n, S) * 8 + dc_huff_sync_chunks(n, S) * 2;
+}
+
 dc_ctx *dc_host_ctx(void)
 {
     HostState *s = nullptr;
@@ -95,8 +101,7 @@ int dc_host_scratch(int which, uint64_t bytes, void **d_out)
 uint64_t dc_huff_compress_bound(uint64_t n, uint32_t sync_syms)
 {
     if (sync_syms == 0) sync_syms = dc_huff_default_sync(n);
-    const uint64_t nsync = (n + sync_syms - 1) / sync_syms;
-    return kHeader + nsync * 8 + n * 4 + 64;   // codes are <= 32 bits per byte
+    return kHeader + index_bytes(n, sync_syms) + n * 4 + 64;   // codes are <= 32 bits per byte
 }
 
 int dc_huff_compress_host(const uint8_t *in, uint64_t n, int n_ary, const int32_t *lengths, int max_symbol_value,
@@ -107,7 +112,7 @@ int dc_huff_compress_host(const uint8_t *in, uint64_t n, int n_ary, const int32_
     RC(state(&s));
     dc_ctx *c = s->ctx;
     if (sync_syms == 0) sync_syms = dc_huff_default_sync(n);
-    if (sync_syms < 16 || (sync_syms & (sync_syms - 1))) return DC_E_ARG;
+    if (sync_syms < 16 || sync_syms > DC_SYNC_MAX || (sync_syms & (sync_syms - 1))) return DC_E_ARG;
     const uint8_t *d_in = nullptr;
     RC(dc_host_upload(in, n, &d_in));
     RC(s->hist.need(256 * 8 + 64));
@@ -132,13 +137,16 @@ int dc_huff_compress_host(const uint8_t *in, uint64_t n, int n_ary, const int32_
     uint64_t total = 0;
     RC(dc_memcpy_d2h(c, &total, d_total, 8));
     const uint64_t words = dc_huff_words_needed(0, total);
-    const uint64_t nsync = n ? (n + sync_syms - 1) / sync_syms : 0;
+    const uint64_t ng = dc_huff_sync_groups(n, sync_syms), nc = dc_huff_sync_chunks(n, sync_syms);
+    const uint64_t ib = index_bytes(n, sync_syms);
     const uint64_t nbytes = (total + 7) / 8;
-    const uint64_t need = kHeader + nsync * 8 + nbytes;
+    const uint64_t need = kHeader + ib + nbytes;
     if (need > cap) return DC_E_CAPACITY;
     RC(s->out.need(words * 4));
-    RC(s->sync.need(nsync * 8 + 8));
-    RC(dc_huff_pack(c, d_in, n, d_tab, 0, (uint32_t *)s->out.p, words, (uint64_t *)s->sync.p, sync_syms));
+    RC(s->sync.need(ib + 16));
+    uint64_t *d_base = (uint64_t *)s->sync.p;
+    uint16_t *d_len = (uint16_t *)(d_base + ng);
+    RC(dc_huff_pack(c, d_in, n, d_tab, 0, (uint32_t *)s->out.p, words, d_base, d_len, sync_syms));
     // header: magic, version, n, w, payload bits, sync granularity, per-byte code lengths
     int32_t enc_len[256];
     RC(dc_memcpy_d2h(c, enc_len, d_tab->enc_len, sizeof(enc_len)));
@@ -154,8 +162,9 @@ int dc_huff_compress_host(const uint8_t *in, uint64_t n, int n_ary, const int32_
     put64(out + 16, total);
     put32(out + 24, sync_syms);
     for (int i = 0; i < 256; ++i) out[32 + i] = (uint8_t)(enc_len[i] > 0 ? enc_len[i] : 0);
-    RC(dc_memcpy_d2h(c, out + kHeader, s->sync.p, nsync * 8));
-    RC(dc_memcpy_d2h(c, out + kHeader + nsync * 8, s->out.p, nbytes));
+    RC(dc_memcpy_d2h(c, out + kHeader, d_base, ng * 8));
+    RC(dc_memcpy_d2h(c, out + kHeader + ng * 8, d_len, nc * 2));
+    RC(dc_memcpy_d2h(c, out + kHeader + ib, s->out.p, nbytes));
     *out_len = need;
     return DC_OK;
 }
@@ -176,10 +185,11 @@ int dc_huff_decompress_host(const uint8_t *in, uint64_t m, uint8_t *out, uint64_
     int nary = 0;
     RC(dc_huff_container_info(in, m, &n, &nary, &bits));
     const uint32_t S = get32(in + 24);
-    if (S < 16 || (S & (S - 1)) || nary < 2) return DC_E_STREAM;
-    const uint64_t nsync = n ? (n + S - 1) / S : 0;
+    if (S < 16 || S > DC_SYNC_MAX || (S & (S - 1)) || nary < 2) return DC_E_STREAM;
+    const uint64_t ng = dc_huff_sync_groups(n, S), nc = dc_huff_sync_chunks(n, S);
+    const uint64_t ib = index_bytes(n, S);
     const uint64_t nbytes = (bits + 7) / 8;
-    if (kHeader + nsync * 8 + nbytes > m) return DC_E_STREAM;
+    if (kHeader + ib + nbytes > m) return DC_E_STREAM;
     if (n > cap) return DC_E_CAPACITY;
     if (n && !out) return DC_E_ARG;
     HostState *s;
@@ -197,13 +207,15 @@ int dc_huff_decompress_host(const uint8_t *in, uint64_t m, uint8_t *out, uint64_
     if (st) return st;
     const uint64_t words = dc_huff_words_needed(0, bits);
     RC(s->in.need(words * 4 + 64));
-    RC(s->sync.need(nsync * 8 + 8));
+    RC(s->sync.need(ib + 16));
     RC(s->out.need(n + 64));
+    uint64_t *d_base = (uint64_t *)s->sync.p;
+    uint16_t *d_len = (uint16_t *)(d_base + ng);
     RC(dc_memset(c, s->in.p, 0, words * 4));
-    RC(dc_memcpy_h2d(c, s->sync.p, in + kHeader, nsync * 8));
-    RC(dc_memcpy_h2d(c, s->in.p, in + kHeader + nsync * 8, nbytes));
-    RC(dc_huff_decode(c, (const uint32_t *)s->in.p, 0, words, (const uint64_t *)s->sync.p, S, n, d_tab,
-                      (uint8_t *)s->out.p));
+    RC(dc_memcpy_h2d(c, d_base, in + kHeader, ng * 8));
+    RC(dc_memcpy_h2d(c, d_len, in + kHeader + ng * 8, nc * 2));
+    RC(dc_memcpy_h2d(c, s->in.p, in + kHeader + ib, nbytes));
+    RC(dc_huff_decode(c, (const uint32_t *)s->in.p, 0, words, d_base, d_len, S, n, d_tab, (uint8_t *)s->out.p));
     RC(dc_huff_decode_status(c));
     RC(dc_memcpy_d2h(c, out, s->out.p, n));
     *out_len = n;

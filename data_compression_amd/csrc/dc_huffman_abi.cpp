@@ -119,7 +119,7 @@ int represent_items_with_codes(const int max_symbol_value, int canonical_lengths
     DC_OR_DIE("represent_items_with_codes", dc_host_scratch(0, words * 4, &d_words));
     const uint64_t nchar = (total + 5) / 6;
     if ((uint64_t)start + nchar > (uint64_t)bufsize + 1) return -1;
-    const int r = dc_huff_pack(c, d_in, n, t, 0, (uint32_t *)d_words, words, nullptr, 0);
+    const int r = dc_huff_pack(c, d_in, n, t, 0, (uint32_t *)d_words, words, nullptr, nullptr, 0);
     if (r) return -1;
     DC_OR_DIE("represent_items_with_codes", dc_host_scratch(1, nchar + 16, &d_text));
     DC_OR_DIE("represent_items_with_codes", dc_huff_base64url(c, (const uint32_t *)d_words, 0, total, (char *)d_text));

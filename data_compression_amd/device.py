@@ -122,21 +122,34 @@ class Codec:
     def words_needed(self, bit_base: int, total_bits: int) -> int:
         return int(self.L.dc_huff_words_needed(bit_base, total_bits))
 
+    def sync_sizes(self, n: int, sync_syms: int):
+        """(groups, chunks) of the sync index for n symbols."""
+        return (int(self.L.dc_huff_sync_groups(n, sync_syms)), int(self.L.dc_huff_sync_chunks(n, sync_syms)))
+
+    def alloc_sync(self, n: int, sync_syms: int):
+        g, c = self.sync_sizes(n, sync_syms)
+        return (self._t(max(g, 1), torch.int64), self._t(max(c, 1), torch.int16))
+
     def pack(self, x, tab, bit_base, words, sync, sync_syms):
+        base, lens = sync if sync is not None else (None, None)
         check("dc_huff_pack", self.L.dc_huff_pack(self.ctx, _ptr(x), x.numel(), _ptr(tab), bit_base, _ptr(words),
-                                                  words.numel(), _ptr(sync), sync_syms if sync is not None else 0))
+                                                  words.numel(), _ptr(base), _ptr(lens),
+                                                  sync_syms if sync is not None else 0))
 
     def pack_async(self, x, tab, bit_base, words, sync, sync_syms):
+        base, lens = sync if sync is not None else (None, None)
         check("dc_huff_pack_async",
               self.L.dc_huff_pack_async(self.ctx, _ptr(x), x.numel(), _ptr(tab), bit_base, _ptr(words),
-                                        words.numel(), _ptr(sync), sync_syms if sync is not None else 0))
+                                        words.numel(), _ptr(base), _ptr(lens),
+                                        sync_syms if sync is not None else 0))
 
     def pack_status(self, tab):
         return int(self.L.dc_huff_pack_status(self.ctx, _ptr(tab)))
 
     def decode(self, words, bit_base, sync, sync_syms, n, tab, out):
-        check("dc_huff_decode", self.L.dc_huff_decode(self.ctx, _ptr(words), bit_base, words.numel(), _ptr(sync),
-                                                      sync_syms, n, _ptr(tab), _ptr(out)))
+        base, lens = sync
+        check("dc_huff_decode", self.L.dc_huff_decode(self.ctx, _ptr(words), bit_base, words.numel(), _ptr(base),
+                                                      _ptr(lens), sync_syms, n, _ptr(tab), _ptr(out)))
 
     def decode_status(self):
         return int(self.L.dc_huff_decode_status(self.ctx))
@@ -153,7 +166,7 @@ class Codec:
         total = self.plan(tab)
         bits = int(total.item())
         words = self._t(self.words_needed(bit_base, bits), torch.int32)
-        sync = self._t(max(1, (n + S - 1) // S), torch.int64)
+        sync = self.alloc_sync(n, S)
         self.pack(x, tab, bit_base, words, sync, S)
         return {"hist": hist, "table": tab, "bits": bits, "words": words, "sync": sync, "S": S,
                 "bit_base": bit_base, "n": n}

@@ -40,6 +40,7 @@ enum {
 #define DC_LUT_BITS 12          /* decoder first-level lookup table: 2^12 entries */
 #define DC_MAX_SYMS 1024        /* max_symbol_value + 1 supported by the table kernel */
 #define DC_MAX_DIGITS 128       /* longest code length (in base-n digits) handled */
+#define DC_SYNC_MAX 1024        /* largest sync granularity (u16 chunk bit lengths) */
 
 typedef struct dc_ctx dc_ctx;
 
@@ -100,11 +101,16 @@ int dc_huff_table_lengths(dc_ctx *ctx, const int32_t *d_lengths, int max_symbol_
  *     writes the payload bit count to *d_total_bits (device u64). */
 int dc_huff_plan(dc_ctx *ctx, const dc_dtable *d_table, uint64_t *d_total_bits);
 /* (4) pack at global bit offset bit_base into d_words (word 0 = stream word bit_base/32,
- *     MSB-first bytes). Capacity: dc_huff_words_needed(). d_sync[c] = absolute bit offset
- *     of symbol c*sync_syms (sync_syms: power of two >= 16, or 0 for no index). */
+ *     MSB-first bytes; 16-B aligned). Capacity: dc_huff_words_needed().
+ *     Sync index (DESIGN.md "Sync index v1"), both arrays NULL for none: chunks of
+ *     sync_syms symbols (power of two, 16..DC_SYNC_MAX): d_sync_len[c] = bit length of
+ *     chunk c (u16, dc_huff_sync_chunks entries); d_sync_base[g] = absolute bit offset of
+ *     chunk 64g (u64, dc_huff_sync_groups entries). */
 int dc_huff_pack(dc_ctx *ctx, const uint8_t *d_in, uint64_t n, const dc_dtable *d_table,
-                 uint64_t bit_base, uint32_t *d_words, uint64_t words_cap, uint64_t *d_sync,
-                 uint32_t sync_syms);
+                 uint64_t bit_base, uint32_t *d_words, uint64_t words_cap,
+                 uint64_t *d_sync_base, uint16_t *d_sync_len, uint32_t sync_syms);
+uint64_t dc_huff_sync_chunks(uint64_t n, uint32_t sync_syms);
+uint64_t dc_huff_sync_groups(uint64_t n, uint32_t sync_syms);
 uint64_t dc_huff_words_needed(uint64_t bit_base, uint64_t total_bits);
 /* inspection (synchronising): the plan's exclusive per-block bit offsets (nblocks+1
  * entries, last = total) and the per-block u16 histograms of the last dc_huff_hist */
@@ -114,21 +120,21 @@ int dc_huff_block_hist(dc_ctx *ctx, uint16_t *h_bh, uint64_t max_entries);
  *     code or words_cap too small makes the kernels write nothing; read the outcome with
  *     dc_huff_pack_status() (synchronising). */
 int dc_huff_pack_async(dc_ctx *ctx, const uint8_t *d_in, uint64_t n, const dc_dtable *d_table,
-                       uint64_t bit_base, uint32_t *d_words, uint64_t words_cap, uint64_t *d_sync,
-                       uint32_t sync_syms);
+                       uint64_t bit_base, uint32_t *d_words, uint64_t words_cap,
+                       uint64_t *d_sync_base, uint16_t *d_sync_len, uint32_t sync_syms);
 int dc_huff_pack_status(dc_ctx *ctx, const dc_dtable *d_table);
 /* Status word written by the table / plan kernels (host-synchronising read). */
 int dc_huff_table_status(dc_ctx *ctx, const dc_dtable *d_table, int32_t *max_bits);
-/* (5) decode n symbols. d_words/bit_base as for pack; d_sync from pack. */
+/* (5) decode n symbols. d_words/bit_base and the sync index as written by pack. */
 int dc_huff_decode(dc_ctx *ctx, const uint32_t *d_words, uint64_t bit_base, uint64_t words,
-                   const uint64_t *d_sync, uint32_t sync_syms, uint64_t n,
-                   const dc_dtable *d_table, uint8_t *d_out);
+                   const uint64_t *d_sync_base, const uint16_t *d_sync_len, uint32_t sync_syms,
+                   uint64_t n, const dc_dtable *d_table, uint8_t *d_out);
 /* status of the last dc_huff_decode on this context (synchronising): 0 or DC_E_STREAM */
 int dc_huff_decode_status(dc_ctx *ctx);
 /* base64url text (6 bits per char, MSB-first) of bits [bit_base, bit_base+bits) */
 int dc_huff_base64url(dc_ctx *ctx, const uint32_t *d_words, uint64_t bit_base, uint64_t bits,
                       char *d_text);
-/* recommended sync granularity for n symbols (keeps >= 2^18 chunks in flight) */
+/* recommended sync granularity (symbols per chunk) */
 uint32_t dc_huff_default_sync(uint64_t n);
 
 /* ---- nybble codec (nybble_compression.c), device-resident ---------------------------- */

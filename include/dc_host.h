@@ -26,7 +26,8 @@ int dc_host_scratch(int which, uint64_t bytes, void **d_out);
  * [0]  "DCH1"  [4] u8 version=1, u8 n_ary, u8 w (bits per digit), u8 flags=0
  * [8]  u64 n symbols   [16] u64 payload bits   [24] u32 sync_syms, u32 0
  * [32] u8 code length (digits) of byte 0..255
- * [288] u64 sync index, ceil(n / sync_syms) entries (bit offset of symbol c*sync_syms)
+ * [288] sync index (dc_gpu.h): u64 group bases (dc_huff_sync_groups entries), then
+ *       u16 chunk bit lengths (dc_huff_sync_chunks entries)
  * then the MSB-first payload, ceil(bits/8) bytes, zero-padded.
  * lengths == NULL: lengths from the input's own histogram (n_ary_huffman.c:2509-2530 flow),
  * else from lengths[0..max_symbol_value] (the caller's huffman() output).

@@ -151,3 +151,12 @@ def small_decompress(c: bytes) -> bytes:
     out = np.zeros(2 * len(c) + 8, dtype=np.uint8)
     n = lib().orc_small_decompress(_p(a, u8p), len(c), _p(out, u8p))
     return out[:n].tobytes()
+
+
+def sync_compact(idx, bit_base, bits, group=64):
+    """Per-chunk absolute bit offsets -> (u64 group bases, u16 chunk bit lengths): the
+    build-defined sync index v1."""
+    idx = np.asarray(idx, dtype=np.uint64)
+    ends = np.append(idx[1:], np.uint64(bit_base + bits))
+    lens = (ends - idx).astype(np.uint16)
+    return idx[::group].copy(), lens

@@ -164,7 +164,9 @@ def test_pack_bit_exact_vs_oracle(torch_cuda, codec, n_ary):
         assert enc["bits"] == bits, name
         got = enc["words"].cpu().numpy().view(np.uint8)[: len(payload)]
         assert np.array_equal(got, payload), name
-        assert np.array_equal(enc["sync"].cpu().numpy().astype(np.uint64)[: len(idx)], idx), name
+        base, lens = orc.sync_compact(idx, 0, bits)
+        assert np.array_equal(enc["sync"][0].cpu().numpy().astype(np.uint64)[: len(base)], base), name
+        assert np.array_equal(enc["sync"][1].cpu().numpy().view(np.uint16)[: len(lens)], lens), name
         out = torch.empty(x.size + 16, dtype=torch.uint8, device="cuda")
         codec.decode_into(enc, out)
         assert codec.decode_status() == 0
@@ -183,31 +185,33 @@ def test_pack_at_bit_offset(torch_cuda, codec, bit_base):
     xt = torch.from_numpy(x).cuda()
     enc = codec.encode(xt, n_ary=2, sync_syms=S, bit_base=bit_base)
     got = enc["words"].cpu().numpy().view(np.uint8)
-    lead = (bit_base & 31) // 8 * 0   # words start at word bit_base/32; oracle at byte bit_base/8
-    off = ((bit_base >> 3) - ((bit_base >> 5) << 2))
+    off = (bit_base >> 3) - ((bit_base >> 5) << 2)   # words start at stream word bit_base/32
     assert np.array_equal(got[off: off + len(payload)], payload)
-    assert not got[:off].any() and lead == 0
-    assert np.array_equal(enc["sync"].cpu().numpy().astype(np.uint64), idx)
+    assert not got[:off].any()
+    base, lens = orc.sync_compact(idx, bit_base, bits)
+    assert np.array_equal(enc["sync"][0].cpu().numpy().astype(np.uint64), base)
+    assert np.array_equal(enc["sync"][1].cpu().numpy().view(np.uint16), lens)
     out = torch.empty(x.size, dtype=torch.uint8, device="cuda")
     codec.decode_into(enc, out)
     assert np.array_equal(out.cpu().numpy(), x)
 
 
-def test_decode_of_oracle_stream(torch_cuda, codec):
+@pytest.mark.parametrize("S", [16, 128, 1024])   # 1024: spans exceed the LDS stage -> HBM path
+def test_decode_of_oracle_stream(torch_cuda, codec, S):
     torch = torch_cuda
     from data_compression_amd import synth
     for n_ary in (2, 3, 16):
         x = synth.log_like(200_000, seed=n_ary)
         L, el, ev, code, nb, mx = _oracle_encode(x, n_ary)
-        S = 128
         payload, bits, idx = orc.huff_pack(x, code, nb, sync_syms=S)
         words = np.zeros((len(payload) + 3) // 4 + 32, np.uint32)
         words.view(np.uint8)[: len(payload)] = payload
         lens = torch.from_numpy(L.astype(np.int32)).cuda()
         tab = codec.table_lengths(lens, n_ary)
         out = torch.empty(x.size, dtype=torch.uint8, device="cuda")
-        codec.decode(torch.from_numpy(words.view(np.int32)).cuda(), 0,
-                     torch.from_numpy(idx.astype(np.int64)).cuda(), S, x.size, tab, out)
+        base, lens = orc.sync_compact(idx, 0, bits)
+        sync = (torch.from_numpy(base.astype(np.int64)).cuda(), torch.from_numpy(lens.view(np.int16)).cuda())
+        codec.decode(torch.from_numpy(words.view(np.int32)).cuda(), 0, sync, S, x.size, tab, out)
         assert codec.decode_status() == 0
         assert np.array_equal(out.cpu().numpy(), x)
 
