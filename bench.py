@@ -68,7 +68,11 @@ def main():
     x = synth.device_text(a.cfg, n, seed=0xC2 + 7919 * rank, device=dev)
     torch.cuda.synchronize()
     c = Codec(local)   # launches on torch's current stream
-    S = a.sync or c.default_sync(n)
+    # sync granularity: chosen once from this stream's planned payload (outside the timed
+    # region), as the encoder would for a stream of these statistics (dc_huff_choose_sync)
+    c.hist(x)
+    probe_tab = c.table(c.hist(x), a.nary)
+    S = a.sync or c.choose_sync(n, int(c.plan(probe_tab).item()))
     ngroups, nchunks = c.sync_sizes(n, S)
 
     hist = torch.empty(256, dtype=torch.int64, device=dev)

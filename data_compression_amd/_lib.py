@@ -99,6 +99,7 @@ def _declare_core(L):
         "dc_huff_decode_status": ([vp], i32),
         "dc_huff_base64url": ([vp, P, u64, u64, P], i32),
         "dc_huff_default_sync": ([u64], u32),
+        "dc_huff_choose_sync": ([u64, u64], u32),
         "dc_nyb_compress": ([vp, P, u64, i32, P, C.POINTER(u64)], i32),
         "dc_nyb_decompress": ([vp, P, u64, i32, P, C.POINTER(u64)], i32),
         "dc_small_compress": ([vp, P, u64, P, C.POINTER(u64)], i32),

@@ -468,14 +468,24 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
         const uint64_t blk_first_word = blk_abs >> 5;
         uint64_t tile_abs = blk_abs;
         if (t == 0) s_stage[0] = 0u;
+        // the whole 32 KiB block: 8 independent 16-B loads per lane in flight at once
+        uint4 blkv[DC_BLOCK_BYTES / PACK_TILE];
+        const bool full = (blk_start + DC_BLOCK_BYTES <= n);
+        if (full) {
+#pragma unroll
+            for (int k = 0; k < (int)(DC_BLOCK_BYTES / PACK_TILE); ++k)
+                blkv[k] = *reinterpret_cast<const uint4 *>(in + blk_start + (uint64_t)k * PACK_TILE + (uint64_t)t * 16);
+        }
         __syncthreads();
-        for (uint64_t tile = blk_start; tile < blk_end; tile += PACK_TILE) {
+#pragma unroll
+        for (int k = 0; k < (int)(DC_BLOCK_BYTES / PACK_TILE); ++k) {
+            const uint64_t tile = blk_start + (uint64_t)k * PACK_TILE;
+            if (tile >= blk_end) break;
             const uint64_t p = tile + (uint64_t)t * 16;
             const int cnt = (p + 16 <= blk_end) ? 16 : (p < blk_end ? (int)(blk_end - p) : 0);
             uint32_t bytes4[4] = {0u, 0u, 0u, 0u};
-            if (cnt == 16) {
-                const uint4 v = *reinterpret_cast<const uint4 *>(in + p);
-                bytes4[0] = v.x; bytes4[1] = v.y; bytes4[2] = v.z; bytes4[3] = v.w;
+            if (full) {
+                bytes4[0] = blkv[k].x; bytes4[1] = blkv[k].y; bytes4[2] = blkv[k].z; bytes4[3] = blkv[k].w;
             } else {
                 for (int i = 0; i < cnt; ++i) bytes4[i >> 2] |= (uint32_t)in[p + i] << (8 * (i & 3));
             }
@@ -566,16 +576,22 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
 // Persistent grid: each workgroup loads the tables once and walks groups grid-stride.
 // ------------------------------------------------------------------------------------
 #define DEC_WAVES 4
-#define DEC_STAGE_WORDS 2560   /* 10 KiB per wave */
+#define DEC_STAGE_WORDS 1664   /* 6.5 KiB per wave -> 4 workgroups (16 waves) per CU */
 
+// Word readers. next() returns the following stream word; peek-ahead keeps the next
+// word's LDS/HBM read one refill ahead of its use, so a refill never waits on a read.
 struct LdsWords {
     const uint32_t *p;
-    __device__ __forceinline__ uint32_t next() { return bswap32(*p++); }
+    uint32_t nx;
+    __device__ __forceinline__ void init() { nx = *p++; }
+    __device__ __forceinline__ uint32_t next() { const uint32_t v = nx; nx = *p++; return bswap32(v); }
 };
 
 struct HbmWords {
     const uint32_t *p;
-    __device__ __forceinline__ uint32_t next() { return bswap32(*p++); }
+    uint32_t nx;
+    __device__ __forceinline__ void init() { nx = *p++; }
+    __device__ __forceinline__ uint32_t next() { const uint32_t v = nx; nx = *p++; return bswap32(v); }
 };
 
 template <class R>
@@ -585,6 +601,7 @@ static __device__ __forceinline__ void decode_chunk(R rd, uint32_t sh, uint64_t 
                                                     const uint16_t *s_syms, const dc_dtable *__restrict__ T,
                                                     int nary, int w, bool pow2, int &bad)
 {
+    rd.init();
     const uint32_t hi = rd.next();
     const uint32_t lo = rd.next();
     uint64_t win = (((uint64_t)hi << 32) | lo) << sh;
@@ -595,7 +612,7 @@ static __device__ __forceinline__ void decode_chunk(R rd, uint32_t sh, uint64_t 
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
             if (k < m) {
-                if (wbits < 32) {
+                if (wbits < 32) {   // taken by ~1 lane in 7: the word is already in a register
                     win |= (uint64_t)rd.next() << (32 - wbits);
                     wbits += 32;
                 }
@@ -695,11 +712,27 @@ __global__ __launch_bounds__(256) void k_huff_decode(const uint32_t *__restrict_
         const uint64_t sym0 = c * S;
         const uint64_t cnt = valid ? ((n - sym0 < S) ? (n - sym0) : S) : 0;
         const uint32_t pos = lead + off;                           // lane start, bits into staging
-        if (nwords <= DEC_STAGE_WORDS) {
+        if (nwords + 1 <= DEC_STAGE_WORDS) {   // +1: the readers peek one word ahead
             const uint4 *src = reinterpret_cast<const uint4 *>(in + w0);
             uint4 *dst = reinterpret_cast<uint4 *>(stage);
-            const uint32_t nvec = (nwords + 3) / 4;
-            for (uint32_t i = lane; i < nvec; i += 64) dst[i] = src[i];
+            const uint32_t nvec = (nwords + 4) / 4;
+            // all loads in flight (named registers: a runtime-indexed array would go to
+            // scratch), then all LDS writes; 7 x 1 KiB covers the 6.5 KiB stage
+            static_assert((DEC_STAGE_WORDS / 4 + 63) / 64 <= 7, "stage larger than 7 KiB");
+            // (indices clamped, not the loads predicated: selecting between two addresses
+            // made hipcc fall back to serialised flat loads)
+            const uint32_t i0 = lane, i1 = lane + 64, i2 = lane + 128, i3 = lane + 192, i4 = lane + 256,
+                           i5 = lane + 320, i6 = lane + 384, last = nvec - 1;
+            const uint4 v0 = src[min(i0, last)], v1 = src[min(i1, last)], v2 = src[min(i2, last)],
+                        v3 = src[min(i3, last)], v4 = src[min(i4, last)], v5 = src[min(i5, last)],
+                        v6 = src[min(i6, last)];
+            if (i0 < nvec) dst[i0] = v0;
+            if (i1 < nvec) dst[i1] = v1;
+            if (i2 < nvec) dst[i2] = v2;
+            if (i3 < nvec) dst[i3] = v3;
+            if (i4 < nvec) dst[i4] = v4;
+            if (i5 < nvec) dst[i5] = v5;
+            if (i6 < nvec) dst[i6] = v6;
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1424,7 +1457,18 @@ int dc_huff_pack(dc_ctx *c, const uint8_t *d_in, uint64_t n, const dc_dtable *d_
 uint32_t dc_huff_default_sync(uint64_t n)
 {
     (void)n;
-    return 128;   // 1.6 % index overhead; a wave's 64 chunks fit its 10 KiB LDS stage below ~9 bits/symbol
+    return 128;   // 1.6 % index overhead
+}
+
+uint32_t dc_huff_choose_sync(uint64_t n, uint64_t total_bits)
+{
+    // largest S in [64, 1024] whose expected 64-chunk span (S * 64 * bits/symbol) stays
+    // under 5.5 KiB, so the decoder's 6.5 KiB per-wave LDS stage holds nearly every group
+    if (n == 0) return 128;
+    const double avg = (double)total_bits / (double)n;
+    uint32_t S = 64;
+    while (S < DC_SYNC_MAX && (double)(2 * S) * 64.0 * avg / 8.0 <= 5632.0) S <<= 1;
+    return S;
 }
 
 int dc_huff_decode(dc_ctx *c, const uint32_t *d_words, uint64_t bit_base, uint64_t words,
@@ -1440,7 +1484,7 @@ int dc_huff_decode(dc_ctx *c, const uint32_t *d_words, uint64_t bit_base, uint64
     const uint64_t groups = dc_huff_sync_groups(n, S);
     HIPCHK(hipMemsetAsync(c->d_err + 1, 0, sizeof(int), c->stream));
     const uint64_t wgs = (groups + DEC_WAVES - 1) / DEC_WAVES;
-    const uint64_t grid = wgs < 256 * 3 ? wgs : 256 * 3;   // persistent: 3 workgroups per CU (LDS)
+    const uint64_t grid = wgs < 256 * 4 ? wgs : 256 * 4;   // persistent: 4 workgroups per CU (LDS)
     LAUNCH(c, "huff_decode", k_huff_decode, grid, 256, d_words, bit_base, d_sync_base, d_sync_len, S, n, d_table,
            d_out, c->d_err + 1);
     return DC_OK;

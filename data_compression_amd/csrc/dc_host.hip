@@ -100,7 +100,7 @@ int dc_host_scratch(int which, uint64_t bytes, void **d_out)
 
 uint64_t dc_huff_compress_bound(uint64_t n, uint32_t sync_syms)
 {
-    if (sync_syms == 0) sync_syms = dc_huff_default_sync(n);
+    if (sync_syms == 0) sync_syms = 64;   // the densest index dc_huff_choose_sync can pick
     return kHeader + index_bytes(n, sync_syms) + n * 4 + 64;   // codes are <= 32 bits per byte
 }
 
@@ -111,8 +111,8 @@ int dc_huff_compress_host(const uint8_t *in, uint64_t n, int n_ary, const int32_
     HostState *s;
     RC(state(&s));
     dc_ctx *c = s->ctx;
-    if (sync_syms == 0) sync_syms = dc_huff_default_sync(n);
-    if (sync_syms < 16 || sync_syms > DC_SYNC_MAX || (sync_syms & (sync_syms - 1))) return DC_E_ARG;
+    if (sync_syms != 0 && (sync_syms < 16 || sync_syms > DC_SYNC_MAX || (sync_syms & (sync_syms - 1))))
+        return DC_E_ARG;
     const uint8_t *d_in = nullptr;
     RC(dc_host_upload(in, n, &d_in));
     RC(s->hist.need(256 * 8 + 64));
@@ -137,6 +137,7 @@ int dc_huff_compress_host(const uint8_t *in, uint64_t n, int n_ary, const int32_
     uint64_t total = 0;
     RC(dc_memcpy_d2h(c, &total, d_total, 8));
     const uint64_t words = dc_huff_words_needed(0, total);
+    if (sync_syms == 0) sync_syms = dc_huff_choose_sync(n, total);
     const uint64_t ng = dc_huff_sync_groups(n, sync_syms), nc = dc_huff_sync_chunks(n, sync_syms);
     const uint64_t ib = index_bytes(n, sync_syms);
     const uint64_t nbytes = (total + 7) / 8;

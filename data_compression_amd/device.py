@@ -157,14 +157,17 @@ class Codec:
     def default_sync(self, n: int) -> int:
         return int(self.L.dc_huff_default_sync(n))
 
+    def choose_sync(self, n: int, total_bits: int) -> int:
+        return int(self.L.dc_huff_choose_sync(n, total_bits))
+
     def encode(self, x, n_ary: int = 2, sync_syms: int | None = None, bit_base: int = 0):
         """hist -> table -> plan -> pack on one device. Returns dict of device tensors."""
         n = x.numel()
-        S = sync_syms or self.default_sync(n)
         hist = self.hist(x)
         tab = self.table(hist, n_ary)
         total = self.plan(tab)
         bits = int(total.item())
+        S = sync_syms or self.choose_sync(n, bits)
         words = self._t(self.words_needed(bit_base, bits), torch.int32)
         sync = self.alloc_sync(n, S)
         self.pack(x, tab, bit_base, words, sync, S)

@@ -134,8 +134,10 @@ int dc_huff_decode_status(dc_ctx *ctx);
 /* base64url text (6 bits per char, MSB-first) of bits [bit_base, bit_base+bits) */
 int dc_huff_base64url(dc_ctx *ctx, const uint32_t *d_words, uint64_t bit_base, uint64_t bits,
                       char *d_text);
-/* recommended sync granularity (symbols per chunk) */
+/* sync granularity (symbols per chunk): a fixed default, and the choice from the
+ * planned payload (keeps a 64-chunk group within the decoder's LDS stage) */
 uint32_t dc_huff_default_sync(uint64_t n);
+uint32_t dc_huff_choose_sync(uint64_t n, uint64_t total_bits);
 
 /* ---- nybble codec (nybble_compression.c), device-resident ---------------------------- */
 /* Full reference byte stream (header, packed nybbles, LITERAL fallback) of d_in[0..n).
