@@ -317,17 +317,33 @@ __global__ __launch_bounds__(256) void k_huff_table(const uint64_t *__restrict__
         else lim = ((uint64_t)s_startv[Ld] + s_cnt[Ld]) << (32 - Ld * w);
         T->lim[t] = lim;
     }
-    for (int e = t; e < (1 << DC_LUT_BITS); e += 256) T->lut[e] = 0;
+    // one-symbol table in LDS (reuses s_key): window -> sym | nbits<<8, 0 = longer code
+    uint32_t *s_lut1 = reinterpret_cast<uint32_t *>(s_key);
+    for (int e = t; e < (1 << DC_LUT_BITS); e += 256) s_lut1[e] = 0;
     __syncthreads();
     T->code[t] = s_code[t];
     T->nbits[t] = s_nb[t];
-    // first-level decode table: every 12-bit window whose prefix is a code of <= 12 bits
     for (int s = 0; s < 256; ++s) {
         const uint32_t nb = s_nb[s];
         if (nb == 0 || nb > DC_LUT_BITS) continue;
         const uint32_t span = 1u << (DC_LUT_BITS - nb);
         const uint32_t base = s_code[s] << (DC_LUT_BITS - nb);
-        for (uint32_t j = t; j < span; j += 256) T->lut[base + j] = (uint16_t)(s | (nb << 8));
+        for (uint32_t j = t; j < span; j += 256) s_lut1[base + j] = s | (nb << 8);
+    }
+    __syncthreads();
+    // two-symbol table: a window holding a whole second code after the first yields both
+    // (DC_LUT_* layout in dc_gpu.h)
+    for (int e = t; e < (1 << DC_LUT_BITS); e += 256) {
+        const uint32_t a = s_lut1[e];
+        uint32_t v = 0;
+        if (a) {
+            const uint32_t s0 = a & 255u, n0 = a >> 8;
+            v = s0 | (n0 << 16) | (n0 << 21);
+            const uint32_t b = s_lut1[((uint32_t)e << n0) & ((1u << DC_LUT_BITS) - 1)];
+            if (b && (b >> 8) <= DC_LUT_BITS - n0)
+                v = s0 | ((b & 255u) << 8) | ((n0 + (b >> 8)) << 16) | (n0 << 21) | (1u << 26);
+        }
+        T->lut[e] = v;
     }
     if (t == 0) {
         T->n_ary = nary;
@@ -575,102 +591,133 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
 // A group whose span exceeds the staging area is decoded straight from HBM (fallback).
 // Persistent grid: each workgroup loads the tables once and walks groups grid-stride.
 // ------------------------------------------------------------------------------------
-#define DEC_WAVES 4
-#define DEC_STAGE_WORDS 1664   /* 6.5 KiB per wave -> 4 workgroups (16 waves) per CU */
+#define DEC_WAVES 8
+#define DEC_STAGE_WORDS 1664   /* 6.5 KiB per wave: 8 waves + tables = 72 KiB -> 2 workgroups per CU */
 
-// Word readers. next() returns the following stream word; peek-ahead keeps the next
-// word's LDS/HBM read one refill ahead of its use, so a refill never waits on a read.
-struct LdsWords {
+// Word readers: next() returns the following stream word (byte-swapped to MSB-first).
+// They read one word ahead so the refill's data is in a register before it is needed.
+// nx = the next word to enter the window, p = the word after it.
+struct LdsWords {   // LDS: read unconditionally every step (cheap), keep it only when taken
     const uint32_t *p;
     uint32_t nx;
     __device__ __forceinline__ void init() { nx = *p++; }
-    __device__ __forceinline__ uint32_t next() { const uint32_t v = nx; nx = *p++; return bswap32(v); }
+    __device__ __forceinline__ uint32_t peek() const { return bswap32(nx); }
+    __device__ __forceinline__ void advance(bool take)
+    {
+        const uint32_t v = *p;
+        nx = take ? v : nx;
+        p += take ? 1 : 0;
+    }
 };
 
-struct HbmWords {
+struct HbmWords {   // HBM fallback: read only when a word is taken
     const uint32_t *p;
     uint32_t nx;
     __device__ __forceinline__ void init() { nx = *p++; }
-    __device__ __forceinline__ uint32_t next() { const uint32_t v = nx; nx = *p++; return bswap32(v); }
+    __device__ __forceinline__ uint32_t peek() const { return bswap32(nx); }
+    __device__ __forceinline__ void advance(bool take)
+    {
+        if (take) { nx = *p; ++p; }
+    }
 };
+
+// slow path for windows the two-symbol table does not cover (codes longer than 12 bits)
+// returns a table-format entry; bit 31 flags an invalid code
+static __device__ __forceinline__ uint32_t decode_long(uint64_t win, const uint32_t *s_first, const uint32_t *s_count,
+                                                       const uint32_t *s_start, const uint16_t *s_syms,
+                                                       const dc_dtable *__restrict__ T, int nary, int w, bool pow2)
+{
+    uint32_t bad = 0;
+    uint32_t sym = 0, nbt;
+    if (pow2) {
+        // smallest bit length b > 12 whose left-justified canonical limit exceeds the window
+        const uint64_t top = win >> 32;
+        uint32_t b = DC_LUT_BITS + 1;
+        for (int bb = DC_LUT_BITS + 1; bb <= 32; ++bb) b += (top >= T->lim[bb]) ? 1u : 0u;
+        if (b > 32) { bad = 1; b = 32; }
+        const uint32_t L = b / (uint32_t)w;
+        const uint32_t v = (uint32_t)(top >> (32 - b));
+        sym = s_syms[(s_start[L] + (v - s_first[L])) & (DC_MAX_SYMS - 1)];
+        nbt = b;
+    } else {
+        uint64_t x = win;
+        uint32_t v = 0;
+        int L = 0;
+        nbt = (uint32_t)w;
+        while (true) {
+            const uint32_t digit = (uint32_t)(x >> (64 - w));
+            x <<= w;
+            v = v * (uint32_t)nary + digit;
+            ++L;
+            if (L * w > 32 || L > DC_MAX_DIGITS) { bad = 1; break; }
+            if (s_count[L] && v - s_first[L] < s_count[L]) {
+                sym = s_syms[s_start[L] + (v - s_first[L])];
+                nbt = (uint32_t)(L * w);
+                break;
+            }
+        }
+    }
+    return (sym & 255u) | (nbt << 16) | (nbt << 21) | (bad << 31);
+}
 
 template <class R>
-static __device__ __forceinline__ void decode_chunk(R rd, uint32_t sh, uint64_t cnt, uint8_t *__restrict__ o,
-                                                    const uint16_t *s_lut, const uint32_t *s_first,
+static __device__ __forceinline__ void decode_chunk(R rd, uint32_t sh, uint32_t cnt, uint8_t *__restrict__ o,
+                                                    const uint32_t *s_lut, const uint32_t *s_first,
                                                     const uint32_t *s_count, const uint32_t *s_start,
                                                     const uint16_t *s_syms, const dc_dtable *__restrict__ T,
                                                     int nary, int w, bool pow2, int &bad)
 {
     rd.init();
-    const uint32_t hi = rd.next();
-    const uint32_t lo = rd.next();
+    const uint32_t hi = rd.peek();
+    rd.advance(true);
+    const uint32_t lo = rd.peek();
+    rd.advance(true);
     uint64_t win = (((uint64_t)hi << 32) | lo) << sh;
     int wbits = 64 - (int)sh;
-    for (uint64_t gsym = 0; gsym < cnt; gsym += 16) {
-        uint32_t ob[4] = {0u, 0u, 0u, 0u};
-        const int m = (cnt - gsym >= 16) ? 16 : (int)(cnt - gsym);
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            if (k < m) {
-                if (wbits < 32) {   // taken by ~1 lane in 7: the word is already in a register
-                    win |= (uint64_t)rd.next() << (32 - wbits);
-                    wbits += 32;
-                }
-                const uint32_t e = s_lut[win >> (64 - DC_LUT_BITS)];
-                uint32_t sym, nbt;
-                if (e != 0) {
-                    sym = e & 255u;
-                    nbt = e >> 8;
-                } else if (pow2) {
-                    // smallest bit length b > 12 whose left-justified limit exceeds the window
-                    const uint64_t top = win >> 32;
-                    uint32_t b = DC_LUT_BITS + 1;
-#pragma unroll
-                    for (int bb = DC_LUT_BITS + 1; bb <= 32; ++bb) b += (top >= T->lim[bb]) ? 1u : 0u;
-                    if (b > 32) { bad = 1; b = 32; }
-                    const uint32_t L = b / (uint32_t)w;
-                    const uint32_t v = (uint32_t)(top >> (32 - b));
-                    sym = s_syms[(s_start[L] + (v - s_first[L])) & (DC_MAX_SYMS - 1)];
-                    nbt = b;
-                } else {
-                    uint64_t x = win;
-                    uint32_t v = 0;
-                    int L = 0;
-                    sym = 0;
-                    nbt = 0;
-                    while (true) {
-                        const uint32_t digit = (uint32_t)(x >> (64 - w));
-                        x <<= w;
-                        v = v * (uint32_t)nary + digit;
-                        ++L;
-                        if (L * w > 32 || L > DC_MAX_DIGITS) { bad = 1; nbt = (uint32_t)w; break; }
-                        if (s_count[L] && v - s_first[L] < s_count[L]) {
-                            sym = s_syms[s_start[L] + (v - s_first[L])];
-                            nbt = (uint32_t)(L * w);
-                            break;
-                        }
-                    }
-                }
-                win <<= nbt;
-                wbits -= (int)nbt;
-                ob[k >> 2] |= (sym & 255u) << (8 * (k & 3));
+    uint64_t acc = 0;     // decoded bytes not yet stored (little-endian = output order)
+    uint32_t na = 0;      // bytes in acc (< 8)
+    uint32_t rem = cnt;   // symbols still to decode
+    while (rem) {
+        // branch-free refill: a word enters the window when fewer than 32 bits remain
+        const bool need = wbits < 32;
+        const uint64_t add = (uint64_t)rd.peek() << (32 - (need ? wbits : 32));
+        win |= need ? add : 0ull;
+        wbits += need ? 32 : 0;
+        rd.advance(need);
+        uint32_t e = s_lut[win >> (64 - DC_LUT_BITS)];
+        if (__builtin_expect(__any(e == 0), 0)) {
+            if (e == 0) {
+                e = decode_long(win, s_first, s_count, s_start, s_syms, T, nary, w, pow2);
+                bad |= (int)(e >> 31);
             }
         }
-        if (m == 16) {
-            *reinterpret_cast<uint4 *>(o + gsym) = make_uint4(ob[0], ob[1], ob[2], ob[3]);
-        } else {
-            for (int k = 0; k < m; ++k) o[gsym + k] = (uint8_t)(ob[k >> 2] >> (8 * (k & 3)));
+        // two symbols when the table found two and both are still wanted
+        const bool two = ((e >> 26) & 1u) && rem >= 2;
+        const uint32_t nbt = two ? ((e >> 16) & 31u) : ((e >> 21) & 31u);
+        const uint32_t syms = two ? (e & 0xFFFFu) : (e & 0xFFu);
+        const uint32_t ns = two ? 2u : 1u;
+        win <<= nbt;
+        wbits -= (int)nbt;
+        rem -= ns;
+        acc |= (uint64_t)syms << (8 * na);
+        na += ns;
+        if (na >= 8) {
+            *reinterpret_cast<uint64_t *>(o) = acc;
+            o += 8;
+            na -= 8;
+            acc = na ? (uint64_t)(syms >> 8) : 0ull;   // the second symbol spilled past byte 7
         }
     }
+    for (uint32_t k = 0; k < na; ++k) o[k] = (uint8_t)(acc >> (8 * k));
 }
 
-__global__ __launch_bounds__(256) void k_huff_decode(const uint32_t *__restrict__ in, uint64_t bit_base,
+__global__ __launch_bounds__(DEC_WAVES * 64) void k_huff_decode(const uint32_t *__restrict__ in, uint64_t bit_base,
                                                      const uint64_t *__restrict__ sync_base,
                                                      const uint16_t *__restrict__ sync_len, uint32_t S,
                                                      uint64_t n, const dc_dtable *__restrict__ T,
                                                      uint8_t *__restrict__ out, int *__restrict__ err)
 {
-    __shared__ uint16_t s_lut[1 << DC_LUT_BITS];
+    __shared__ __attribute__((aligned(16))) uint32_t s_lut[1 << DC_LUT_BITS];
     __shared__ uint32_t s_first[DC_MAX_DIGITS + 1], s_count[DC_MAX_DIGITS + 1], s_start[DC_MAX_DIGITS + 1];
     __shared__ uint16_t s_syms[DC_MAX_SYMS];
     __shared__ __attribute__((aligned(16))) uint32_t s_stage[DEC_WAVES][DEC_STAGE_WORDS];
@@ -678,11 +725,11 @@ __global__ __launch_bounds__(256) void k_huff_decode(const uint32_t *__restrict_
     {
         const uint4 *src = reinterpret_cast<const uint4 *>(T->lut);
         uint4 *dst = reinterpret_cast<uint4 *>(s_lut);
-        for (int i = t; i < (1 << DC_LUT_BITS) / 8; i += 256) dst[i] = src[i];
-        for (int L = t; L <= DC_MAX_DIGITS; L += 256) {
+        for (int i = t; i < (1 << DC_LUT_BITS) / 4; i += DEC_WAVES * 64) dst[i] = src[i];
+        for (int L = t; L <= DC_MAX_DIGITS; L += DEC_WAVES * 64) {
             s_first[L] = T->first[L]; s_count[L] = T->count[L]; s_start[L] = T->start[L];
         }
-        for (int i = t; i < DC_MAX_SYMS; i += 256) s_syms[i] = T->syms[i];
+        for (int i = t; i < DC_MAX_SYMS; i += DEC_WAVES * 64) s_syms[i] = T->syms[i];
     }
     const int nary = T->n_ary, w = T->w;
     const bool pow2 = (nary & (nary - 1)) == 0;
@@ -710,17 +757,15 @@ __global__ __launch_bounds__(256) void k_huff_decode(const uint32_t *__restrict_
         const uint32_t lead = (uint32_t)(rel0 - (w0 << 5));        // bits before the group start
         const uint32_t nwords = (lead + span_bits + 31) / 32 + 2;  // + window look-ahead
         const uint64_t sym0 = c * S;
-        const uint64_t cnt = valid ? ((n - sym0 < S) ? (n - sym0) : S) : 0;
+        const uint32_t cnt = valid ? (uint32_t)((n - sym0 < S) ? (n - sym0) : S) : 0u;
         const uint32_t pos = lead + off;                           // lane start, bits into staging
         if (nwords + 1 <= DEC_STAGE_WORDS) {   // +1: the readers peek one word ahead
             const uint4 *src = reinterpret_cast<const uint4 *>(in + w0);
             uint4 *dst = reinterpret_cast<uint4 *>(stage);
             const uint32_t nvec = (nwords + 4) / 4;
-            // all loads in flight (named registers: a runtime-indexed array would go to
-            // scratch), then all LDS writes; 7 x 1 KiB covers the 6.5 KiB stage
+            // all loads in flight (named registers; indices clamped rather than loads
+            // predicated, which made hipcc emit serialised flat loads), then the LDS writes
             static_assert((DEC_STAGE_WORDS / 4 + 63) / 64 <= 7, "stage larger than 7 KiB");
-            // (indices clamped, not the loads predicated: selecting between two addresses
-            // made hipcc fall back to serialised flat loads)
             const uint32_t i0 = lane, i1 = lane + 64, i2 = lane + 128, i3 = lane + 192, i4 = lane + 256,
                            i5 = lane + 320, i6 = lane + 384, last = nvec - 1;
             const uint4 v0 = src[min(i0, last)], v1 = src[min(i1, last)], v2 = src[min(i2, last)],
@@ -733,17 +778,15 @@ __global__ __launch_bounds__(256) void k_huff_decode(const uint32_t *__restrict_
             if (i4 < nvec) dst[i4] = v4;
             if (i5 < nvec) dst[i5] = v5;
             if (i6 < nvec) dst[i6] = v6;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             if (valid) {
-                LdsWords rd{stage + (pos >> 5)};
+                LdsWords rd{stage + (pos >> 5), 0u};
                 decode_chunk(rd, pos & 31, cnt, out + sym0, s_lut, s_first, s_count, s_start, s_syms, T, nary, w,
                              pow2, bad);
             }
             __builtin_amdgcn_wave_barrier();   // staging reused by the next group
         } else if (valid) {
-            HbmWords rd{in + w0 + (pos >> 5)};
+            HbmWords rd{in + w0 + (pos >> 5), 0u};
             decode_chunk(rd, pos & 31, cnt, out + sym0, s_lut, s_first, s_count, s_start, s_syms, T, nary, w,
                          pow2, bad);
         }
@@ -1484,8 +1527,8 @@ int dc_huff_decode(dc_ctx *c, const uint32_t *d_words, uint64_t bit_base, uint64
     const uint64_t groups = dc_huff_sync_groups(n, S);
     HIPCHK(hipMemsetAsync(c->d_err + 1, 0, sizeof(int), c->stream));
     const uint64_t wgs = (groups + DEC_WAVES - 1) / DEC_WAVES;
-    const uint64_t grid = wgs < 256 * 4 ? wgs : 256 * 4;   // persistent: 4 workgroups per CU (LDS)
-    LAUNCH(c, "huff_decode", k_huff_decode, grid, 256, d_words, bit_base, d_sync_base, d_sync_len, S, n, d_table,
+    const uint64_t grid = wgs < 256 * 2 ? wgs : 256 * 2;   // persistent: 2 workgroups (16 waves) per CU
+    LAUNCH(c, "huff_decode", k_huff_decode, grid, DEC_WAVES * 64, d_words, bit_base, d_sync_base, d_sync_len, S, n, d_table,
            d_out, c->d_err + 1);
     return DC_OK;
 }
