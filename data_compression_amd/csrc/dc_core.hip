@@ -591,8 +591,10 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
 // A group whose span exceeds the staging area is decoded straight from HBM (fallback).
 // Persistent grid: each workgroup loads the tables once and walks groups grid-stride.
 // ------------------------------------------------------------------------------------
-#define DEC_WAVES 8
-#define DEC_STAGE_WORDS 1664   /* 6.5 KiB per wave: 8 waves + tables = 72 KiB -> 2 workgroups per CU */
+#define DEC_WAVES 16            /* one 1024-thread workgroup per CU shares the 16 KiB table   */
+#define DEC_STAGE_WORDS 1088   /* 4.25 KiB compressed input per wave (LDS total 159.5 KiB)    */
+#define DEC_OUT_SYMS 64        /* chunks of <= 64 symbols are staged through LDS for output   */
+#define DEC_OUT_STRIDE 72      /* bytes per lane: 64 + 8 pad -> conflict-free ds_write_b64      */
 
 // Word readers: next() returns the following stream word (byte-swapped to MSB-first).
 // They read one word ahead so the refill's data is in a register before it is needed.
@@ -660,8 +662,20 @@ static __device__ __forceinline__ uint32_t decode_long(uint64_t win, const uint3
     return (sym & 255u) | (nbt << 16) | (nbt << 21) | (bad << 31);
 }
 
-template <class R>
-static __device__ __forceinline__ void decode_chunk(R rd, uint32_t sh, uint32_t cnt, uint8_t *__restrict__ o,
+// output policies: 8-byte flushes into the lane's LDS row, or straight to HBM
+struct LdsOut {
+    uint8_t *o;
+    __device__ __forceinline__ void put8(uint64_t v) { *reinterpret_cast<uint64_t *>(o) = v; o += 8; }
+    __device__ __forceinline__ void put1(uint32_t k, uint8_t v) { o[k] = v; }
+};
+struct HbmOut {
+    uint8_t *o;
+    __device__ __forceinline__ void put8(uint64_t v) { *reinterpret_cast<uint64_t *>(o) = v; o += 8; }
+    __device__ __forceinline__ void put1(uint32_t k, uint8_t v) { o[k] = v; }
+};
+
+template <class R, class W>
+static __device__ __forceinline__ void decode_chunk(R rd, uint32_t sh, uint32_t cnt, W o,
                                                     const uint32_t *s_lut, const uint32_t *s_first,
                                                     const uint32_t *s_count, const uint32_t *s_start,
                                                     const uint16_t *s_syms, const dc_dtable *__restrict__ T,
@@ -702,13 +716,12 @@ static __device__ __forceinline__ void decode_chunk(R rd, uint32_t sh, uint32_t 
         acc |= (uint64_t)syms << (8 * na);
         na += ns;
         if (na >= 8) {
-            *reinterpret_cast<uint64_t *>(o) = acc;
-            o += 8;
+            o.put8(acc);
             na -= 8;
             acc = na ? (uint64_t)(syms >> 8) : 0ull;   // the second symbol spilled past byte 7
         }
     }
-    for (uint32_t k = 0; k < na; ++k) o[k] = (uint8_t)(acc >> (8 * k));
+    for (uint32_t k = 0; k < na; ++k) o.put1(k, (uint8_t)(acc >> (8 * k)));
 }
 
 __global__ __launch_bounds__(DEC_WAVES * 64) void k_huff_decode(const uint32_t *__restrict__ in, uint64_t bit_base,
@@ -721,6 +734,7 @@ __global__ __launch_bounds__(DEC_WAVES * 64) void k_huff_decode(const uint32_t *
     __shared__ uint32_t s_first[DC_MAX_DIGITS + 1], s_count[DC_MAX_DIGITS + 1], s_start[DC_MAX_DIGITS + 1];
     __shared__ uint16_t s_syms[DC_MAX_SYMS];
     __shared__ __attribute__((aligned(16))) uint32_t s_stage[DEC_WAVES][DEC_STAGE_WORDS];
+    __shared__ __attribute__((aligned(16))) uint8_t s_out[DEC_WAVES][64 * DEC_OUT_STRIDE];
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     {
         const uint4 *src = reinterpret_cast<const uint4 *>(T->lut);
@@ -739,6 +753,8 @@ __global__ __launch_bounds__(DEC_WAVES * 64) void k_huff_decode(const uint32_t *
     const uint64_t ngroups = (nchunks + DC_SYNC_GROUP - 1) / DC_SYNC_GROUP;
     const uint64_t word_base = bit_base >> 5;
     uint32_t *stage = s_stage[wv];
+    uint8_t *ostage = s_out[wv];
+    const bool stage_out = S <= DEC_OUT_SYMS;
     int bad = 0;
     for (uint64_t g = (uint64_t)blockIdx.x * DEC_WAVES + wv; g < ngroups; g += (uint64_t)gridDim.x * DEC_WAVES) {
         const uint64_t c = g * DC_SYNC_GROUP + lane;
@@ -781,15 +797,40 @@ __global__ __launch_bounds__(DEC_WAVES * 64) void k_huff_decode(const uint32_t *
             __builtin_amdgcn_wave_barrier();
             if (valid) {
                 LdsWords rd{stage + (pos >> 5), 0u};
-                decode_chunk(rd, pos & 31, cnt, out + sym0, s_lut, s_first, s_count, s_start, s_syms, T, nary, w,
-                             pow2, bad);
+                if (stage_out)
+                    decode_chunk(rd, pos & 31, cnt, LdsOut{ostage + lane * DEC_OUT_STRIDE}, s_lut, s_first, s_count,
+                                 s_start, s_syms, T, nary, w, pow2, bad);
+                else
+                    decode_chunk(rd, pos & 31, cnt, HbmOut{out + sym0}, s_lut, s_first, s_count, s_start, s_syms,
+                                 T, nary, w, pow2, bad);
             }
-            __builtin_amdgcn_wave_barrier();   // staging reused by the next group
         } else if (valid) {
             HbmWords rd{in + w0 + (pos >> 5), 0u};
-            decode_chunk(rd, pos & 31, cnt, out + sym0, s_lut, s_first, s_count, s_start, s_syms, T, nary, w,
-                         pow2, bad);
+            if (stage_out)
+                decode_chunk(rd, pos & 31, cnt, LdsOut{ostage + lane * DEC_OUT_STRIDE}, s_lut, s_first, s_count,
+                             s_start, s_syms, T, nary, w, pow2, bad);
+            else
+                decode_chunk(rd, pos & 31, cnt, HbmOut{out + sym0}, s_lut, s_first, s_count, s_start, s_syms, T,
+                             nary, w, pow2, bad);
         }
+        if (stage_out) {
+            // the group's 64 chunks are one contiguous output range: coalesced 16-B stores,
+            // 1 KiB per wave-instruction (rows are 8-B aligned: two ds_read_b64 per piece)
+            __builtin_amdgcn_wave_barrier();
+            const uint64_t gbase = g * DC_SYNC_GROUP * (uint64_t)S;
+            const uint64_t gbytes = (n - gbase < DC_SYNC_GROUP * (uint64_t)S) ? n - gbase : DC_SYNC_GROUP * (uint64_t)S;
+            const uint32_t pieces_per_row = S / 16;
+            for (uint32_t j = lane; j < (uint32_t)(gbytes / 16); j += 64) {
+                const uint32_t r = j / pieces_per_row, q = j % pieces_per_row;
+                const uint64_t *src = reinterpret_cast<const uint64_t *>(ostage + r * DEC_OUT_STRIDE + q * 16);
+                const uint64_t a = src[0], b = src[1];
+                *reinterpret_cast<uint4 *>(out + gbase + (uint64_t)j * 16) =
+                    make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
+            }
+            for (uint32_t k = (uint32_t)(gbytes & ~15ull) + lane; k < (uint32_t)gbytes; k += 64)
+                out[gbase + k] = ostage[(k / S) * DEC_OUT_STRIDE + (k % S)];
+        }
+        __builtin_amdgcn_wave_barrier();   // staging areas reused by the next group
     }
     if (bad) atomicOr(err, 1);
 }
@@ -1500,18 +1541,16 @@ int dc_huff_pack(dc_ctx *c, const uint8_t *d_in, uint64_t n, const dc_dtable *d_
 uint32_t dc_huff_default_sync(uint64_t n)
 {
     (void)n;
-    return 128;   // 1.6 % index overhead
+    return 64;
 }
 
 uint32_t dc_huff_choose_sync(uint64_t n, uint64_t total_bits)
 {
-    // largest S in [64, 1024] whose expected 64-chunk span (S * 64 * bits/symbol) stays
-    // under 5.5 KiB, so the decoder's 6.5 KiB per-wave LDS stage holds nearly every group
-    if (n == 0) return 128;
+    // 64 symbols per chunk: the decoder stages a group's input (4.5 KiB) and output (64 x
+    // 64 B) through LDS. Denser streams (> ~8.5 bits/symbol) use 32 so the input still fits.
+    if (n == 0) return 64;
     const double avg = (double)total_bits / (double)n;
-    uint32_t S = 64;
-    while (S < DC_SYNC_MAX && (double)(2 * S) * 64.0 * avg / 8.0 <= 5632.0) S <<= 1;
-    return S;
+    return (64.0 * 64.0 * avg / 8.0 <= 4200.0) ? 64u : 32u;
 }
 
 int dc_huff_decode(dc_ctx *c, const uint32_t *d_words, uint64_t bit_base, uint64_t words,
@@ -1527,7 +1566,7 @@ int dc_huff_decode(dc_ctx *c, const uint32_t *d_words, uint64_t bit_base, uint64
     const uint64_t groups = dc_huff_sync_groups(n, S);
     HIPCHK(hipMemsetAsync(c->d_err + 1, 0, sizeof(int), c->stream));
     const uint64_t wgs = (groups + DEC_WAVES - 1) / DEC_WAVES;
-    const uint64_t grid = wgs < 256 * 2 ? wgs : 256 * 2;   // persistent: 2 workgroups (16 waves) per CU
+    const uint64_t grid = wgs < 256 ? wgs : 256;   // persistent: one 16-wave workgroup per CU
     LAUNCH(c, "huff_decode", k_huff_decode, grid, DEC_WAVES * 64, d_words, bit_base, d_sync_base, d_sync_len, S, n, d_table,
            d_out, c->d_err + 1);
     return DC_OK;
