@@ -70,35 +70,29 @@ def main():
     c = Codec(local)   # launches on torch's current stream
     # sync granularity: chosen once from this stream's planned payload (outside the timed
     # region), as the encoder would for a stream of these statistics (dc_huff_choose_sync)
-    c.hist(x)
     probe_tab = c.table(c.hist(x), a.nary)
     S = a.sync or c.choose_sync(n, int(c.plan(probe_tab).item()))
+    if world > 1:   # one granularity for the whole stream
+        st = torch.tensor([S], dtype=torch.int64, device=dev)
+        dist.all_reduce(st, op=dist.ReduceOp.MIN)
+        S = int(st.item())
     ngroups, nchunks = c.sync_sizes(n, S)
 
+    from data_compression_amd.dist import ShardedHuffman
+    sh = ShardedHuffman(c)
     hist = torch.empty(256, dtype=torch.int64, device=dev)
     tab = torch.empty(c.table_bytes, dtype=torch.uint8, device=dev)
     total = torch.empty(1, dtype=torch.int64, device=dev)
-    allt = torch.empty(world, dtype=torch.int64, device=dev)
     words = torch.empty(c.words_needed(2**40, 32 * n) + 8, dtype=torch.int32, device=dev)
     sync = c.alloc_sync(n, S)
     out = torch.empty(n, dtype=torch.uint8, device=dev)
     state = {}
 
-    def encode():
-        c.hist(x, out=hist)
-        if world > 1:
-            dist.all_reduce(hist)
-        c.table(hist, a.nary, out=tab)
-        c.plan(tab, total=total)
-        base = 0
-        if world > 1:
-            dist.all_gather_into_tensor(allt, total)
-            base = int(allt[:rank].sum().item()) if rank else 0
-        c.pack_async(x, tab, base, words, sync, S)
-        state["base"] = base
+    def encode():   # hist -> [all_reduce] -> table -> plan -> [all_gather] -> pack
+        state["s"] = sh.encode(x, a.nary, S, words=words, sync=sync, hist=hist, table=tab, total=total)
 
     def decode():
-        c.decode(words, state["base"], sync, S, n, tab, out)
+        sh.decode(state["s"], out=out)
 
     def step():
         encode()
@@ -126,7 +120,7 @@ def main():
     # ---- correctness of the measured configuration (outside the timed region) ----------
     st = c.pack_status(tab)
     ok = st == 0 and c.decode_status() == 0 and bool(torch.equal(out, x))
-    bits = int(total.item())
+    bits = int(total.item())   # this rank's payload bits
     if world > 1:
         okt = torch.tensor([1 if ok else 0], device=dev)
         dist.all_reduce(okt, op=dist.ReduceOp.MIN)

@@ -117,7 +117,11 @@ class Codec:
     def plan(self, tab, total=None):
         total = total if total is not None else self._t(1, torch.int64)
         check("dc_huff_plan", self.L.dc_huff_plan(self.ctx, _ptr(tab), _ptr(total)))
+        self._last_total = total
         return total
+
+    def plan_total(self) -> int:
+        return int(self._last_total.item())
 
     def words_needed(self, bit_base: int, total_bits: int) -> int:
         return int(self.L.dc_huff_words_needed(bit_base, total_bits))
@@ -176,6 +180,13 @@ class Codec:
 
     def decode_into(self, enc, out):
         self.decode(enc["words"], enc["bit_base"], enc["sync"], enc["S"], enc["n"], enc["table"], out)
+
+    # ---- allocation helpers (the engine interface used by dist.ShardedHuffman) -----------
+    def alloc_words(self, bit_base: int, bits: int):
+        return self._t(self.words_needed(bit_base, bits), torch.int32)
+
+    def alloc_bytes(self, n: int):
+        return self._t(max(n, 1))
 
     # ---- host helpers -------------------------------------------------------------------
     def histogram_host(self, x: np.ndarray, max_symbol_value: int = 258) -> np.ndarray:
