@@ -338,10 +338,10 @@ __global__ __launch_bounds__(256) void k_huff_table(const uint64_t *__restrict__
         uint32_t v = 0;
         if (a) {
             const uint32_t s0 = a & 255u, n0 = a >> 8;
-            v = s0 | (n0 << 16) | (n0 << 21);
+            v = s0 | (n0 << 8) | (n0 << 24) | (1u << 29);
             const uint32_t b = s_lut1[((uint32_t)e << n0) & ((1u << DC_LUT_BITS) - 1)];
             if (b && (b >> 8) <= DC_LUT_BITS - n0)
-                v = s0 | ((b & 255u) << 8) | ((n0 + (b >> 8)) << 16) | (n0 << 21) | (1u << 26);
+                v = s0 | ((n0 + (b >> 8)) << 8) | ((b & 255u) << 16) | (n0 << 24) | (2u << 29);
         }
         T->lut[e] = v;
     }
@@ -592,19 +592,30 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
 // Persistent grid: each workgroup loads the tables once and walks groups grid-stride.
 // ------------------------------------------------------------------------------------
 #define DEC_WAVES 16            /* one 1024-thread workgroup per CU shares the 16 KiB table   */
-#define DEC_STAGE_WORDS 1088   /* 4.25 KiB compressed input per wave (LDS total 159.5 KiB)    */
+#define DEC_STAGE_WORDS 1088   /* 4.25 KiB compressed input per wave                          */
 #define DEC_OUT_SYMS 64        /* chunks of <= 64 symbols are staged through LDS for output   */
-#define DEC_OUT_STRIDE 72      /* bytes per lane: 64 + 8 pad -> conflict-free ds_write_b64      */
+#define DEC_OUT_STRIDE 72      /* bytes per lane: 64 + 8 pad (overshoot room), 18-dword rows  */
 
-// Word readers: next() returns the following stream word (byte-swapped to MSB-first).
-// They read one word ahead so the refill's data is in a register before it is needed.
-// nx = the next word to enter the window, p = the word after it.
-struct LdsWords {   // LDS: read unconditionally every step (cheap), keep it only when taken
+// table entry (dc_gpu.h): sym0 | bits(all)<<8 | sym1<<16 | bits(sym0)<<24 | count<<29
+#define E_BITS(e) (((e) >> 8) & 255u)
+#define E_BITS0(e) (((e) >> 24) & 31u)
+#define E_COUNT(e) (((e) >> 29) & 3u)
+
+struct DecLds {
+    uint32_t lut[1 << DC_LUT_BITS];   // first: its addresses fit the ds_read offset field
+    uint32_t first[DC_MAX_DIGITS + 1], count[DC_MAX_DIGITS + 1], start[DC_MAX_DIGITS + 1];
+    uint16_t syms[DC_MAX_SYMS];
+    __attribute__((aligned(16))) uint32_t stage[DEC_WAVES][DEC_STAGE_WORDS];
+    __attribute__((aligned(16))) uint8_t out[DEC_WAVES][64 * DEC_OUT_STRIDE];
+};
+
+// Word readers; nx = the next word to enter the window (already MSB-first), p = the one after.
+struct LdsWords {   // staged words are byte-swapped once at staging time
     const uint32_t *p;
     uint32_t nx;
     __device__ __forceinline__ void init() { nx = *p++; }
-    __device__ __forceinline__ uint32_t peek() const { return bswap32(nx); }
-    __device__ __forceinline__ void advance(bool take)
+    __device__ __forceinline__ uint32_t peek() const { return nx; }
+    __device__ __forceinline__ void advance(bool take)   // LDS read every step, kept when taken
     {
         const uint32_t v = *p;
         nx = take ? v : nx;
@@ -612,74 +623,80 @@ struct LdsWords {   // LDS: read unconditionally every step (cheap), keep it onl
     }
 };
 
-struct HbmWords {   // HBM fallback: read only when a word is taken
+struct HbmWords {   // HBM fallback: byte-swap on read, read only when a word is taken
     const uint32_t *p;
     uint32_t nx;
-    __device__ __forceinline__ void init() { nx = *p++; }
-    __device__ __forceinline__ uint32_t peek() const { return bswap32(nx); }
+    __device__ __forceinline__ void init() { nx = bswap32(*p++); }
+    __device__ __forceinline__ uint32_t peek() const { return nx; }
     __device__ __forceinline__ void advance(bool take)
     {
-        if (take) { nx = *p; ++p; }
+        if (take) { nx = bswap32(*p); ++p; }
     }
 };
 
-// slow path for windows the two-symbol table does not cover (codes longer than 12 bits)
-// returns a table-format entry; bit 31 flags an invalid code
-static __device__ __forceinline__ uint32_t decode_long(uint64_t win, const uint32_t *s_first, const uint32_t *s_count,
-                                                       const uint32_t *s_start, const uint16_t *s_syms,
-                                                       const dc_dtable *__restrict__ T, int nary, int w, bool pow2)
+// slow path for windows the two-symbol table does not cover (codes longer than 12 bits);
+// returns a one-symbol table entry, bit 31 set for an invalid code
+static __device__ __forceinline__ uint32_t decode_long(uint64_t win, const DecLds &L, const dc_dtable *__restrict__ T,
+                                                       int nary, int w, bool pow2)
 {
-    uint32_t bad = 0;
-    uint32_t sym = 0, nbt;
+    uint32_t bad = 0, sym = 0, nbt;
     if (pow2) {
         // smallest bit length b > 12 whose left-justified canonical limit exceeds the window
         const uint64_t top = win >> 32;
         uint32_t b = DC_LUT_BITS + 1;
         for (int bb = DC_LUT_BITS + 1; bb <= 32; ++bb) b += (top >= T->lim[bb]) ? 1u : 0u;
         if (b > 32) { bad = 1; b = 32; }
-        const uint32_t L = b / (uint32_t)w;
+        const uint32_t Ld = b / (uint32_t)w;
         const uint32_t v = (uint32_t)(top >> (32 - b));
-        sym = s_syms[(s_start[L] + (v - s_first[L])) & (DC_MAX_SYMS - 1)];
+        sym = L.syms[(L.start[Ld] + (v - L.first[Ld])) & (DC_MAX_SYMS - 1)];
         nbt = b;
     } else {
         uint64_t x = win;
         uint32_t v = 0;
-        int L = 0;
+        int Ld = 0;
         nbt = (uint32_t)w;
         while (true) {
             const uint32_t digit = (uint32_t)(x >> (64 - w));
             x <<= w;
             v = v * (uint32_t)nary + digit;
-            ++L;
-            if (L * w > 32 || L > DC_MAX_DIGITS) { bad = 1; break; }
-            if (s_count[L] && v - s_first[L] < s_count[L]) {
-                sym = s_syms[s_start[L] + (v - s_first[L])];
-                nbt = (uint32_t)(L * w);
+            ++Ld;
+            if (Ld * w > 32 || Ld > DC_MAX_DIGITS) { bad = 1; break; }
+            if (L.count[Ld] && v - L.first[Ld] < L.count[Ld]) {
+                sym = L.syms[L.start[Ld] + (v - L.first[Ld])];
+                nbt = (uint32_t)(Ld * w);
                 break;
             }
         }
     }
-    return (sym & 255u) | (nbt << 16) | (nbt << 21) | (bad << 31);
+    return (sym & 255u) | (nbt << 8) | (nbt << 24) | (1u << 29) | (bad << 31);
 }
 
-// output policies: 8-byte flushes into the lane's LDS row, or straight to HBM
-struct LdsOut {
-    uint8_t *o;
-    __device__ __forceinline__ void put8(uint64_t v) { *reinterpret_cast<uint64_t *>(o) = v; o += 8; }
-    __device__ __forceinline__ void put1(uint32_t k, uint8_t v) { o[k] = v; }
-};
-struct HbmOut {
-    uint8_t *o;
-    __device__ __forceinline__ void put8(uint64_t v) { *reinterpret_cast<uint64_t *>(o) = v; o += 8; }
-    __device__ __forceinline__ void put1(uint32_t k, uint8_t v) { o[k] = v; }
-};
+// One lookup step: refill (branch-free), table lookup, slow path for long codes.
+template <class R>
+static __device__ __forceinline__ uint32_t decode_step(R &rd, uint64_t &win, int &wbits, const DecLds &L,
+                                                       const dc_dtable *__restrict__ T, int nary, int w, bool pow2,
+                                                       int &bad)
+{
+    const bool need = wbits < 32;
+    const uint64_t add = ((uint64_t)rd.peek() << 32) >> (need ? wbits : 0);
+    win |= need ? add : 0ull;
+    wbits += need ? 32 : 0;
+    rd.advance(need);
+    uint32_t e = L.lut[win >> (64 - DC_LUT_BITS)];
+    if (__builtin_expect(__any(e == 0), 0)) {
+        if (e == 0) {
+            e = decode_long(win, L, T, nary, w, pow2);
+            bad |= (int)(e >> 31);
+        }
+    }
+    return e;
+}
 
-template <class R, class W>
-static __device__ __forceinline__ void decode_chunk(R rd, uint32_t sh, uint32_t cnt, W o,
-                                                    const uint32_t *s_lut, const uint32_t *s_first,
-                                                    const uint32_t *s_count, const uint32_t *s_start,
-                                                    const uint16_t *s_syms, const dc_dtable *__restrict__ T,
-                                                    int nary, int w, bool pow2, int &bad)
+// decode into the lane's LDS row; the last step may write one byte past cnt (row padding)
+template <class R>
+static __device__ __forceinline__ void decode_chunk_lds(R rd, uint32_t sh, uint32_t cnt, uint8_t *row,
+                                                        const DecLds &L, const dc_dtable *__restrict__ T, int nary,
+                                                        int w, bool pow2, int &bad)
 {
     rd.init();
     const uint32_t hi = rd.peek();
@@ -688,40 +705,40 @@ static __device__ __forceinline__ void decode_chunk(R rd, uint32_t sh, uint32_t 
     rd.advance(true);
     uint64_t win = (((uint64_t)hi << 32) | lo) << sh;
     int wbits = 64 - (int)sh;
-    uint64_t acc = 0;     // decoded bytes not yet stored (little-endian = output order)
-    uint32_t na = 0;      // bytes in acc (< 8)
-    uint32_t rem = cnt;   // symbols still to decode
-    while (rem) {
-        // branch-free refill: a word enters the window when fewer than 32 bits remain
-        const bool need = wbits < 32;
-        const uint64_t add = (uint64_t)rd.peek() << (32 - (need ? wbits : 32));
-        win |= need ? add : 0ull;
-        wbits += need ? 32 : 0;
-        rd.advance(need);
-        uint32_t e = s_lut[win >> (64 - DC_LUT_BITS)];
-        if (__builtin_expect(__any(e == 0), 0)) {
-            if (e == 0) {
-                e = decode_long(win, s_first, s_count, s_start, s_syms, T, nary, w, pow2);
-                bad |= (int)(e >> 31);
-            }
-        }
-        // two symbols when the table found two and both are still wanted
-        const bool two = ((e >> 26) & 1u) && rem >= 2;
-        const uint32_t nbt = two ? ((e >> 16) & 31u) : ((e >> 21) & 31u);
-        const uint32_t syms = two ? (e & 0xFFFFu) : (e & 0xFFu);
-        const uint32_t ns = two ? 2u : 1u;
+    for (uint32_t pos = 0; pos < cnt;) {
+        const uint32_t e = decode_step(rd, win, wbits, L, T, nary, w, pow2, bad);
+        row[pos] = (uint8_t)e;
+        row[pos + 1] = (uint8_t)(e >> 16);   // sym1, or a byte the next step overwrites
+        const uint32_t nbt = E_BITS(e);
         win <<= nbt;
         wbits -= (int)nbt;
-        rem -= ns;
-        acc |= (uint64_t)syms << (8 * na);
-        na += ns;
-        if (na >= 8) {
-            o.put8(acc);
-            na -= 8;
-            acc = na ? (uint64_t)(syms >> 8) : 0ull;   // the second symbol spilled past byte 7
-        }
+        pos += E_COUNT(e);
     }
-    for (uint32_t k = 0; k < na; ++k) o.put1(k, (uint8_t)(acc >> (8 * k)));
+}
+
+// exact variant writing straight to HBM (chunks of more than 64 symbols)
+template <class R>
+static __device__ __forceinline__ void decode_chunk_hbm(R rd, uint32_t sh, uint32_t cnt, uint8_t *__restrict__ o,
+                                                        const DecLds &L, const dc_dtable *__restrict__ T, int nary,
+                                                        int w, bool pow2, int &bad)
+{
+    rd.init();
+    const uint32_t hi = rd.peek();
+    rd.advance(true);
+    const uint32_t lo = rd.peek();
+    rd.advance(true);
+    uint64_t win = (((uint64_t)hi << 32) | lo) << sh;
+    int wbits = 64 - (int)sh;
+    for (uint32_t pos = 0; pos < cnt;) {
+        const uint32_t e = decode_step(rd, win, wbits, L, T, nary, w, pow2, bad);
+        const bool two = E_COUNT(e) == 2 && pos + 1 < cnt;
+        o[pos] = (uint8_t)e;
+        if (two) o[pos + 1] = (uint8_t)(e >> 16);
+        const uint32_t nbt = two ? E_BITS(e) : E_BITS0(e);
+        win <<= nbt;
+        wbits -= (int)nbt;
+        pos += two ? 2 : 1;
+    }
 }
 
 __global__ __launch_bounds__(DEC_WAVES * 64) void k_huff_decode(const uint32_t *__restrict__ in, uint64_t bit_base,
@@ -730,20 +747,16 @@ __global__ __launch_bounds__(DEC_WAVES * 64) void k_huff_decode(const uint32_t *
                                                      uint64_t n, const dc_dtable *__restrict__ T,
                                                      uint8_t *__restrict__ out, int *__restrict__ err)
 {
-    __shared__ __attribute__((aligned(16))) uint32_t s_lut[1 << DC_LUT_BITS];
-    __shared__ uint32_t s_first[DC_MAX_DIGITS + 1], s_count[DC_MAX_DIGITS + 1], s_start[DC_MAX_DIGITS + 1];
-    __shared__ uint16_t s_syms[DC_MAX_SYMS];
-    __shared__ __attribute__((aligned(16))) uint32_t s_stage[DEC_WAVES][DEC_STAGE_WORDS];
-    __shared__ __attribute__((aligned(16))) uint8_t s_out[DEC_WAVES][64 * DEC_OUT_STRIDE];
+    __shared__ DecLds L;
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     {
         const uint4 *src = reinterpret_cast<const uint4 *>(T->lut);
-        uint4 *dst = reinterpret_cast<uint4 *>(s_lut);
+        uint4 *dst = reinterpret_cast<uint4 *>(L.lut);
         for (int i = t; i < (1 << DC_LUT_BITS) / 4; i += DEC_WAVES * 64) dst[i] = src[i];
-        for (int L = t; L <= DC_MAX_DIGITS; L += DEC_WAVES * 64) {
-            s_first[L] = T->first[L]; s_count[L] = T->count[L]; s_start[L] = T->start[L];
+        for (int k = t; k <= DC_MAX_DIGITS; k += DEC_WAVES * 64) {
+            L.first[k] = T->first[k]; L.count[k] = T->count[k]; L.start[k] = T->start[k];
         }
-        for (int i = t; i < DC_MAX_SYMS; i += DEC_WAVES * 64) s_syms[i] = T->syms[i];
+        for (int i = t; i < DC_MAX_SYMS; i += DEC_WAVES * 64) L.syms[i] = T->syms[i];
     }
     const int nary = T->n_ary, w = T->w;
     const bool pow2 = (nary & (nary - 1)) == 0;
@@ -752,8 +765,8 @@ __global__ __launch_bounds__(DEC_WAVES * 64) void k_huff_decode(const uint32_t *
     const uint64_t nchunks = (n + S - 1) / S;
     const uint64_t ngroups = (nchunks + DC_SYNC_GROUP - 1) / DC_SYNC_GROUP;
     const uint64_t word_base = bit_base >> 5;
-    uint32_t *stage = s_stage[wv];
-    uint8_t *ostage = s_out[wv];
+    uint32_t *stage = L.stage[wv];
+    uint8_t *ostage = L.out[wv];
     const bool stage_out = S <= DEC_OUT_SYMS;
     int bad = 0;
     for (uint64_t g = (uint64_t)blockIdx.x * DEC_WAVES + wv; g < ngroups; g += (uint64_t)gridDim.x * DEC_WAVES) {
@@ -775,43 +788,36 @@ __global__ __launch_bounds__(DEC_WAVES * 64) void k_huff_decode(const uint32_t *
         const uint64_t sym0 = c * S;
         const uint32_t cnt = valid ? (uint32_t)((n - sym0 < S) ? (n - sym0) : S) : 0u;
         const uint32_t pos = lead + off;                           // lane start, bits into staging
-        if (nwords + 1 <= DEC_STAGE_WORDS) {   // +1: the readers peek one word ahead
+        uint8_t *row = ostage + lane * DEC_OUT_STRIDE;
+        if (nwords + 1 <= DEC_STAGE_WORDS) {   // +1: the reader peeks one word ahead
             const uint4 *src = reinterpret_cast<const uint4 *>(in + w0);
             uint4 *dst = reinterpret_cast<uint4 *>(stage);
             const uint32_t nvec = (nwords + 4) / 4;
             // all loads in flight (named registers; indices clamped rather than loads
-            // predicated, which made hipcc emit serialised flat loads), then the LDS writes
-            static_assert((DEC_STAGE_WORDS / 4 + 63) / 64 <= 7, "stage larger than 7 KiB");
+            // predicated, which made hipcc emit serialised flat loads), then byte-swapped
+            // LDS writes
+            static_assert((DEC_STAGE_WORDS / 4 + 63) / 64 <= 5, "stage larger than 5 KiB");
             const uint32_t i0 = lane, i1 = lane + 64, i2 = lane + 128, i3 = lane + 192, i4 = lane + 256,
-                           i5 = lane + 320, i6 = lane + 384, last = nvec - 1;
+                           last = nvec - 1;
             const uint4 v0 = src[min(i0, last)], v1 = src[min(i1, last)], v2 = src[min(i2, last)],
-                        v3 = src[min(i3, last)], v4 = src[min(i4, last)], v5 = src[min(i5, last)],
-                        v6 = src[min(i6, last)];
-            if (i0 < nvec) dst[i0] = v0;
-            if (i1 < nvec) dst[i1] = v1;
-            if (i2 < nvec) dst[i2] = v2;
-            if (i3 < nvec) dst[i3] = v3;
-            if (i4 < nvec) dst[i4] = v4;
-            if (i5 < nvec) dst[i5] = v5;
-            if (i6 < nvec) dst[i6] = v6;
+                        v3 = src[min(i3, last)], v4 = src[min(i4, last)];
+#define DC_SWZ(v) make_uint4(bswap32(v.x), bswap32(v.y), bswap32(v.z), bswap32(v.w))
+            if (i0 < nvec) dst[i0] = DC_SWZ(v0);
+            if (i1 < nvec) dst[i1] = DC_SWZ(v1);
+            if (i2 < nvec) dst[i2] = DC_SWZ(v2);
+            if (i3 < nvec) dst[i3] = DC_SWZ(v3);
+            if (i4 < nvec) dst[i4] = DC_SWZ(v4);
+#undef DC_SWZ
             __builtin_amdgcn_wave_barrier();
             if (valid) {
                 LdsWords rd{stage + (pos >> 5), 0u};
-                if (stage_out)
-                    decode_chunk(rd, pos & 31, cnt, LdsOut{ostage + lane * DEC_OUT_STRIDE}, s_lut, s_first, s_count,
-                                 s_start, s_syms, T, nary, w, pow2, bad);
-                else
-                    decode_chunk(rd, pos & 31, cnt, HbmOut{out + sym0}, s_lut, s_first, s_count, s_start, s_syms,
-                                 T, nary, w, pow2, bad);
+                if (stage_out) decode_chunk_lds(rd, pos & 31, cnt, row, L, T, nary, w, pow2, bad);
+                else decode_chunk_hbm(rd, pos & 31, cnt, out + sym0, L, T, nary, w, pow2, bad);
             }
         } else if (valid) {
             HbmWords rd{in + w0 + (pos >> 5), 0u};
-            if (stage_out)
-                decode_chunk(rd, pos & 31, cnt, LdsOut{ostage + lane * DEC_OUT_STRIDE}, s_lut, s_first, s_count,
-                             s_start, s_syms, T, nary, w, pow2, bad);
-            else
-                decode_chunk(rd, pos & 31, cnt, HbmOut{out + sym0}, s_lut, s_first, s_count, s_start, s_syms, T,
-                             nary, w, pow2, bad);
+            if (stage_out) decode_chunk_lds(rd, pos & 31, cnt, row, L, T, nary, w, pow2, bad);
+            else decode_chunk_hbm(rd, pos & 31, cnt, out + sym0, L, T, nary, w, pow2, bad);
         }
         if (stage_out) {
             // the group's 64 chunks are one contiguous output range: coalesced 16-B stores,

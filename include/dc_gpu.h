@@ -48,8 +48,8 @@ typedef struct dc_ctx dc_ctx;
 typedef struct dc_dtable {
     uint32_t code[256];             /* packed MSB-first code bits of byte s           */
     uint32_t nbits[256];            /* its bit length (0: byte has no code)           */
-    uint32_t lut[1 << DC_LUT_BITS]; /* next 12 bits -> sym0 | sym1<<8 | bits(both)<<16 |
-                                       bits(sym0)<<21 | two<<26 ; 0 = code > 12 bits   */
+    uint32_t lut[1 << DC_LUT_BITS]; /* next 12 bits -> sym0 | bits(all)<<8 | sym1<<16 |
+                                       bits(sym0)<<24 | count(1|2)<<29; 0: code > 12 b */
     uint32_t first[DC_MAX_DIGITS + 1]; /* canonical first value per digit length      */
     uint32_t count[DC_MAX_DIGITS + 1];
     uint32_t start[DC_MAX_DIGITS + 1];
