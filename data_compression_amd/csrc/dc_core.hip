@@ -457,6 +457,8 @@ __global__ void k_zero_bounds(const uint64_t *__restrict__ off, uint64_t nblocks
 // ------------------------------------------------------------------------------------
 #define PACK_TILE 4096
 #define PACK_STAGE (PACK_TILE + 64)
+#define PACK_BLK_WORDS 9216     /* 36 KiB: a full block of <= 9 bits/symbol is staged whole  */
+#define PACK_PIECES (DC_BLOCK_BYTES / PACK_TILE)
 
 __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ in, uint64_t n,
                                                    const dc_dtable *__restrict__ T,
@@ -467,8 +469,9 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
                                                    const int *__restrict__ err)
 {
     __shared__ uint2 s_tab[256];
-    __shared__ uint32_t s_stage[PACK_STAGE];
+    __shared__ __attribute__((aligned(16))) uint32_t s_stage[PACK_BLK_WORDS];
     __shared__ uint32_t s_scan[4];
+    __shared__ uint32_t s_tot[PACK_PIECES][4];
     const int t = threadIdx.x;
     // device-side guards (no host round trip): a byte without a code (plan error) or an
     // output buffer smaller than the planned stream -> write nothing
@@ -491,6 +494,94 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
 #pragma unroll
             for (int k = 0; k < (int)(DC_BLOCK_BYTES / PACK_TILE); ++k)
                 blkv[k] = *reinterpret_cast<const uint4 *>(in + blk_start + (uint64_t)k * PACK_TILE + (uint64_t)t * 16);
+        }
+        const uint32_t nw_blk = (uint32_t)(((blk_abs & 31) + (block_off[b + 1] - block_off[b]) + 31) >> 5);
+        if (full && nw_blk <= PACK_BLK_WORDS) {
+            // ---- fast path: the whole block at once, 3 barriers ----
+            // lane t of wave w codes piece k = bytes [k*4096 + t*16, +16) of the block
+            const int lane = t & 63, wid = t >> 6;
+            for (uint32_t i = 4u * t; i < nw_blk; i += 1024u)
+                *reinterpret_cast<uint4 *>(&s_stage[i]) = make_uint4(0u, 0u, 0u, 0u);
+            uint32_t Tk[PACK_PIECES], Ik[PACK_PIECES];
+#pragma unroll
+            for (int k = 0; k < PACK_PIECES; ++k) {
+                const uint32_t w4[4] = {blkv[k].x, blkv[k].y, blkv[k].z, blkv[k].w};
+                uint32_t s = 0;
+#pragma unroll
+                for (int i = 0; i < 16; ++i) s += s_tab[(w4[i >> 2] >> (8 * (i & 3))) & 255u].y;
+                Tk[k] = s;
+                Ik[k] = s;
+                __builtin_amdgcn_sched_barrier(0);
+            }
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+#pragma unroll
+                for (int k = 0; k < PACK_PIECES; ++k) {
+                    const uint32_t y = __shfl_up(Ik[k], d, 64);
+                    if (lane >= d) Ik[k] += y;
+                }
+            }
+            if (lane == 63) {
+#pragma unroll
+                for (int k = 0; k < PACK_PIECES; ++k) s_tot[k][wid] = Ik[k];
+            }
+            __syncthreads();
+            uint64_t run = blk_abs;   // absolute bit where piece k starts
+#pragma unroll
+            for (int k = 0; k < PACK_PIECES; ++k) {
+                uint32_t wo = 0, kt = 0;
+#pragma unroll
+                for (int w = 0; w < 4; ++w) {
+                    const uint32_t v = s_tot[k][w];
+                    wo += (w < wid) ? v : 0u;
+                    kt += v;
+                }
+                const uint64_t As = run + wo + (Ik[k] - Tk[k]);
+                run += kt;
+                const uint64_t p = blk_start + (uint64_t)k * PACK_TILE + (uint64_t)t * 16;
+                if (sync_len != nullptr) {
+                    uint32_t cb = Tk[k];
+                    for (uint32_t d = 1; d < (sync_syms >> 4); d <<= 1) cb += __shfl_xor(cb, (int)d, 64);
+                    if ((p & (uint64_t)(sync_syms - 1)) == 0) {
+                        sync_len[p / sync_syms] = (uint16_t)cb;
+                        if ((p & ((uint64_t)sync_syms * DC_SYNC_GROUP - 1)) == 0)
+                            sync_base[p / ((uint64_t)sync_syms * DC_SYNC_GROUP)] = As;
+                    }
+                }
+                uint32_t w4[4] = {blkv[k].x, blkv[k].y, blkv[k].z, blkv[k].w};
+                // opaque copy: stops the compiler from keeping pass A's 128 lookup addresses live
+                asm volatile("" : "+v"(w4[0]), "+v"(w4[1]), "+v"(w4[2]), "+v"(w4[3]));
+                uint64_t acc = 0;
+                uint32_t nacc = (uint32_t)(As & 31);
+                uint32_t wi = (uint32_t)((As >> 5) - blk_first_word);
+                bool first = true;
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const uint2 e = s_tab[(w4[i >> 2] >> (8 * (i & 3))) & 255u];
+                    acc = (acc << e.y) | e.x;
+                    nacc += e.y;
+                    if (nacc >= 32) {
+                        nacc -= 32;
+                        const uint32_t word = (uint32_t)(acc >> nacc);
+                        if (first) atomicOr(&s_stage[wi], word);
+                        else s_stage[wi] = word;
+                        first = false;
+                        ++wi;
+                    }
+                }
+                if (nacc > 0) atomicOr(&s_stage[wi], (uint32_t)(acc << (32 - nacc)));
+                __builtin_amdgcn_sched_barrier(0);   // keep the pieces' lookups from being hoisted
+            }
+            __syncthreads();
+            const bool end_shared = (run & 31) != 0;
+            for (uint32_t i = t; i < nw_blk; i += 256) {
+                const uint32_t v = bswap32(s_stage[i]);
+                uint32_t *dst = &out[blk_first_word + i - word_base];
+                if (i == 0 || (i == nw_blk - 1 && end_shared)) atomicOr(dst, v);
+                else *dst = v;
+            }
+            __syncthreads();
+            continue;
         }
         __syncthreads();
 #pragma unroll
