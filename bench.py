@@ -159,6 +159,7 @@ def main():
     dom_ms = float(np.mean(per[dom]))
     dom_bytes = alg.get(dom, n)
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic("k_" + dom, a, n)
 
     value = world * n / (ms_step * 1e-3) / 1e9
     res = {
@@ -179,7 +180,8 @@ def main():
                    "bytes_per_gpu": n, "n_ary": a.nary, "sync_syms": S,
                    "parallelism": f"shard{world}" if world > 1 else "single"},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK / 1e9,
-                     "unit": "GB/s", "frac": round(achieved * 1e9 / HBM_PEAK, 4), "traffic": None,
+                     "unit": "GB/s", "frac": round(achieved * 1e9 / HBM_PEAK, 4), "traffic": traffic,
+                     "traffic_source": traffic_src,
                      "alg_bytes_per_launch": dom_bytes, "mean_ms": round(dom_ms, 4)},
         "encode_GBps": round(n / (enc_ms * 1e-3) / 1e9, 2),
         "decode_GBps": round(n / (dec_ms * 1e-3) / 1e9, 2),
@@ -193,6 +195,28 @@ def main():
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def pmc_traffic(kernel, a, n):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary
+    (profiles/*_pmc_traffic.json, written by tools/pmc.sh + tools/pmc_report.py from separate
+    --pmc passes of this same bench command; FETCH_SIZE x2 per MI355X_MICROARCH.md). PMC
+    counters cannot be read inside the timed run, so the figure is the profiled run's,
+    reported only when that run's workload matches this one."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic.json")))   # rNN_ prefix: newest last
+    for f in reversed(files):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        w = d.get("workload", {})
+        if (w.get("cfg"), w.get("size"), w.get("n_ary")) != (a.cfg, n, a.nary):
+            continue
+        k = d.get("kernels", {}).get(kernel)
+        if k:
+            return k["traffic_bytes"], os.path.relpath(f, REPO)
+    return None, None
 
 
 def cpu_baseline(x, a):
