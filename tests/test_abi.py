@@ -88,3 +88,24 @@ def test_no_device_fails_loudly():
     from data_compression_amd._lib import DcError
     with pytest.raises(DcError):
         Codec()
+
+
+# ---- C callers of the drop-in (tests/c/): the headers compile as C and every symbol a
+# reference-style caller uses resolves against its one library ------------------------
+C_DRIVERS = ("huffman", "nybble")
+
+
+def build_c_driver(name, outdir):
+    import subprocess
+    lib = os.path.join(REPO, "data_compression_amd", "lib")
+    exe = os.path.join(str(outdir), f"dropin_{name}")
+    subprocess.run(["gcc", "-std=c11", "-O2", "-Wall", "-Werror", "-I", os.path.join(REPO, "include"),
+                    os.path.join(REPO, "tests", "c", f"dropin_{name}.c"), "-L", lib, f"-ldc_{name}",
+                    f"-Wl,-rpath,{lib}", "-o", exe], check=True)
+    return exe
+
+
+@pytest.mark.parametrize("name", C_DRIVERS)
+def test_c_driver_links(name, tmp_path):
+    exe = build_c_driver(name, tmp_path)
+    assert os.path.exists(exe)

@@ -300,3 +300,14 @@ def test_nybble_static_large_vs_oracle(torch_cuda):
     c = N.compress_bytestring(y, True)
     assert c == orc.nybble_compress(y, True)
     assert N.decompress_bytestring(c, True) == y
+
+
+# ---------------------------------------------------------------- C callers of the drop-in
+@pytest.mark.parametrize("name", ["huffman", "nybble"])
+def test_c_driver_runs(torch_cuda, name, tmp_path):
+    import subprocess
+    from tests.test_abi import build_c_driver
+    exe = build_c_driver(name, tmp_path)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert f"dropin_{name} ok" in r.stdout
