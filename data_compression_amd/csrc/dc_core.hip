@@ -17,6 +17,7 @@
 
 #define DC_VERSION "dc-mi355x 0.1 (gfx950)"
 #define DC_SYNC_GROUP 64
+#define DC_SYNC_GROUP_LOG 6
 
 // ------------------------------------------------------------------------------------
 // small device helpers
@@ -61,10 +62,12 @@ static __device__ __forceinline__ uint32_t wg_scan_excl_u32(uint32_t v, uint32_t
 __global__ __launch_bounds__(256) void k_hist_blocks(const uint8_t *__restrict__ in, uint64_t n,
                                                      uint64_t nblocks, uint16_t *__restrict__ bh)
 {
-    __shared__ uint32_t cnt[256 * 64];
+    __shared__ __attribute__((aligned(16))) uint32_t cnt[256 * 64];
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const uint32_t inc = 1u << (8 * wv);
-    for (int i = t; i < 256 * 64; i += 256) cnt[i] = 0u;
+    const uint32_t lane4 = 4u * (uint32_t)lane;
+    char *const cbase = reinterpret_cast<char *>(cnt);
+    for (int i = t; i < 256 * 16; i += 256) reinterpret_cast<uint4 *>(cnt)[i] = make_uint4(0u, 0u, 0u, 0u);
     __syncthreads();
     for (uint64_t b = blockIdx.x; b < nblocks; b += gridDim.x) {
         const uint64_t base = b * (uint64_t)DC_BLOCK_BYTES;
@@ -79,8 +82,12 @@ __global__ __launch_bounds__(256) void k_hist_blocks(const uint8_t *__restrict__
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
 #pragma unroll
-                    for (int q = 0; q < 4; ++q)
-                        atomicAdd(&cnt[((w4[j] >> (8 * q)) & 255u) * 64 + lane], inc);
+                    for (int q = 0; q < 4; ++q) {
+                        // byte address bin*256 + lane*4 in one v_perm_b32: byte 0 = lane*4,
+                        // byte 1 = byte q of the input word, bytes 2-3 = 0
+                        const uint32_t addr = __builtin_amdgcn_perm(w4[j], lane4, 0x0c0c0000u | ((4u + q) << 8));
+                        atomicAdd(reinterpret_cast<uint32_t *>(cbase + addr), inc);
+                    }
                 }
             }
         } else {
@@ -88,15 +95,21 @@ __global__ __launch_bounds__(256) void k_hist_blocks(const uint8_t *__restrict__
             for (uint64_t i = base + t; i < end; i += 256) atomicAdd(&cnt[in[i] * 64 + lane], inc);
         }
         __syncthreads();
+        // bin t: its 64 lane columns (16-B reads, rotated so a wave's reads spread over all
+        // banks); v_dot4_u32_u8 with 0x01010101 adds the four wave counters of a dword
+        uint4 *row = reinterpret_cast<uint4 *>(&cnt[t * 64]);
         uint32_t acc = 0;
-#pragma unroll 8
-        for (int j = 0; j < 64; ++j) {
-            const int idx = t * 64 + ((j + t) & 63);
-            const uint32_t d = cnt[idx];
-            cnt[idx] = 0u;
-            acc += (d & 0x00FF00FFu) + ((d >> 8) & 0x00FF00FFu);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int c = (k + t) & 15;
+            const uint4 d = row[c];
+            row[c] = make_uint4(0u, 0u, 0u, 0u);
+            acc = __builtin_amdgcn_udot4(d.x, 0x01010101u, acc, false);
+            acc = __builtin_amdgcn_udot4(d.y, 0x01010101u, acc, false);
+            acc = __builtin_amdgcn_udot4(d.z, 0x01010101u, acc, false);
+            acc = __builtin_amdgcn_udot4(d.w, 0x01010101u, acc, false);
         }
-        bh[b * 256 + t] = (uint16_t)((acc & 0xFFFFu) + (acc >> 16));
+        bh[b * 256 + t] = (uint16_t)acc;
         __syncthreads();
     }
 }
@@ -478,6 +491,7 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
     if (err[0] != 0 || ((bit_base & 31) + block_off[nblocks] + 31) / 32 > words_cap) return;
     s_tab[t] = make_uint2(T->code[t], T->nbits[t]);
     const uint64_t word_base = bit_base >> 5;
+    const uint32_t slog = sync_syms ? (uint32_t)__builtin_ctz(sync_syms) : 0u;   // S is a power of two
     __syncthreads();
 
     for (uint64_t b = blockIdx.x; b < nblocks; b += gridDim.x) {
@@ -543,9 +557,9 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
                     uint32_t cb = Tk[k];
                     for (uint32_t d = 1; d < (sync_syms >> 4); d <<= 1) cb += __shfl_xor(cb, (int)d, 64);
                     if ((p & (uint64_t)(sync_syms - 1)) == 0) {
-                        sync_len[p / sync_syms] = (uint16_t)cb;
+                        sync_len[p >> slog] = (uint16_t)cb;
                         if ((p & ((uint64_t)sync_syms * DC_SYNC_GROUP - 1)) == 0)
-                            sync_base[p / ((uint64_t)sync_syms * DC_SYNC_GROUP)] = As;
+                            sync_base[p >> (slog + DC_SYNC_GROUP_LOG)] = As;
                     }
                 }
                 uint32_t w4[4] = {blkv[k].x, blkv[k].y, blkv[k].z, blkv[k].w};
@@ -573,13 +587,13 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
                 __builtin_amdgcn_sched_barrier(0);   // keep the pieces' lookups from being hoisted
             }
             __syncthreads();
-            const bool end_shared = (run & 31) != 0;
-            for (uint32_t i = t; i < nw_blk; i += 256) {
-                const uint32_t v = bswap32(s_stage[i]);
-                uint32_t *dst = &out[blk_first_word + i - word_base];
-                if (i == 0 || (i == nw_blk - 1 && end_shared)) atomicOr(dst, v);
-                else *dst = v;
-            }
+            // words 0 and (when the next block starts inside it) nw_blk-1 are shared with the
+            // neighbour blocks: OR-ed by one lane each; the rest are plain coalesced stores
+            const uint32_t last_plain = ((run & 31) != 0) ? nw_blk - 1 : nw_blk;
+            uint32_t *dst = out + (blk_first_word - word_base);
+            for (uint32_t i = t + 1; i < last_plain; i += 256) dst[i] = bswap32(s_stage[i]);
+            if (t == 0) atomicOr(&dst[0], bswap32(s_stage[0]));
+            if (t == 64 && last_plain < nw_blk && nw_blk > 1) atomicOr(&dst[nw_blk - 1], bswap32(s_stage[nw_blk - 1]));
             __syncthreads();
             continue;
         }
@@ -615,9 +629,9 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
                 uint32_t cb = T_bits;
                 for (uint32_t d = 1; d < (sync_syms >> 4); d <<= 1) cb += __shfl_xor(cb, (int)d, 64);
                 if (cnt > 0 && (p & (uint64_t)(sync_syms - 1)) == 0) {
-                    sync_len[p / sync_syms] = (uint16_t)cb;
+                    sync_len[p >> slog] = (uint16_t)cb;
                     if ((p & ((uint64_t)sync_syms * DC_SYNC_GROUP - 1)) == 0)
-                        sync_base[p / ((uint64_t)sync_syms * DC_SYNC_GROUP)] = As;
+                        sync_base[p >> (slog + DC_SYNC_GROUP_LOG)] = As;
                 }
             }
             const uint32_t ws = (uint32_t)((As >> 5) - TB);
@@ -853,7 +867,8 @@ __global__ __launch_bounds__(DEC_WAVES * 64) void k_huff_decode(const uint32_t *
     const bool pow2 = (nary & (nary - 1)) == 0;
     __syncthreads();
 
-    const uint64_t nchunks = (n + S - 1) / S;
+    const uint32_t slog = (uint32_t)__builtin_ctz(S);   // S is a power of two (checked by the host)
+    const uint64_t nchunks = (n + S - 1) >> slog;
     const uint64_t ngroups = (nchunks + DC_SYNC_GROUP - 1) / DC_SYNC_GROUP;
     const uint64_t word_base = bit_base >> 5;
     uint32_t *stage = L.stage[wv];
@@ -916,16 +931,16 @@ __global__ __launch_bounds__(DEC_WAVES * 64) void k_huff_decode(const uint32_t *
             __builtin_amdgcn_wave_barrier();
             const uint64_t gbase = g * DC_SYNC_GROUP * (uint64_t)S;
             const uint64_t gbytes = (n - gbase < DC_SYNC_GROUP * (uint64_t)S) ? n - gbase : DC_SYNC_GROUP * (uint64_t)S;
-            const uint32_t pieces_per_row = S / 16;
+            const uint32_t ppr_log = (uint32_t)__builtin_ctz(S) - 4;   // 16-B pieces per row, S power of two
             for (uint32_t j = lane; j < (uint32_t)(gbytes / 16); j += 64) {
-                const uint32_t r = j / pieces_per_row, q = j % pieces_per_row;
+                const uint32_t r = j >> ppr_log, q = j & ((1u << ppr_log) - 1);
                 const uint64_t *src = reinterpret_cast<const uint64_t *>(ostage + r * DEC_OUT_STRIDE + q * 16);
                 const uint64_t a = src[0], b = src[1];
                 *reinterpret_cast<uint4 *>(out + gbase + (uint64_t)j * 16) =
                     make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
             }
             for (uint32_t k = (uint32_t)(gbytes & ~15ull) + lane; k < (uint32_t)gbytes; k += 64)
-                out[gbase + k] = ostage[(k / S) * DEC_OUT_STRIDE + (k % S)];
+                out[gbase + k] = ostage[(k >> slog) * DEC_OUT_STRIDE + (k & (S - 1))];
         }
         __builtin_amdgcn_wave_barrier();   // staging areas reused by the next group
     }
