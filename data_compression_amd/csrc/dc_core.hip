@@ -947,6 +947,296 @@ __global__ __launch_bounds__(DEC_WAVES * 64) void k_huff_decode(const uint32_t *
     if (bad) atomicOr(err, 1);
 }
 
+// ------------------------------------------------------------------------------------
+// (H8) decode, fast path for the default sync granularity S = 64 (k_huff_decode8).
+// Same stream, same sync index, same output as k_huff_decode; built for ILP instead of
+// per-step latency:
+//  * staged words are bit-reversed within each byte (bfrev(bswap(w))), which turns the
+//    MSB-first stream into an LSB-first one: stream bits [c, c+64) are two v_alignbit of
+//    three consecutive words at c>>5, so a refill has no state but c;
+//  * a lane decodes exactly 64 symbols per chunk, so every loop is fully unrolled with a
+//    fixed trip count: no divergence, no loop control, and the output byte of symbol k
+//    lands in register k/4 (v_perm); the lane's 64 output bytes stay in registers;
+//  * batches of 4 symbols share one 64-bit window; a symbol is one v_lshrrev_b64, a
+//    12-bit index and one 16-bit LUT read (len | sym << 8);
+//  * two chains per lane (groups 2p and 2p+1) are interleaved symbol by symbol for ILP;
+//  * codes of 13..12+K bits (K <= 8): the first-level entry names a second-level table
+//    indexed by the next K bits (rare, wave-uniform branch per symbol pair); anything
+//    rarer (longer codes, a batch whose codes overflow the 64-bit window, invalid codes)
+//    makes the wave redo its two chunks exactly (d8_chunk_hbm).
+// Partial groups and groups whose span exceeds the stage also go through d8_chunk_hbm.
+// ------------------------------------------------------------------------------------
+#define D8_WAVES 16
+#define D8_STAGE_WORDS 1088    /* per chain: 4352 B = 4096 symbols at <= 8.4 bits/symbol   */
+#define D8_L2_CAP 7168         /* second-level entries (u16)                               */
+#define D8_K_MAX 8
+
+struct Dec8Lds {
+    uint16_t lut[1 << DC_LUT_BITS];   // LSB-first 12-bit window -> len | sym << 8; len 0: sub-table id << 8
+    uint16_t lut2[D8_L2_CAP];         // [sub][K bits] -> len | sym << 8; 0: longer than 12+K bits / invalid
+    uint32_t scan[D8_WAVES];
+    uint16_t esc_pre[256];            // first-level index of escape prefix #id
+    __attribute__((aligned(16))) uint32_t stage[D8_WAVES][2][D8_STAGE_WORDS];
+    uint32_t tail_pad[64];   // a corrupt stream's windows may run past the last stage
+};
+
+static __device__ __forceinline__ uint32_t brev8(uint32_t v) { return __builtin_bitreverse32(__builtin_bswap32(v)); }
+
+// exact slow decode of the code at the start of an LSB-first 64-bit window (lo, hi):
+// returns nbits | sym << 8; an invalid code sets *bad and returns 0
+static __device__ uint32_t d8_long(uint32_t lo, uint32_t hi, const dc_dtable *__restrict__ T, int nary, int w,
+                                   bool pow2, int *bad)
+{
+    const uint64_t win = ((uint64_t)__builtin_bitreverse32(lo) << 32) | __builtin_bitreverse32(hi);   // MSB-first
+    if (pow2) {
+        const uint64_t top = win >> 32;
+        uint32_t b = 1;
+        while (b <= 32 && top >= T->lim[b]) ++b;
+        if (b > 32) { *bad = 1; return 0u; }
+        const uint32_t Ld = b / (uint32_t)w;
+        const uint32_t v = (uint32_t)(top >> (32 - b));
+        return b | ((T->syms[(T->start[Ld] + (v - T->first[Ld])) & (DC_MAX_SYMS - 1)] & 255u) << 8);
+    }
+    uint64_t x = win;
+    uint32_t v = 0;
+    for (int Ld = 1; Ld <= DC_MAX_DIGITS && Ld * w <= 32; ++Ld) {
+        v = v * (uint32_t)nary + (uint32_t)(x >> (64 - w));
+        x <<= w;
+        const uint32_t cnt = T->count[Ld];
+        if (cnt && v - T->first[Ld] < cnt) return (uint32_t)(Ld * w) | ((T->syms[T->start[Ld] + (v - T->first[Ld])] & 255u) << 8);
+    }
+    *bad = 1;
+    return 0u;
+}
+
+// any chunk, any count, exact: words read from HBM (MSB-first bytes; reads clamped to the
+// nwords of the buffer), bytes written one by one
+static __device__ void d8_chunk_hbm(const uint32_t *__restrict__ in, uint64_t nwords, uint64_t pos, uint32_t cnt,
+                                    uint8_t *__restrict__ o, const dc_dtable *__restrict__ T, int nary, int w,
+                                    bool pow2, int &bad)
+{
+    for (uint32_t i = 0; i < cnt; ++i) {
+        const uint64_t a = pos >> 5;
+        if (a >= nwords) { bad = 1; return; }
+        const uint32_t s = (uint32_t)pos & 31u;
+        const uint32_t w0 = brev8(in[a]), w1 = brev8(in[min(a + 1, nwords - 1)]), w2 = brev8(in[min(a + 2, nwords - 1)]);
+        const uint32_t e = d8_long(__builtin_amdgcn_alignbit(w1, w0, s), __builtin_amdgcn_alignbit(w2, w1, s), T, nary,
+                                   w, pow2, &bad);
+        if (e == 0) return;   // invalid code: stop this chunk (status reported)
+        o[i] = (uint8_t)(e >> 8);
+        pos += e & 255u;
+    }
+}
+
+struct D8Tabs {
+    const uint16_t *lut, *lut2;
+    uint32_t K, kmask;   // wave-uniform
+};
+
+// second level for an escape entry e of the symbol at window offset off (k = index in the
+// batch): returns the final entry; sets giveup when the code is not resolvable here
+static __device__ __forceinline__ uint32_t d8_esc(uint32_t e, uint32_t x, uint32_t off, int k, const D8Tabs &tb,
+                                                  int &giveup)
+{
+    if ((e & 255u) == 0) {
+        uint32_t e2 = 0;
+        if (tb.K) e2 = tb.lut2[((e >> 8) << tb.K) | ((x >> DC_LUT_BITS) & tb.kmask)];
+        if (e2 == 0 || off + (e2 & 255u) + DC_LUT_BITS * (3 - k) > 64) { giveup = 1; e2 = 1; }
+        e = e2;
+    }
+    return e;
+}
+
+// one batch (4 symbols) of both chains; returns the two output dwords
+static __device__ __forceinline__ void d8_pair(const uint32_t *sa, const uint32_t *sb, uint32_t &ca, uint32_t &cb,
+                                               uint32_t &oa, uint32_t &ob, const D8Tabs &tb, int &giveup)
+{
+    const uint32_t a0 = ca >> 5, b0 = cb >> 5;
+    const uint32_t wa0 = sa[a0], wa1 = sa[a0 + 1], wa2 = sa[a0 + 2];
+    const uint32_t wb0 = sb[b0], wb1 = sb[b0 + 1], wb2 = sb[b0 + 2];
+    const uint64_t winA = ((uint64_t)__builtin_amdgcn_alignbit(wa2, wa1, ca) << 32) | __builtin_amdgcn_alignbit(wa1, wa0, ca);
+    const uint64_t winB = ((uint64_t)__builtin_amdgcn_alignbit(wb2, wb1, cb) << 32) | __builtin_amdgcn_alignbit(wb1, wb0, cb);
+    uint32_t offA = 0, offB = 0;
+    // output byte k <- entry byte 1 (v_perm: S0 = entry bytes 4-7, S1 = output bytes 0-3)
+    constexpr uint32_t SEL[4] = {0x0c0c0c05u, 0x0c0c0500u, 0x0c050100u, 0x05020100u};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t xA = (uint32_t)(winA >> offA), xB = (uint32_t)(winB >> offB);
+        uint32_t ea = tb.lut[xA & ((1u << DC_LUT_BITS) - 1)];
+        uint32_t eb = tb.lut[xB & ((1u << DC_LUT_BITS) - 1)];
+        if (__builtin_expect(__any(min(ea & 255u, eb & 255u) == 0), 0)) {
+            ea = d8_esc(ea, xA, offA, k, tb, giveup);
+            eb = d8_esc(eb, xB, offB, k, tb, giveup);
+        }
+        oa = __builtin_amdgcn_perm(ea, k ? oa : 0u, SEL[k]);
+        ob = __builtin_amdgcn_perm(eb, k ? ob : 0u, SEL[k]);
+        offA += ea & 255u;
+        offB += eb & 255u;
+    }
+    ca += offA;
+    cb += offB;
+}
+
+// the 16 batches of a 64-symbol chunk for both chains, unrolled by template recursion;
+// every 4 batches the lane's 16 output bytes per chain are stored (uint4 at lane*64 + 16q),
+// so only 8 output registers are live
+template <int Q>
+struct D8Batches {
+    static __device__ __forceinline__ void run(const uint32_t *sa, const uint32_t *sb, uint32_t &ca, uint32_t &cb,
+                                               uint4 *da, uint4 *db, const D8Tabs &tb, int &giveup)
+    {
+        uint32_t a0, a1, a2, a3, b0, b1, b2, b3;
+        d8_pair(sa, sb, ca, cb, a0, b0, tb, giveup);
+        d8_pair(sa, sb, ca, cb, a1, b1, tb, giveup);
+        d8_pair(sa, sb, ca, cb, a2, b2, tb, giveup);
+        d8_pair(sa, sb, ca, cb, a3, b3, tb, giveup);
+        da[Q] = make_uint4(a0, a1, a2, a3);
+        db[Q] = make_uint4(b0, b1, b2, b3);
+        D8Batches<Q + 1>::run(sa, sb, ca, cb, da, db, tb, giveup);
+    }
+};
+template <>
+struct D8Batches<4> {
+    static __device__ __forceinline__ void run(const uint32_t *, const uint32_t *, uint32_t &, uint32_t &, uint4 *,
+                                               uint4 *, const D8Tabs &, int &)
+    {
+    }
+};
+
+__global__ __launch_bounds__(D8_WAVES * 64) void k_huff_decode8(const uint32_t *__restrict__ in, uint64_t bit_base,
+                                                                const uint64_t *__restrict__ sync_base,
+                                                                const uint16_t *__restrict__ sync_len, uint64_t n,
+                                                                uint64_t nwords, const dc_dtable *__restrict__ T,
+                                                                uint8_t *__restrict__ out, int *__restrict__ err)
+{
+    constexpr uint32_t S = 64, GSYM = DC_SYNC_GROUP * S;
+    constexpr int NT = D8_WAVES * 64;
+    __shared__ Dec8Lds L;
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const int nary = T->n_ary, w = T->w;
+    const bool pow2 = (nary & (nary - 1)) == 0;
+    int bad = 0;
+    // ---- tables: first level (bit-reversed index of the MSB-first table), escape
+    // prefixes numbered in index order, second level decoded exactly once per entry
+    constexpr int PER = (1 << DC_LUT_BITS) / NT;   // 4 entries per thread
+    uint32_t e1[PER];
+    uint32_t nesc = 0;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const uint32_t i = (uint32_t)(t * PER + j);
+        const uint32_t e = T->lut[__builtin_bitreverse32(i) >> (32 - DC_LUT_BITS)];
+        e1[j] = e ? (E_BITS0(e) | ((e & 255u) << 8)) : 0u;
+        nesc += e ? 0u : 1u;
+    }
+    uint32_t incl = nesc;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += y;
+    }
+    if (lane == 63) L.scan[wv] = incl;
+    __syncthreads();
+    uint32_t base = 0, E = 0;
+    for (int v = 0; v < D8_WAVES; ++v) {
+        const uint32_t s = L.scan[v];
+        base += (v < wv) ? s : 0u;
+        E += s;
+    }
+    const int maxbits = T->max_bits;
+    const uint32_t K = (uint32_t)min(max(maxbits - DC_LUT_BITS, 1), D8_K_MAX);
+    const bool l2ok = E > 0 && E <= 256 && (E << K) <= D8_L2_CAP;
+    uint32_t id = base + incl - nesc;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const uint32_t i = (uint32_t)(t * PER + j);
+        if (!e1[j] && id < 256) L.esc_pre[id] = (uint16_t)i;
+        L.lut[i] = (uint16_t)(e1[j] ? e1[j] : ((id++ & 255u) << 8));
+    }
+    __syncthreads();
+    if (l2ok) {
+        for (uint32_t q = (uint32_t)t; q < (E << K); q += NT) {
+            // the escape prefix numbered q >> K
+            const uint32_t pre = L.esc_pre[q >> K];
+            const uint32_t lo = pre | ((q & ((1u << K) - 1)) << DC_LUT_BITS);
+            int b2 = 0;
+            const uint32_t r = d8_long(lo, 0u, T, nary, w, pow2, &b2);
+            L.lut2[q] = (uint16_t)((b2 || (r & 255u) > DC_LUT_BITS + K) ? 0u : r);
+        }
+    }
+    __syncthreads();
+    D8Tabs tb{L.lut, L.lut2, l2ok ? K : 0u, (1u << K) - 1};
+
+    const uint64_t nchunks = (n + S - 1) / S;
+    const uint64_t ngroups = (nchunks + DC_SYNC_GROUP - 1) / DC_SYNC_GROUP;
+    const uint64_t npairs = (ngroups + 1) / 2;
+    const uint64_t word_base = bit_base >> 5;
+    uint32_t *stA = L.stage[wv][0], *stB = L.stage[wv][1];
+    for (uint64_t pr = (uint64_t)blockIdx.x * D8_WAVES + wv; pr < npairs; pr += (uint64_t)gridDim.x * D8_WAVES) {
+        const uint64_t gA = 2 * pr, gB = gA + 1;
+        // chunk lengths of both groups -> lane offsets (bits from each group start)
+        const uint64_t cA = gA * DC_SYNC_GROUP + lane, cB = gB * DC_SYNC_GROUP + lane;
+        const uint32_t lenA = (cA < nchunks) ? sync_len[cA] : 0u;
+        const uint32_t lenB = (cB < nchunks) ? sync_len[cB] : 0u;
+        uint32_t inA = lenA, inB = lenB;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t ya = __shfl_up(inA, d, 64), yb = __shfl_up(inB, d, 64);
+            if (lane >= d) { inA += ya; inB += yb; }
+        }
+        const uint32_t spanA = __shfl(inA, 63, 64), spanB = __shfl(inB, 63, 64);
+        const bool hasB = gB < ngroups;
+        const uint64_t relA = sync_base[gA] - (word_base << 5);
+        const uint64_t relB = hasB ? sync_base[gB] - (word_base << 5) : relA;
+        const uint64_t wA = (relA >> 5) & ~3ull, wB = (relB >> 5) & ~3ull;
+        const uint32_t leadA = (uint32_t)(relA - (wA << 5)), leadB = (uint32_t)(relB - (wB << 5));
+        const uint32_t nwA = (leadA + spanA) / 32 + 3, nwB = (leadB + spanB) / 32 + 3;
+        bool slow = !(hasB && (gB + 1) * (uint64_t)GSYM <= n && nwA + 4 <= D8_STAGE_WORDS && nwB + 4 <= D8_STAGE_WORDS &&
+                      wA + nwA + 4 <= nwords && wB + nwB + 4 <= nwords);
+        if (!slow) {
+            // stage both spans: 16-B loads (clamped, all in flight), byte-wise bit reversal
+            static_assert((D8_STAGE_WORDS / 4 + 63) / 64 <= 5, "stage larger than 5 KiB");
+            const uint4 *srcA = reinterpret_cast<const uint4 *>(in + wA);
+            const uint4 *srcB = reinterpret_cast<const uint4 *>(in + wB);
+            const uint32_t lastA = (nwA + 3) / 4 - 1, lastB = (nwB + 3) / 4 - 1;
+            uint4 va[5], vb[5];
+#pragma unroll
+            for (int k = 0; k < 5; ++k) {
+                va[k] = srcA[min((uint32_t)(lane + 64 * k), lastA)];
+                vb[k] = srcB[min((uint32_t)(lane + 64 * k), lastB)];
+            }
+#pragma unroll
+            for (int k = 0; k < 5; ++k) {
+                const uint32_t i = lane + 64 * k;
+                if (i <= lastA)
+                    reinterpret_cast<uint4 *>(stA)[i] = make_uint4(brev8(va[k].x), brev8(va[k].y), brev8(va[k].z), brev8(va[k].w));
+                if (i <= lastB)
+                    reinterpret_cast<uint4 *>(stB)[i] = make_uint4(brev8(vb[k].x), brev8(vb[k].y), brev8(vb[k].z), brev8(vb[k].w));
+            }
+            __builtin_amdgcn_wave_barrier();
+            uint32_t pa = leadA + inA - lenA, pb = leadB + inB - lenB;
+            int giveup = 0;
+            D8Batches<0>::run(stA, stB, pa, pb, reinterpret_cast<uint4 *>(out + gA * GSYM + (uint64_t)lane * S),
+                              reinterpret_cast<uint4 *>(out + gB * GSYM + (uint64_t)lane * S), tb, giveup);
+            if (__any(giveup)) slow = true;   // exact redo below overwrites the two chunks
+            __builtin_amdgcn_wave_barrier();   // stage reused by the next pair
+        }
+        if (slow) {
+            // partial groups, over-long spans, rare codes: exact per-symbol decode from HBM
+            if (cA < nchunks) {
+                const uint64_t s0 = cA * S;
+                const uint32_t cnt = (uint32_t)((n - s0 < S) ? n - s0 : S);
+                d8_chunk_hbm(in, nwords, relA + inA - lenA, cnt, out + s0, T, nary, w, pow2, bad);
+            }
+            if (hasB && cB < nchunks) {
+                const uint64_t s0 = cB * S;
+                const uint32_t cnt = (uint32_t)((n - s0 < S) ? n - s0 : S);
+                d8_chunk_hbm(in, nwords, relB + inB - lenB, cnt, out + s0, T, nary, w, pow2, bad);
+            }
+        }
+    }
+    if (bad) atomicOr(err, 1);
+}
+
 // base64url rendering of a bit range (int2digit alphabet, n_ary_huffman.c:371-378)
 __global__ void k_base64url(const uint32_t *__restrict__ words, uint64_t bit_base, uint64_t bits,
                             char *__restrict__ text)
@@ -1673,10 +1963,18 @@ int dc_huff_decode(dc_ctx *c, const uint32_t *d_words, uint64_t bit_base, uint64
     if (!sync_ok(S)) return DC_E_ARG;
     if (((uintptr_t)d_out) & 15) return DC_E_ARG;
     if (((uintptr_t)d_words) & 15) return DC_E_ARG;
-    (void)words;
     if (n == 0) return DC_OK;
+    if (words < 4) return DC_E_ARG;
     const uint64_t groups = dc_huff_sync_groups(n, S);
     HIPCHK(hipMemsetAsync(c->d_err + 1, 0, sizeof(int), c->stream));
+    if (S == 64 && !getenv("DC_DECODE_V7")) {
+        const uint64_t pairs = (groups + 1) / 2;
+        const uint64_t wgs = (pairs + D8_WAVES - 1) / D8_WAVES;
+        const uint64_t grid = wgs < 256 ? wgs : 256;   // persistent: one 16-wave workgroup per CU
+        LAUNCH(c, "huff_decode", k_huff_decode8, grid, D8_WAVES * 64, d_words, bit_base, d_sync_base, d_sync_len, n,
+               words, d_table, d_out, c->d_err + 1);
+        return DC_OK;
+    }
     const uint64_t wgs = (groups + DEC_WAVES - 1) / DEC_WAVES;
     const uint64_t grid = wgs < 256 ? wgs : 256;   // persistent: one 16-wave workgroup per CU
     LAUNCH(c, "huff_decode", k_huff_decode, grid, DEC_WAVES * 64, d_words, bit_base, d_sync_base, d_sync_len, S, n, d_table,

@@ -311,3 +311,79 @@ def test_c_driver_runs(torch_cuda, name, tmp_path):
     r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     assert f"dropin_{name} ok" in r.stdout
+
+
+# ---------------------------------------------------------------- decoder paths (S = 64)
+def _chain_stream(nsym, seed):
+    """Symbol counts 2^0 .. 2^(nsym-1): the Huffman tree is a chain, so binary code lengths
+    reach about nsym bits and codes longer than the decoder's 12 + 8 bit two-level table occur."""
+    f = [1 << i for i in range(nsym)]
+    syms = np.repeat(np.arange(1, nsym + 1, dtype=np.uint8), f)
+    rng = np.random.default_rng(seed)
+    rng.shuffle(syms)
+    return syms
+
+
+@pytest.mark.parametrize("case", ["chain16", "chain23", "enwik", "two-long-per-batch"])
+def test_decode_fast_path_rare_codes(torch_cuda, codec, case):
+    """k_huff_decode8: codes of 13..20 bits (second-level table), > 20 bits (the wave's
+    exact redo), several long codes inside one 4-symbol batch (window overflow)."""
+    torch = torch_cuda
+    from data_compression_amd import synth
+    if case == "chain16":
+        x = _chain_stream(16, 1)
+    elif case == "chain23":
+        x = _chain_stream(23, 2)
+    elif case == "enwik":
+        x = synth.enwik_like(3 << 20, seed=11)
+    else:
+        # mostly one frequent byte, with runs of rare bytes (long codes back to back)
+        rng = np.random.default_rng(4)
+        x = np.full(1 << 20, 32, np.uint8)
+        rare = rng.integers(0, x.size - 8, 3000)
+        for r in rare:
+            x[r:r + 4] = rng.integers(128, 256, 4)
+    L, el, ev, code, nb, mx = _oracle_encode(x, 2)
+    assert 0 < mx <= 32
+    payload, bits, idx = orc.huff_pack(x, code, nb, sync_syms=64)
+    xt = torch.from_numpy(x).cuda()
+    enc = codec.encode(xt, n_ary=2, sync_syms=64)
+    assert enc["bits"] == bits
+    out = torch.empty_like(xt)
+    codec.decode_into(enc, out)
+    assert codec.decode_status() == 0
+    assert np.array_equal(out.cpu().numpy(), x), case
+
+
+@pytest.mark.parametrize("n_ary", [2, 3, 16])
+def test_decode_v8_equals_v7(torch_cuda, codec, n_ary, monkeypatch):
+    """The S = 64 fast decoder and the general decoder give identical bytes."""
+    torch = torch_cuda
+    from data_compression_amd import synth
+    x = synth.log_like((2 << 20) + 12345, seed=n_ary)
+    xt = torch.from_numpy(x).cuda()
+    enc = codec.encode(xt, n_ary=n_ary, sync_syms=64)
+    a = torch.empty_like(xt)
+    codec.decode_into(enc, a)
+    assert codec.decode_status() == 0
+    monkeypatch.setenv("DC_DECODE_V7", "1")
+    b = torch.empty_like(xt)
+    codec.decode_into(enc, b)
+    assert codec.decode_status() == 0
+    assert torch.equal(a, b) and torch.equal(a, xt)
+
+
+def test_decode_corrupt_stream_reports(torch_cuda, codec):
+    """Garbage payload under a valid index: the decoder stays in bounds and flags it or
+    decodes garbage; it never faults."""
+    torch = torch_cuda
+    from data_compression_amd import synth
+    x = synth.enwik_like(1 << 20, seed=12)
+    xt = torch.from_numpy(x).cuda()
+    enc = codec.encode(xt, n_ary=3, sync_syms=64)
+    g = torch.Generator(device="cpu").manual_seed(1)
+    enc["words"].copy_(torch.randint(-2**31, 2**31 - 1, enc["words"].shape, generator=g, dtype=torch.int32).cuda())
+    out = torch.empty_like(xt)
+    codec.decode_into(enc, out)
+    codec.decode_status()   # 0 or DC_E_STREAM; it must return
+    torch.cuda.synchronize()

@@ -1,0 +1,48 @@
+"""A/B timing of decode kernels on one encoded stream (same process, interleaved rounds).
+
+    python tools/dec_ab.py [--cfg C2] [--size BYTES] [--nary 2] [--rounds 5] [--iters 10]
+Prints per-variant HIP-event mean ms of the huff_decode launch (v8 default vs DC_DECODE_V7).
+"""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from data_compression_amd import synth  # noqa: E402
+from data_compression_amd.device import Codec  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--cfg", default="C2")
+ap.add_argument("--size", type=int, default=1 << 30)
+ap.add_argument("--nary", type=int, default=2)
+ap.add_argument("--rounds", type=int, default=5)
+ap.add_argument("--iters", type=int, default=10)
+ap.add_argument("--variants", default="v8,v7")
+a = ap.parse_args()
+dev = torch.device("cuda", 0)
+x = synth.device_text(a.cfg, a.size, seed=0xC2, device=dev)
+c = Codec(0)
+enc = c.encode(x, n_ary=a.nary, sync_syms=64)
+out = torch.empty_like(x)
+res = {v: [] for v in a.variants.split(",")}
+for r in range(a.rounds):
+    for v in res:
+        if v == "v7":
+            os.environ["DC_DECODE_V7"] = "1"
+        else:
+            os.environ.pop("DC_DECODE_V7", None)
+        c.decode_into(enc, out)
+        torch.cuda.synchronize()
+        c.timing(True)
+        for _ in range(a.iters):
+            c.decode_into(enc, out)
+        kt = c.timings()
+        c.timing(False)
+        ms = [m for name, m in kt if name == "huff_decode"]
+        res[v].append(float(np.mean(ms)))
+        assert c.decode_status() == 0 and torch.equal(out, x), v
+for v, l in res.items():
+    print(f"{v}: median {np.median(l):.4f} ms  min {np.min(l):.4f}  ({a.cfg} {a.size >> 20} MiB n={a.nary})", flush=True)
