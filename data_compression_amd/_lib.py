@@ -43,6 +43,8 @@ def check(fn, rc):
 
 
 def lib_path(name: str) -> str:
+    if name == "libdc_core.so" and os.environ.get("DC_CORE_LIB"):   # diagnostic builds (tools/)
+        return os.environ["DC_CORE_LIB"]
     return os.path.join(LIBDIR, name)
 
 

@@ -959,28 +959,44 @@ __global__ __launch_bounds__(DEC_WAVES * 64) void k_huff_decode(const uint32_t *
 //    lands in register k/4 (v_perm); the lane's 64 output bytes stay in registers;
 //  * batches of 4 symbols share one 64-bit window; a symbol is one v_lshrrev_b64, a
 //    12-bit index and one 16-bit LUT read (len | sym << 8);
-//  * two chains per lane (groups 2p and 2p+1) are interleaved symbol by symbol for ILP;
+//  * several chains per lane (consecutive groups) are interleaved symbol by symbol (ILP);
 //  * codes of 13..12+K bits (K <= 8): the first-level entry names a second-level table
 //    indexed by the next K bits (rare, wave-uniform branch per symbol pair); anything
 //    rarer (longer codes, a batch whose codes overflow the 64-bit window, invalid codes)
 //    makes the wave redo its two chunks exactly (d8_chunk_hbm).
 // Partial groups and groups whose span exceeds the stage also go through d8_chunk_hbm.
 // ------------------------------------------------------------------------------------
-#define D8_WAVES 16
+#define D8_CHAINS 32           /* chains (groups being decoded) per CU: waves x chains/wave */
 #define D8_STAGE_WORDS 1088    /* per chain: 4352 B = 4096 symbols at <= 8.4 bits/symbol   */
 #define D8_L2_CAP 7168         /* second-level entries (u16)                               */
 #define D8_K_MAX 8
+#define D8_MAX_WAVES 16
 
 struct Dec8Lds {
     uint16_t lut[1 << DC_LUT_BITS];   // LSB-first 12-bit window -> len | sym << 8; len 0: sub-table id << 8
     uint16_t lut2[D8_L2_CAP];         // [sub][K bits] -> len | sym << 8; 0: longer than 12+K bits / invalid
-    uint32_t scan[D8_WAVES];
+    uint32_t scan[D8_MAX_WAVES];
+    uint32_t exhausted;               // scheduler: bit h = slice h is empty
     uint16_t esc_pre[256];            // first-level index of escape prefix #id
-    __attribute__((aligned(16))) uint32_t stage[D8_WAVES][2][D8_STAGE_WORDS];
-    uint32_t tail_pad[64];   // a corrupt stream's windows may run past the last stage
+    __attribute__((aligned(16))) uint32_t stage[D8_CHAINS][D8_STAGE_WORDS];
+    uint32_t tail_pad[64];            // a corrupt stream's windows may run past the last stage
 };
 
 static __device__ __forceinline__ uint32_t brev8(uint32_t v) { return __builtin_bitreverse32(__builtin_bswap32(v)); }
+
+// inclusive wave64 prefix sum in DPP (VALU only: __shfl_up is ds_bpermute, i.e. an LDS
+// instruction queued behind the decoder's LUT reads): row_shr 1/2/4/8 within each row of
+// 16 lanes, then row_bcast:15 and row_bcast:31 across rows (GFX9 DPP)
+static __device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x)
+{
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);   // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);   // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);   // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);   // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);   // row_bcast:15
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);   // row_bcast:31
+    return x;
+}
 
 // exact slow decode of the code at the start of an LSB-first 64-bit window (lo, hi):
 // returns nbits | sym << 8; an invalid code sets *bad and returns 0
@@ -1047,78 +1063,242 @@ static __device__ __forceinline__ uint32_t d8_esc(uint32_t e, uint32_t x, uint32
     return e;
 }
 
-// one batch (4 symbols) of both chains; returns the two output dwords
-static __device__ __forceinline__ void d8_pair(const uint32_t *sa, const uint32_t *sb, uint32_t &ca, uint32_t &cb,
-                                               uint32_t &oa, uint32_t &ob, const D8Tabs &tb, int &giveup)
+// one batch (4 symbols) of the NC chains of a lane, interleaved symbol by symbol;
+// o[j] receives chain j's 4 output bytes
+template <int NC>
+static __device__ __forceinline__ void d8_batch(const uint32_t *const *st, uint32_t *c, uint32_t *o, const D8Tabs &tb,
+                                                int &giveup)
 {
-    const uint32_t a0 = ca >> 5, b0 = cb >> 5;
-    const uint32_t wa0 = sa[a0], wa1 = sa[a0 + 1], wa2 = sa[a0 + 2];
-    const uint32_t wb0 = sb[b0], wb1 = sb[b0 + 1], wb2 = sb[b0 + 2];
-    const uint64_t winA = ((uint64_t)__builtin_amdgcn_alignbit(wa2, wa1, ca) << 32) | __builtin_amdgcn_alignbit(wa1, wa0, ca);
-    const uint64_t winB = ((uint64_t)__builtin_amdgcn_alignbit(wb2, wb1, cb) << 32) | __builtin_amdgcn_alignbit(wb1, wb0, cb);
-    uint32_t offA = 0, offB = 0;
+    uint64_t win[NC];
+    uint32_t off[NC];
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+        const uint32_t a = c[j] >> 5;
+        const uint32_t w0 = st[j][a], w1 = st[j][a + 1], w2 = st[j][a + 2];
+        win[j] = ((uint64_t)__builtin_amdgcn_alignbit(w2, w1, c[j]) << 32) | __builtin_amdgcn_alignbit(w1, w0, c[j]);
+        off[j] = 0;
+    }
     // output byte k <- entry byte 1 (v_perm: S0 = entry bytes 4-7, S1 = output bytes 0-3)
     constexpr uint32_t SEL[4] = {0x0c0c0c05u, 0x0c0c0500u, 0x0c050100u, 0x05020100u};
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        const uint32_t xA = (uint32_t)(winA >> offA), xB = (uint32_t)(winB >> offB);
-        uint32_t ea = tb.lut[xA & ((1u << DC_LUT_BITS) - 1)];
-        uint32_t eb = tb.lut[xB & ((1u << DC_LUT_BITS) - 1)];
-        if (__builtin_expect(__any(min(ea & 255u, eb & 255u) == 0), 0)) {
-            ea = d8_esc(ea, xA, offA, k, tb, giveup);
-            eb = d8_esc(eb, xB, offB, k, tb, giveup);
+        uint32_t x[NC], e[NC], mn = 255u;
+#pragma unroll
+        for (int j = 0; j < NC; ++j) {
+            x[j] = (uint32_t)(win[j] >> off[j]);
+            e[j] = tb.lut[x[j] & ((1u << DC_LUT_BITS) - 1)];
         }
-        oa = __builtin_amdgcn_perm(ea, k ? oa : 0u, SEL[k]);
-        ob = __builtin_amdgcn_perm(eb, k ? ob : 0u, SEL[k]);
-        offA += ea & 255u;
-        offB += eb & 255u;
+#pragma unroll
+        for (int j = 0; j < NC; ++j) mn = min(mn, e[j] & 255u);
+#ifdef DC_DIAG_NOESC   // timing ablation only: escapes decode as garbage
+        giveup |= (int)(mn == 0);
+#else
+        if (__builtin_expect(__any(mn == 0), 0)) {
+#pragma unroll
+            for (int j = 0; j < NC; ++j) e[j] = d8_esc(e[j], x[j], off[j], k, tb, giveup);
+        }
+#endif
+#pragma unroll
+        for (int j = 0; j < NC; ++j) {
+            o[j] = __builtin_amdgcn_perm(e[j], k ? o[j] : 0u, SEL[k]);
+            off[j] += e[j] & 255u;
+        }
     }
-    ca += offA;
-    cb += offB;
+#pragma unroll
+    for (int j = 0; j < NC; ++j) c[j] += off[j];
 }
 
-// the 16 batches of a 64-symbol chunk for both chains, unrolled by template recursion;
-// every 4 batches the lane's 16 output bytes per chain are stored (uint4 at lane*64 + 16q),
-// so only 8 output registers are live
-template <int Q>
+// the 16 batches of a 64-symbol chunk, unrolled by template recursion; every 4 batches
+// the lane's 16 output bytes per chain are stored (uint4 at chunk + 16q)
+template <int NC, int Q>
 struct D8Batches {
-    static __device__ __forceinline__ void run(const uint32_t *sa, const uint32_t *sb, uint32_t &ca, uint32_t &cb,
-                                               uint4 *da, uint4 *db, const D8Tabs &tb, int &giveup)
+    static __device__ __forceinline__ void run(const uint32_t *const *st, uint32_t *c, uint4 *const *dst,
+                                               const D8Tabs &tb, int &giveup)
     {
-        uint32_t a0, a1, a2, a3, b0, b1, b2, b3;
-        d8_pair(sa, sb, ca, cb, a0, b0, tb, giveup);
-        d8_pair(sa, sb, ca, cb, a1, b1, tb, giveup);
-        d8_pair(sa, sb, ca, cb, a2, b2, tb, giveup);
-        d8_pair(sa, sb, ca, cb, a3, b3, tb, giveup);
-        da[Q] = make_uint4(a0, a1, a2, a3);
-        db[Q] = make_uint4(b0, b1, b2, b3);
-        D8Batches<Q + 1>::run(sa, sb, ca, cb, da, db, tb, giveup);
+        uint32_t o0[NC], o1[NC], o2[NC], o3[NC];
+        d8_batch<NC>(st, c, o0, tb, giveup);
+        d8_batch<NC>(st, c, o1, tb, giveup);
+        d8_batch<NC>(st, c, o2, tb, giveup);
+        d8_batch<NC>(st, c, o3, tb, giveup);
+#pragma unroll
+        for (int j = 0; j < NC; ++j) {
+#ifdef DC_DIAG_NOSTORE
+            asm volatile("" ::"v"(o0[j]), "v"(o1[j]), "v"(o2[j]), "v"(o3[j]));
+#else
+            dst[j][Q] = make_uint4(o0[j], o1[j], o2[j], o3[j]);
+#endif
+        }
+        D8Batches<NC, Q + 1>::run(st, c, dst, tb, giveup);
     }
 };
-template <>
-struct D8Batches<4> {
-    static __device__ __forceinline__ void run(const uint32_t *, const uint32_t *, uint32_t &, uint32_t &, uint4 *,
-                                               uint4 *, const D8Tabs &, int &)
+template <int NC>
+struct D8Batches<NC, 4> {
+    static __device__ __forceinline__ void run(const uint32_t *const *, uint32_t *, uint4 *const *, const D8Tabs &,
+                                               int &)
     {
     }
 };
 
-__global__ __launch_bounds__(D8_WAVES * 64) void k_huff_decode8(const uint32_t *__restrict__ in, uint64_t bit_base,
-                                                                const uint64_t *__restrict__ sync_base,
-                                                                const uint16_t *__restrict__ sync_len, uint64_t n,
-                                                                uint64_t nwords, const dc_dtable *__restrict__ T,
-                                                                uint8_t *__restrict__ out, int *__restrict__ err)
+#ifdef DC_DIAG   // diagnostic build only (tools/diag_build.sh): per-wave s_memtime split
+__device__ unsigned long long g_d8diag[256 * D8_MAX_WAVES * 4];
+extern "C" int dc_diag_read(void *h, size_t bytes)
 {
+    return hipMemcpyFromSymbol(h, HIP_SYMBOL(g_d8diag), bytes) == hipSuccess ? 0 : -2;
+}
+#define D8_STAMP(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#else
+#define D8_STAMP(v)
+#endif
+
+template <int NC>
+struct D8Meta { uint32_t len[NC]; uint64_t base[NC]; };   // sync index of one tuple (per lane)
+template <int NC>
+struct D8Geo {                                             // where a tuple's spans and chunks lie
+    uint64_t g0;
+    uint64_t rel[NC], wo[NC];
+    uint32_t off[NC], lead[NC], last[NC];
+    bool fast;
+};
+
+template <int NC>
+static __device__ __forceinline__ void d8_load_meta(D8Meta<NC> &m, uint64_t tp, uint64_t ntuples, uint64_t ngroups,
+                                                    uint64_t nchunks, int lane, const uint16_t *__restrict__ sync_len,
+                                                    const uint64_t *__restrict__ sync_base)
+{
+    // unconditional loads of clamped indices: a conditional load would make the compiler
+    // wait for it (and for every older load: the prefetched spans) at the join; the
+    // validity mask is applied where the values are used, an iteration later
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+        const uint64_t g = tp * NC + j, ch = g * DC_SYNC_GROUP + lane;
+        m.len[j] = sync_len[min(ch, nchunks - 1)];
+        m.base[j] = sync_base[min(g, ngroups - 1)];
+    }
+}
+
+template <int NC>
+static __device__ __forceinline__ void d8_geometry(D8Geo<NC> &g, const D8Meta<NC> &m, uint64_t tp, uint64_t ntuples,
+                                                   uint64_t n, uint64_t nwords, uint64_t word_base, int lane)
+{
+    constexpr uint64_t GSYM = DC_SYNC_GROUP * 64;
+    g.g0 = tp * NC;
+    const uint64_t nchunks = (n + 63) / 64;
+    uint32_t in[NC], len[NC];
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {   // branch-free mask (a branch here makes the compiler drain vmcnt)
+        const uint32_t ok = (uint32_t)(tp < ntuples) & (uint32_t)((g.g0 + j) * DC_SYNC_GROUP + lane < nchunks);
+        len[j] = m.len[j] & (0u - ok);
+        in[j] = len[j];
+    }
+#pragma unroll
+    for (int j = 0; j < NC; ++j) in[j] = wave_scan_incl(in[j]);
+    bool fast = tp < ntuples && (g.g0 + NC) * GSYM <= n;
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+        const uint32_t span = __builtin_amdgcn_readlane(in[j], 63);
+        g.off[j] = in[j] - len[j];
+        g.rel[j] = m.base[j] - (word_base << 5);
+        g.wo[j] = (g.rel[j] >> 5) & ~3ull;
+        g.lead[j] = (uint32_t)(g.rel[j] - (g.wo[j] << 5));
+        const uint32_t nw = (g.lead[j] + span) / 32 + 3;
+        g.last[j] = (nw + 3) / 4 - 1;
+        fast = fast && nw + 4 <= D8_STAGE_WORDS && g.wo[j] + nw + 4 <= nwords;
+    }
+    g.fast = fast;
+}
+
+// the tuple's span loads: 16 B per lane, clamped to each span; word 0 when not staged
+template <int NC>
+static __device__ __forceinline__ void d8_issue(uint4 (&v)[NC][5], const D8Geo<NC> &g,
+                                                const uint32_t *__restrict__ in, int lane)
+{
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+#pragma unroll
+        for (int j = 0; j < NC; ++j) {
+            const uint4 *src = reinterpret_cast<const uint4 *>(in + (g.fast ? g.wo[j] : 0ull));
+            v[j][k] = src[g.fast ? min((uint32_t)(lane + 64 * k), g.last[j]) : 0u];
+        }
+    }
+}
+
+// Tuple scheduler of the persistent decoder. Waves of one SIMD get unequal issue slots
+// (priority, then age) and XCDs run at slightly different speeds, so a static split ends
+// when the slowest wave does (measured 1.5x max/min inside a workgroup). The first
+// D8_STATIC_PCT % of the tuples are dealt statically (wave i: i, i + P, i + 2P, ...); the
+// rest are cut into 8 slices, each with its own dequeue head (a u32 counter on a 4 KiB
+// line of its own: one word saturates at ~88 dequeues/us, MI355X_MICROARCH.md 'dequeue').
+// A wave dequeues from the slice of its block's group label (blockIdx % 8), then steals
+// from the other slices; a workgroup remembers exhausted slices in LDS. The last wave out
+// resets the heads for the next launch on the stream.
+#define D8_STATIC_PCT 60
+#define D8_QSTRIDE 1024   /* u32 between heads */
+#define D8_QWORDS (9 * D8_QSTRIDE)
+
+struct D8Sched {
+    uint64_t Ts, Dh, ntuples;   // static tuples, slice size, all tuples
+    uint64_t wid, P;            // wave id, waves in the grid
+    uint32_t k, Ks;             // static tuples taken / per wave
+    int head, tried;            // slice being drained, slices given up
+    bool dyn;                   // pending value is a dequeue result
+    uint32_t pend;              // lane 0: dequeued index
+    uint64_t spend;             // static index
+};
+
+static __device__ __forceinline__ void d8_fetch(D8Sched &s, uint32_t *__restrict__ queue, int lane)
+{
+    if (s.k < s.Ks) {
+        s.spend = s.wid + (uint64_t)s.k * s.P;
+        ++s.k;
+        s.dyn = false;
+    } else {
+        s.dyn = true;
+        if (lane == 0 && s.tried < 8) s.pend = atomicAdd(queue + s.head * D8_QSTRIDE, 1u);
+    }
+}
+
+static __device__ __forceinline__ uint64_t d8_resolve(D8Sched &s, uint32_t *__restrict__ queue, uint32_t *exhausted,
+                                                      int lane)
+{
+    if (!s.dyn) return s.spend;
+    while (s.tried < 8) {
+        const uint64_t i = (uint32_t)__builtin_amdgcn_readlane((int)s.pend, 0);
+        const uint64_t lo = s.Ts + (uint64_t)s.head * s.Dh;
+        const uint64_t hi = min(lo + s.Dh, s.ntuples);
+        if (lo + i < hi) return lo + i;
+        if (lane == 0) atomicOr(exhausted, 1u << s.head);
+        ++s.tried;
+        s.head = (s.head + 1) & 7;
+        // skip slices this workgroup already found empty
+        const uint32_t ex = __builtin_amdgcn_readfirstlane(__atomic_load_n(exhausted, __ATOMIC_RELAXED));
+        while (s.tried < 8 && ((ex >> s.head) & 1u)) { ++s.tried; s.head = (s.head + 1) & 7; }
+        if (s.tried < 8 && lane == 0) s.pend = atomicAdd(queue + s.head * D8_QSTRIDE, 1u);
+    }
+    return s.ntuples;
+}
+
+// NW waves per workgroup (one workgroup per CU), NC chains per wave: wave w of workgroup b
+// decodes the NC consecutive groups of "tuple" b*NW + w (+ grid stride), lane = chunk.
+template <int NW, int NC>
+__global__ __launch_bounds__(NW * 64) void k_huff_decode8(const uint32_t *__restrict__ in, uint64_t bit_base,
+                                                          const uint64_t *__restrict__ sync_base,
+                                                          const uint16_t *__restrict__ sync_len, uint64_t n,
+                                                          uint64_t nwords, const dc_dtable *__restrict__ T,
+                                                          uint8_t *__restrict__ out, int *__restrict__ err,
+                                                          uint32_t *__restrict__ queue, uint32_t static_pct)
+{
+    static_assert(NW * NC == D8_CHAINS && NW <= D8_MAX_WAVES, "stage slots");
     constexpr uint32_t S = 64, GSYM = DC_SYNC_GROUP * S;
-    constexpr int NT = D8_WAVES * 64;
+    constexpr int NT = NW * 64;
     __shared__ Dec8Lds L;
-    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const int t = threadIdx.x, lane = t & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
     const int nary = T->n_ary, w = T->w;
     const bool pow2 = (nary & (nary - 1)) == 0;
     int bad = 0;
     // ---- tables: first level (bit-reversed index of the MSB-first table), escape
     // prefixes numbered in index order, second level decoded exactly once per entry
-    constexpr int PER = (1 << DC_LUT_BITS) / NT;   // 4 entries per thread
+    constexpr int PER = (1 << DC_LUT_BITS) / NT;
     uint32_t e1[PER];
     uint32_t nesc = 0;
 #pragma unroll
@@ -1135,9 +1315,10 @@ __global__ __launch_bounds__(D8_WAVES * 64) void k_huff_decode8(const uint32_t *
         if (lane >= d) incl += y;
     }
     if (lane == 63) L.scan[wv] = incl;
+    if (t == 0) L.exhausted = 0;
     __syncthreads();
     uint32_t base = 0, E = 0;
-    for (int v = 0; v < D8_WAVES; ++v) {
+    for (int v = 0; v < NW; ++v) {
         const uint32_t s = L.scan[v];
         base += (v < wv) ? s : 0u;
         E += s;
@@ -1155,7 +1336,6 @@ __global__ __launch_bounds__(D8_WAVES * 64) void k_huff_decode8(const uint32_t *
     __syncthreads();
     if (l2ok) {
         for (uint32_t q = (uint32_t)t; q < (E << K); q += NT) {
-            // the escape prefix numbered q >> K
             const uint32_t pre = L.esc_pre[q >> K];
             const uint32_t lo = pre | ((q & ((1u << K) - 1)) << DC_LUT_BITS);
             int b2 = 0;
@@ -1164,76 +1344,132 @@ __global__ __launch_bounds__(D8_WAVES * 64) void k_huff_decode8(const uint32_t *
         }
     }
     __syncthreads();
-    D8Tabs tb{L.lut, L.lut2, l2ok ? K : 0u, (1u << K) - 1};
+    const D8Tabs tb{L.lut, L.lut2, l2ok ? K : 0u, (1u << K) - 1};
 
     const uint64_t nchunks = (n + S - 1) / S;
     const uint64_t ngroups = (nchunks + DC_SYNC_GROUP - 1) / DC_SYNC_GROUP;
-    const uint64_t npairs = (ngroups + 1) / 2;
+    const uint64_t ntuples = (ngroups + NC - 1) / NC;
     const uint64_t word_base = bit_base >> 5;
-    uint32_t *stA = L.stage[wv][0], *stB = L.stage[wv][1];
-    for (uint64_t pr = (uint64_t)blockIdx.x * D8_WAVES + wv; pr < npairs; pr += (uint64_t)gridDim.x * D8_WAVES) {
-        const uint64_t gA = 2 * pr, gB = gA + 1;
-        // chunk lengths of both groups -> lane offsets (bits from each group start)
-        const uint64_t cA = gA * DC_SYNC_GROUP + lane, cB = gB * DC_SYNC_GROUP + lane;
-        const uint32_t lenA = (cA < nchunks) ? sync_len[cA] : 0u;
-        const uint32_t lenB = (cB < nchunks) ? sync_len[cB] : 0u;
-        uint32_t inA = lenA, inB = lenB;
+    const uint32_t *st[NC];
+    uint32_t *stw[NC];
 #pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t ya = __shfl_up(inA, d, 64), yb = __shfl_up(inB, d, 64);
-            if (lane >= d) { inA += ya; inB += yb; }
-        }
-        const uint32_t spanA = __shfl(inA, 63, 64), spanB = __shfl(inB, 63, 64);
-        const bool hasB = gB < ngroups;
-        const uint64_t relA = sync_base[gA] - (word_base << 5);
-        const uint64_t relB = hasB ? sync_base[gB] - (word_base << 5) : relA;
-        const uint64_t wA = (relA >> 5) & ~3ull, wB = (relB >> 5) & ~3ull;
-        const uint32_t leadA = (uint32_t)(relA - (wA << 5)), leadB = (uint32_t)(relB - (wB << 5));
-        const uint32_t nwA = (leadA + spanA) / 32 + 3, nwB = (leadB + spanB) / 32 + 3;
-        bool slow = !(hasB && (gB + 1) * (uint64_t)GSYM <= n && nwA + 4 <= D8_STAGE_WORDS && nwB + 4 <= D8_STAGE_WORDS &&
-                      wA + nwA + 4 <= nwords && wB + nwB + 4 <= nwords);
-        if (!slow) {
-            // stage both spans: 16-B loads (clamped, all in flight), byte-wise bit reversal
-            static_assert((D8_STAGE_WORDS / 4 + 63) / 64 <= 5, "stage larger than 5 KiB");
-            const uint4 *srcA = reinterpret_cast<const uint4 *>(in + wA);
-            const uint4 *srcB = reinterpret_cast<const uint4 *>(in + wB);
-            const uint32_t lastA = (nwA + 3) / 4 - 1, lastB = (nwB + 3) / 4 - 1;
-            uint4 va[5], vb[5];
-#pragma unroll
-            for (int k = 0; k < 5; ++k) {
-                va[k] = srcA[min((uint32_t)(lane + 64 * k), lastA)];
-                vb[k] = srcB[min((uint32_t)(lane + 64 * k), lastB)];
-            }
+    for (int j = 0; j < NC; ++j) { stw[j] = L.stage[wv * NC + j]; st[j] = stw[j]; }
+    const uint64_t stride = (uint64_t)gridDim.x * NW;
+    // Software pipeline (per wave, one tuple of NC groups per iteration): while tuple i
+    // decodes, the spans of tuple i+1 are in flight into registers and the sync index of
+    // tuple i+2 too, so no iteration waits for a global round trip (nor for its stores).
+    // The span loads are issued for every tuple (clamped to word 0 when it is not staged),
+    // so the prefetch registers never need merging.
+    static_assert((D8_STAGE_WORDS / 4 + 63) / 64 <= 5, "stage larger than 5 KiB");
+    D8Geo<NC> g, cur;
+    D8Meta<NC> m1, m2;   // m2: the first tuple's index only
+    uint4 v[NC][5];
+#ifdef DC_DIAG
+    unsigned long long d_stage = 0, d_dec = 0, d_slow = 0;
+    D8_STAMP(d_begin);
+#endif
+    D8Sched sc;
+    sc.ntuples = ntuples;
+    sc.P = stride;
+    sc.wid = (uint64_t)blockIdx.x * NW + wv;
+    sc.Ks = (uint32_t)(ntuples * static_pct / 100 / stride);
+    sc.Ts = (uint64_t)sc.Ks * stride;
+    sc.Dh = (ntuples - sc.Ts + 7) / 8;
+    sc.k = 0;
+    sc.head = blockIdx.x & 7;
+    sc.tried = 0;
+    sc.pend = 0;
+    d8_fetch(sc, queue, lane);
+    uint64_t tp = d8_resolve(sc, queue, &L.exhausted, lane);
+    d8_fetch(sc, queue, lane);
+    uint64_t t1 = d8_resolve(sc, queue, &L.exhausted, lane);
+    d8_fetch(sc, queue, lane);
+    d8_load_meta<NC>(m2, tp, ntuples, ngroups, nchunks, lane, sync_len, sync_base);
+    d8_geometry<NC>(g, m2, tp, ntuples, n, nwords, word_base, lane);
+    d8_issue<NC>(v, g, in, lane);
+    d8_load_meta<NC>(m1, t1, ntuples, ngroups, nchunks, lane, sync_len, sync_base);
+    while (tp < ntuples) {
+        D8_STAMP(s0);
+        cur = g;
+        if (cur.fast) {   // byte-wise bit reversal into the LDS stage
 #pragma unroll
             for (int k = 0; k < 5; ++k) {
                 const uint32_t i = lane + 64 * k;
-                if (i <= lastA)
-                    reinterpret_cast<uint4 *>(stA)[i] = make_uint4(brev8(va[k].x), brev8(va[k].y), brev8(va[k].z), brev8(va[k].w));
-                if (i <= lastB)
-                    reinterpret_cast<uint4 *>(stB)[i] = make_uint4(brev8(vb[k].x), brev8(vb[k].y), brev8(vb[k].z), brev8(vb[k].w));
+#pragma unroll
+                for (int j = 0; j < NC; ++j)
+                    if (i <= cur.last[j])
+                        reinterpret_cast<uint4 *>(stw[j])[i] =
+                            make_uint4(brev8(v[j][k].x), brev8(v[j][k].y), brev8(v[j][k].z), brev8(v[j][k].w));
             }
+        }
+        d8_geometry<NC>(g, m1, t1, ntuples, n, nwords, word_base, lane);
+        const uint64_t t2 = d8_resolve(sc, queue, &L.exhausted, lane);
+        d8_load_meta<NC>(m1, t2, ntuples, ngroups, nchunks, lane, sync_len, sync_base);
+        d8_fetch(sc, queue, lane);
+        d8_issue<NC>(v, g, in, lane);   // after the index loads: waiting for these covers both
+        bool slow = !cur.fast;
+        if (cur.fast) {
             __builtin_amdgcn_wave_barrier();
-            uint32_t pa = leadA + inA - lenA, pb = leadB + inB - lenB;
+#ifdef DC_DIAG
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            D8_STAMP(s1);
+            d_stage += s1 - s0;
+#endif
+            uint32_t c[NC];
+            uint4 *dst[NC];
+#pragma unroll
+            for (int j = 0; j < NC; ++j) {
+                c[j] = cur.lead[j] + cur.off[j];
+                dst[j] = reinterpret_cast<uint4 *>(out + (cur.g0 + j) * GSYM + (uint64_t)lane * S);
+            }
             int giveup = 0;
-            D8Batches<0>::run(stA, stB, pa, pb, reinterpret_cast<uint4 *>(out + gA * GSYM + (uint64_t)lane * S),
-                              reinterpret_cast<uint4 *>(out + gB * GSYM + (uint64_t)lane * S), tb, giveup);
-            if (__any(giveup)) slow = true;   // exact redo below overwrites the two chunks
-            __builtin_amdgcn_wave_barrier();   // stage reused by the next pair
+            D8Batches<NC, 0>::run(st, c, dst, tb, giveup);
+#ifndef DC_DIAG_NOESC
+            if (__any(giveup)) slow = true;   // exact redo below overwrites the chunks
+#endif
+#ifdef DC_DIAG
+            D8_STAMP(s2);
+            d_dec += s2 - s1;
+#endif
+            __builtin_amdgcn_wave_barrier();   // stage reused by the next tuple
         }
         if (slow) {
             // partial groups, over-long spans, rare codes: exact per-symbol decode from HBM
-            if (cA < nchunks) {
-                const uint64_t s0 = cA * S;
-                const uint32_t cnt = (uint32_t)((n - s0 < S) ? n - s0 : S);
-                d8_chunk_hbm(in, nwords, relA + inA - lenA, cnt, out + s0, T, nary, w, pow2, bad);
+#pragma unroll
+            for (int j = 0; j < NC; ++j) {
+                const uint64_t ch = (cur.g0 + j) * DC_SYNC_GROUP + lane;
+                if (cur.g0 + j < ngroups && ch < nchunks) {
+                    const uint64_t s0 = ch * S;
+                    const uint32_t cnt = (uint32_t)((n - s0 < S) ? n - s0 : S);
+                    d8_chunk_hbm(in, nwords, cur.rel[j] + cur.off[j], cnt, out + s0, T, nary, w, pow2, bad);
+                }
             }
-            if (hasB && cB < nchunks) {
-                const uint64_t s0 = cB * S;
-                const uint32_t cnt = (uint32_t)((n - s0 < S) ? n - s0 : S);
-                d8_chunk_hbm(in, nwords, relB + inB - lenB, cnt, out + s0, T, nary, w, pow2, bad);
-            }
+#ifdef DC_DIAG
+            D8_STAMP(s3);
+            d_slow += s3 - s0;
+#endif
         }
+        tp = t1;
+        t1 = t2;
     }
+    if (lane == 0) {
+        // a dequeue issued for a tuple past the end may still be in flight: it must land
+        // before this wave counts itself out, or it would bump a head after the reset
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (atomicAdd(queue + 8 * D8_QSTRIDE, 1u) == gridDim.x * NW - 1)
+            for (int h = 0; h <= 8; ++h) atomicExch(queue + h * D8_QSTRIDE, 0u);
+    }
+#ifdef DC_DIAG
+    D8_STAMP(d_end);
+    if (lane == 0) {
+        unsigned long long *gg = g_d8diag + (blockIdx.x * NW + wv) * 4;
+        unsigned xcc, hwid;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
+        gg[0] = d_end - d_begin; gg[1] = d_stage; gg[2] = d_dec;
+        gg[3] = ((unsigned long long)(xcc & 15) << 56) | ((unsigned long long)hwid << 24) | (d_slow & 0xffffff);
+    }
+#endif
     if (bad) atomicOr(err, 1);
 }
 
@@ -1607,6 +1843,7 @@ struct dc_ctx {
     uint64_t *d_partials;                         // 1024 x 256
     uint64_t *d_off;        size_t off_cap;       // nblocks + 1
     int *d_err;                                   // [0] plan, [1] decode
+    uint32_t *d_queue;                            // decode tuple scheduler heads (D8Sched)
     uint64_t *d_meta;                             // small device scalars
     uint4 *d_summ;          size_t summ_cap;
     uint64_t *d_entry;      size_t entry_cap;
@@ -1689,6 +1926,11 @@ static int ctx_create(dc_ctx **out, int device, void *stream, bool own)
         free(c);
         return DC_E_HIP;
     }
+    if (hipMalloc((void **)&c->d_queue, D8_QWORDS * sizeof(uint32_t)) != hipSuccess ||
+        hipMemset(c->d_queue, 0, D8_QWORDS * sizeof(uint32_t)) != hipSuccess) {
+        free(c);
+        return DC_E_HIP;
+    }
     if (g_rank_uploaded != device) {
         uint8_t rank[256];
         memset(rank, 0xFF, sizeof(rank));
@@ -1710,6 +1952,7 @@ void dc_ctx_destroy(dc_ctx *c)
     if (c->d_partials) (void)hipFree(c->d_partials);
     if (c->d_off) (void)hipFree(c->d_off);
     if (c->d_err) (void)hipFree(c->d_err);
+    if (c->d_queue) (void)hipFree(c->d_queue);
     if (c->d_meta) (void)hipFree(c->d_meta);
     if (c->d_summ) (void)hipFree(c->d_summ);
     if (c->d_entry) (void)hipFree(c->d_entry);
@@ -1968,11 +2211,19 @@ int dc_huff_decode(dc_ctx *c, const uint32_t *d_words, uint64_t bit_base, uint64
     const uint64_t groups = dc_huff_sync_groups(n, S);
     HIPCHK(hipMemsetAsync(c->d_err + 1, 0, sizeof(int), c->stream));
     if (S == 64 && !getenv("DC_DECODE_V7")) {
-        const uint64_t pairs = (groups + 1) / 2;
-        const uint64_t wgs = (pairs + D8_WAVES - 1) / D8_WAVES;
-        const uint64_t grid = wgs < 256 ? wgs : 256;   // persistent: one 16-wave workgroup per CU
-        LAUNCH(c, "huff_decode", k_huff_decode8, grid, D8_WAVES * 64, d_words, bit_base, d_sync_base, d_sync_len, n,
-               words, d_table, d_out, c->d_err + 1);
+        const char *cfg = getenv("DC_D8_CFG");   // A/B of the wave x chain split (tools/dec_ab.py)
+        const int nw = (cfg && cfg[0] == '1') ? 16 : 8;
+        const char *sp = getenv("DC_D8_STATIC");   // A/B of the static share (tools/dec_ab.py)
+        const uint32_t spct = sp ? (uint32_t)atoi(sp) : D8_STATIC_PCT;
+        const uint64_t tuples = (groups + D8_CHAINS / nw - 1) / (D8_CHAINS / nw);
+        const uint64_t wgs = (tuples + nw - 1) / nw;
+        const uint64_t grid = wgs < 256 ? wgs : 256;   // persistent: one workgroup per CU
+        if (nw == 16)
+            LAUNCH(c, "huff_decode", (k_huff_decode8<16, 2>), grid, 16 * 64, d_words, bit_base, d_sync_base, d_sync_len,
+                   n, words, d_table, d_out, c->d_err + 1, c->d_queue, spct);
+        else
+            LAUNCH(c, "huff_decode", (k_huff_decode8<8, 4>), grid, 8 * 64, d_words, bit_base, d_sync_base, d_sync_len,
+                   n, words, d_table, d_out, c->d_err + 1, c->d_queue, spct);
         return DC_OK;
     }
     const uint64_t wgs = (groups + DEC_WAVES - 1) / DEC_WAVES;

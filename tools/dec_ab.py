@@ -20,7 +20,7 @@ ap.add_argument("--size", type=int, default=1 << 30)
 ap.add_argument("--nary", type=int, default=2)
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--iters", type=int, default=10)
-ap.add_argument("--variants", default="v8,v7")
+ap.add_argument("--variants", default="8x4,16x2,v7")
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
 x = synth.device_text(a.cfg, a.size, seed=0xC2, device=dev)
@@ -30,10 +30,17 @@ out = torch.empty_like(x)
 res = {v: [] for v in a.variants.split(",")}
 for r in range(a.rounds):
     for v in res:
-        if v == "v7":
+        os.environ.pop("DC_DECODE_V7", None)
+        os.environ.pop("DC_D8_CFG", None)
+        os.environ.pop("DC_D8_STATIC", None)
+        if "s" in v:   # e.g. 16x2s80: static share 80 %
+            v0, sp = v.split("s")
+            os.environ["DC_D8_STATIC"] = sp
+            os.environ["DC_D8_CFG"] = v0
+        elif v == "v7":
             os.environ["DC_DECODE_V7"] = "1"
-        else:
-            os.environ.pop("DC_DECODE_V7", None)
+        elif v != "v8":
+            os.environ["DC_D8_CFG"] = v
         c.decode_into(enc, out)
         torch.cuda.synchronize()
         c.timing(True)

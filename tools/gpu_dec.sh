@@ -9,7 +9,7 @@ i=0
 for PASS in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY" \
             "SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_BRANCH SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE"; do
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $PASS -d gpurun_out/dpmc/p$i -o run --output-format csv -- python tools/dec_ab.py --variants v8 --rounds 1 --iters 2 > gpurun_out/dpmc_p$i.log 2>&1 || { echo "pass $i failed"; tail -5 gpurun_out/dpmc_p$i.log; exit 1; }
+  timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $PASS -d gpurun_out/dpmc/p$i -o run --output-format csv -- python tools/dec_ab.py --variants 8x4 --rounds 1 --iters 2 > gpurun_out/dpmc_p$i.log 2>&1 || { echo "pass $i failed"; tail -5 gpurun_out/dpmc_p$i.log; exit 1; }
 done
 python - <<'PY'
 import csv, glob, collections
