@@ -2211,19 +2211,15 @@ int dc_huff_decode(dc_ctx *c, const uint32_t *d_words, uint64_t bit_base, uint64
     const uint64_t groups = dc_huff_sync_groups(n, S);
     HIPCHK(hipMemsetAsync(c->d_err + 1, 0, sizeof(int), c->stream));
     if (S == 64 && !getenv("DC_DECODE_V7")) {
-        const char *cfg = getenv("DC_D8_CFG");   // A/B of the wave x chain split (tools/dec_ab.py)
-        const int nw = (cfg && cfg[0] == '1') ? 16 : 8;
+        // 16 waves x 2 chains (one workgroup per CU): the 8 x 4 split measured 0.89 vs
+        // 0.70 ms on 1 GiB C2 (fewer waves to cover the LDS round trips, spills)
         const char *sp = getenv("DC_D8_STATIC");   // A/B of the static share (tools/dec_ab.py)
         const uint32_t spct = sp ? (uint32_t)atoi(sp) : D8_STATIC_PCT;
-        const uint64_t tuples = (groups + D8_CHAINS / nw - 1) / (D8_CHAINS / nw);
-        const uint64_t wgs = (tuples + nw - 1) / nw;
+        const uint64_t tuples = (groups + 1) / 2;
+        const uint64_t wgs = (tuples + 15) / 16;
         const uint64_t grid = wgs < 256 ? wgs : 256;   // persistent: one workgroup per CU
-        if (nw == 16)
-            LAUNCH(c, "huff_decode", (k_huff_decode8<16, 2>), grid, 16 * 64, d_words, bit_base, d_sync_base, d_sync_len,
-                   n, words, d_table, d_out, c->d_err + 1, c->d_queue, spct);
-        else
-            LAUNCH(c, "huff_decode", (k_huff_decode8<8, 4>), grid, 8 * 64, d_words, bit_base, d_sync_base, d_sync_len,
-                   n, words, d_table, d_out, c->d_err + 1, c->d_queue, spct);
+        LAUNCH(c, "huff_decode", (k_huff_decode8<16, 2>), grid, 16 * 64, d_words, bit_base, d_sync_base, d_sync_len,
+               n, words, d_table, d_out, c->d_err + 1, c->d_queue, spct);
         return DC_OK;
     }
     const uint64_t wgs = (groups + DEC_WAVES - 1) / DEC_WAVES;

@@ -20,7 +20,7 @@ ap.add_argument("--size", type=int, default=1 << 30)
 ap.add_argument("--nary", type=int, default=2)
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--iters", type=int, default=10)
-ap.add_argument("--variants", default="8x4,16x2,v7")
+ap.add_argument("--variants", default="v8,v7")
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
 x = synth.device_text(a.cfg, a.size, seed=0xC2, device=dev)

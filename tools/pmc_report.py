@@ -11,7 +11,9 @@ vals = defaultdict(lambda: defaultdict(list))
 for f in sorted(glob.glob(os.path.join(root, "p*", "run_counter_collection.csv"))):
     per = defaultdict(float)
     for r in csv.DictReader(open(f)):
-        k = r["Kernel_Name"].split("(")[0]
+        k = r["Kernel_Name"].split("(")[0].replace("void ", "").split("<")[0].strip()
+        if k.startswith("k_huff_decode"):   # k_huff_decode8<NW, NC> is the decode launch
+            k = "k_huff_decode"
         if k not in want:
             continue
         key = (k, r["Dispatch_Id"], r["Counter_Name"])
