@@ -459,6 +459,20 @@ __global__ void k_zero_bounds(const uint64_t *__restrict__ off, uint64_t nblocks
     words[(abs >> 5) - (bit_base >> 5)] = 0u;
 }
 
+// inclusive wave64 prefix sum in DPP (VALU only: __shfl_up is ds_bpermute, i.e. an LDS
+// instruction queued behind the table reads): row_shr 1/2/4/8 within each row of
+// 16 lanes, then row_bcast:15 and row_bcast:31 across rows (GFX9 DPP)
+static __device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x)
+{
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);   // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);   // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);   // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);   // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);   // row_bcast:15
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);   // row_bcast:31
+    return x;
+}
+
 // ------------------------------------------------------------------------------------
 // (H7) pack. One workgroup per 32 KiB block (grid-stride), 8 tiles of 4 KiB; a lane
 // codes 16 bytes (one 16-B load). Per tile: LDS table lookups -> workgroup scan of bit
@@ -482,6 +496,7 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
                                                    const int *__restrict__ err)
 {
     __shared__ uint2 s_tab[256];
+    __shared__ uint8_t s_nb8[256];   // bit lengths alone: pass A reads 1 byte, not 8
     __shared__ __attribute__((aligned(16))) uint32_t s_stage[PACK_BLK_WORDS];
     __shared__ uint32_t s_scan[4];
     __shared__ uint32_t s_tot[PACK_PIECES][4];
@@ -490,6 +505,8 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
     // output buffer smaller than the planned stream -> write nothing
     if (err[0] != 0 || ((bit_base & 31) + block_off[nblocks] + 31) / 32 > words_cap) return;
     s_tab[t] = make_uint2(T->code[t], T->nbits[t]);
+    s_nb8[t] = (uint8_t)T->nbits[t];
+    const bool vec_out = ((uintptr_t)out & 15) == 0;
     const uint64_t word_base = bit_base >> 5;
     const uint32_t slog = sync_syms ? (uint32_t)__builtin_ctz(sync_syms) : 0u;   // S is a power of two
     __syncthreads();
@@ -510,36 +527,41 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
                 blkv[k] = *reinterpret_cast<const uint4 *>(in + blk_start + (uint64_t)k * PACK_TILE + (uint64_t)t * 16);
         }
         const uint32_t nw_blk = (uint32_t)(((blk_abs & 31) + (block_off[b + 1] - block_off[b]) + 31) >> 5);
-        if (full && nw_blk <= PACK_BLK_WORDS) {
+        // stage origin: the block's first word rounded down to a 16-B boundary of `out`, so
+        // the store phase moves whole uint4s (sh = stage index of the block's first word)
+        const uint32_t sh = vec_out ? (uint32_t)((blk_first_word - word_base) & 3) : 0u;
+        if (full && nw_blk + sh <= PACK_BLK_WORDS) {
             // ---- fast path: the whole block at once, 3 barriers ----
-            // lane t of wave w codes piece k = bytes [k*4096 + t*16, +16) of the block
+            // lane t of wave w codes piece k = bytes [k*4096 + t*16, +16) of the block, as
+            // two halves of 8 codes, each gathered into a 64-bit register (no per-code
+            // flush) and OR-ed into the stage as at most 3 words. A half of more than 64
+            // bits takes the per-code flush loop instead (exact, rare on text).
             const int lane = t & 63, wid = t >> 6;
-            for (uint32_t i = 4u * t; i < nw_blk; i += 1024u)
+            const uint32_t nwa = sh + nw_blk;
+            for (uint32_t i = 4u * t; i < nwa; i += 1024u)
                 *reinterpret_cast<uint4 *>(&s_stage[i]) = make_uint4(0u, 0u, 0u, 0u);
-            uint32_t Tk[PACK_PIECES], Ik[PACK_PIECES];
+            uint32_t Tk[PACK_PIECES], Hk[PACK_PIECES], Ik[PACK_PIECES];
 #pragma unroll
             for (int k = 0; k < PACK_PIECES; ++k) {
                 const uint32_t w4[4] = {blkv[k].x, blkv[k].y, blkv[k].z, blkv[k].w};
-                uint32_t s = 0;
+                uint32_t s0 = 0, s1 = 0;
 #pragma unroll
-                for (int i = 0; i < 16; ++i) s += s_tab[(w4[i >> 2] >> (8 * (i & 3))) & 255u].y;
-                Tk[k] = s;
-                Ik[k] = s;
+                for (int i = 0; i < 8; ++i) s0 += s_nb8[(w4[i >> 2] >> (8 * (i & 3))) & 255u];
+#pragma unroll
+                for (int i = 8; i < 16; ++i) s1 += s_nb8[(w4[i >> 2] >> (8 * (i & 3))) & 255u];
+                Hk[k] = s0;
+                Tk[k] = s0 + s1;
                 __builtin_amdgcn_sched_barrier(0);
             }
 #pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-#pragma unroll
-                for (int k = 0; k < PACK_PIECES; ++k) {
-                    const uint32_t y = __shfl_up(Ik[k], d, 64);
-                    if (lane >= d) Ik[k] += y;
-                }
-            }
+            for (int k = 0; k < PACK_PIECES; ++k) Ik[k] = wave_scan_incl(Tk[k]);
             if (lane == 63) {
 #pragma unroll
                 for (int k = 0; k < PACK_PIECES; ++k) s_tot[k][wid] = Ik[k];
             }
             __syncthreads();
+            const uint64_t org = (blk_first_word - sh) << 5;   // absolute bit of stage bit 0
+            const uint32_t cm = sync_syms >> 4;                 // lanes per sync chunk
             uint64_t run = blk_abs;   // absolute bit where piece k starts
 #pragma unroll
             for (int k = 0; k < PACK_PIECES; ++k) {
@@ -554,46 +576,78 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
                 run += kt;
                 const uint64_t p = blk_start + (uint64_t)k * PACK_TILE + (uint64_t)t * 16;
                 if (sync_len != nullptr) {
-                    uint32_t cb = Tk[k];
-                    for (uint32_t d = 1; d < (sync_syms >> 4); d <<= 1) cb += __shfl_xor(cb, (int)d, 64);
+                    // chunk bits = inclusive scan at the chunk's last lane - exclusive at its first
+                    const uint32_t last = (cm == 4) ? (uint32_t)__builtin_amdgcn_update_dpp(0, (int)Ik[k], 0xff, 0xf, 0xf, false)
+                                                    : (uint32_t)__shfl((int)Ik[k], lane | (int)(cm - 1), 64);
                     if ((p & (uint64_t)(sync_syms - 1)) == 0) {
-                        sync_len[p >> slog] = (uint16_t)cb;
+                        sync_len[p >> slog] = (uint16_t)(last - (Ik[k] - Tk[k]));
                         if ((p & ((uint64_t)sync_syms * DC_SYNC_GROUP - 1)) == 0)
                             sync_base[p >> (slog + DC_SYNC_GROUP_LOG)] = As;
                     }
                 }
                 uint32_t w4[4] = {blkv[k].x, blkv[k].y, blkv[k].z, blkv[k].w};
-                // opaque copy: stops the compiler from keeping pass A's 128 lookup addresses live
+                // opaque copy: stops the compiler from keeping pass A's lookup addresses live
                 asm volatile("" : "+v"(w4[0]), "+v"(w4[1]), "+v"(w4[2]), "+v"(w4[3]));
-                uint64_t acc = 0;
-                uint32_t nacc = (uint32_t)(As & 31);
-                uint32_t wi = (uint32_t)((As >> 5) - blk_first_word);
-                bool first = true;
+                const uint32_t rel = (uint32_t)(As - org);
+                if (Hk[k] <= 64u && Tk[k] - Hk[k] <= 64u) {
 #pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    const uint2 e = s_tab[(w4[i >> 2] >> (8 * (i & 3))) & 255u];
-                    acc = (acc << e.y) | e.x;
-                    nacc += e.y;
-                    if (nacc >= 32) {
-                        nacc -= 32;
-                        const uint32_t word = (uint32_t)(acc >> nacc);
-                        if (first) atomicOr(&s_stage[wi], word);
-                        else s_stage[wi] = word;
-                        first = false;
-                        ++wi;
+                    for (int h = 0; h < 2; ++h) {
+                        uint64_t acc = 0;
+#pragma unroll
+                        for (int i = 8 * h; i < 8 * h + 8; ++i) {
+                            const uint2 e = s_tab[(w4[i >> 2] >> (8 * (i & 3))) & 255u];
+                            acc = (acc << e.y) | e.x;
+                        }
+                        const uint32_t Th = h ? Tk[k] - Hk[k] : Hk[k];
+                        const uint32_t pos = h ? rel + Hk[k] : rel;
+                        // left-justify, then split over the (up to) 3 stage words it touches
+                        const uint64_t al = Th ? acc << (64u - Th) : 0ull;
+                        const uint32_t hi = (uint32_t)(al >> 32), lo = (uint32_t)al, r = pos & 31u, wi = pos >> 5;
+                        atomicOr(&s_stage[wi], hi >> r);
+                        if (r + Th > 32u) atomicOr(&s_stage[wi + 1], __builtin_amdgcn_alignbit(hi, lo, r));
+                        if (r + Th > 64u) atomicOr(&s_stage[wi + 2], __builtin_amdgcn_alignbit(lo, 0u, r));
                     }
+                } else {
+                    uint64_t acc = 0;
+                    uint32_t nacc = rel & 31u;
+                    uint32_t wi = rel >> 5;
+#pragma unroll 1
+                    for (int i = 0; i < 16; ++i) {
+                        const uint2 e = s_tab[(w4[i >> 2] >> (8 * (i & 3))) & 255u];
+                        acc = (acc << e.y) | e.x;
+                        nacc += e.y;
+                        if (nacc >= 32) {
+                            nacc -= 32;
+                            atomicOr(&s_stage[wi], (uint32_t)(acc >> nacc));
+                            ++wi;
+                        }
+                    }
+                    if (nacc > 0) atomicOr(&s_stage[wi], (uint32_t)(acc << (32 - nacc)));
                 }
-                if (nacc > 0) atomicOr(&s_stage[wi], (uint32_t)(acc << (32 - nacc)));
                 __builtin_amdgcn_sched_barrier(0);   // keep the pieces' lookups from being hoisted
             }
             __syncthreads();
-            // words 0 and (when the next block starts inside it) nw_blk-1 are shared with the
-            // neighbour blocks: OR-ed by one lane each; the rest are plain coalesced stores
-            const uint32_t last_plain = ((run & 31) != 0) ? nw_blk - 1 : nw_blk;
-            uint32_t *dst = out + (blk_first_word - word_base);
-            for (uint32_t i = t + 1; i < last_plain; i += 256) dst[i] = bswap32(s_stage[i]);
-            if (t == 0) atomicOr(&dst[0], bswap32(s_stage[0]));
-            if (t == 64 && last_plain < nw_blk && nw_blk > 1) atomicOr(&dst[nw_blk - 1], bswap32(s_stage[nw_blk - 1]));
+            // stage word sh = the block's first word, shared with the previous block; the last
+            // word is shared with the next one when the block ends inside it: those two are
+            // OR-ed into HBM by one lane each, the rest are plain stores (uint4 where whole)
+            const uint32_t last_plain = ((run & 31) != 0) ? nwa - 1 : nwa;   // plain: [sh+1, last_plain)
+            uint32_t *dst = out + (blk_first_word - word_base) - sh;
+            if (vec_out) {
+                const uint32_t nq = last_plain >> 2;   // uint4 q covers stage words [4q, 4q+4)
+                for (uint32_t q = 1 + t; q < nq; q += 256) {
+                    const uint4 v = *reinterpret_cast<const uint4 *>(&s_stage[4 * q]);
+                    *reinterpret_cast<uint4 *>(dst + 4 * q) = make_uint4(bswap32(v.x), bswap32(v.y), bswap32(v.z), bswap32(v.w));
+                }
+                // head: words sh+1..3 of uint4 0; tail: words of the last, partial uint4
+                const uint32_t hend = last_plain < 4u ? last_plain : 4u;
+                if (t < 4 && (uint32_t)t > sh && (uint32_t)t < hend) dst[t] = bswap32(s_stage[t]);
+                const uint32_t tb = nq > 0 ? 4 * nq : 4u;
+                if (t >= 8 && t < 12 && tb + (t - 8) < last_plain) dst[tb + (t - 8)] = bswap32(s_stage[tb + (t - 8)]);
+            } else {
+                for (uint32_t i = t + 1; i < last_plain; i += 256) dst[i] = bswap32(s_stage[i]);
+            }
+            if (t == 0) atomicOr(&dst[sh], bswap32(s_stage[sh]));
+            if (t == 64 && last_plain < nwa && nw_blk > 1) atomicOr(&dst[nwa - 1], bswap32(s_stage[nwa - 1]));
             __syncthreads();
             continue;
         }
@@ -984,19 +1038,6 @@ struct Dec8Lds {
 
 static __device__ __forceinline__ uint32_t brev8(uint32_t v) { return __builtin_bitreverse32(__builtin_bswap32(v)); }
 
-// inclusive wave64 prefix sum in DPP (VALU only: __shfl_up is ds_bpermute, i.e. an LDS
-// instruction queued behind the decoder's LUT reads): row_shr 1/2/4/8 within each row of
-// 16 lanes, then row_bcast:15 and row_bcast:31 across rows (GFX9 DPP)
-static __device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x)
-{
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);   // row_shr:1
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);   // row_shr:2
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);   // row_shr:4
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);   // row_shr:8
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);   // row_bcast:15
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);   // row_bcast:31
-    return x;
-}
 
 // exact slow decode of the code at the start of an LSB-first 64-bit window (lo, hi):
 // returns nbits | sym << 8; an invalid code sets *bad and returns 0

@@ -196,6 +196,33 @@ def test_pack_at_bit_offset(torch_cuda, codec, bit_base):
     assert np.array_equal(out.cpu().numpy(), x)
 
 
+@pytest.mark.parametrize("case", ["unaligned-out", "long-halves"])
+def test_pack_store_paths(torch_cuda, codec, case):
+    """k_huff_pack fast path: word stores when the output is not 16-B aligned, and the
+    per-code flush fallback for 8-code halves of more than 64 bits."""
+    torch = torch_cuda
+    from data_compression_amd import synth
+    if case == "unaligned-out":
+        x = synth.enwik_like(200_000, seed=21)
+    else:
+        x = _chain_stream(20, 3)   # codes up to 20 bits: many halves above 64 bits
+    L, el, ev, code, nb, mx = _oracle_encode(x, 2)
+    payload, bits, idx = orc.huff_pack(x, code, nb, sync_syms=64)
+    xt = torch.from_numpy(x).cuda()
+    tab = codec.table(codec.hist(xt), 2)
+    assert int(codec.plan(tab).item()) == bits
+    nw = codec.words_needed(0, bits)
+    shift = 1 if case == "unaligned-out" else 0
+    buf = torch.zeros(nw + 8, dtype=torch.int32, device="cuda")
+    words = buf[shift: shift + nw]
+    sync = codec.alloc_sync(x.size, 64)
+    codec.pack(xt, tab, 0, words, sync, 64)
+    assert codec.pack_status(tab) == 0
+    got = words.cpu().numpy().view(np.uint8)[: len(payload)]
+    assert np.array_equal(got, payload), case
+    assert not buf[:shift].any() and not buf[shift + nw:].any()
+
+
 @pytest.mark.parametrize("S", [16, 128, 1024])   # 1024: spans exceed the LDS stage -> HBM path
 def test_decode_of_oracle_stream(torch_cuda, codec, S):
     torch = torch_cuda
