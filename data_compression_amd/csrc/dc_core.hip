@@ -1127,7 +1127,11 @@ static __device__ __forceinline__ void d8_batch(const uint32_t *const *st, uint3
 #pragma unroll
         for (int j = 0; j < NC; ++j) {
             x[j] = (uint32_t)(win[j] >> off[j]);
+#ifdef DC_DIAG_LUTMASK   // timing ablation only: lookups confined to the first entries
+            e[j] = tb.lut[x[j] & DC_DIAG_LUTMASK];
+#else
             e[j] = tb.lut[x[j] & ((1u << DC_LUT_BITS) - 1)];
+#endif
         }
 #pragma unroll
         for (int j = 0; j < NC; ++j) mn = min(mn, e[j] & 255u);
@@ -1149,33 +1153,55 @@ static __device__ __forceinline__ void d8_batch(const uint32_t *const *st, uint3
     for (int j = 0; j < NC; ++j) c[j] += off[j];
 }
 
-// the 16 batches of a 64-symbol chunk, unrolled by template recursion; every 4 batches
-// the lane's 16 output bytes per chain are stored (uint4 at chunk + 16q)
-template <int NC, int Q>
-struct D8Batches {
+// The 16 batches of a 64-symbol chunk as two halves of 8, unrolled by template recursion.
+// After each half a lane holds pieces 2H and 2H+1 (16 B each) of its own chunk. Stored as
+// they are (lane = chunk, 64 B apart) every wave store would touch 32 cache lines with 32 B
+// each; the L2 request rate then bounds the decoder (a contiguous-store ablation ran 0.72 ->
+// 0.48 ms on 1 GiB C2). So each 4-lane quad swaps pieces by DPP first (quad_perm): store A
+// gives lanes 4m+p piece 2H+(p&1) of chunk 4m+(p>>1), store B the same of chunk 4m+2+(p>>1):
+// 32 contiguous bytes per lane pair, 16 lines of 64 B per store.
+template <int NC, int H>
+struct D8Halves {
     static __device__ __forceinline__ void run(const uint32_t *const *st, uint32_t *c, uint4 *const *dst,
-                                               const D8Tabs &tb, int &giveup)
+                                               const D8Tabs &tb, int &giveup, bool odd)
     {
-        uint32_t o0[NC], o1[NC], o2[NC], o3[NC];
-        d8_batch<NC>(st, c, o0, tb, giveup);
-        d8_batch<NC>(st, c, o1, tb, giveup);
-        d8_batch<NC>(st, c, o2, tb, giveup);
-        d8_batch<NC>(st, c, o3, tb, giveup);
+        uint32_t a0[NC], a1[NC], a2[NC], a3[NC], b0[NC], b1[NC], b2[NC], b3[NC];
+        d8_batch<NC>(st, c, a0, tb, giveup);
+        d8_batch<NC>(st, c, a1, tb, giveup);
+        d8_batch<NC>(st, c, a2, tb, giveup);
+        d8_batch<NC>(st, c, a3, tb, giveup);
+        d8_batch<NC>(st, c, b0, tb, giveup);
+        d8_batch<NC>(st, c, b1, tb, giveup);
+        d8_batch<NC>(st, c, b2, tb, giveup);
+        d8_batch<NC>(st, c, b3, tb, giveup);
 #pragma unroll
         for (int j = 0; j < NC; ++j) {
 #ifdef DC_DIAG_NOSTORE
-            asm volatile("" ::"v"(o0[j]), "v"(o1[j]), "v"(o2[j]), "v"(o3[j]));
+            asm volatile("" ::"v"(a0[j]), "v"(a1[j]), "v"(a2[j]), "v"(a3[j]), "v"(b0[j]), "v"(b1[j]), "v"(b2[j]),
+                         "v"(b3[j]));
 #else
-            dst[j][Q] = make_uint4(o0[j], o1[j], o2[j], o3[j]);
+            const uint32_t a[4] = {a0[j], a1[j], a2[j], a3[j]}, b[4] = {b0[j], b1[j], b2[j], b3[j]};
+            uint32_t A[4], B[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint32_t xa = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)a[i], 0x50, 0xf, 0xf, false);   // [0,0,1,1]
+                const uint32_t xb = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)b[i], 0x50, 0xf, 0xf, false);
+                const uint32_t ya = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)a[i], 0xfa, 0xf, 0xf, false);   // [2,2,3,3]
+                const uint32_t yb = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)b[i], 0xfa, 0xf, 0xf, false);
+                A[i] = odd ? xb : xa;
+                B[i] = odd ? yb : ya;
+            }
+            dst[j][2 * H] = make_uint4(A[0], A[1], A[2], A[3]);
+            dst[j][2 * H + 8] = make_uint4(B[0], B[1], B[2], B[3]);
 #endif
         }
-        D8Batches<NC, Q + 1>::run(st, c, dst, tb, giveup);
+        D8Halves<NC, H + 1>::run(st, c, dst, tb, giveup, odd);
     }
 };
 template <int NC>
-struct D8Batches<NC, 4> {
+struct D8Halves<NC, 2> {
     static __device__ __forceinline__ void run(const uint32_t *const *, uint32_t *, uint4 *const *, const D8Tabs &,
-                                               int &)
+                                               int &, bool)
     {
     }
 };
@@ -1191,39 +1217,44 @@ extern "C" int dc_diag_read(void *h, size_t bytes)
 #define D8_STAMP(v)
 #endif
 
+typedef __attribute__((address_space(4))) const uint64_t c_u64;   // scalar (s_load) reads
+
 template <int NC>
-struct D8Meta { uint32_t len[NC]; uint64_t base[NC]; };   // sync index of one tuple (per lane)
+struct D8Meta { uint32_t len[NC]; uint64_t base[NC]; };   // sync index of one tuple: len per lane, base uniform
 template <int NC>
-struct D8Geo {                                             // where a tuple's spans and chunks lie
-    uint64_t g0;
-    uint64_t rel[NC], wo[NC];
-    uint32_t off[NC], lead[NC], last[NC];
+struct D8Geo {            // where a tuple's spans and chunks lie; all uniform except off
+    uint32_t g0;          // first group
+    uint32_t wo[NC];      // first staged word (16-B aligned), relative to word_base
+    uint32_t lead[NC];    // stage bit of the group's first chunk
+    uint32_t last[NC];    // last uint4 of the stage
+    uint32_t off[NC];     // this lane's chunk: bit offset inside the group span
     bool fast;
 };
 
 template <int NC>
-static __device__ __forceinline__ void d8_load_meta(D8Meta<NC> &m, uint64_t tp, uint64_t ntuples, uint64_t ngroups,
-                                                    uint64_t nchunks, int lane, const uint16_t *__restrict__ sync_len,
+static __device__ __forceinline__ void d8_load_meta(D8Meta<NC> &m, uint32_t tp, uint32_t ngroups, uint32_t nchunks,
+                                                    int lane, const uint16_t *__restrict__ sync_len,
                                                     const uint64_t *__restrict__ sync_base)
 {
     // unconditional loads of clamped indices: a conditional load would make the compiler
     // wait for it (and for every older load: the prefetched spans) at the join; the
-    // validity mask is applied where the values are used, an iteration later
+    // validity mask is applied where the values are used, an iteration later. The group
+    // bases are wave-uniform: scalar loads (lgkmcnt, SGPRs), no vector registers.
 #pragma unroll
     for (int j = 0; j < NC; ++j) {
-        const uint64_t g = tp * NC + j, ch = g * DC_SYNC_GROUP + lane;
+        const uint32_t g = tp * NC + j, ch = g * DC_SYNC_GROUP + lane;
         m.len[j] = sync_len[min(ch, nchunks - 1)];
-        m.base[j] = sync_base[min(g, ngroups - 1)];
+        m.base[j] = ((c_u64 *)sync_base)[min(g, ngroups - 1)];
     }
 }
 
 template <int NC>
-static __device__ __forceinline__ void d8_geometry(D8Geo<NC> &g, const D8Meta<NC> &m, uint64_t tp, uint64_t ntuples,
-                                                   uint64_t n, uint64_t nwords, uint64_t word_base, int lane)
+static __device__ __forceinline__ void d8_geometry(D8Geo<NC> &g, const D8Meta<NC> &m, uint32_t tp, uint32_t ntuples,
+                                                   uint64_t n, uint32_t nchunks, uint64_t nwords, uint64_t word_base,
+                                                   int lane)
 {
     constexpr uint64_t GSYM = DC_SYNC_GROUP * 64;
     g.g0 = tp * NC;
-    const uint64_t nchunks = (n + 63) / 64;
     uint32_t in[NC], len[NC];
 #pragma unroll
     for (int j = 0; j < NC; ++j) {   // branch-free mask (a branch here makes the compiler drain vmcnt)
@@ -1233,17 +1264,17 @@ static __device__ __forceinline__ void d8_geometry(D8Geo<NC> &g, const D8Meta<NC
     }
 #pragma unroll
     for (int j = 0; j < NC; ++j) in[j] = wave_scan_incl(in[j]);
-    bool fast = tp < ntuples && (g.g0 + NC) * GSYM <= n;
+    bool fast = tp < ntuples && (uint64_t)(g.g0 + NC) * GSYM <= n;
 #pragma unroll
     for (int j = 0; j < NC; ++j) {
         const uint32_t span = __builtin_amdgcn_readlane(in[j], 63);
         g.off[j] = in[j] - len[j];
-        g.rel[j] = m.base[j] - (word_base << 5);
-        g.wo[j] = (g.rel[j] >> 5) & ~3ull;
-        g.lead[j] = (uint32_t)(g.rel[j] - (g.wo[j] << 5));
+        const uint64_t rel = m.base[j] - (word_base << 5);
+        g.wo[j] = (uint32_t)(rel >> 5) & ~3u;
+        g.lead[j] = (uint32_t)rel & 127u;
         const uint32_t nw = (g.lead[j] + span) / 32 + 3;
         g.last[j] = (nw + 3) / 4 - 1;
-        fast = fast && nw + 4 <= D8_STAGE_WORDS && g.wo[j] + nw + 4 <= nwords;
+        fast = fast && nw + 4 <= D8_STAGE_WORDS && (uint64_t)g.wo[j] + nw + 4 <= nwords;
     }
     g.fast = fast;
 }
@@ -1257,7 +1288,7 @@ static __device__ __forceinline__ void d8_issue(uint4 (&v)[NC][5], const D8Geo<N
     for (int k = 0; k < 5; ++k) {
 #pragma unroll
         for (int j = 0; j < NC; ++j) {
-            const uint4 *src = reinterpret_cast<const uint4 *>(in + (g.fast ? g.wo[j] : 0ull));
+            const uint4 *src = reinterpret_cast<const uint4 *>(in + (g.fast ? g.wo[j] : 0u));
             v[j][k] = src[g.fast ? min((uint32_t)(lane + 64 * k), g.last[j]) : 0u];
         }
     }
@@ -1274,22 +1305,25 @@ static __device__ __forceinline__ void d8_issue(uint4 (&v)[NC][5], const D8Geo<N
 // resets the heads for the next launch on the stream.
 #define D8_STATIC_PCT 60
 #define D8_QSTRIDE 1024   /* u32 between heads */
-#define D8_QWORDS (9 * D8_QSTRIDE)
+#define D8_FIX_CNT (9 * D8_QSTRIDE)                /* tuples queued for the exact redo        */
+#define D8_FIX_DONE (10 * D8_QSTRIDE)              /* redo waves finished                    */
+#define D8_TRASH_OFF (11 * D8_QSTRIDE)             /* u32 offset of the trash slots: 2 x 64 x 256 B */
+#define D8_QWORDS (D8_TRASH_OFF + 2 * 64 * 256 / 4)
 
 struct D8Sched {
-    uint64_t Ts, Dh, ntuples;   // static tuples, slice size, all tuples
-    uint64_t wid, P;            // wave id, waves in the grid
+    uint32_t Ts, Dh, ntuples;   // static tuples, slice size, all tuples
+    uint32_t wid, P;            // wave id, waves in the grid
     uint32_t k, Ks;             // static tuples taken / per wave
     int head, tried;            // slice being drained, slices given up
     bool dyn;                   // pending value is a dequeue result
     uint32_t pend;              // lane 0: dequeued index
-    uint64_t spend;             // static index
+    uint32_t spend;             // static index
 };
 
 static __device__ __forceinline__ void d8_fetch(D8Sched &s, uint32_t *__restrict__ queue, int lane)
 {
     if (s.k < s.Ks) {
-        s.spend = s.wid + (uint64_t)s.k * s.P;
+        s.spend = s.wid + s.k * s.P;
         ++s.k;
         s.dyn = false;
     } else {
@@ -1298,24 +1332,57 @@ static __device__ __forceinline__ void d8_fetch(D8Sched &s, uint32_t *__restrict
     }
 }
 
-static __device__ __forceinline__ uint64_t d8_resolve(D8Sched &s, uint32_t *__restrict__ queue, uint32_t *exhausted,
-                                                      int lane)
+// a dequeued index past its slice: mark the slice empty, then probe the others in turn
+static __device__ uint32_t d8_resolve_retry(D8Sched &s, uint32_t *__restrict__ queue, uint32_t *exhausted, int lane)
 {
-    if (!s.dyn) return s.spend;
     while (s.tried < 8) {
-        const uint64_t i = (uint32_t)__builtin_amdgcn_readlane((int)s.pend, 0);
-        const uint64_t lo = s.Ts + (uint64_t)s.head * s.Dh;
-        const uint64_t hi = min(lo + s.Dh, s.ntuples);
-        if (lo + i < hi) return lo + i;
         if (lane == 0) atomicOr(exhausted, 1u << s.head);
         ++s.tried;
         s.head = (s.head + 1) & 7;
         // skip slices this workgroup already found empty
         const uint32_t ex = __builtin_amdgcn_readfirstlane(__atomic_load_n(exhausted, __ATOMIC_RELAXED));
         while (s.tried < 8 && ((ex >> s.head) & 1u)) { ++s.tried; s.head = (s.head + 1) & 7; }
-        if (s.tried < 8 && lane == 0) s.pend = atomicAdd(queue + s.head * D8_QSTRIDE, 1u);
+        if (s.tried >= 8) break;
+        if (lane == 0) s.pend = atomicAdd(queue + s.head * D8_QSTRIDE, 1u);
+        const uint32_t i = (uint32_t)__builtin_amdgcn_readlane((int)s.pend, 0);
+        const uint32_t lo = s.Ts + (uint32_t)s.head * s.Dh;
+        const uint32_t hi = min(lo + s.Dh, s.ntuples);
+        if (i < hi - min(lo, hi)) return lo + i;
     }
     return s.ntuples;
+}
+
+// The common case is loop-free, so the compiler's wait for the dequeue issued an iteration
+// earlier counts only the ops issued since (spans, output stores): vmcnt(N), not vmcnt(0)
+// (a loop here would make it drain every outstanding store first).
+static __device__ __forceinline__ uint32_t d8_resolve(D8Sched &s, uint32_t *__restrict__ queue, uint32_t *exhausted,
+                                                      int lane)
+{
+    if (!s.dyn) return s.spend;
+    if (s.tried < 8) {
+        const uint32_t i = (uint32_t)__builtin_amdgcn_readlane((int)s.pend, 0);
+        const uint32_t lo = s.Ts + (uint32_t)s.head * s.Dh;
+        const uint32_t hi = min(lo + s.Dh, s.ntuples);
+        if (i < hi - min(lo, hi)) return lo + i;
+    }
+    return d8_resolve_retry(s, queue, exhausted, lane);
+}
+
+// byte-wise bit reversal of a tuple's spans (registers) into its LDS stage rows
+template <int NC>
+static __device__ __forceinline__ void d8_stage(const D8Geo<NC> &cur, const uint4 (&v)[NC][5], uint32_t *const *stw,
+                                                int lane)
+{
+    if (!cur.fast) return;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        const uint32_t i = lane + 64 * k;
+#pragma unroll
+        for (int j = 0; j < NC; ++j)
+            if (i <= cur.last[j])
+                reinterpret_cast<uint4 *>(stw[j])[i] =
+                    make_uint4(brev8(v[j][k].x), brev8(v[j][k].y), brev8(v[j][k].z), brev8(v[j][k].w));
+    }
 }
 
 // NW waves per workgroup (one workgroup per CU), NC chains per wave: wave w of workgroup b
@@ -1326,10 +1393,11 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode8(const uint32_t *__rest
                                                           const uint16_t *__restrict__ sync_len, uint64_t n,
                                                           uint64_t nwords, const dc_dtable *__restrict__ T,
                                                           uint8_t *__restrict__ out, int *__restrict__ err,
-                                                          uint32_t *__restrict__ queue, uint32_t static_pct)
+                                                          uint32_t *__restrict__ queue, uint32_t static_pct,
+                                                          uint32_t *__restrict__ fix_list)
 {
-    static_assert(NW * NC == D8_CHAINS && NW <= D8_MAX_WAVES, "stage slots");
-    constexpr uint32_t S = 64, GSYM = DC_SYNC_GROUP * S;
+    static_assert(NW * NC <= D8_CHAINS && NW <= D8_MAX_WAVES, "stage slots");
+    constexpr uint32_t S = 64;
     constexpr int NT = NW * 64;
     __shared__ Dec8Lds L;
     const int t = threadIdx.x, lane = t & 63;
@@ -1339,13 +1407,13 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode8(const uint32_t *__rest
     int bad = 0;
     // ---- tables: first level (bit-reversed index of the MSB-first table), escape
     // prefixes numbered in index order, second level decoded exactly once per entry
-    constexpr int PER = (1 << DC_LUT_BITS) / NT;
+    constexpr int PER = ((1 << DC_LUT_BITS) + NT - 1) / NT;   // entries per thread (last ones may be past the end)
     uint32_t e1[PER];
     uint32_t nesc = 0;
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
         const uint32_t i = (uint32_t)(t * PER + j);
-        const uint32_t e = T->lut[__builtin_bitreverse32(i) >> (32 - DC_LUT_BITS)];
+        const uint32_t e = i < (1u << DC_LUT_BITS) ? T->lut[__builtin_bitreverse32(i) >> (32 - DC_LUT_BITS)] : 1u;
         e1[j] = e ? (E_BITS0(e) | ((e & 255u) << 8)) : 0u;
         nesc += e ? 0u : 1u;
     }
@@ -1371,8 +1439,12 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode8(const uint32_t *__rest
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
         const uint32_t i = (uint32_t)(t * PER + j);
+        if (i >= (1u << DC_LUT_BITS)) break;
         if (!e1[j] && id < 256) L.esc_pre[id] = (uint16_t)i;
         L.lut[i] = (uint16_t)(e1[j] ? e1[j] : ((id++ & 255u) << 8));
+#ifdef DC_DIAG_SYNTH_LUT   // timing ablation only: every window is a 4-bit code (garbage output)
+        L.lut[i] = (uint16_t)(4u | ((i & 255u) << 8));
+#endif
     }
     __syncthreads();
     if (l2ok) {
@@ -1387,18 +1459,19 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode8(const uint32_t *__rest
     __syncthreads();
     const D8Tabs tb{L.lut, L.lut2, l2ok ? K : 0u, (1u << K) - 1};
 
-    const uint64_t nchunks = (n + S - 1) / S;
-    const uint64_t ngroups = (nchunks + DC_SYNC_GROUP - 1) / DC_SYNC_GROUP;
-    const uint64_t ntuples = (ngroups + NC - 1) / NC;
+    // the launcher guarantees n < 2^37 (chunk and tuple indices fit 32 bits)
+    const uint32_t nchunks = (uint32_t)((n + S - 1) / S);
+    const uint32_t ngroups = (nchunks + DC_SYNC_GROUP - 1) / DC_SYNC_GROUP;
+    const uint32_t ntuples = (ngroups + NC - 1) / NC;
     const uint64_t word_base = bit_base >> 5;
     const uint32_t *st[NC];
     uint32_t *stw[NC];
 #pragma unroll
     for (int j = 0; j < NC; ++j) { stw[j] = L.stage[wv * NC + j]; st[j] = stw[j]; }
-    const uint64_t stride = (uint64_t)gridDim.x * NW;
+    const uint32_t stride = gridDim.x * NW;
     // Software pipeline (per wave, one tuple of NC groups per iteration): while tuple i
     // decodes, the spans of tuple i+1 are in flight into registers and the sync index of
-    // tuple i+2 too, so no iteration waits for a global round trip (nor for its stores).
+    // tuple i+2 too, so no iteration waits for a global round trip.
     // The span loads are issued for every tuple (clamped to word 0 when it is not staged),
     // so the prefetch registers never need merging.
     static_assert((D8_STAGE_WORDS / 4 + 63) / 64 <= 5, "stage larger than 5 KiB");
@@ -1412,86 +1485,87 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode8(const uint32_t *__rest
     D8Sched sc;
     sc.ntuples = ntuples;
     sc.P = stride;
-    sc.wid = (uint64_t)blockIdx.x * NW + wv;
-    sc.Ks = (uint32_t)(ntuples * static_pct / 100 / stride);
-    sc.Ts = (uint64_t)sc.Ks * stride;
+    sc.wid = blockIdx.x * NW + wv;
+    sc.Ks = (uint32_t)((uint64_t)ntuples * static_pct / 100 / stride);
+    sc.Ts = sc.Ks * stride;
     sc.Dh = (ntuples - sc.Ts + 7) / 8;
     sc.k = 0;
     sc.head = blockIdx.x & 7;
     sc.tried = 0;
     sc.pend = 0;
     d8_fetch(sc, queue, lane);
-    uint64_t tp = d8_resolve(sc, queue, &L.exhausted, lane);
+    uint32_t tp = d8_resolve(sc, queue, &L.exhausted, lane);
     d8_fetch(sc, queue, lane);
-    uint64_t t1 = d8_resolve(sc, queue, &L.exhausted, lane);
+    uint32_t t1 = d8_resolve(sc, queue, &L.exhausted, lane);
     d8_fetch(sc, queue, lane);
-    d8_load_meta<NC>(m2, tp, ntuples, ngroups, nchunks, lane, sync_len, sync_base);
-    d8_geometry<NC>(g, m2, tp, ntuples, n, nwords, word_base, lane);
+    // Rotated software pipeline (per wave): the loop body decodes the staged tuple, then
+    // stages the next one from registers and issues the loads of the one after. The span
+    // loads are thereby always older than the decode's 32 output stores (vector memory ops
+    // retire in issue order), so staging waits for vmcnt(32), not for the stores to drain.
+    // That needs the 32 stores on every path: a tuple the fast decoder cannot take (partial
+    // group, over-long span) still runs it, on whatever the stage holds, with its stores sent
+    // to the trash rows wherever a chunk is not whole inside the output; the exact redo
+    // rewrites the real bytes afterwards (same wave, program order).
+    uint4 *const trash = reinterpret_cast<uint4 *>(queue + D8_TRASH_OFF) + (size_t)lane * 16;   // 256 B per lane and chain
+    d8_load_meta<NC>(m2, tp, ngroups, nchunks, lane, sync_len, sync_base);
+    d8_geometry<NC>(g, m2, tp, ntuples, n, nchunks, nwords, word_base, lane);
     d8_issue<NC>(v, g, in, lane);
-    d8_load_meta<NC>(m1, t1, ntuples, ngroups, nchunks, lane, sync_len, sync_base);
+    d8_load_meta<NC>(m1, t1, ngroups, nchunks, lane, sync_len, sync_base);
+    cur = g;
+    d8_stage<NC>(cur, v, stw, lane);
+    d8_geometry<NC>(g, m1, t1, ntuples, n, nchunks, nwords, word_base, lane);
+    uint32_t t2 = d8_resolve(sc, queue, &L.exhausted, lane);
+    d8_load_meta<NC>(m1, t2, ngroups, nchunks, lane, sync_len, sync_base);
+    d8_fetch(sc, queue, lane);
+    d8_issue<NC>(v, g, in, lane);
     while (tp < ntuples) {
-        D8_STAMP(s0);
-        cur = g;
-        if (cur.fast) {   // byte-wise bit reversal into the LDS stage
+        __builtin_amdgcn_wave_barrier();
+        D8_STAMP(s1);
+        uint32_t c[NC];
+        uint4 *dst[NC];
 #pragma unroll
-            for (int k = 0; k < 5; ++k) {
-                const uint32_t i = lane + 64 * k;
-#pragma unroll
-                for (int j = 0; j < NC; ++j)
-                    if (i <= cur.last[j])
-                        reinterpret_cast<uint4 *>(stw[j])[i] =
-                            make_uint4(brev8(v[j][k].x), brev8(v[j][k].y), brev8(v[j][k].z), brev8(v[j][k].w));
-            }
+        for (int j = 0; j < NC; ++j) {
+            // this lane stores chunk (lane & ~3) | ((lane >> 1) & 1) of the group (+2 for store
+            // B), pieces (lane & 1) + 2H (D8Halves); a tuple that is not fast (its chunks are
+            // all rewritten by the redo) stores into the lane's trash slot instead
+            const uint64_t ch = (uint64_t)(cur.g0 + j) * DC_SYNC_GROUP + (uint32_t)((lane & ~3) | ((lane >> 1) & 1));
+            c[j] = cur.fast ? cur.lead[j] + cur.off[j] : 0u;
+            dst[j] = cur.fast ? reinterpret_cast<uint4 *>(out + ch * S + (uint32_t)(lane & 1) * 16u) : trash + j * 64 * 16;
         }
-        d8_geometry<NC>(g, m1, t1, ntuples, n, nwords, word_base, lane);
-        const uint64_t t2 = d8_resolve(sc, queue, &L.exhausted, lane);
-        d8_load_meta<NC>(m1, t2, ntuples, ngroups, nchunks, lane, sync_len, sync_base);
-        d8_fetch(sc, queue, lane);
-        d8_issue<NC>(v, g, in, lane);   // after the index loads: waiting for these covers both
+        int giveup = 0;
+        D8Halves<NC, 0>::run(st, c, dst, tb, giveup, (lane & 1) != 0);
         bool slow = !cur.fast;
-        if (cur.fast) {
-            __builtin_amdgcn_wave_barrier();
-#ifdef DC_DIAG
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            D8_STAMP(s1);
-            d_stage += s1 - s0;
-#endif
-            uint32_t c[NC];
-            uint4 *dst[NC];
-#pragma unroll
-            for (int j = 0; j < NC; ++j) {
-                c[j] = cur.lead[j] + cur.off[j];
-                dst[j] = reinterpret_cast<uint4 *>(out + (cur.g0 + j) * GSYM + (uint64_t)lane * S);
-            }
-            int giveup = 0;
-            D8Batches<NC, 0>::run(st, c, dst, tb, giveup);
 #ifndef DC_DIAG_NOESC
-            if (__any(giveup)) slow = true;   // exact redo below overwrites the chunks
+        if (__any(giveup)) slow = true;   // exact redo below overwrites the chunks
 #endif
 #ifdef DC_DIAG
-            D8_STAMP(s2);
-            d_dec += s2 - s1;
+        D8_STAMP(s2);
+        d_dec += s2 - s1;
 #endif
-            __builtin_amdgcn_wave_barrier();   // stage reused by the next tuple
-        }
-        if (slow) {
-            // partial groups, over-long spans, rare codes: exact per-symbol decode from HBM
-#pragma unroll
-            for (int j = 0; j < NC; ++j) {
-                const uint64_t ch = (cur.g0 + j) * DC_SYNC_GROUP + lane;
-                if (cur.g0 + j < ngroups && ch < nchunks) {
-                    const uint64_t s0 = ch * S;
-                    const uint32_t cnt = (uint32_t)((n - s0 < S) ? n - s0 : S);
-                    d8_chunk_hbm(in, nwords, cur.rel[j] + cur.off[j], cnt, out + s0, T, nary, w, pow2, bad);
-                }
-            }
-#ifdef DC_DIAG
-            D8_STAMP(s3);
-            d_slow += s3 - s0;
-#endif
-        }
+        // partial groups, over-long spans, rare codes: the exact redo (k_huff_decode8_fix,
+        // next launch) rewrites the tuple's chunks; out of the loop, it costs no registers here
+        if (slow && lane == 0) fix_list[atomicAdd(queue + D8_FIX_CNT, 1u)] = tp;
+        // next tuple: stage it (its spans are in v), then start the loads of the one after
         tp = t1;
         t1 = t2;
+        cur = g;
+        __builtin_amdgcn_wave_barrier();   // the stage is rewritten
+        D8_STAMP(s4);
+        d8_stage<NC>(cur, v, stw, lane);
+#ifdef DC_DIAG
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        D8_STAMP(s5);
+        d_stage += s5 - s4;
+#endif
+        d8_geometry<NC>(g, m1, t1, ntuples, n, nchunks, nwords, word_base, lane);
+        t2 = d8_resolve(sc, queue, &L.exhausted, lane);
+        d8_load_meta<NC>(m1, t2, ngroups, nchunks, lane, sync_len, sync_base);
+        d8_fetch(sc, queue, lane);
+        d8_issue<NC>(v, g, in, lane);   // after the index loads: waiting for these covers both
+#ifdef DC_DIAG
+        D8_STAMP(s6);
+        d_slow += s6 - s5;   // diag slot 3: geometry + scheduling + issue
+#endif
     }
     if (lane == 0) {
         // a dequeue issued for a tuple past the end may still be in flight: it must land
@@ -1508,10 +1582,57 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode8(const uint32_t *__rest
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
         gg[0] = d_end - d_begin; gg[1] = d_stage; gg[2] = d_dec;
-        gg[3] = ((unsigned long long)(xcc & 15) << 56) | ((unsigned long long)hwid << 24) | (d_slow & 0xffffff);
+        gg[3] = ((unsigned long long)(xcc & 15) << 56) | ((unsigned long long)(hwid & 0xffff) << 40) | (d_slow & 0xffffffffffull);
     }
 #endif
     if (bad) atomicOr(err, 1);
+}
+
+// Exact redo of the tuples k_huff_decode8 listed (fix_list[0 .. queue[D8_FIX_CNT])): one
+// wave per tuple, lane = chunk, per-symbol decode from HBM (d8_chunk_hbm). The last wave
+// out resets the list for the next launch on the stream.
+template <int NC>
+__global__ __launch_bounds__(256) void k_huff_decode8_fix(const uint32_t *__restrict__ in, uint64_t bit_base,
+                                                         const uint64_t *__restrict__ sync_base,
+                                                         const uint16_t *__restrict__ sync_len, uint64_t n,
+                                                         uint64_t nwords, const dc_dtable *__restrict__ T,
+                                                         uint8_t *__restrict__ out, int *__restrict__ err,
+                                                         uint32_t *__restrict__ queue,
+                                                         const uint32_t *__restrict__ fix_list)
+{
+    constexpr uint32_t S = 64;
+    const int lane = threadIdx.x & 63;
+    const uint32_t wave = blockIdx.x * 4 + (threadIdx.x >> 6), nwaves = gridDim.x * 4;
+    const uint32_t cnt = __atomic_load_n(queue + D8_FIX_CNT, __ATOMIC_RELAXED);
+    const int nary = T->n_ary, w = T->w;
+    const bool pow2 = (nary & (nary - 1)) == 0;
+    const uint32_t nchunks = (uint32_t)((n + S - 1) / S);
+    const uint32_t ngroups = (nchunks + DC_SYNC_GROUP - 1) / DC_SYNC_GROUP;
+    const uint64_t word_base = bit_base >> 5;
+    int bad = 0;
+    for (uint32_t i = wave; i < cnt; i += nwaves) {
+        const uint32_t tp = fix_list[i];
+        for (int j = 0; j < NC; ++j) {
+            const uint32_t g = tp * NC + j;
+            if (g >= ngroups) break;
+            const uint32_t ch = g * DC_SYNC_GROUP + lane;
+            const uint32_t len = ch < nchunks ? sync_len[ch] : 0u;
+            const uint32_t off = wave_scan_incl(len) - len;
+            if (ch < nchunks) {
+                const uint64_t s0 = (uint64_t)ch * S;
+                const uint32_t m = (uint32_t)((n - s0 < S) ? n - s0 : S);
+                d8_chunk_hbm(in, nwords, sync_base[g] - (word_base << 5) + off, m, out + s0, T, nary, w, pow2, bad);
+            }
+        }
+    }
+    if (bad) atomicOr(err, 1);
+    if (lane == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (atomicAdd(queue + D8_FIX_DONE, 1u) == nwaves - 1) {
+            atomicExch(queue + D8_FIX_CNT, 0u);
+            atomicExch(queue + D8_FIX_DONE, 0u);
+        }
+    }
 }
 
 // base64url rendering of a bit range (int2digit alphabet, n_ary_huffman.c:371-378)
@@ -1885,6 +2006,7 @@ struct dc_ctx {
     uint64_t *d_off;        size_t off_cap;       // nblocks + 1
     int *d_err;                                   // [0] plan, [1] decode
     uint32_t *d_queue;                            // decode tuple scheduler heads (D8Sched)
+    uint32_t *d_fix;        size_t fix_cap;       // tuples for the exact decode redo
     uint64_t *d_meta;                             // small device scalars
     uint4 *d_summ;          size_t summ_cap;
     uint64_t *d_entry;      size_t entry_cap;
@@ -1994,6 +2116,7 @@ void dc_ctx_destroy(dc_ctx *c)
     if (c->d_off) (void)hipFree(c->d_off);
     if (c->d_err) (void)hipFree(c->d_err);
     if (c->d_queue) (void)hipFree(c->d_queue);
+    if (c->d_fix) (void)hipFree(c->d_fix);
     if (c->d_meta) (void)hipFree(c->d_meta);
     if (c->d_summ) (void)hipFree(c->d_summ);
     if (c->d_entry) (void)hipFree(c->d_entry);
@@ -2251,16 +2374,25 @@ int dc_huff_decode(dc_ctx *c, const uint32_t *d_words, uint64_t bit_base, uint64
     if (words < 4) return DC_E_ARG;
     const uint64_t groups = dc_huff_sync_groups(n, S);
     HIPCHK(hipMemsetAsync(c->d_err + 1, 0, sizeof(int), c->stream));
-    if (S == 64 && !getenv("DC_DECODE_V7")) {
+    if (S == 64 && n < (1ull << 37) && words < (1ull << 31) && !getenv("DC_DECODE_V7")) {
         // 16 waves x 2 chains (one workgroup per CU): the 8 x 4 split measured 0.89 vs
         // 0.70 ms on 1 GiB C2 (fewer waves to cover the LDS round trips, spills)
         const char *sp = getenv("DC_D8_STATIC");   // A/B of the static share (tools/dec_ab.py)
         const uint32_t spct = sp ? (uint32_t)atoi(sp) : D8_STATIC_PCT;
+        const char *nwe = getenv("DC_D8_WAVES");   // A/B of the waves per CU (tools/dec_ab.py)
+        const int nw = nwe ? atoi(nwe) : 12;
         const uint64_t tuples = (groups + 1) / 2;
-        const uint64_t wgs = (tuples + 15) / 16;
+        const uint64_t wgs = (tuples + nw - 1) / nw;
         const uint64_t grid = wgs < 256 ? wgs : 256;   // persistent: one workgroup per CU
-        LAUNCH(c, "huff_decode", (k_huff_decode8<16, 2>), grid, 16 * 64, d_words, bit_base, d_sync_base, d_sync_len,
-               n, words, d_table, d_out, c->d_err + 1, c->d_queue, spct);
+        if (ensure((void **)&c->d_fix, &c->fix_cap, tuples * sizeof(uint32_t))) return DC_E_HIP;
+        if (nw == 12)
+            LAUNCH(c, "huff_decode", (k_huff_decode8<12, 2>), grid, 12 * 64, d_words, bit_base, d_sync_base,
+                   d_sync_len, n, words, d_table, d_out, c->d_err + 1, c->d_queue, spct, c->d_fix);
+        else
+            LAUNCH(c, "huff_decode", (k_huff_decode8<16, 2>), grid, 16 * 64, d_words, bit_base, d_sync_base,
+                   d_sync_len, n, words, d_table, d_out, c->d_err + 1, c->d_queue, spct, c->d_fix);
+        LAUNCH(c, "huff_decode_fix", (k_huff_decode8_fix<2>), 256, 256, d_words, bit_base, d_sync_base, d_sync_len, n,
+               words, d_table, d_out, c->d_err + 1, c->d_queue, (const uint32_t *)c->d_fix);
         return DC_OK;
     }
     const uint64_t wgs = (groups + DEC_WAVES - 1) / DEC_WAVES;

@@ -33,7 +33,10 @@ for r in range(a.rounds):
         os.environ.pop("DC_DECODE_V7", None)
         os.environ.pop("DC_D8_CFG", None)
         os.environ.pop("DC_D8_STATIC", None)
-        if "s" in v:   # e.g. 16x2s80: static share 80 %
+        os.environ.pop("DC_D8_WAVES", None)
+        if v.startswith("w"):   # e.g. w12: 12 waves per CU
+            os.environ["DC_D8_WAVES"] = v[1:]
+        elif "s" in v:   # e.g. 16x2s80: static share 80 %
             v0, sp = v.split("s")
             os.environ["DC_D8_STATIC"] = sp
             os.environ["DC_D8_CFG"] = v0

@@ -25,14 +25,15 @@ L = _lib.load("libdc_core.so")
 buf = np.zeros(256 * 16 * 4, np.uint64)
 assert L.dc_diag_read(buf.ctypes.data_as(C.c_void_p), C.c_size_t(buf.nbytes)) == 0
 d = buf.reshape(-1, 4).astype(np.float64)
-tot, st, de, sl = d.T
+tot, st, de, _ = d.T
+sl = (buf.reshape(-1, 4)[:, 3] & np.uint64(0xffffffffff)).astype(np.float64)   # loop bottom: geometry, scheduling, issue
 print(f"{cfg} n={nary}: per wave cycles total {tot.mean():.0f}  stage {st.mean():.0f} ({st.sum()/tot.sum():.1%})  "
-      f"decode {de.mean():.0f} ({de.sum()/tot.sum():.1%})  slow {sl.mean():.0f} ({sl.sum()/tot.sum():.1%})  "
+      f"decode {de.mean():.0f} ({de.sum()/tot.sum():.1%})  bottom {sl.mean():.0f} ({sl.sum()/tot.sum():.1%})  "
       f"max total {tot.max():.0f} min {tot.min():.0f}")
 assert torch.equal(out, x)
 meta = buf.reshape(-1, 4)[:, 3]
 xcc = (meta >> np.uint64(56)).astype(np.int64)
-hwid = ((meta >> np.uint64(24)) & np.uint64(0xffffffff)).astype(np.int64)
+hwid = ((meta >> np.uint64(40)) & np.uint64(0xffff)).astype(np.int64)
 cu = (hwid >> 8) & 15
 sh = (hwid >> 12) & 1
 se = (hwid >> 13) & 7
