@@ -99,6 +99,7 @@ def _declare_core(L):
         "dc_huff_block_hist": ([vp, P, u64], i32),
         "dc_huff_decode": ([vp, P, u64, u64, P, P, u32, u64, P, P], i32),
         "dc_huff_decode_status": ([vp], i32),
+        "dc_huff_decode_redo_count": ([vp, C.POINTER(u64)], i32),
         "dc_huff_base64url": ([vp, P, u64, u64, P], i32),
         "dc_huff_default_sync": ([u64], u32),
         "dc_huff_choose_sync": ([u64, u64], u32),
@@ -117,6 +118,8 @@ def _declare_core(L):
         "dc_small_decompress_host": ([u8p, u64, u8p, u64, C.POINTER(u64)], i32),
     }
     for name, (args, res) in sig.items():
+        if os.environ.get("DC_CORE_LIB") and not hasattr(L, name):   # older diagnostic build
+            continue
         f = getattr(L, name)
         f.argtypes = args
         f.restype = res

@@ -166,6 +166,7 @@ __global__ __launch_bounds__(256) void k_huff_table(const uint64_t *__restrict__
     __shared__ uint32_t s_code[256];
     __shared__ uint32_t s_nb[256];
     __shared__ int s_k, s_min, s_max, s_maxbits, s_bad;
+    __shared__ uint32_t s_tot_esc[256];
 
     const int t = threadIdx.x;
     const int leaves = M + 1;
@@ -358,7 +359,53 @@ __global__ __launch_bounds__(256) void k_huff_table(const uint64_t *__restrict__
         }
         T->lut[e] = v;
     }
+    // decoder tables on the LSB-first window (dc_gpu.h): dlut = the one-symbol table at the
+    // bit-reversed index; escape prefixes (entries 0) numbered in index order; dlut2 filled
+    // per symbol: a code of 12 < b <= 12 + k bits covers 2^(12 + k - b) entries of its
+    // prefix's sub-table (no per-entry search)
+    uint16_t *s_esc = reinterpret_cast<uint16_t *>(s_q2);   // escape id per dlut entry
+    constexpr int PER = (1 << DC_LUT_BITS) / 256;
+    uint32_t d1[PER], nesc = 0;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const uint32_t i = (uint32_t)(t * PER + j);
+        const uint32_t a = s_lut1[__builtin_bitreverse32(i) >> (32 - DC_LUT_BITS)];
+        d1[j] = a ? ((a >> 8) | ((a & 255u) << 8)) : 0u;
+        nesc += a ? 0u : 1u;
+    }
+    s_tot_esc[t] = nesc;
+    __syncthreads();
     if (t == 0) {
+        uint32_t run = 0;
+        for (int q = 0; q < 256; ++q) { const uint32_t v = s_tot_esc[q]; s_tot_esc[q] = run; run += v; }
+        s_k = (int)run;   // escape prefixes
+    }
+    __syncthreads();
+    const uint32_t E = (uint32_t)s_k;
+    const uint32_t K = (uint32_t)min(max(s_maxbits - DC_LUT_BITS, 1), 8);
+    const bool l2ok = E > 0 && E <= 256 && (E << K) <= DC_LUT2_CAP && s_maxbits <= 32;
+    uint32_t id = s_tot_esc[t];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const uint32_t i = (uint32_t)(t * PER + j);
+        uint32_t v = d1[j];
+        if (!v) { s_esc[i] = (uint16_t)id; v = (id & 255u) << 8; ++id; }
+        T->dlut[i] = (uint16_t)v;
+    }
+    for (int q = t; q < DC_LUT2_CAP; q += 256) T->dlut2[q] = 0;
+    __syncthreads();   // s_esc complete; dlut2 zeroed (same workgroup: global writes ordered by the barrier)
+    if (l2ok) {
+        const uint32_t nb = s_nb[t];
+        if (nb > DC_LUT_BITS && nb <= DC_LUT_BITS + K) {
+            const uint32_t c = s_code[t], tl = nb - DC_LUT_BITS;
+            const uint32_t pre = __builtin_bitreverse32(c >> tl) >> (32 - DC_LUT_BITS);   // first 12 stream bits
+            const uint32_t rt = __builtin_bitreverse32(c & ((1u << tl) - 1)) >> (32 - tl);
+            const uint32_t base = (uint32_t)s_esc[pre] << K;
+            for (uint32_t j = 0; j < (1u << (K - tl)); ++j) T->dlut2[base | rt | (j << tl)] = (uint16_t)(nb | ((uint32_t)t << 8));
+        }
+    }
+    if (t == 0) {
+        T->dlut2_k = l2ok ? (int32_t)K : 0;
         T->n_ary = nary;
         T->w = w;
         T->max_symbol_value = M;
@@ -1020,18 +1067,16 @@ __global__ __launch_bounds__(DEC_WAVES * 64) void k_huff_decode(const uint32_t *
 //    makes the wave redo its two chunks exactly (d8_chunk_hbm).
 // Partial groups and groups whose span exceeds the stage also go through d8_chunk_hbm.
 // ------------------------------------------------------------------------------------
-#define D8_CHAINS 32           /* chains (groups being decoded) per CU: waves x chains/wave */
+#define D8_CHAINS 24           /* chains (groups being decoded) per CU: waves x chains/wave */
+#define D8_LUT_BITS 14         /* first-level table of the fast decoder (32 KiB of LDS)      */
 #define D8_STAGE_WORDS 1088    /* per chain: 4352 B = 4096 symbols at <= 8.4 bits/symbol   */
 #define D8_L2_CAP 7168         /* second-level entries (u16)                               */
 #define D8_K_MAX 8
 #define D8_MAX_WAVES 16
 
 struct Dec8Lds {
-    uint16_t lut[1 << DC_LUT_BITS];   // LSB-first 12-bit window -> len | sym << 8; len 0: sub-table id << 8
-    uint16_t lut2[D8_L2_CAP];         // [sub][K bits] -> len | sym << 8; 0: longer than 12+K bits / invalid
-    uint32_t scan[D8_MAX_WAVES];
+    uint16_t lut[1 << D8_LUT_BITS];   // LSB-first 14-bit window -> len | sym << 8; len 0: a longer code
     uint32_t exhausted;               // scheduler: bit h = slice h is empty
-    uint16_t esc_pre[256];            // first-level index of escape prefix #id
     __attribute__((aligned(16))) uint32_t stage[D8_CHAINS][D8_STAGE_WORDS];
     uint32_t tail_pad[64];            // a corrupt stream's windows may run past the last stage
 };
@@ -1085,30 +1130,14 @@ static __device__ void d8_chunk_hbm(const uint32_t *__restrict__ in, uint64_t nw
     }
 }
 
-struct D8Tabs {
-    const uint16_t *lut, *lut2;
-    uint32_t K, kmask;   // wave-uniform
-};
-
-// second level for an escape entry e of the symbol at window offset off (k = index in the
-// batch): returns the final entry; sets giveup when the code is not resolvable here
-static __device__ __forceinline__ uint32_t d8_esc(uint32_t e, uint32_t x, uint32_t off, int k, const D8Tabs &tb,
-                                                  int &giveup)
-{
-    if ((e & 255u) == 0) {
-        uint32_t e2 = 0;
-        if (tb.K) e2 = tb.lut2[((e >> 8) << tb.K) | ((x >> DC_LUT_BITS) & tb.kmask)];
-        if (e2 == 0 || off + (e2 & 255u) + DC_LUT_BITS * (3 - k) > 64) { giveup = 1; e2 = 1; }
-        e = e2;
-    }
-    return e;
-}
-
-// one batch (4 symbols) of the NC chains of a lane, interleaved symbol by symbol;
-// o[j] receives chain j's 4 output bytes
+// one batch (4 symbols) of the NC chains of a lane, interleaved symbol by symbol, with no
+// branch: a window whose code is longer than 12 bits reads entry 0 (length 0), so the chain
+// stops advancing and mn[j] records it; such a chunk is decoded again exactly by
+// k_huff_decode8_fix (codes > 12 bits are ~0.13% of the symbols of C2 text, ~8% of chunks).
+// o[j] receives chain j's 4 output bytes.
 template <int NC>
-static __device__ __forceinline__ void d8_batch(const uint32_t *const *st, uint32_t *c, uint32_t *o, const D8Tabs &tb,
-                                                int &giveup)
+static __device__ __forceinline__ void d8_batch(const uint32_t *const *st, uint32_t *c, uint32_t *o,
+                                                const uint16_t *__restrict__ lut, uint32_t *mn)
 {
     uint64_t win[NC];
     uint32_t off[NC];
@@ -1123,88 +1152,79 @@ static __device__ __forceinline__ void d8_batch(const uint32_t *const *st, uint3
     constexpr uint32_t SEL[4] = {0x0c0c0c05u, 0x0c0c0500u, 0x0c050100u, 0x05020100u};
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        uint32_t x[NC], e[NC], mn = 255u;
 #pragma unroll
         for (int j = 0; j < NC; ++j) {
-            x[j] = (uint32_t)(win[j] >> off[j]);
+            const uint32_t x = (uint32_t)(win[j] >> off[j]);
 #ifdef DC_DIAG_LUTMASK   // timing ablation only: lookups confined to the first entries
-            e[j] = tb.lut[x[j] & DC_DIAG_LUTMASK];
+            const uint32_t e = lut[x & DC_DIAG_LUTMASK];
 #else
-            e[j] = tb.lut[x[j] & ((1u << DC_LUT_BITS) - 1)];
+            const uint32_t e = lut[x & ((1u << D8_LUT_BITS) - 1)];
 #endif
-        }
-#pragma unroll
-        for (int j = 0; j < NC; ++j) mn = min(mn, e[j] & 255u);
-#ifdef DC_DIAG_NOESC   // timing ablation only: escapes decode as garbage
-        giveup |= (int)(mn == 0);
-#else
-        if (__builtin_expect(__any(mn == 0), 0)) {
-#pragma unroll
-            for (int j = 0; j < NC; ++j) e[j] = d8_esc(e[j], x[j], off[j], k, tb, giveup);
-        }
-#endif
-#pragma unroll
-        for (int j = 0; j < NC; ++j) {
-            o[j] = __builtin_amdgcn_perm(e[j], k ? o[j] : 0u, SEL[k]);
-            off[j] += e[j] & 255u;
+            mn[j] = min(mn[j], e & 255u);
+            o[j] = __builtin_amdgcn_perm(e, k ? o[j] : 0u, SEL[k]);
+            off[j] += e & 255u;
         }
     }
 #pragma unroll
     for (int j = 0; j < NC; ++j) c[j] += off[j];
 }
 
-// The 16 batches of a 64-symbol chunk as two halves of 8, unrolled by template recursion.
-// After each half a lane holds pieces 2H and 2H+1 (16 B each) of its own chunk. Stored as
-// they are (lane = chunk, 64 B apart) every wave store would touch 32 cache lines with 32 B
-// each; the L2 request rate then bounds the decoder (a contiguous-store ablation ran 0.72 ->
-// 0.48 ms on 1 GiB C2). So each 4-lane quad swaps pieces by DPP first (quad_perm): store A
-// gives lanes 4m+p piece 2H+(p&1) of chunk 4m+(p>>1), store B the same of chunk 4m+2+(p>>1):
-// 32 contiguous bytes per lane pair, 16 lines of 64 B per store.
-template <int NC, int H>
-struct D8Halves {
-    static __device__ __forceinline__ void run(const uint32_t *const *st, uint32_t *c, uint4 *const *dst,
-                                               const D8Tabs &tb, int &giveup, bool odd)
+// The 16 batches of a 64-symbol chunk (4 pieces of 16 B per lane), unrolled by template
+// recursion; the pieces stay in registers until the chunk is done.
+template <int NC, int Q>
+struct D8Pieces {
+    static __device__ __forceinline__ void run(const uint32_t *const *st, uint32_t *c, uint32_t (*o)[16],
+                                               const uint16_t *__restrict__ lut, uint32_t *mn)
     {
-        uint32_t a0[NC], a1[NC], a2[NC], a3[NC], b0[NC], b1[NC], b2[NC], b3[NC];
-        d8_batch<NC>(st, c, a0, tb, giveup);
-        d8_batch<NC>(st, c, a1, tb, giveup);
-        d8_batch<NC>(st, c, a2, tb, giveup);
-        d8_batch<NC>(st, c, a3, tb, giveup);
-        d8_batch<NC>(st, c, b0, tb, giveup);
-        d8_batch<NC>(st, c, b1, tb, giveup);
-        d8_batch<NC>(st, c, b2, tb, giveup);
-        d8_batch<NC>(st, c, b3, tb, giveup);
+        uint32_t b[NC];
+        d8_batch<NC>(st, c, b, lut, mn);
 #pragma unroll
-        for (int j = 0; j < NC; ++j) {
-#ifdef DC_DIAG_NOSTORE
-            asm volatile("" ::"v"(a0[j]), "v"(a1[j]), "v"(a2[j]), "v"(a3[j]), "v"(b0[j]), "v"(b1[j]), "v"(b2[j]),
-                         "v"(b3[j]));
-#else
-            const uint32_t a[4] = {a0[j], a1[j], a2[j], a3[j]}, b[4] = {b0[j], b1[j], b2[j], b3[j]};
-            uint32_t A[4], B[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const uint32_t xa = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)a[i], 0x50, 0xf, 0xf, false);   // [0,0,1,1]
-                const uint32_t xb = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)b[i], 0x50, 0xf, 0xf, false);
-                const uint32_t ya = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)a[i], 0xfa, 0xf, 0xf, false);   // [2,2,3,3]
-                const uint32_t yb = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)b[i], 0xfa, 0xf, 0xf, false);
-                A[i] = odd ? xb : xa;
-                B[i] = odd ? yb : ya;
-            }
-            dst[j][2 * H] = make_uint4(A[0], A[1], A[2], A[3]);
-            dst[j][2 * H + 8] = make_uint4(B[0], B[1], B[2], B[3]);
-#endif
-        }
-        D8Halves<NC, H + 1>::run(st, c, dst, tb, giveup, odd);
+        for (int j = 0; j < NC; ++j) o[j][Q] = b[j];
+        D8Pieces<NC, Q + 1>::run(st, c, o, lut, mn);
     }
 };
 template <int NC>
-struct D8Halves<NC, 2> {
-    static __device__ __forceinline__ void run(const uint32_t *const *, uint32_t *, uint4 *const *, const D8Tabs &,
-                                               int &, bool)
+struct D8Pieces<NC, 16> {
+    static __device__ __forceinline__ void run(const uint32_t *const *, uint32_t *, uint32_t (*)[16],
+                                               const uint16_t *__restrict__, uint32_t *)
     {
     }
 };
+
+// A lane's 64 decoded bytes belong to its own chunk (lane = chunk): stored from registers,
+// every wave store would touch 32 cache lines with 32 B each, and the L2 request rate then
+// bounds the decoder (a contiguous-store ablation ran 0.72 -> 0.48 ms on 1 GiB C2). So the
+// chain's 4 KiB of output go through its LDS stage, which the decode no longer needs: each
+// lane writes its 4 pieces as a row (piece slots XOR-swizzled by lane so the 16-B writes of
+// 8 lanes hit 8 distinct bank groups), then every store moves 1 KiB of contiguous output.
+template <int NC>
+static __device__ __forceinline__ void d8_out(uint32_t *const *stw, const uint32_t (*o)[16], uint4 *const *dst,
+                                              int lane)
+{
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+        uint4 *row = reinterpret_cast<uint4 *>(stw[j]) + lane * 4;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            row[q ^ ((lane >> 1) & 3)] = make_uint4(o[j][4 * q], o[j][4 * q + 1], o[j][4 * q + 2], o[j][4 * q + 3]);
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+        const uint4 *rows = reinterpret_cast<const uint4 *>(stw[j]);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const uint32_t ch = 16 * s + (lane >> 2), p = lane & 3;
+            const uint4 v = rows[ch * 4 + (p ^ ((ch >> 1) & 3))];
+#ifdef DC_DIAG_NOSTORE
+            asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
+#else
+            dst[j][s * 64 + lane] = v;
+#endif
+        }
+    }
+}
 
 #ifdef DC_DIAG   // diagnostic build only (tools/diag_build.sh): per-wave s_memtime split
 __device__ unsigned long long g_d8diag[256 * D8_MAX_WAVES * 4];
@@ -1307,8 +1327,9 @@ static __device__ __forceinline__ void d8_issue(uint4 (&v)[NC][5], const D8Geo<N
 #define D8_QSTRIDE 1024   /* u32 between heads */
 #define D8_FIX_CNT (9 * D8_QSTRIDE)                /* tuples queued for the exact redo        */
 #define D8_FIX_DONE (10 * D8_QSTRIDE)              /* redo waves finished                    */
-#define D8_TRASH_OFF (11 * D8_QSTRIDE)             /* u32 offset of the trash slots: 2 x 64 x 256 B */
-#define D8_QWORDS (D8_TRASH_OFF + 2 * 64 * 256 / 4)
+#define D8_QWORDS (11 * D8_QSTRIDE)
+#define D8_WSCR (2 * 4096 + 66 * 8 + 512)            /* per-wave scratch of the decoders (bytes)  */
+#define D8_SCRATCH_WAVES 4096                        /* waves with a scratch slot (both kernels)  */
 
 struct D8Sched {
     uint32_t Ts, Dh, ntuples;   // static tuples, slice size, all tuples
@@ -1394,7 +1415,8 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode8(const uint32_t *__rest
                                                           uint64_t nwords, const dc_dtable *__restrict__ T,
                                                           uint8_t *__restrict__ out, int *__restrict__ err,
                                                           uint32_t *__restrict__ queue, uint32_t static_pct,
-                                                          uint32_t *__restrict__ fix_list)
+                                                          uint64_t *__restrict__ fix_mask, uint64_t *__restrict__ fix_pos,
+                                                          uint8_t *__restrict__ scratch)
 {
     static_assert(NW * NC <= D8_CHAINS && NW <= D8_MAX_WAVES, "stage slots");
     constexpr uint32_t S = 64;
@@ -1402,62 +1424,24 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode8(const uint32_t *__rest
     __shared__ Dec8Lds L;
     const int t = threadIdx.x, lane = t & 63;
     const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
-    const int nary = T->n_ary, w = T->w;
-    const bool pow2 = (nary & (nary - 1)) == 0;
-    int bad = 0;
-    // ---- tables: first level (bit-reversed index of the MSB-first table), escape
-    // prefixes numbered in index order, second level decoded exactly once per entry
-    constexpr int PER = ((1 << DC_LUT_BITS) + NT - 1) / NT;   // entries per thread (last ones may be past the end)
-    uint32_t e1[PER];
-    uint32_t nesc = 0;
-#pragma unroll
-    for (int j = 0; j < PER; ++j) {
-        const uint32_t i = (uint32_t)(t * PER + j);
-        const uint32_t e = i < (1u << DC_LUT_BITS) ? T->lut[__builtin_bitreverse32(i) >> (32 - DC_LUT_BITS)] : 1u;
-        e1[j] = e ? (E_BITS0(e) | ((e & 255u) << 8)) : 0u;
-        nesc += e ? 0u : 1u;
-    }
-    uint32_t incl = nesc;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(incl, d, 64);
-        if (lane >= d) incl += y;
-    }
-    if (lane == 63) L.scan[wv] = incl;
-    if (t == 0) L.exhausted = 0;
-    __syncthreads();
-    uint32_t base = 0, E = 0;
-    for (int v = 0; v < NW; ++v) {
-        const uint32_t s = L.scan[v];
-        base += (v < wv) ? s : 0u;
-        E += s;
-    }
-    const int maxbits = T->max_bits;
-    const uint32_t K = (uint32_t)min(max(maxbits - DC_LUT_BITS, 1), D8_K_MAX);
-    const bool l2ok = E > 0 && E <= 256 && (E << K) <= D8_L2_CAP;
-    uint32_t id = base + incl - nesc;
-#pragma unroll
-    for (int j = 0; j < PER; ++j) {
-        const uint32_t i = (uint32_t)(t * PER + j);
-        if (i >= (1u << DC_LUT_BITS)) break;
-        if (!e1[j] && id < 256) L.esc_pre[id] = (uint16_t)i;
-        L.lut[i] = (uint16_t)(e1[j] ? e1[j] : ((id++ & 255u) << 8));
+    // ---- table: the LSB-first 12-bit table (dc_dtable.dlut); codes longer than 12 bits
+    // read length 0
+    // D8_LUT_BITS first level from the 12-bit one and its second level: 2.9% of C2 chunks hold a
+    // code of > 14 bits (to the exact redo), 6.6% one of > 12
+    const uint32_t K2 = (uint32_t)T->dlut2_k;
+    for (int i = t; i < (1 << D8_LUT_BITS); i += NT) {
+        uint32_t e = T->dlut[i & ((1 << DC_LUT_BITS) - 1)];
+        if ((e & 255u) == 0 && K2 >= D8_LUT_BITS - DC_LUT_BITS) {
+            const uint32_t e2 = T->dlut2[((e >> 8) << K2) | ((uint32_t)i >> DC_LUT_BITS)];
+            e = (e2 && (e2 & 255u) <= D8_LUT_BITS) ? e2 : (e & 0xff00u);
+        }
+        L.lut[i] = (uint16_t)e;
 #ifdef DC_DIAG_SYNTH_LUT   // timing ablation only: every window is a 4-bit code (garbage output)
         L.lut[i] = (uint16_t)(4u | ((i & 255u) << 8));
 #endif
     }
+    if (t == 0) L.exhausted = 0;
     __syncthreads();
-    if (l2ok) {
-        for (uint32_t q = (uint32_t)t; q < (E << K); q += NT) {
-            const uint32_t pre = L.esc_pre[q >> K];
-            const uint32_t lo = pre | ((q & ((1u << K) - 1)) << DC_LUT_BITS);
-            int b2 = 0;
-            const uint32_t r = d8_long(lo, 0u, T, nary, w, pow2, &b2);
-            L.lut2[q] = (uint16_t)((b2 || (r & 255u) > DC_LUT_BITS + K) ? 0u : r);
-        }
-    }
-    __syncthreads();
-    const D8Tabs tb{L.lut, L.lut2, l2ok ? K : 0u, (1u << K) - 1};
 
     // the launcher guarantees n < 2^37 (chunk and tuple indices fit 32 bits)
     const uint32_t nchunks = (uint32_t)((n + S - 1) / S);
@@ -1506,7 +1490,11 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode8(const uint32_t *__rest
     // group, over-long span) still runs it, on whatever the stage holds, with its stores sent
     // to the trash rows wherever a chunk is not whole inside the output; the exact redo
     // rewrites the real bytes afterwards (same wave, program order).
-    uint4 *const trash = reinterpret_cast<uint4 *>(queue + D8_TRASH_OFF) + (size_t)lane * 16;   // 256 B per lane and chain
+    // per-wave scratch (garbage sinks): stores that land on lines every wave shares would
+    // serialise in L2, so each wave has its own: 2 chains x 4 KiB of trash rows, 65 u64 dummies
+    uint8_t *const wscr = scratch + (size_t)(blockIdx.x * NW + wv) * D8_WSCR;
+    uint4 *const trash = reinterpret_cast<uint4 *>(wscr);
+    uint32_t *const dummy = reinterpret_cast<uint32_t *>(wscr + 2 * 4096);
     d8_load_meta<NC>(m2, tp, ngroups, nchunks, lane, sync_len, sync_base);
     d8_geometry<NC>(g, m2, tp, ntuples, n, nchunks, nwords, word_base, lane);
     d8_issue<NC>(v, g, in, lane);
@@ -1525,26 +1513,40 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode8(const uint32_t *__rest
         uint4 *dst[NC];
 #pragma unroll
         for (int j = 0; j < NC; ++j) {
-            // this lane stores chunk (lane & ~3) | ((lane >> 1) & 1) of the group (+2 for store
-            // B), pieces (lane & 1) + 2H (D8Halves); a tuple that is not fast (its chunks are
-            // all rewritten by the redo) stores into the lane's trash slot instead
-            const uint64_t ch = (uint64_t)(cur.g0 + j) * DC_SYNC_GROUP + (uint32_t)((lane & ~3) | ((lane >> 1) & 1));
+            // the group's 4 KiB of output (d8_out); a tuple that is not fast (its chunks are
+            // all rewritten by the redo) stores into the chain's trash rows instead
             c[j] = cur.fast ? cur.lead[j] + cur.off[j] : 0u;
-            dst[j] = cur.fast ? reinterpret_cast<uint4 *>(out + ch * S + (uint32_t)(lane & 1) * 16u) : trash + j * 64 * 16;
+            dst[j] = cur.fast ? reinterpret_cast<uint4 *>(out + (uint64_t)(cur.g0 + j) * DC_SYNC_GROUP * S)
+                              : trash + j * 256;
         }
-        int giveup = 0;
-        D8Halves<NC, 0>::run(st, c, dst, tb, giveup, (lane & 1) != 0);
-        bool slow = !cur.fast;
-#ifndef DC_DIAG_NOESC
-        if (__any(giveup)) slow = true;   // exact redo below overwrites the chunks
-#endif
+        // mn[j] == 0 after the decode <=> chunk redone: starts at 0 for a tuple that is not
+        // fast (the fixup skips chunks past the end), reaches 0 on a code of > 12 bits
+        uint32_t o[NC][16], mn[NC];
+#pragma unroll
+        for (int j = 0; j < NC; ++j) mn[j] = cur.fast ? 255u : 0u;
+        D8Pieces<NC, 0>::run(st, c, o, L.lut, mn);
+        d8_out<NC>(stw, o, dst, lane);
 #ifdef DC_DIAG
         D8_STAMP(s2);
         d_dec += s2 - s1;
 #endif
-        // partial groups, over-long spans, rare codes: the exact redo (k_huff_decode8_fix,
-        // next launch) rewrites the tuple's chunks; out of the loop, it costs no registers here
-        if (slow && lane == 0) fix_list[atomicAdd(queue + D8_FIX_CNT, 1u)] = tp;
+        // chunks with a code of > 12 bits (and every chunk of a tuple that was not fast:
+        // partial group, over-long span) are decoded again exactly by k_huff_decode8_fix:
+        // a bit per chunk, and for those chunks their bit offset inside the group
+        // (no branch: any exec-masked store in this loop body costs ~80 VGPRs of allocation,
+        // so lanes without something to record write a per-lane dummy slot instead)
+        // (cur.fast is not read after the decode either: that made the compiler keep two
+        // versions of the whole decode live, 168 VGPRs + spills instead of 91)
+#pragma unroll
+        for (int j = 0; j < NC; ++j) {
+            const uint32_t g = cur.g0 + j;
+            const bool redo = mn[j] == 0;
+            const uint64_t m = __ballot(redo);
+            uint64_t *pp = redo ? fix_pos + (uint64_t)g * DC_SYNC_GROUP + lane : reinterpret_cast<uint64_t *>(dummy) + lane;
+            *pp = (uint64_t)cur.wo[j] * 32 + cur.lead[j] + cur.off[j];   // chunk start, bits from word_base
+            uint64_t *mp = g < ngroups ? fix_mask + g : reinterpret_cast<uint64_t *>(dummy) + 64;
+            *mp = m;
+        }
         // next tuple: stage it (its spans are in v), then start the loads of the one after
         tp = t1;
         t1 = t2;
@@ -1585,54 +1587,281 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode8(const uint32_t *__rest
         gg[3] = ((unsigned long long)(xcc & 15) << 56) | ((unsigned long long)(hwid & 0xffff) << 40) | (d_slow & 0xffffffffffull);
     }
 #endif
-    if (bad) atomicOr(err, 1);
 }
 
-// Exact redo of the tuples k_huff_decode8 listed (fix_list[0 .. queue[D8_FIX_CNT])): one
-// wave per tuple, lane = chunk, per-symbol decode from HBM (d8_chunk_hbm). The last wave
-// out resets the list for the next launch on the stream.
-template <int NC>
-__global__ __launch_bounds__(256) void k_huff_decode8_fix(const uint32_t *__restrict__ in, uint64_t bit_base,
-                                                         const uint64_t *__restrict__ sync_base,
-                                                         const uint16_t *__restrict__ sync_len, uint64_t n,
-                                                         uint64_t nwords, const dc_dtable *__restrict__ T,
-                                                         uint8_t *__restrict__ out, int *__restrict__ err,
-                                                         uint32_t *__restrict__ queue,
-                                                         const uint32_t *__restrict__ fix_list)
+// position of the rank-th set bit of m (rank < popcount(m))
+static __device__ __forceinline__ uint32_t select_bit(uint64_t m, uint32_t rank)
+{
+    uint32_t pos = 0;
+#pragma unroll
+    for (int sh = 32; sh >= 1; sh >>= 1) {
+        const uint32_t c = (uint32_t)__popcll(m & ((1ull << sh) - 1));
+        if (rank >= c) { rank -= c; m >>= sh; pos += (uint32_t)sh; }
+    }
+    return pos;
+}
+
+// Exact decode of the chunks k_huff_decode8 flagged (fix_mask: a bit per chunk, fix_pos: the
+// chunk's bit offset inside its group span). A wave takes 64 groups at a time, compacts their
+// flagged chunks (popcount scan, then a search per lane) and decodes one chunk per lane from
+// HBM with a sliding 3-word window and the next word already in flight: the 12-bit table and
+// the canonical tables for longer codes (d8_long's rule) are all in LDS.
+#define D8F_WAVES 12
+#define D8F_ROW 16   /* words of a lane's staged span (longer chunks re-stage it further on) */
+struct FixLds {
+    uint16_t lut[1 << DC_LUT_BITS];
+    uint16_t lut2[DC_LUT2_CAP];
+    uint64_t lim[33];
+    uint32_t first[DC_MAX_DIGITS + 1], count[DC_MAX_DIGITS + 1], start[DC_MAX_DIGITS + 1];
+    uint16_t syms[DC_MAX_SYMS];
+    uint64_t mask[D8F_WAVES][64];
+    uint32_t excl[D8F_WAVES][64];
+    uint32_t rows[D8F_WAVES][64 * (D8F_ROW + 1)];   // a lane's chunk span (odd stride: conflict-free)
+    uint32_t orow[D8F_WAVES][64 * 17];              // a lane's output bytes (odd stride)
+};
+
+// d8_long on the LDS copies: the code at the start of an LSB-first 64-bit window
+static __device__ uint32_t d8_long_lds(uint32_t lo, uint32_t hi, const FixLds &F, int nary, int w, bool pow2, int *bad)
+{
+    const uint64_t win = ((uint64_t)__builtin_bitreverse32(lo) << 32) | __builtin_bitreverse32(hi);   // MSB-first
+    if (pow2) {
+        const uint64_t top = win >> 32;
+        uint32_t b = 1;
+        while (b <= 32 && top >= F.lim[b]) ++b;
+        if (b > 32) { *bad = 1; return 0u; }
+        const uint32_t Ld = b / (uint32_t)w;
+        const uint32_t v = (uint32_t)(top >> (32 - b));
+        return b | ((F.syms[(F.start[Ld] + (v - F.first[Ld])) & (DC_MAX_SYMS - 1)] & 255u) << 8);
+    }
+    uint64_t x = win;
+    uint32_t v = 0;
+    for (int Ld = 1; Ld <= DC_MAX_DIGITS && Ld * w <= 32; ++Ld) {
+        v = v * (uint32_t)nary + (uint32_t)(x >> (64 - w));
+        x <<= w;
+        const uint32_t cnt = F.count[Ld];
+        if (cnt && v - F.first[Ld] < cnt)
+            return (uint32_t)(Ld * w) | ((F.syms[(F.start[Ld] + (v - F.first[Ld])) & (DC_MAX_SYMS - 1)] & 255u) << 8);
+    }
+    *bad = 1;
+    return 0u;
+}
+
+// one code from the window (lo, hi): 12-bit table, second level, canonical search
+static __device__ __forceinline__ uint32_t d8f_code(uint32_t lo, uint32_t hi, const FixLds &F, uint32_t K2,
+                                                    uint32_t kmask, int nary, int w, bool pow2, int *bad)
+{
+    uint32_t e = F.lut[lo & ((1u << DC_LUT_BITS) - 1)];
+    if ((e & 255u) == 0) {
+        e = K2 ? F.lut2[((e >> 8) << K2) | ((lo >> DC_LUT_BITS) & kmask)] : 0u;
+        if (e == 0) e = d8_long_lds(lo, hi, F, nary, w, pow2, bad);
+    }
+    return e;
+}
+
+// Where the fixup's rounds come from: windows of 64 groups (a wave's own, grid stride), the
+// flagged chunks of a window compacted by a popcount scan, 64 per round.
+struct D8FCur {
+    uint32_t win, r, tot;   // window, first item of the round, items in the window
+    bool live;
+};
+
+static __device__ __forceinline__ void d8f_window(D8FCur &q, uint32_t ngroups, uint32_t nwin, uint32_t wstride,
+                                                  const uint64_t *__restrict__ fix_mask, FixLds &F, int wv, int lane)
+{
+    // from q.win on, the next window with flagged chunks; its masks and scan into LDS
+    for (; q.win < nwin; q.win += wstride) {
+        const uint32_t g = q.win * 64 + lane;
+        const uint64_t m = g < ngroups ? fix_mask[g] : 0ull;
+        const uint32_t cnt = (uint32_t)__popcll(m);
+        const uint32_t incl = wave_scan_incl(cnt);
+        q.tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        if (q.tot) {
+            F.mask[wv][lane] = m;
+            F.excl[wv][lane] = incl - cnt;
+            __builtin_amdgcn_wave_barrier();
+            q.r = 0;
+            q.live = true;
+            return;
+        }
+    }
+    q.live = false;
+}
+
+static __device__ __forceinline__ void d8f_next(D8FCur &q, uint32_t ngroups, uint32_t nwin, uint32_t wstride,
+                                                const uint64_t *__restrict__ fix_mask, FixLds &F, int wv, int lane)
+{
+    if (!q.live) return;
+    if (q.r + 64 < q.tot) { q.r += 64; return; }
+    q.win += wstride;
+    d8f_window(q, ngroups, nwin, wstride, fix_mask, F, wv, lane);
+}
+
+// this lane's chunk in round q (or ~0u)
+static __device__ __forceinline__ uint32_t d8f_chunk(const D8FCur &q, uint32_t nchunks, const FixLds &F, int wv,
+                                                     int lane)
+{
+    const uint32_t item = q.r + (uint32_t)lane;
+    if (!q.live || item >= q.tot) return ~0u;
+    uint32_t wi = 0;   // last word whose exclusive count is <= item
+#pragma unroll
+    for (uint32_t step = 32; step >= 1; step >>= 1)
+        if (wi + step <= 63 && F.excl[wv][wi + step] <= item) wi += step;
+    const uint32_t ch = (q.win * 64 + wi) * DC_SYNC_GROUP + select_bit(F.mask[wv][wi], item - F.excl[wv][wi]);
+    return ch < nchunks ? ch : ~0u;
+}
+
+// Exact decode of the chunks k_huff_decode8 flagged (fix_mask: a bit per chunk, fix_pos: the
+// chunk's first bit, from word_base). Persistent, D8F_WAVES waves per CU; per wave a pipeline
+// over rounds of 64 chunks (one per lane): while round A decodes from its LDS rows, the spans
+// of round B are in flight into registers and the start position of round C too. A round
+// decodes from LDS: 12-bit table, second level, canonical search for longer codes.
+__global__ __launch_bounds__(D8F_WAVES * 64) void k_huff_decode8_fix(const uint32_t *__restrict__ in, uint64_t n,
+                                                                    uint64_t nwords, const dc_dtable *__restrict__ T,
+                                                                    uint8_t *__restrict__ out, int *__restrict__ err,
+                                                                    const uint64_t *__restrict__ fix_mask,
+                                                                    const uint64_t *__restrict__ fix_pos,
+                                                                    uint4 *__restrict__ trash)
 {
     constexpr uint32_t S = 64;
-    const int lane = threadIdx.x & 63;
-    const uint32_t wave = blockIdx.x * 4 + (threadIdx.x >> 6), nwaves = gridDim.x * 4;
-    const uint32_t cnt = __atomic_load_n(queue + D8_FIX_CNT, __ATOMIC_RELAXED);
+    __shared__ FixLds F;
+    const int t = threadIdx.x, lane = t & 63, wv = __builtin_amdgcn_readfirstlane(t >> 6);
+#ifdef DC_DIAG
+    D8_STAMP(f0);
+    unsigned long long f_dec = 0, f_rounds = 0;
+#endif
+    for (int i = t; i < (1 << DC_LUT_BITS); i += D8F_WAVES * 64) F.lut[i] = T->dlut[i];
+    for (int i = t; i < DC_LUT2_CAP; i += D8F_WAVES * 64) F.lut2[i] = T->dlut2[i];
+    for (int i = t; i < DC_MAX_SYMS; i += D8F_WAVES * 64) F.syms[i] = T->syms[i];
+    for (int i = t; i <= DC_MAX_DIGITS; i += D8F_WAVES * 64) {
+        F.first[i] = T->first[i];
+        F.count[i] = T->count[i];
+        F.start[i] = T->start[i];
+    }
+    if (t < 33) F.lim[t] = T->lim[t];
+    __syncthreads();
     const int nary = T->n_ary, w = T->w;
     const bool pow2 = (nary & (nary - 1)) == 0;
+    const uint32_t K2 = (uint32_t)T->dlut2_k, kmask = (1u << K2) - 1;
     const uint32_t nchunks = (uint32_t)((n + S - 1) / S);
     const uint32_t ngroups = (nchunks + DC_SYNC_GROUP - 1) / DC_SYNC_GROUP;
-    const uint64_t word_base = bit_base >> 5;
+    const uint32_t nwin = (ngroups + 63) / 64;
+    const uint32_t wstride = gridDim.x * D8F_WAVES;
+    uint32_t *row = F.rows[wv] + lane * (D8F_ROW + 1);
+    uint32_t *orow = F.orow[wv] + lane * 17;
+    uint4 *const ftrash = reinterpret_cast<uint4 *>(trash) + (size_t)(blockIdx.x * D8F_WAVES + wv) * (D8_WSCR / 16);
     int bad = 0;
-    for (uint32_t i = wave; i < cnt; i += nwaves) {
-        const uint32_t tp = fix_list[i];
-        for (int j = 0; j < NC; ++j) {
-            const uint32_t g = tp * NC + j;
-            if (g >= ngroups) break;
-            const uint32_t ch = g * DC_SYNC_GROUP + lane;
-            const uint32_t len = ch < nchunks ? sync_len[ch] : 0u;
-            const uint32_t off = wave_scan_incl(len) - len;
-            if (ch < nchunks) {
-                const uint64_t s0 = (uint64_t)ch * S;
-                const uint32_t m = (uint32_t)((n - s0 < S) ? n - s0 : S);
-                d8_chunk_hbm(in, nwords, sync_base[g] - (word_base << 5) + off, m, out + s0, T, nary, w, pow2, bad);
+
+#ifdef DC_DIAG
+    D8_STAMP(f1);
+#endif
+#ifdef DC_DIAG_FIX_EMPTY
+    if (t < 100000) return;
+#endif
+    D8FCur qa, qb, qc;
+    qa.win = blockIdx.x * D8F_WAVES + wv;
+    d8f_window(qa, ngroups, nwin, wstride, fix_mask, F, wv, lane);
+    uint32_t cha = d8f_chunk(qa, nchunks, F, wv, lane);
+    uint64_t posa = fix_pos[cha != ~0u ? cha : 0u];
+    qb = qa;
+    d8f_next(qb, ngroups, nwin, wstride, fix_mask, F, wv, lane);
+    uint32_t chb = d8f_chunk(qb, nchunks, F, wv, lane);
+    uint64_t posb = fix_pos[chb != ~0u ? chb : 0u];
+    // spans of round A into registers: 4 uint4 from the 16-B aligned word below its start
+    uint4 sv[D8F_ROW / 4];
+    {
+        const uint64_t a0 = min((posa >> 5) & ~3ull, (nwords & ~3ull) - 4);
+#pragma unroll
+        for (int k = 0; k < D8F_ROW / 4; ++k)
+            sv[k] = reinterpret_cast<const uint4 *>(in + a0)[min((uint64_t)k, (nwords - a0) / 4 - 1)];
+    }
+    while (qa.live) {
+        // stage round A's spans, then start round B's spans and round C's positions
+        const uint64_t a0 = min((posa >> 5) & ~3ull, (nwords & ~3ull) - 4);
+#pragma unroll
+        for (int k = 0; k < D8F_ROW / 4; ++k) {
+            row[4 * k] = brev8(sv[k].x);
+            row[4 * k + 1] = brev8(sv[k].y);
+            row[4 * k + 2] = brev8(sv[k].z);
+            row[4 * k + 3] = brev8(sv[k].w);
+        }
+        {
+            const uint64_t b0 = min((posb >> 5) & ~3ull, (nwords & ~3ull) - 4);
+#pragma unroll
+            for (int k = 0; k < D8F_ROW / 4; ++k)
+                sv[k] = reinterpret_cast<const uint4 *>(in + b0)[min((uint64_t)k, (nwords - b0) / 4 - 1)];
+        }
+        qc = qb;
+        d8f_next(qc, ngroups, nwin, wstride, fix_mask, F, wv, lane);
+        const uint32_t chc = d8f_chunk(qc, nchunks, F, wv, lane);
+        const uint64_t posc = fix_pos[chc != ~0u ? chc : 0u];
+        // decode round A
+        const bool valid = cha != ~0u;
+        const uint64_t s0 = (uint64_t)(valid ? cha : 0u) * S;
+        const uint32_t cntc = valid ? (uint32_t)((n - s0 < S) ? n - s0 : S) : 0u;
+        uint32_t c = (uint32_t)(posa - (a0 << 5));
+#ifdef DC_DIAG
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        D8_STAMP(f2);
+#endif
+        uint64_t rb = a0;   // word of `in` at row word 0
+        uint32_t off = 0, ob = 0;
+        uint64_t W = 0;
+        bool over = false;
+        // one code per iteration, rolled (one copy of the code path: few registers, no spills,
+        // so no scratch reload makes the wave wait for its outstanding stores); a 64-bit
+        // window per 4 codes, re-read after 32 consumed bits; a span longer than the row
+        // re-stages the row from the current word on (rare: long chunks)
+#ifdef DC_DIAG_FIX_NODEC
+        for (uint32_t i = 0; i < 0; ++i) {
+#else
+        for (uint32_t i = 0; i < cntc && !over; ++i) {
+#endif
+            if ((i & 3) == 0 || off > 32) {
+                c += off;
+                off = 0;
+                if (c >= 32 * (D8F_ROW - 2)) {
+                    const uint32_t adv = (c >> 5) & ~3u;
+                    rb += adv;
+                    c -= adv * 32;
+                    if (rb + 4 > nwords) { bad = 1; break; }
+                    const uint64_t nq = (nwords - rb) / 4;
+                    for (int m = 0; m < D8F_ROW / 4; ++m) {
+                        const uint4 v = (uint64_t)m < nq ? reinterpret_cast<const uint4 *>(in + rb)[m] : make_uint4(0u, 0u, 0u, 0u);
+                        row[4 * m] = brev8(v.x);
+                        row[4 * m + 1] = brev8(v.y);
+                        row[4 * m + 2] = brev8(v.z);
+                        row[4 * m + 3] = brev8(v.w);
+                    }
+                }
+                const uint32_t a = c >> 5;
+                W = ((uint64_t)__builtin_amdgcn_alignbit(row[a + 2], row[a + 1], c) << 32) |
+                    __builtin_amdgcn_alignbit(row[a + 1], row[a], c);
             }
+            const uint32_t e = d8f_code((uint32_t)(W >> off), 0u, F, K2, kmask, nary, w, pow2, &bad);
+            if (e == 0) { bad = 1; over = true; }
+            ob |= (e >> 8 & 255u) << (8 * (i & 3));
+            off += e & 255u;
+            if ((i & 3) == 3) { orow[i >> 2] = ob; ob = 0; }
         }
+        if (cntc & 3) orow[cntc >> 2] = ob;
+        // 64 bytes out: whole chunks as 4 uint4 (other lanes: to the trash row, so every path
+        // issues the same stores); the stream's partial last chunk afterwards, byte by byte
+        uint4 *dst = (valid && cntc == S && !over) ? reinterpret_cast<uint4 *>(out + s0) : ftrash + lane * 4;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) dst[k] = make_uint4(orow[4 * k], orow[4 * k + 1], orow[4 * k + 2], orow[4 * k + 3]);
+        if (valid && !over && cntc < S)
+            for (uint32_t i = 0; i < cntc; ++i) out[s0 + i] = (uint8_t)(orow[i >> 2] >> (8 * (i & 3)));
+        qa = qb; cha = chb; posa = posb;
+        qb = qc; chb = chc; posb = posc;
     }
-    if (bad) atomicOr(err, 1);
+#ifdef DC_DIAG
+    D8_STAMP(f4);
     if (lane == 0) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (atomicAdd(queue + D8_FIX_DONE, 1u) == nwaves - 1) {
-            atomicExch(queue + D8_FIX_CNT, 0u);
-            atomicExch(queue + D8_FIX_DONE, 0u);
-        }
+        unsigned long long *gg = g_d8diag + (blockIdx.x * D8F_WAVES + wv) * 4;
+        gg[0] = f4 - f0; gg[1] = f1 - f0; gg[2] = f_dec; gg[3] = f_rounds;
     }
+#endif
+    if (bad) atomicOr(err, 1);
 }
 
 // base64url rendering of a bit range (int2digit alphabet, n_ary_huffman.c:371-378)
@@ -2006,7 +2235,10 @@ struct dc_ctx {
     uint64_t *d_off;        size_t off_cap;       // nblocks + 1
     int *d_err;                                   // [0] plan, [1] decode
     uint32_t *d_queue;                            // decode tuple scheduler heads (D8Sched)
-    uint32_t *d_fix;        size_t fix_cap;       // tuples for the exact decode redo
+    uint32_t *d_fix;        size_t fix_cap;       // decode redo: a u64 chunk mask per group
+    uint32_t *d_fixpos;     size_t fixpos_cap;    // decode redo: bit offset of a flagged chunk
+    uint64_t last_groups;                         // groups of the last S = 64 decode (redo mask length)
+    void *d_scr;            size_t scr_cap;       // per-wave garbage sinks of the decoders
     uint64_t *d_meta;                             // small device scalars
     uint4 *d_summ;          size_t summ_cap;
     uint64_t *d_entry;      size_t entry_cap;
@@ -2117,6 +2349,8 @@ void dc_ctx_destroy(dc_ctx *c)
     if (c->d_err) (void)hipFree(c->d_err);
     if (c->d_queue) (void)hipFree(c->d_queue);
     if (c->d_fix) (void)hipFree(c->d_fix);
+    if (c->d_fixpos) (void)hipFree(c->d_fixpos);
+    if (c->d_scr) (void)hipFree(c->d_scr);
     if (c->d_meta) (void)hipFree(c->d_meta);
     if (c->d_summ) (void)hipFree(c->d_summ);
     if (c->d_entry) (void)hipFree(c->d_entry);
@@ -2384,15 +2618,18 @@ int dc_huff_decode(dc_ctx *c, const uint32_t *d_words, uint64_t bit_base, uint64
         const uint64_t tuples = (groups + 1) / 2;
         const uint64_t wgs = (tuples + nw - 1) / nw;
         const uint64_t grid = wgs < 256 ? wgs : 256;   // persistent: one workgroup per CU
-        if (ensure((void **)&c->d_fix, &c->fix_cap, tuples * sizeof(uint32_t))) return DC_E_HIP;
-        if (nw == 12)
-            LAUNCH(c, "huff_decode", (k_huff_decode8<12, 2>), grid, 12 * 64, d_words, bit_base, d_sync_base,
-                   d_sync_len, n, words, d_table, d_out, c->d_err + 1, c->d_queue, spct, c->d_fix);
-        else
-            LAUNCH(c, "huff_decode", (k_huff_decode8<16, 2>), grid, 16 * 64, d_words, bit_base, d_sync_base,
-                   d_sync_len, n, words, d_table, d_out, c->d_err + 1, c->d_queue, spct, c->d_fix);
-        LAUNCH(c, "huff_decode_fix", (k_huff_decode8_fix<2>), 256, 256, d_words, bit_base, d_sync_base, d_sync_len, n,
-               words, d_table, d_out, c->d_err + 1, c->d_queue, (const uint32_t *)c->d_fix);
+        if (ensure((void **)&c->d_fix, &c->fix_cap, (groups + 64) * sizeof(uint64_t)) ||
+            ensure((void **)&c->d_fixpos, &c->fixpos_cap, (groups * 64 + 64) * sizeof(uint64_t)))
+            return DC_E_HIP;
+        (void)nw;   // 12 waves x 2 chains: the stage and the 14-bit table fill the LDS
+        if (ensure((void **)&c->d_scr, &c->scr_cap, (size_t)D8_SCRATCH_WAVES * D8_WSCR)) return DC_E_HIP;
+        LAUNCH(c, "huff_decode", (k_huff_decode8<12, 2>), grid, 12 * 64, d_words, bit_base, d_sync_base, d_sync_len,
+               n, words, d_table, d_out, c->d_err + 1, c->d_queue, spct, (uint64_t *)c->d_fix,
+               (uint64_t *)c->d_fixpos, (uint8_t *)c->d_scr);
+        c->last_groups = groups;
+        LAUNCH(c, "huff_decode_fix", k_huff_decode8_fix, 256, D8F_WAVES * 64, d_words, n, words, d_table, d_out,
+               c->d_err + 1, (const uint64_t *)c->d_fix, (const uint64_t *)c->d_fixpos,
+               reinterpret_cast<uint4 *>(c->d_scr));
         return DC_OK;
     }
     const uint64_t wgs = (groups + DEC_WAVES - 1) / DEC_WAVES;
@@ -2400,6 +2637,22 @@ int dc_huff_decode(dc_ctx *c, const uint32_t *d_words, uint64_t bit_base, uint64
     LAUNCH(c, "huff_decode", k_huff_decode, grid, DEC_WAVES * 64, d_words, bit_base, d_sync_base, d_sync_len, S, n, d_table,
            d_out, c->d_err + 1);
     return DC_OK;
+}
+
+int dc_huff_decode_redo_count(dc_ctx *c, uint64_t *count)
+{
+    if (!c || !count) return DC_E_ARG;
+    *count = 0;
+    if (!c->d_fix || !c->last_groups) return DC_OK;
+    uint64_t *h = (uint64_t *)malloc(c->last_groups * sizeof(uint64_t));
+    if (!h) return DC_E_ARG;
+    const bool ok = hipMemcpyAsync(h, c->d_fix, c->last_groups * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream) ==
+                        hipSuccess &&
+                    hipStreamSynchronize(c->stream) == hipSuccess;
+    if (ok)
+        for (uint64_t g = 0; g < c->last_groups; ++g) *count += (uint64_t)__builtin_popcountll(h[g]);
+    free(h);
+    return ok ? DC_OK : DC_E_HIP;
 }
 
 int dc_huff_decode_status(dc_ctx *c)

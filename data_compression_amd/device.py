@@ -158,6 +158,12 @@ class Codec:
     def decode_status(self):
         return int(self.L.dc_huff_decode_status(self.ctx))
 
+    def decode_redo_count(self) -> int:
+        """Chunks of the last S = 64 decode that took the exact redo (diagnostic)."""
+        v = C.c_uint64(0)
+        check("dc_huff_decode_redo_count", self.L.dc_huff_decode_redo_count(self.ctx, C.byref(v)))
+        return int(v.value)
+
     def default_sync(self, n: int) -> int:
         return int(self.L.dc_huff_default_sync(n))
 

@@ -40,6 +40,7 @@ enum {
 #define DC_LUT_BITS 12          /* decoder first-level lookup table: 2^12 entries */
 #define DC_MAX_SYMS 1024        /* max_symbol_value + 1 supported by the table kernel */
 #define DC_MAX_DIGITS 128       /* longest code length (in base-n digits) handled */
+#define DC_LUT2_CAP 7168        /* second-level decode entries (escape prefixes x 2^k) */
 #define DC_SYNC_MAX 1024        /* largest sync granularity (u16 chunk bit lengths) */
 
 typedef struct dc_ctx dc_ctx;
@@ -60,6 +61,13 @@ typedef struct dc_dtable {
     uint32_t enc_val[DC_MAX_SYMS];
     int32_t n_ary, w, max_symbol_value, max_bits;
     int32_t min_len, max_len, status, last_written; /* last_written: index M assigned */
+    /* decoder tables indexed by the LSB-first window (the stream's bits in order):
+     * dlut: next 12 bits -> bits | sym << 8; bits 0: a longer code (or no code), whose
+     *       12-bit prefix has escape id sym; dlut2: [id << dlut2_k | next dlut2_k bits] ->
+     *       bits | sym << 8, 0: longer than 12 + dlut2_k bits or invalid (dlut2_k 0: none) */
+    uint16_t dlut[1 << DC_LUT_BITS];
+    uint16_t dlut2[DC_LUT2_CAP];
+    int32_t dlut2_k, pad_[3];
 } dc_dtable;
 
 /* ---- context ------------------------------------------------------------------------ */
@@ -132,6 +140,9 @@ int dc_huff_decode(dc_ctx *ctx, const uint32_t *d_words, uint64_t bit_base, uint
                    uint64_t n, const dc_dtable *d_table, uint8_t *d_out);
 /* status of the last dc_huff_decode on this context (synchronising): 0 or DC_E_STREAM */
 int dc_huff_decode_status(dc_ctx *ctx);
+/* chunks of the last S = 64 dc_huff_decode on this context that took the exact redo (codes
+ * longer than the 12-bit table, partial or over-long groups); synchronising, diagnostic */
+int dc_huff_decode_redo_count(dc_ctx *ctx, uint64_t *count);
 /* base64url text (6 bits per char, MSB-first) of bits [bit_base, bit_base+bits) */
 int dc_huff_base64url(dc_ctx *ctx, const uint32_t *d_words, uint64_t bit_base, uint64_t bits,
                       char *d_text);

@@ -21,6 +21,7 @@ ap.add_argument("--nary", type=int, default=2)
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--iters", type=int, default=10)
 ap.add_argument("--variants", default="v8,v7")
+ap.add_argument("--nocheck", action="store_true", help="ablation builds: skip the output check")
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
 x = synth.device_text(a.cfg, a.size, seed=0xC2, device=dev)
@@ -28,6 +29,7 @@ c = Codec(0)
 enc = c.encode(x, n_ary=a.nary, sync_syms=64)
 out = torch.empty_like(x)
 res = {v: [] for v in a.variants.split(",")}
+fix = {}
 for r in range(a.rounds):
     for v in res:
         os.environ.pop("DC_DECODE_V7", None)
@@ -52,7 +54,10 @@ for r in range(a.rounds):
         kt = c.timings()
         c.timing(False)
         ms = [m for name, m in kt if name == "huff_decode"]
-        res[v].append(float(np.mean(ms)))
-        assert c.decode_status() == 0 and torch.equal(out, x), v
+        fx = [m for name, m in kt if name == "huff_decode_fix"]
+        res[v].append(float(np.mean(ms)) + (float(np.mean(fx)) if fx else 0.0))
+        fix.setdefault(v, []).append(float(np.mean(fx)) if fx else 0.0)
+        assert a.nocheck or (c.decode_status() == 0 and torch.equal(out, x)), v
 for v, l in res.items():
-    print(f"{v}: median {np.median(l):.4f} ms  min {np.min(l):.4f}  ({a.cfg} {a.size >> 20} MiB n={a.nary})", flush=True)
+    print(f"{v}: median {np.median(l):.4f} ms  min {np.min(l):.4f}  (fixup {np.median(fix[v]):.4f}; {a.cfg} "
+          f"{a.size >> 20} MiB n={a.nary}; redo chunks {c.decode_redo_count()})", flush=True)

@@ -1,0 +1,28 @@
+"""Per-wave time split of k_huff_decode8_fix from the -DDC_DIAG build (tools/diag_build.sh _diag -DDC_DIAG)."""
+import ctypes as C
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ["DC_CORE_LIB"] = os.path.join(REPO, "tools", "_diag", "libdc_core.so")
+sys.path.insert(0, REPO)
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from data_compression_amd import _lib, synth  # noqa: E402
+from data_compression_amd.device import Codec  # noqa: E402
+
+x = synth.device_text("C2", 1 << 30, seed=0xC2, device=torch.device("cuda", 0))
+c = Codec(0)
+enc = c.encode(x, n_ary=2, sync_syms=64)
+out = torch.empty_like(x)
+for _ in range(3):
+    c.decode_into(enc, out)
+torch.cuda.synchronize()
+L = _lib.load("libdc_core.so")
+buf = np.zeros(256 * 16 * 4, np.uint64)
+assert L.dc_diag_read(buf.ctypes.data_as(C.c_void_p), C.c_size_t(buf.nbytes)) == 0
+d = buf.reshape(-1, 4)[: 256 * 16].astype(np.float64)
+tot, tab, dec, rounds = d.T
+print(f"fix waves {len(tot)}: total {tot.mean():.0f} cyc (max {tot.max():.0f})  tables {tab.mean():.0f}  "
+      f"decode {dec.mean():.0f} ({dec.sum()/tot.sum():.1%})  rounds {rounds.mean():.2f} (max {rounds.max():.0f})")
