@@ -149,6 +149,30 @@ __global__ __launch_bounds__(256) void k_hist_reduce(const uint16_t *__restrict_
 //     leaf for n = 2.
 //   * canonical values (:1540-1568) with the reference's index-M quirks (:1336, :1421).
 // ------------------------------------------------------------------------------------
+// inclusive wave64 prefix sum in DPP (VALU only: __shfl_up is ds_bpermute, i.e. an LDS
+// instruction queued behind the table reads): row_shr 1/2/4/8 within each row of
+// 16 lanes, then row_bcast:15 and row_bcast:31 across rows (GFX9 DPP)
+static __device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x)
+{
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);   // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);   // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);   // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);   // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);   // row_bcast:15
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);   // row_bcast:31
+    return x;
+}
+
+#ifdef DC_DIAG
+__device__ unsigned long long g_tbldiag[16];
+extern "C" int dc_diag_tbl_read(void *h)
+{
+    return hipMemcpyFromSymbol(h, HIP_SYMBOL(g_tbldiag), sizeof(g_tbldiag)) == hipSuccess ? 0 : -2;
+}
+#define TBL_STAMP(k) do { __syncthreads(); if (threadIdx.x == 0) g_tbldiag[k] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define TBL_STAMP(k)
+#endif
 #define TBL_SORT_MAX 2048
 #define TBL_NODES 4096
 
@@ -167,9 +191,13 @@ __global__ __launch_bounds__(256) void k_huff_table(const uint64_t *__restrict__
     __shared__ uint32_t s_nb[256];
     __shared__ int s_k, s_min, s_max, s_maxbits, s_bad;
     __shared__ uint32_t s_tot_esc[256];
+    __shared__ uint32_t s_rbase[DC_MAX_DIGITS + 1];
+    __shared__ uint32_t s_wcnt[4][DC_MAX_DIGITS + 1];
+    __shared__ uint16_t s_syms[DC_MAX_SYMS];
 
     const int t = threadIdx.x;
     const int leaves = M + 1;
+    TBL_STAMP(0);
     int w = 0;
     while ((1 << w) < nary) ++w;
 
@@ -195,6 +223,7 @@ __global__ __launch_bounds__(256) void k_huff_table(const uint64_t *__restrict__
             s_key[i] = (i < items) ? ((1ull << 11) | (uint64_t)(leaves + (i - k))) : ~0ull;
         for (int i = t; i < TBL_NODES; i += 256) s_parent[i] = 0;
         __syncthreads();
+    TBL_STAMP(1);
         // bitonic sort, ascending
         for (int size = 2; size <= P; size <<= 1) {
             for (int stride = size >> 1; stride > 0; stride >>= 1) {
@@ -208,36 +237,52 @@ __global__ __launch_bounds__(256) void k_huff_table(const uint64_t *__restrict__
                 __syncthreads();
             }
         }
+        TBL_STAMP(8);
         if (t == 0) {
+            // two-queue merge; both queues' heads and next elements held in registers, the
+            // element after them prefetched from LDS when a head is consumed, so no pick
+            // waits for an LDS round trip (the internal queue's next element may not exist
+            // yet: then it is the sum this step appends, taken from a register)
             int h1 = 0, h2 = 0, t2 = 0, active = items;
             const int first_internal = leaves + dummies;
             int next = first_internal;
-            uint64_t head1 = (items > 0) ? s_key[0] : ~0ull;
+            // leaf queue: key[h1 .. h1 + 3] in registers (a 4-deep window refilled from LDS as it
+            // moves); internal queue: q2[h2], q2[h2 + 1] in registers
+            uint64_t a0 = items > 0 ? s_key[0] : ~0ull, a1 = items > 1 ? s_key[1] : ~0ull;
+            uint64_t a2 = items > 2 ? s_key[2] : ~0ull, a3 = items > 3 ? s_key[3] : ~0ull;
+            uint64_t head2 = ~0ull, nxt2 = ~0ull;
             while (active > 1) {
                 uint64_t sum = 0;
                 for (int q = 0; q < nary; ++q) {
-                    const uint64_t c1 = (h1 < items) ? (head1 >> 11) : ~0ull;
-                    const uint64_t c2 = (h2 < t2) ? s_q2[h2] : ~0ull;
+                    const uint64_t c1 = (h1 < items) ? (a0 >> 11) : ~0ull;
+                    const uint64_t c2 = (h2 < t2) ? head2 : ~0ull;
                     int idx;
                     if (h1 < items && (h2 == t2 || c1 <= c2)) {
-                        idx = (int)(head1 & 2047u);
+                        idx = (int)(a0 & 2047u);
                         sum += c1;
                         ++h1;
-                        head1 = (h1 < items) ? s_key[h1] : ~0ull;
+                        a0 = a1; a1 = a2; a2 = a3;
+                        a3 = (h1 + 3 < items) ? s_key[h1 + 3] : ~0ull;
                     } else {
                         idx = first_internal + h2;
                         sum += c2;
                         ++h2;
+                        head2 = nxt2;
+                        nxt2 = (h2 + 1 < t2) ? s_q2[h2 + 1] : ~0ull;
                     }
-                    if (idx < TBL_NODES) s_parent[idx] = (int16_t)next;
+                    if (t == 0 && idx < TBL_NODES) s_parent[idx] = (int16_t)next;
                 }
-                s_q2[t2++] = sum;
+                if (t == 0) s_q2[t2] = sum;
+                if (t2 == h2) head2 = sum;            // the queue was empty
+                else if (t2 == h2 + 1) nxt2 = sum;   // it held one element
+                ++t2;
                 ++next;
                 active -= nary - 1;
             }
-            if (next >= TBL_NODES) s_bad = 1;
+            if (t == 0 && next >= TBL_NODES) s_bad = 1;
         }
         __syncthreads();
+    TBL_STAMP(2);
         // depth = number of parent hops to the root (n_ary_huffman.c:1069-1076)
         for (int i = t; i < leaves; i += 256) {
             int d = 0, c = i;
@@ -250,25 +295,44 @@ __global__ __launch_bounds__(256) void k_huff_table(const uint64_t *__restrict__
     for (int L = t; L < DC_MAX_DIGITS + 2; L += 256) s_cnt[L] = 0;
     __syncthreads();
 
+    TBL_STAMP(3);
     // canonical codes: min/max over i < M, assignment over i <= M
-    for (int i = t; i < M; i += 256) {
-        const int L = s_len[i];
-        atomicMax(&s_max, L);
-        if (L > 0) atomicMin(&s_min, L);
+    {   // min / max length over i < M: per thread, per wave (shuffles), one atomic per wave
+        int mx = 0, mnl = 300;
+        for (int i = t; i < M; i += 256) {
+            const int L = s_len[i];
+            mx = max(mx, L);
+            if (L > 0) mnl = min(mnl, L);
+        }
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            mx = max(mx, __shfl_xor(mx, d, 64));
+            mnl = min(mnl, __shfl_xor(mnl, d, 64));
+        }
+        if ((t & 63) == 0) { atomicMax(&s_max, mx); atomicMin(&s_min, mnl); }
     }
     __syncthreads();
     const int minL = s_min, maxL = s_max;
     if (maxL > DC_MAX_DIGITS) {
         if (t == 0) s_bad = 1;
     }
-    for (int i = t; i < leaves; i += 256) {
-        const int L = s_len[i];
-        if (L >= minL && L <= maxL && L <= DC_MAX_DIGITS) atomicAdd(&s_cnt[L], 1u);
+    for (int i0 = 0; i0 < leaves; i0 += 256) {   // counts per length: a ballot per distinct length
+        const int i = i0 + t;
+        const int L = i < leaves ? s_len[i] : 0;
+        const int key = (i < leaves && L >= minL && L <= maxL && L <= DC_MAX_DIGITS) ? L : -1;
+        uint64_t todo = __ballot(key >= 0);
+        while (todo) {
+            const int L0 = __builtin_amdgcn_readlane(key, __builtin_ctzll(todo));
+            const uint64_t m = __ballot(key == L0);
+            if ((t & 63) == 0) atomicAdd(&s_cnt[L0], (uint32_t)__popcll(m));
+            todo &= ~m;
+        }
     }
     __syncthreads();
     if (t == 0) {
         uint32_t code = 0, acc = 0;   // reference: int arithmetic, wraps mod 2^32
         for (int L = 0; L <= DC_MAX_DIGITS; ++L) {
+            if (L > maxL) { s_starti[L] = acc; s_startv[L] = 0; continue; }
             s_starti[L] = acc;
             if (L >= minL && L <= maxL) {
                 s_startv[L] = code;
@@ -281,23 +345,58 @@ __global__ __launch_bounds__(256) void k_huff_table(const uint64_t *__restrict__
     }
     for (int s = t; s < 256; s += 256) { s_code[s] = 0; s_nb[s] = 0; }
     __syncthreads();
-    for (int i = t; i < leaves; i += 256) {
-        const int L = s_len[i];
+    for (int L = t; L <= DC_MAX_DIGITS; L += 256) s_rbase[L] = 0;
+    for (int q = t; q < 4 * (DC_MAX_DIGITS + 1); q += 256) (&s_wcnt[0][0])[q] = 0;
+    __syncthreads();
+    const int wvt = t >> 6, lnt = t & 63;
+    for (int i0 = 0; i0 < leaves; i0 += 256) {
+        // canonical rank = symbols of the same length before this one (index order):
+        // within the wave by ballot per distinct length, across waves and chunks from counts
+        const int i = i0 + t;
+        const int L = i < leaves ? s_len[i] : 0;
+        const bool coded = i < leaves && L >= minL && L <= maxL && L <= DC_MAX_DIGITS;
+        const int key = coded ? L : -1;
+        uint32_t r_in = 0;
+        uint64_t todo = __ballot(coded);
+        while (todo) {
+            const int L0 = __builtin_amdgcn_readlane(key, __builtin_ctzll(todo));
+            const uint64_t m = __ballot(key == L0);
+            if (key == L0) r_in = (uint32_t)__popcll(m & ((1ull << lnt) - 1));
+            if (lnt == 0) s_wcnt[wvt][L0] = (uint32_t)__popcll(m);
+            todo &= ~m;
+        }
+        __syncthreads();
+        uint32_t rank = r_in;
+        if (coded) {
+            rank += s_rbase[L];
+            for (int q = 0; q < wvt; ++q) rank += s_wcnt[q][L];
+        }
+        __syncthreads();
+        for (int LL = t; LL <= DC_MAX_DIGITS; LL += 256) {
+            s_rbase[LL] += s_wcnt[0][LL] + s_wcnt[1][LL] + s_wcnt[2][LL] + s_wcnt[3][LL];
+            s_wcnt[0][LL] = s_wcnt[1][LL] = s_wcnt[2][LL] = s_wcnt[3][LL] = 0;
+        }
+        __syncthreads();
+        if (i >= leaves) continue;
         T->lengths[i] = L;
-        if (L >= minL && L <= maxL && L <= DC_MAX_DIGITS) {
-            uint32_t rank = 0;
-            for (int j = 0; j < i; ++j) rank += (s_len[j] == L);
+        if (coded) {
             const uint32_t val = s_startv[L] + rank;
             T->enc_len[i] = L;
             T->enc_val[i] = val;
             T->syms[s_starti[L] + rank] = (uint16_t)i;
+            s_syms[(s_starti[L] + rank) & (DC_MAX_SYMS - 1)] = (uint16_t)i;
             if (i < 256) {
-                // L base-n digits of val, MSB-first, w bits each
+                // L base-n digits of val, MSB-first, w bits each (n = 2^w: the bits of val)
                 if ((long long)L * w <= 32) {
-                    uint64_t v = val, packed = 0;
-                    for (int d = 0; d < L; ++d) {
-                        packed |= (v % (uint64_t)nary) << (w * d);
-                        v /= (uint64_t)nary;
+                    uint32_t v = val;
+                    uint64_t packed = 0;
+                    if ((nary & (nary - 1)) == 0) {
+                        packed = (L * w >= 32) ? (uint64_t)val : ((uint64_t)val & ((1ull << (L * w)) - 1));
+                    } else {
+                        for (int d = 0; d < L; ++d) {
+                            packed |= (uint64_t)(v % (uint32_t)nary) << (w * d);
+                            v /= (uint32_t)nary;
+                        }
                     }
                     s_code[i] = (uint32_t)packed;
                     s_nb[i] = (uint32_t)(L * w);
@@ -331,20 +430,38 @@ __global__ __launch_bounds__(256) void k_huff_table(const uint64_t *__restrict__
         else lim = ((uint64_t)s_startv[Ld] + s_cnt[Ld]) << (32 - Ld * w);
         T->lim[t] = lim;
     }
+    TBL_STAMP(4);
     // one-symbol table in LDS (reuses s_key): window -> sym | nbits<<8, 0 = longer code
     uint32_t *s_lut1 = reinterpret_cast<uint32_t *>(s_key);
     for (int e = t; e < (1 << DC_LUT_BITS); e += 256) s_lut1[e] = 0;
     __syncthreads();
     T->code[t] = s_code[t];
     T->nbits[t] = s_nb[t];
-    for (int s = 0; s < 256; ++s) {
-        const uint32_t nb = s_nb[s];
-        if (nb == 0 || nb > DC_LUT_BITS) continue;
-        const uint32_t span = 1u << (DC_LUT_BITS - nb);
-        const uint32_t base = s_code[s] << (DC_LUT_BITS - nb);
-        for (uint32_t j = t; j < span; j += 256) s_lut1[base + j] = s | (nb << 8);
+    if ((nary & (nary - 1)) == 0) {
+        // n = 2^w: a 12-bit window's code is the canonical one whose value at its length
+        // matches (lengths ascending), decoded per entry
+        for (int e = t; e < (1 << DC_LUT_BITS); e += 256) {
+            uint32_t v1 = 0;
+            for (int L = minL; L <= maxL && L * w <= DC_LUT_BITS; ++L) {
+                const uint32_t b = (uint32_t)(L * w), v = (uint32_t)e >> (DC_LUT_BITS - b);
+                if (v - s_startv[L] < s_cnt[L]) {
+                    const uint32_t sym = s_syms[(s_starti[L] + v - s_startv[L]) & (DC_MAX_SYMS - 1)];
+                    v1 = sym < 256 ? (sym | (b << 8)) : 0u;
+                    break;
+                }
+            }
+            s_lut1[e] = v1;
+        }
+    } else {   // thread s fills its own code's span
+        const uint32_t nb = s_nb[t];
+        if (nb != 0 && nb <= DC_LUT_BITS) {
+            const uint32_t span = 1u << (DC_LUT_BITS - nb);
+            const uint32_t base = s_code[t] << (DC_LUT_BITS - nb);
+            for (uint32_t j = 0; j < span; ++j) s_lut1[base + j] = (uint32_t)t | (nb << 8);
+        }
     }
     __syncthreads();
+    TBL_STAMP(5);
     // two-symbol table: a window holding a whole second code after the first yields both
     // (DC_LUT_* layout in dc_gpu.h)
     for (int e = t; e < (1 << DC_LUT_BITS); e += 256) {
@@ -359,6 +476,7 @@ __global__ __launch_bounds__(256) void k_huff_table(const uint64_t *__restrict__
         }
         T->lut[e] = v;
     }
+    TBL_STAMP(6);
     // decoder tables on the LSB-first window (dc_gpu.h): dlut = the one-symbol table at the
     // bit-reversed index; escape prefixes (entries 0) numbered in index order; dlut2 filled
     // per symbol: a code of 12 < b <= 12 + k bits covers 2^(12 + k - b) entries of its
@@ -373,14 +491,21 @@ __global__ __launch_bounds__(256) void k_huff_table(const uint64_t *__restrict__
         d1[j] = a ? ((a >> 8) | ((a & 255u) << 8)) : 0u;
         nesc += a ? 0u : 1u;
     }
-    s_tot_esc[t] = nesc;
-    __syncthreads();
-    if (t == 0) {
-        uint32_t run = 0;
-        for (int q = 0; q < 256; ++q) { const uint32_t v = s_tot_esc[q]; s_tot_esc[q] = run; run += v; }
-        s_k = (int)run;   // escape prefixes
+    {   // exclusive scan of the per-thread escape counts: DPP inside each wave, 4 wave totals
+        const uint32_t inc = wave_scan_incl(nesc);
+        if ((t & 63) == 63) s_tot_esc[t >> 6] = inc;
+        __syncthreads();
+        uint32_t before = 0, all = 0;
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t v = s_tot_esc[q];
+            before += (q < (t >> 6)) ? v : 0u;
+            all += v;
+        }
+        __syncthreads();
+        s_tot_esc[t] = before + inc - nesc;
+        if (t == 0) s_k = (int)all;   // escape prefixes
+        __syncthreads();
     }
-    __syncthreads();
     const uint32_t E = (uint32_t)s_k;
     const uint32_t K = (uint32_t)min(max(s_maxbits - DC_LUT_BITS, 1), 8);
     const bool l2ok = E > 0 && E <= 256 && (E << K) <= DC_LUT2_CAP && s_maxbits <= 32;
@@ -406,6 +531,9 @@ __global__ __launch_bounds__(256) void k_huff_table(const uint64_t *__restrict__
     }
     if (t == 0) {
         T->dlut2_k = l2ok ? (int32_t)K : 0;
+#ifdef DC_DIAG
+        g_tbldiag[7] = __builtin_amdgcn_s_memtime();
+#endif
         T->n_ary = nary;
         T->w = w;
         T->max_symbol_value = M;
@@ -506,19 +634,6 @@ __global__ void k_zero_bounds(const uint64_t *__restrict__ off, uint64_t nblocks
     words[(abs >> 5) - (bit_base >> 5)] = 0u;
 }
 
-// inclusive wave64 prefix sum in DPP (VALU only: __shfl_up is ds_bpermute, i.e. an LDS
-// instruction queued behind the table reads): row_shr 1/2/4/8 within each row of
-// 16 lanes, then row_bcast:15 and row_bcast:31 across rows (GFX9 DPP)
-static __device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x)
-{
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);   // row_shr:1
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);   // row_shr:2
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);   // row_shr:4
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);   // row_shr:8
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);   // row_bcast:15
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);   // row_bcast:31
-    return x;
-}
 
 // ------------------------------------------------------------------------------------
 // (H7) pack. One workgroup per 32 KiB block (grid-stride), 8 tiles of 4 KiB; a lane
