@@ -618,6 +618,87 @@ __global__ __launch_bounds__(1024) void k_block_scan(uint64_t *__restrict__ bits
     }
 }
 
+// Plan in two launches (k_block_bits + the single-workgroup k_block_scan read 32768
+// offsets with strided, uncoalesced loads: 40 us on 1 GiB): (1) a workgroup per 64 blocks
+// computes their bit counts and scans them locally; (2) one workgroup scans the workgroup
+// totals and writes every block's absolute offset, coalesced.
+#define PLAN_WG_BLOCKS 64
+#define PLAN_MAX_WG 16384   /* workgroup bases in LDS (128 KiB): streams up to 32 GiB per call */
+__global__ __launch_bounds__(256) void k_block_local(const uint16_t *__restrict__ bh, uint64_t nblocks,
+                                                     const dc_dtable *__restrict__ T, uint32_t *__restrict__ local,
+                                                     uint32_t *__restrict__ wgtot, int *__restrict__ err)
+{
+    __shared__ uint32_t s_nb[256];
+    __shared__ uint32_t s_bits[PLAN_WG_BLOCKS];
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    s_nb[t] = T->nbits[t];
+    __syncthreads();
+    const uint64_t b0 = (uint64_t)blockIdx.x * PLAN_WG_BLOCKS;
+    int missing = 0;
+    for (int k = 0; k < PLAN_WG_BLOCKS / 4; ++k) {
+        const int j = wv * (PLAN_WG_BLOCKS / 4) + k;
+        const uint64_t b = b0 + j;
+        uint32_t acc = 0;
+        if (b < nblocks) {
+            const uint2 h = *reinterpret_cast<const uint2 *>(bh + b * 256 + lane * 4);
+            const uint32_t c[4] = {h.x & 0xFFFFu, h.x >> 16, h.y & 0xFFFFu, h.y >> 16};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t nb = s_nb[lane * 4 + q];
+                acc += c[q] * nb;
+                missing |= (c[q] != 0 && nb == 0);
+            }
+        }
+        acc = (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_incl(acc), 63);   // <= 2^20 per block
+        if (lane == 0) s_bits[j] = acc;
+    }
+    if (__any(missing) && lane == 0) atomicOr(err, 1);
+    __syncthreads();
+    if (wv == 0) {
+        const uint32_t v = s_bits[lane];
+        const uint32_t incl = wave_scan_incl(v);   // <= 2^26 per workgroup
+        if (b0 + lane < nblocks) local[b0 + lane] = incl - v;
+        if (lane == 63) wgtot[blockIdx.x] = incl;
+    }
+}
+
+__global__ __launch_bounds__(1024) void k_block_final(const uint32_t *__restrict__ local,
+                                                      const uint32_t *__restrict__ wgtot, uint64_t nblocks,
+                                                      uint32_t nwg, uint64_t *__restrict__ off,
+                                                      uint64_t *__restrict__ d_total)
+{
+    __shared__ uint64_t s_base[PLAN_MAX_WG];
+    __shared__ uint64_t s_w[16];
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    uint64_t run = 0;
+    for (uint32_t c0 = 0; c0 < nwg; c0 += 1024) {
+        const uint32_t i = c0 + t;
+        const uint64_t v = i < nwg ? wgtot[i] : 0ull;
+        uint64_t incl = v;   // 64-bit wave scan (a small kernel: shuffles are fine)
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint64_t y = __shfl_up(incl, d, 64);
+            if (lane >= d) incl += y;
+        }
+        if (lane == 63) s_w[wv] = incl;
+        __syncthreads();
+        uint64_t before = 0, all = 0;
+        for (int q = 0; q < 16; ++q) {
+            const uint64_t x = s_w[q];
+            before += (q < wv) ? x : 0ull;
+            all += x;
+        }
+        if (i < nwg) s_base[i] = run + before + incl - v;
+        run += all;
+        __syncthreads();
+    }
+    for (uint64_t b = t; b < nblocks; b += 1024) off[b] = s_base[b / PLAN_WG_BLOCKS] + local[b];
+    if (t == 0) {
+        off[nblocks] = run;
+        *d_total = run;
+    }
+}
+
 // zero every word that two blocks share (the words holding a block start) before
 // k_huff_pack OR-merges into them
 __global__ void k_zero_bounds(const uint64_t *__restrict__ off, uint64_t nblocks, uint64_t bit_base,
@@ -2348,6 +2429,7 @@ struct dc_ctx {
     uint16_t *d_bh;         size_t bh_cap;        // block histograms (u16 x 256 per block)
     uint64_t *d_partials;                         // 1024 x 256
     uint64_t *d_off;        size_t off_cap;       // nblocks + 1
+    uint32_t *d_plan;       size_t plan_cap;      // plan: per-block local offsets + workgroup totals
     int *d_err;                                   // [0] plan, [1] decode
     uint32_t *d_queue;                            // decode tuple scheduler heads (D8Sched)
     uint32_t *d_fix;        size_t fix_cap;       // decode redo: a u64 chunk mask per group
@@ -2461,6 +2543,7 @@ void dc_ctx_destroy(dc_ctx *c)
     if (c->d_bh) (void)hipFree(c->d_bh);
     if (c->d_partials) (void)hipFree(c->d_partials);
     if (c->d_off) (void)hipFree(c->d_off);
+    if (c->d_plan) (void)hipFree(c->d_plan);
     if (c->d_err) (void)hipFree(c->d_err);
     if (c->d_queue) (void)hipFree(c->d_queue);
     if (c->d_fix) (void)hipFree(c->d_fix);
@@ -2602,9 +2685,18 @@ int dc_huff_plan(dc_ctx *c, const dc_dtable *d_table, uint64_t *d_total_bits)
         c->plan_ok = true;
         return DC_OK;
     }
-    LAUNCH(c, "block_bits", k_block_bits, (nb + 3) / 4, 256, (const uint16_t *)c->d_bh, nb, d_table, c->d_off,
-           c->d_err);
-    LAUNCH(c, "block_scan", k_block_scan, 1, 1024, c->d_off, nb, d_total_bits);
+    const uint64_t nwg = (nb + PLAN_WG_BLOCKS - 1) / PLAN_WG_BLOCKS;
+    if (nwg <= PLAN_MAX_WG) {
+        if (ensure((void **)&c->d_plan, &c->plan_cap, (nb + nwg + 64) * sizeof(uint32_t))) return DC_E_HIP;
+        uint32_t *loc = c->d_plan, *tot = c->d_plan + nb + 32;
+        LAUNCH(c, "block_bits", k_block_local, nwg, 256, (const uint16_t *)c->d_bh, nb, d_table, loc, tot, c->d_err);
+        LAUNCH(c, "block_scan", k_block_final, 1, 1024, (const uint32_t *)loc, (const uint32_t *)tot, nb,
+               (uint32_t)nwg, c->d_off, d_total_bits);
+    } else {
+        LAUNCH(c, "block_bits", k_block_bits, (nb + 3) / 4, 256, (const uint16_t *)c->d_bh, nb, d_table, c->d_off,
+               c->d_err);
+        LAUNCH(c, "block_scan", k_block_scan, 1, 1024, c->d_off, nb, d_total_bits);
+    }
     c->plan_ok = true;
     return DC_OK;
 }
