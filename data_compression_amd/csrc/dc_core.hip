@@ -529,6 +529,31 @@ __global__ __launch_bounds__(256) void k_huff_table(const uint64_t *__restrict__
             for (uint32_t j = 0; j < (1u << (K - tl)); ++j) T->dlut2[base | rt | (j << tl)] = (uint16_t)(nb | ((uint32_t)t << 8));
         }
     }
+    __syncthreads();   // dlut2 complete
+    // dlut14, two entries per u32 store (coalesced): entry x = dlut entry x & 4095 (from
+    // s_lut1, as d1 above), an escape there resolved on the next 2 bits by dlut2 when that
+    // code fits 14 bits
+    {
+        const bool l2_14 = l2ok && K >= DC_LUT14_BITS - DC_LUT_BITS;
+        uint32_t *const d14 = reinterpret_cast<uint32_t *>(T->dlut14);
+#pragma unroll 8
+        for (uint32_t p = t; p < (1u << DC_LUT14_BITS) / 2; p += 256) {
+            uint32_t pr = 0;
+#pragma unroll
+            for (uint32_t q = 0; q < 2; ++q) {
+                const uint32_t x = 2 * p + q, i = x & ((1u << DC_LUT_BITS) - 1), h = x >> DC_LUT_BITS;
+                const uint32_t a = s_lut1[__builtin_bitreverse32(i) >> (32 - DC_LUT_BITS)];
+                uint32_t e = (a >> 8) | ((a & 255u) << 8);
+                if (!a) {
+                    const uint32_t esc = s_esc[i];
+                    const uint32_t e2 = l2_14 ? T->dlut2[(esc << K) | h] : 0u;
+                    e = (e2 && (e2 & 255u) <= DC_LUT14_BITS) ? e2 : ((esc & 255u) << 8);
+                }
+                pr |= e << (16 * q);
+            }
+            d14[p] = pr;
+        }
+    }
     if (t == 0) {
         T->dlut2_k = l2ok ? (int32_t)K : 0;
 #ifdef DC_DIAG
@@ -1271,7 +1296,7 @@ __global__ __launch_bounds__(DEC_WAVES * 64) void k_huff_decode(const uint32_t *
 #define D8_MAX_WAVES 16
 
 struct Dec8Lds {
-    uint16_t lut[1 << D8_LUT_BITS];   // LSB-first 14-bit window -> len | sym << 8; len 0: a longer code
+    __attribute__((aligned(16))) uint16_t lut[1 << D8_LUT_BITS];   // LSB-first 14-bit window -> len | sym << 8; len 0: a longer code
     uint32_t exhausted;               // scheduler: bit h = slice h is empty
     __attribute__((aligned(16))) uint32_t stage[D8_CHAINS][D8_STAGE_WORDS];
     uint32_t tail_pad[64];            // a corrupt stream's windows may run past the last stage
@@ -1521,8 +1546,7 @@ static __device__ __forceinline__ void d8_issue(uint4 (&v)[NC][5], const D8Geo<N
 // resets the heads for the next launch on the stream.
 #define D8_STATIC_PCT 60
 #define D8_QSTRIDE 1024   /* u32 between heads */
-#define D8_FIX_CNT (9 * D8_QSTRIDE)                /* tuples queued for the exact redo        */
-#define D8_FIX_DONE (10 * D8_QSTRIDE)              /* redo waves finished                    */
+#define D8_FIX_CNT (9 * D8_QSTRIDE)                /* chunks listed for the exact redo        */
 #define D8_QWORDS (11 * D8_QSTRIDE)
 #define D8_WSCR (2 * 4096 + 66 * 8 + 512)            /* per-wave scratch of the decoders (bytes)  */
 #define D8_SCRATCH_WAVES 4096                        /* waves with a scratch slot (both kernels)  */
@@ -1624,19 +1648,16 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode8(const uint32_t *__rest
     // read length 0
     // D8_LUT_BITS first level from the 12-bit one and its second level: 2.9% of C2 chunks hold a
     // code of > 14 bits (to the exact redo), 6.6% one of > 12
-    const uint32_t K2 = (uint32_t)T->dlut2_k;
-    for (int i = t; i < (1 << D8_LUT_BITS); i += NT) {
-        uint32_t e = T->dlut[i & ((1 << DC_LUT_BITS) - 1)];
-        if ((e & 255u) == 0 && K2 >= D8_LUT_BITS - DC_LUT_BITS) {
-            const uint32_t e2 = T->dlut2[((e >> 8) << K2) | ((uint32_t)i >> DC_LUT_BITS)];
-            e = (e2 && (e2 & 255u) <= D8_LUT_BITS) ? e2 : (e & 0xff00u);
-        }
-        L.lut[i] = (uint16_t)e;
+    // the 14-bit first level (dc_dtable.dlut14, built by k_huff_table): 2.5% of C2 chunks
+    // hold a code of > 14 bits (to the exact redo)
+    static_assert(D8_LUT_BITS == DC_LUT14_BITS, "table width");
+    for (int i = t; i < (1 << D8_LUT_BITS) / 8; i += NT)
+        reinterpret_cast<uint4 *>(L.lut)[i] = reinterpret_cast<const uint4 *>(T->dlut14)[i];
 #ifdef DC_DIAG_SYNTH_LUT   // timing ablation only: every window is a 4-bit code (garbage output)
-        L.lut[i] = (uint16_t)(4u | ((i & 255u) << 8));
+    for (int i = t; i < (1 << D8_LUT_BITS); i += NT) L.lut[i] = (uint16_t)(4u | ((i & 255u) << 8));
 #endif
-    }
     if (t == 0) L.exhausted = 0;
+    if (blockIdx.x == 0 && t == 0) queue[D8_FIX_CNT] = 0u;   // k_huff_fix_list's counter (runs after)
     __syncthreads();
 
     // the launcher guarantees n < 2^37 (chunk and tuple indices fit 32 bits)
@@ -1785,46 +1806,32 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode8(const uint32_t *__rest
 #endif
 }
 
-// position of the rank-th set bit of m (rank < popcount(m))
-static __device__ __forceinline__ uint32_t select_bit(uint64_t m, uint32_t rank)
-{
-    uint32_t pos = 0;
-#pragma unroll
-    for (int sh = 32; sh >= 1; sh >>= 1) {
-        const uint32_t c = (uint32_t)__popcll(m & ((1ull << sh) - 1));
-        if (rank >= c) { rank -= c; m >>= sh; pos += (uint32_t)sh; }
-    }
-    return pos;
-}
-
 // Exact decode of the chunks k_huff_decode8 flagged (fix_mask: a bit per chunk, fix_pos: the
-// chunk's bit offset inside its group span). A wave takes 64 groups at a time, compacts their
-// flagged chunks (popcount scan, then a search per lane) and decodes one chunk per lane from
-// HBM with a sliding 3-word window and the next word already in flight: the 12-bit table and
-// the canonical tables for longer codes (d8_long's rule) are all in LDS.
+// chunk's first bit), compacted into one list by k_huff_fix_list: one chunk per lane, decoded
+// from its span staged in LDS; the 12-bit table and the canonical tables for longer codes
+// (d8_long's rule) are all in LDS.
 #define D8F_WAVES 12
-#define D8F_ROW 16   /* words of a lane's staged span (longer chunks re-stage it further on) */
+#define D8F_ROW 32   /* words of a lane's staged span (longer chunks re-stage it further on) */
+static_assert(offsetof(dc_dtable, dlut14) % 16 == 0 && offsetof(dc_dtable, dlut2) % 8 == 0, "table copies");
 struct FixLds {
-    uint16_t lut[1 << DC_LUT_BITS];
+    __attribute__((aligned(16))) uint16_t lut[1 << D8_LUT_BITS];   // the fast decoder's 14-bit first level
     uint16_t lut2[DC_LUT2_CAP];
     uint64_t lim[33];
     uint32_t first[DC_MAX_DIGITS + 1], count[DC_MAX_DIGITS + 1], start[DC_MAX_DIGITS + 1];
     uint16_t syms[DC_MAX_SYMS];
-    uint64_t mask[D8F_WAVES][64];
-    uint32_t excl[D8F_WAVES][64];
     uint32_t rows[D8F_WAVES][64 * (D8F_ROW + 1)];   // a lane's chunk span (odd stride: conflict-free)
-    uint32_t orow[D8F_WAVES][64 * 17];              // a lane's output bytes (odd stride)
 };
 
-// d8_long on the LDS copies: the code at the start of an LSB-first 64-bit window
-static __device__ uint32_t d8_long_lds(uint32_t lo, uint32_t hi, const FixLds &F, int nary, int w, bool pow2, int *bad)
+// d8_long on the LDS copies: the code at the start of an LSB-first 64-bit window; 0 for an
+// invalid code (out of line: rare, and inlined 4 times it cost 70 VGPRs)
+static __device__ __noinline__ uint32_t d8_long_lds(uint32_t lo, uint32_t hi, const FixLds &F, int nary, int w, bool pow2)
 {
     const uint64_t win = ((uint64_t)__builtin_bitreverse32(lo) << 32) | __builtin_bitreverse32(hi);   // MSB-first
     if (pow2) {
         const uint64_t top = win >> 32;
         uint32_t b = 1;
         while (b <= 32 && top >= F.lim[b]) ++b;
-        if (b > 32) { *bad = 1; return 0u; }
+        if (b > 32) return 0u;
         const uint32_t Ld = b / (uint32_t)w;
         const uint32_t v = (uint32_t)(top >> (32 - b));
         return b | ((F.syms[(F.start[Ld] + (v - F.first[Ld])) & (DC_MAX_SYMS - 1)] & 255u) << 8);
@@ -1838,95 +1845,74 @@ static __device__ uint32_t d8_long_lds(uint32_t lo, uint32_t hi, const FixLds &F
         if (cnt && v - F.first[Ld] < cnt)
             return (uint32_t)(Ld * w) | ((F.syms[(F.start[Ld] + (v - F.first[Ld])) & (DC_MAX_SYMS - 1)] & 255u) << 8);
     }
-    *bad = 1;
     return 0u;
 }
 
-// one code from the window (lo, hi): 12-bit table, second level, canonical search
-static __device__ __forceinline__ uint32_t d8f_code(uint32_t lo, uint32_t hi, const FixLds &F, uint32_t K2,
-                                                    uint32_t kmask, int nary, int w, bool pow2, int *bad)
+// The flagged chunks as one compact list (chunk indices, any order), so the fixup deals
+// them out in full rounds of 64, evenly over its waves. A 1024-thread workgroup covers 16
+// windows of 64 groups and reserves its room with ONE atomic on `cnt` (a single word
+// saturates near 88 atomics/us: one per wave cost 50 us on 1 GiB). (Dealing whole windows
+// to the fixup's waves instead left them 1 or 2 windows of ~100 chunks each: 2.3x max/mean.)
+__global__ __launch_bounds__(1024) void k_huff_fix_list(const uint64_t *__restrict__ fix_mask, uint32_t ngroups,
+                                                        uint32_t nchunks, uint32_t *__restrict__ list,
+                                                        uint32_t *__restrict__ cnt)
 {
-    uint32_t e = F.lut[lo & ((1u << DC_LUT_BITS) - 1)];
-    if ((e & 255u) == 0) {
-        e = K2 ? F.lut2[((e >> 8) << K2) | ((lo >> DC_LUT_BITS) & kmask)] : 0u;
-        if (e == 0) e = d8_long_lds(lo, hi, F, nary, w, pow2, bad);
-    }
-    return e;
-}
-
-// Where the fixup's rounds come from: windows of 64 groups (a wave's own, grid stride), the
-// flagged chunks of a window compacted by a popcount scan, 64 per round.
-struct D8FCur {
-    uint32_t win, r, tot;   // window, first item of the round, items in the window
-    bool live;
-};
-
-static __device__ __forceinline__ void d8f_window(D8FCur &q, uint32_t ngroups, uint32_t nwin, uint32_t wstride,
-                                                  const uint64_t *__restrict__ fix_mask, FixLds &F, int wv, int lane)
-{
-    // from q.win on, the next window with flagged chunks; its masks and scan into LDS
-    for (; q.win < nwin; q.win += wstride) {
-        const uint32_t g = q.win * 64 + lane;
-        const uint64_t m = g < ngroups ? fix_mask[g] : 0ull;
-        const uint32_t cnt = (uint32_t)__popcll(m);
-        const uint32_t incl = wave_scan_incl(cnt);
-        q.tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-        if (q.tot) {
-            F.mask[wv][lane] = m;
-            F.excl[wv][lane] = incl - cnt;
-            __builtin_amdgcn_wave_barrier();
-            q.r = 0;
-            q.live = true;
-            return;
-        }
-    }
-    q.live = false;
-}
-
-static __device__ __forceinline__ void d8f_next(D8FCur &q, uint32_t ngroups, uint32_t nwin, uint32_t wstride,
-                                                const uint64_t *__restrict__ fix_mask, FixLds &F, int wv, int lane)
-{
-    if (!q.live) return;
-    if (q.r + 64 < q.tot) { q.r += 64; return; }
-    q.win += wstride;
-    d8f_window(q, ngroups, nwin, wstride, fix_mask, F, wv, lane);
-}
-
-// this lane's chunk in round q (or ~0u)
-static __device__ __forceinline__ uint32_t d8f_chunk(const D8FCur &q, uint32_t nchunks, const FixLds &F, int wv,
-                                                     int lane)
-{
-    const uint32_t item = q.r + (uint32_t)lane;
-    if (!q.live || item >= q.tot) return ~0u;
-    uint32_t wi = 0;   // last word whose exclusive count is <= item
+    __shared__ uint32_t s_w[16];
+    __shared__ uint32_t s_base;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t g = blockIdx.x * 1024 + threadIdx.x;
+    uint64_t m = g < ngroups ? fix_mask[g] : 0ull;
+    const uint64_t c0 = (uint64_t)g * DC_SYNC_GROUP;   // chunks past the end are never redone
+    if (c0 + DC_SYNC_GROUP > nchunks) m = c0 >= nchunks ? 0ull : m & ((1ull << (nchunks - c0)) - 1);
+    const uint32_t c = (uint32_t)__popcll(m);
+    const uint32_t incl = wave_scan_incl(c);
+    if (lane == 63) s_w[wv] = incl;
+    __syncthreads();
+    uint32_t before = 0, all = 0;
 #pragma unroll
-    for (uint32_t step = 32; step >= 1; step >>= 1)
-        if (wi + step <= 63 && F.excl[wv][wi + step] <= item) wi += step;
-    const uint32_t ch = (q.win * 64 + wi) * DC_SYNC_GROUP + select_bit(F.mask[wv][wi], item - F.excl[wv][wi]);
-    return ch < nchunks ? ch : ~0u;
+    for (int q = 0; q < 16; ++q) {
+        const uint32_t x = s_w[q];
+        before += q < wv ? x : 0u;
+        all += x;
+    }
+    if (all == 0) return;   // uniform over the workgroup
+    if (threadIdx.x == 0) s_base = atomicAdd(cnt, all);
+    __syncthreads();
+    uint32_t e = s_base + before + incl - c;
+    while (m) {
+        list[e++] = (uint32_t)c0 + (uint32_t)__builtin_ctzll(m);
+        m &= m - 1;
+    }
 }
 
-// Exact decode of the chunks k_huff_decode8 flagged (fix_mask: a bit per chunk, fix_pos: the
-// chunk's first bit, from word_base). Persistent, D8F_WAVES waves per CU; per wave a pipeline
-// over rounds of 64 chunks (one per lane): while round A decodes from its LDS rows, the spans
-// of round B are in flight into registers and the start position of round C too. A round
-// decodes from LDS: 12-bit table, second level, canonical search for longer codes.
+// Exact decode of the chunks k_huff_decode8 flagged (fix_pos: the chunk's first bit, from
+// word_base), listed by k_huff_fix_list. Persistent, D8F_WAVES waves per CU; wave w takes
+// rounds w, w + P, ... of 64 list items (one chunk per lane). Per wave a pipeline: while round
+// A decodes from its LDS rows, the spans of round B are in flight into registers and the
+// start positions of round C too. Per symbol a branch-free two-level lookup (the fast
+// decoder's 14-bit table, then the second level on the next K bits: both always read, the
+// first entry's length selects) and a canonical search only for codes past the second level.
+// Output leaves as one u32 per 4 symbols straight to HBM (26 MB on 1 GiB C2: L2 request rate
+// is no concern here).
 __global__ __launch_bounds__(D8F_WAVES * 64) void k_huff_decode8_fix(const uint32_t *__restrict__ in, uint64_t n,
                                                                     uint64_t nwords, const dc_dtable *__restrict__ T,
                                                                     uint8_t *__restrict__ out, int *__restrict__ err,
-                                                                    const uint64_t *__restrict__ fix_mask,
+                                                                    const uint32_t *__restrict__ list,
                                                                     const uint64_t *__restrict__ fix_pos,
-                                                                    uint4 *__restrict__ trash)
+                                                                    uint32_t *__restrict__ queue)
 {
     constexpr uint32_t S = 64;
     __shared__ FixLds F;
     const int t = threadIdx.x, lane = t & 63, wv = __builtin_amdgcn_readfirstlane(t >> 6);
 #ifdef DC_DIAG
     D8_STAMP(f0);
-    unsigned long long f_dec = 0, f_rounds = 0;
+    unsigned long long f_dec = 0, f_rounds = 0, f_wait = 0, f_first = 0;
 #endif
-    for (int i = t; i < (1 << DC_LUT_BITS); i += D8F_WAVES * 64) F.lut[i] = T->dlut[i];
-    for (int i = t; i < DC_LUT2_CAP; i += D8F_WAVES * 64) F.lut2[i] = T->dlut2[i];
+    const uint32_t K2 = (uint32_t)T->dlut2_k, kmask = (1u << K2) - 1;
+    for (int i = t; i < (1 << D8_LUT_BITS) / 8; i += D8F_WAVES * 64)
+        reinterpret_cast<uint4 *>(F.lut)[i] = reinterpret_cast<const uint4 *>(T->dlut14)[i];
+    for (int i = t; i < DC_LUT2_CAP / 4; i += D8F_WAVES * 64)   // dlut2 is 8-B aligned
+        reinterpret_cast<uint2 *>(F.lut2)[i] = reinterpret_cast<const uint2 *>(T->dlut2)[i];
     for (int i = t; i < DC_MAX_SYMS; i += D8F_WAVES * 64) F.syms[i] = T->syms[i];
     for (int i = t; i <= DC_MAX_DIGITS; i += D8F_WAVES * 64) {
         F.first[i] = T->first[i];
@@ -1937,124 +1923,138 @@ __global__ __launch_bounds__(D8F_WAVES * 64) void k_huff_decode8_fix(const uint3
     __syncthreads();
     const int nary = T->n_ary, w = T->w;
     const bool pow2 = (nary & (nary - 1)) == 0;
-    const uint32_t K2 = (uint32_t)T->dlut2_k, kmask = (1u << K2) - 1;
-    const uint32_t nchunks = (uint32_t)((n + S - 1) / S);
-    const uint32_t ngroups = (nchunks + DC_SYNC_GROUP - 1) / DC_SYNC_GROUP;
-    const uint32_t nwin = (ngroups + 63) / 64;
+    // rounds of 64 list items: wave wid takes rounds wid, wid + P, ...
+    // written by k_huff_fix_list (an earlier launch): a plain scalar load
+    const uint32_t total = ((const __attribute__((address_space(4))) uint32_t *)queue)[D8_FIX_CNT];
+    const uint32_t nrounds = (total + 63) / 64;
     const uint32_t wstride = gridDim.x * D8F_WAVES;
     uint32_t *row = F.rows[wv] + lane * (D8F_ROW + 1);
-    uint32_t *orow = F.orow[wv] + lane * 17;
-    uint4 *const ftrash = reinterpret_cast<uint4 *>(trash) + (size_t)(blockIdx.x * D8F_WAVES + wv) * (D8_WSCR / 16);
     int bad = 0;
 
 #ifdef DC_DIAG
     D8_STAMP(f1);
 #endif
-#ifdef DC_DIAG_FIX_EMPTY
-    if (t < 100000) return;
-#endif
-    D8FCur qa, qb, qc;
-    qa.win = blockIdx.x * D8F_WAVES + wv;
-    d8f_window(qa, ngroups, nwin, wstride, fix_mask, F, wv, lane);
-    uint32_t cha = d8f_chunk(qa, nchunks, F, wv, lane);
-    uint64_t posa = fix_pos[cha != ~0u ? cha : 0u];
-    qb = qa;
-    d8f_next(qb, ngroups, nwin, wstride, fix_mask, F, wv, lane);
-    uint32_t chb = d8f_chunk(qb, nchunks, F, wv, lane);
-    uint64_t posb = fix_pos[chb != ~0u ? chb : 0u];
-    // spans of round A into registers: 4 uint4 from the 16-B aligned word below its start
-    uint4 sv[D8F_ROW / 4];
-    {
-        const uint64_t a0 = min((posa >> 5) & ~3ull, (nwords & ~3ull) - 4);
+    uint32_t ra = blockIdx.x * D8F_WAVES + wv;   // round of A; B and C follow by the stride
+    auto chunk_of = [&](uint32_t r) -> uint32_t {
+        const uint32_t item = r * 64 + (uint32_t)lane;
+        return (r < nrounds && item < total) ? list[item] : ~0u;
+    };
+    // a span's 16-B aligned first word (clamped so that a whole row can be read)
+    auto row_base = [&](uint64_t pos) -> uint64_t {
+        const uint64_t lim = nwords > D8F_ROW ? (nwords - D8F_ROW) & ~3ull : 0ull;
+        return min((pos >> 5) & ~3ull, lim);
+    };
+    auto load_row = [&](uint4 (&v)[D8F_ROW / 4], uint64_t a0) {
+        const uint64_t nq = (nwords - a0) / 4;
 #pragma unroll
         for (int k = 0; k < D8F_ROW / 4; ++k)
-            sv[k] = reinterpret_cast<const uint4 *>(in + a0)[min((uint64_t)k, (nwords - a0) / 4 - 1)];
-    }
-    while (qa.live) {
-        // stage round A's spans, then start round B's spans and round C's positions
-        const uint64_t a0 = min((posa >> 5) & ~3ull, (nwords & ~3ull) - 4);
+            v[k] = (uint64_t)k < nq ? reinterpret_cast<const uint4 *>(in + a0)[k] : make_uint4(0u, 0u, 0u, 0u);
+    };
+    auto put_row = [&](const uint4 (&v)[D8F_ROW / 4]) {
 #pragma unroll
         for (int k = 0; k < D8F_ROW / 4; ++k) {
-            row[4 * k] = brev8(sv[k].x);
-            row[4 * k + 1] = brev8(sv[k].y);
-            row[4 * k + 2] = brev8(sv[k].z);
-            row[4 * k + 3] = brev8(sv[k].w);
+            row[4 * k] = brev8(v[k].x);
+            row[4 * k + 1] = brev8(v[k].y);
+            row[4 * k + 2] = brev8(v[k].z);
+            row[4 * k + 3] = brev8(v[k].w);
         }
-        {
-            const uint64_t b0 = min((posb >> 5) & ~3ull, (nwords & ~3ull) - 4);
-#pragma unroll
-            for (int k = 0; k < D8F_ROW / 4; ++k)
-                sv[k] = reinterpret_cast<const uint4 *>(in + b0)[min((uint64_t)k, (nwords - b0) / 4 - 1)];
-        }
-        qc = qb;
-        d8f_next(qc, ngroups, nwin, wstride, fix_mask, F, wv, lane);
-        const uint32_t chc = d8f_chunk(qc, nchunks, F, wv, lane);
+    };
+    uint32_t cha = chunk_of(ra);
+    uint64_t posa = fix_pos[cha != ~0u ? cha : 0u];
+    uint32_t chb = chunk_of(ra + wstride);
+    uint64_t posb = fix_pos[chb != ~0u ? chb : 0u];
+    uint4 sv[D8F_ROW / 4];
+#ifdef DC_DIAG
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    D8_STAMP(fp0);
+    const unsigned long long f_pos = fp0 - f1;
+#endif
+    if (ra < nrounds) load_row(sv, row_base(posa));
+    while (ra < nrounds) {
+        // stage round A's spans, then start round B's spans and round C's positions
+        const uint64_t a0 = row_base(posa);
+#ifdef DC_DIAG
+        D8_STAMP(fw0);
+#endif
+        put_row(sv);
+#ifdef DC_DIAG
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        D8_STAMP(fw1);
+        f_wait += fw1 - fw0;
+        if (f_rounds == 0) f_first = fw1 - f1;
+#endif
+        load_row(sv, row_base(posb));
+        const uint32_t chc = chunk_of(ra + 2 * wstride);
         const uint64_t posc = fix_pos[chc != ~0u ? chc : 0u];
         // decode round A
         const bool valid = cha != ~0u;
         const uint64_t s0 = (uint64_t)(valid ? cha : 0u) * S;
         const uint32_t cntc = valid ? (uint32_t)((n - s0 < S) ? n - s0 : S) : 0u;
         uint32_t c = (uint32_t)(posa - (a0 << 5));
+        uint64_t rb = a0;   // word of `in` at row word 0
 #ifdef DC_DIAG
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         D8_STAMP(f2);
 #endif
-        uint64_t rb = a0;   // word of `in` at row word 0
-        uint32_t off = 0, ob = 0;
-        uint64_t W = 0;
-        bool over = false;
-        // one code per iteration, rolled (one copy of the code path: few registers, no spills,
-        // so no scratch reload makes the wave wait for its outstanding stores); a 64-bit
-        // window per 4 codes, re-read after 32 consumed bits; a span longer than the row
-        // re-stages the row from the current word on (rare: long chunks)
-#ifdef DC_DIAG_FIX_NODEC
-        for (uint32_t i = 0; i < 0; ++i) {
-#else
-        for (uint32_t i = 0; i < cntc && !over; ++i) {
-#endif
-            if ((i & 3) == 0 || off > 32) {
-                c += off;
-                off = 0;
-                if (c >= 32 * (D8F_ROW - 2)) {
-                    const uint32_t adv = (c >> 5) & ~3u;
-                    rb += adv;
-                    c -= adv * 32;
-                    if (rb + 4 > nwords) { bad = 1; break; }
-                    const uint64_t nq = (nwords - rb) / 4;
-                    for (int m = 0; m < D8F_ROW / 4; ++m) {
-                        const uint4 v = (uint64_t)m < nq ? reinterpret_cast<const uint4 *>(in + rb)[m] : make_uint4(0u, 0u, 0u, 0u);
-                        row[4 * m] = brev8(v.x);
-                        row[4 * m + 1] = brev8(v.y);
-                        row[4 * m + 2] = brev8(v.z);
-                        row[4 * m + 3] = brev8(v.w);
-                    }
-                }
-                const uint32_t a = c >> 5;
-                W = ((uint64_t)__builtin_amdgcn_alignbit(row[a + 2], row[a + 1], c) << 32) |
-                    __builtin_amdgcn_alignbit(row[a + 1], row[a], c);
-            }
-            const uint32_t e = d8f_code((uint32_t)(W >> off), 0u, F, K2, kmask, nary, w, pow2, &bad);
-            if (e == 0) { bad = 1; over = true; }
-            ob |= (e >> 8 & 255u) << (8 * (i & 3));
-            off += e & 255u;
-            if ((i & 3) == 3) { orow[i >> 2] = ob; ob = 0; }
-        }
-        if (cntc & 3) orow[cntc >> 2] = ob;
-        // 64 bytes out: whole chunks as 4 uint4 (other lanes: to the trash row, so every path
-        // issues the same stores); the stream's partial last chunk afterwards, byte by byte
-        uint4 *dst = (valid && cntc == S && !over) ? reinterpret_cast<uint4 *>(out + s0) : ftrash + lane * 4;
+        uint4 *const o128 = reinterpret_cast<uint4 *>(out + s0);
+        for (uint32_t p = 0; p < (cntc + 15) / 16; ++p) {
+          uint32_t ov[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) dst[k] = make_uint4(orow[4 * k], orow[4 * k + 1], orow[4 * k + 2], orow[4 * k + 3]);
-        if (valid && !over && cntc < S)
-            for (uint32_t i = 0; i < cntc; ++i) out[s0 + i] = (uint8_t)(orow[i >> 2] >> (8 * (i & 3)));
-        qa = qb; cha = chb; posa = posb;
-        qb = qc; chb = chc; posb = posc;
+          for (int q4 = 0; q4 < 4; ++q4) {
+            const uint32_t q = 4 * p + q4;
+            // 4 codes take <= 128 bits (+ 64 of window): re-stage a row that runs short
+            if (c >= 32 * (D8F_ROW - 6)) {
+                const uint32_t adv = (c >> 5) & ~3u;
+                rb += adv;
+                c -= adv * 32;
+                const uint64_t nq = rb < nwords ? (nwords - rb) / 4 : 0ull;
+#pragma unroll 1
+                for (int k = 0; k < D8F_ROW / 4; ++k) {   // rolled: no second set of row registers
+                    const uint4 v = (uint64_t)k < nq ? reinterpret_cast<const uint4 *>(in + rb)[k] : make_uint4(0u, 0u, 0u, 0u);
+                    row[4 * k] = brev8(v.x);
+                    row[4 * k + 1] = brev8(v.y);
+                    row[4 * k + 2] = brev8(v.z);
+                    row[4 * k + 3] = brev8(v.w);
+                }
+            }
+            uint32_t ob = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t a = c >> 5;
+                const uint32_t lo = __builtin_amdgcn_alignbit(row[a + 1], row[a], c);
+                uint32_t e = F.lut[lo & ((1u << D8_LUT_BITS) - 1)];
+                const uint32_t i2 = min(((e >> 8) << K2) | ((lo >> DC_LUT_BITS) & kmask), (uint32_t)DC_LUT2_CAP - 1);
+                const uint32_t e2 = F.lut2[i2];
+                e = (e & 255u) ? e : e2;
+                if (e == 0) {   // past the second level (rare): canonical search
+                    const uint32_t hi = __builtin_amdgcn_alignbit(row[a + 2], row[a + 1], c);
+                    e = d8_long_lds(lo, hi, F, nary, w, pow2);
+                    // the stream's partial last chunk decodes past its end: no error there
+                    bad |= (e == 0 && 4 * q + k < cntc);
+                }
+                ob |= ((e >> 8) & 255u) << (8 * k);
+                c += e & 255u;
+            }
+            ov[q4] = ob;
+          }
+          if (16 * p + 16 <= cntc) o128[p] = make_uint4(ov[0], ov[1], ov[2], ov[3]);
+          else   // the stream's partial last chunk
+            for (uint32_t k = 0; 16 * p + k < cntc; ++k) out[s0 + 16 * p + k] = (uint8_t)(ov[k >> 2] >> (8 * (k & 3)));
+        }
+#ifdef DC_DIAG
+        D8_STAMP(f3);
+        f_dec += f3 - f2;
+        ++f_rounds;
+#endif
+        ra += wstride;
+        cha = chb; posa = posb;
+        chb = chc; posb = posc;
     }
 #ifdef DC_DIAG
     D8_STAMP(f4);
     if (lane == 0) {
         unsigned long long *gg = g_d8diag + (blockIdx.x * D8F_WAVES + wv) * 4;
-        gg[0] = f4 - f0; gg[1] = f1 - f0; gg[2] = f_dec; gg[3] = f_rounds;
+        gg[0] = f4 - f0; gg[1] = (f1 - f0) | (f_pos << 32); gg[2] = f_dec; gg[3] = f_rounds | (f_wait << 8) | (f_first << 36);
     }
 #endif
     if (bad) atomicOr(err, 1);
@@ -2433,6 +2433,7 @@ struct dc_ctx {
     int *d_err;                                   // [0] plan, [1] decode
     uint32_t *d_queue;                            // decode tuple scheduler heads (D8Sched)
     uint32_t *d_fix;        size_t fix_cap;       // decode redo: a u64 chunk mask per group
+    uint32_t *d_fixlist;    size_t fixlist_cap;   // decode redo: flagged chunk indices, compacted
     uint32_t *d_fixpos;     size_t fixpos_cap;    // decode redo: bit offset of a flagged chunk
     uint64_t last_groups;                         // groups of the last S = 64 decode (redo mask length)
     void *d_scr;            size_t scr_cap;       // per-wave garbage sinks of the decoders
@@ -2547,6 +2548,7 @@ void dc_ctx_destroy(dc_ctx *c)
     if (c->d_err) (void)hipFree(c->d_err);
     if (c->d_queue) (void)hipFree(c->d_queue);
     if (c->d_fix) (void)hipFree(c->d_fix);
+    if (c->d_fixlist) (void)hipFree(c->d_fixlist);
     if (c->d_fixpos) (void)hipFree(c->d_fixpos);
     if (c->d_scr) (void)hipFree(c->d_scr);
     if (c->d_meta) (void)hipFree(c->d_meta);
@@ -2834,9 +2836,12 @@ int dc_huff_decode(dc_ctx *c, const uint32_t *d_words, uint64_t bit_base, uint64
                n, words, d_table, d_out, c->d_err + 1, c->d_queue, spct, (uint64_t *)c->d_fix,
                (uint64_t *)c->d_fixpos, (uint8_t *)c->d_scr);
         c->last_groups = groups;
+        if (ensure((void **)&c->d_fixlist, &c->fixlist_cap, (groups * 64 + 64) * sizeof(uint32_t))) return DC_E_HIP;
+        const uint64_t nchunks = (n + 63) / 64;
+        LAUNCH(c, "huff_fix_list", k_huff_fix_list, (groups + 1023) / 1024, 1024, (const uint64_t *)c->d_fix,
+               (uint32_t)groups, (uint32_t)nchunks, c->d_fixlist, c->d_queue + D8_FIX_CNT);
         LAUNCH(c, "huff_decode_fix", k_huff_decode8_fix, 256, D8F_WAVES * 64, d_words, n, words, d_table, d_out,
-               c->d_err + 1, (const uint64_t *)c->d_fix, (const uint64_t *)c->d_fixpos,
-               reinterpret_cast<uint4 *>(c->d_scr));
+               c->d_err + 1, (const uint32_t *)c->d_fixlist, (const uint64_t *)c->d_fixpos, c->d_queue);
         return DC_OK;
     }
     const uint64_t wgs = (groups + DEC_WAVES - 1) / DEC_WAVES;

@@ -22,7 +22,14 @@ torch.cuda.synchronize()
 L = _lib.load("libdc_core.so")
 buf = np.zeros(256 * 16 * 4, np.uint64)
 assert L.dc_diag_read(buf.ctypes.data_as(C.c_void_p), C.c_size_t(buf.nbytes)) == 0
-d = buf.reshape(-1, 4)[: 256 * 16].astype(np.float64)
-tot, tab, dec, rounds = d.T
+raw = buf.reshape(-1, 4)[: 256 * 12]
+d = raw.astype(np.float64)
+tot, _, dec, _ = d.T
+tab = (raw[:, 1] & 0xffffffff).astype(np.float64)
+pos = (raw[:, 1] >> 32).astype(np.float64)
+rounds = (raw[:, 3] & 255).astype(np.float64)
+wait = ((raw[:, 3] >> 8) & ((1 << 28) - 1)).astype(np.float64)
+first = (raw[:, 3] >> 36).astype(np.float64)
 print(f"fix waves {len(tot)}: total {tot.mean():.0f} cyc (max {tot.max():.0f})  tables {tab.mean():.0f}  "
-      f"decode {dec.mean():.0f} ({dec.sum()/tot.sum():.1%})  rounds {rounds.mean():.2f} (max {rounds.max():.0f})")
+      f"decode {dec.mean():.0f} ({dec.sum()/tot.sum():.1%})  rounds {rounds.mean():.2f} (max {rounds.max():.0f})  "
+      f"stage waits {wait.mean():.0f}  first positions at {pos.mean():.0f} (max {pos.max():.0f})  first stage at {first.mean():.0f} (max {first.max():.0f})")
