@@ -6,13 +6,16 @@ import sys
 from collections import defaultdict
 
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
-want = ("k_hist_blocks", "k_huff_pack", "k_huff_decode", "k_huff_table", "k_hist_reduce", "k_block_scan")
+want = ("k_hist_blocks", "k_huff_pack", "k_huff_decode", "k_huff_decode_fix", "k_huff_table", "k_hist_reduce",
+        "k_block_local", "k_block_final", "k_huff_fix_list", "k_zero_bounds")
 vals = defaultdict(lambda: defaultdict(list))
 for f in sorted(glob.glob(os.path.join(root, "p*", "run_counter_collection.csv"))):
     per = defaultdict(float)
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"].split("(")[0].replace("void ", "").split("<")[0].strip()
-        if k.startswith("k_huff_decode"):   # k_huff_decode8<NW, NC> is the decode launch
+        if k == "k_huff_decode8_fix":       # the exact redo of flagged chunks
+            k = "k_huff_decode_fix"
+        elif k.startswith("k_huff_decode"):   # k_huff_decode8<NW, NC> is the decode launch
             k = "k_huff_decode"
         if k not in want:
             continue
