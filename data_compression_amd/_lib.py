@@ -101,6 +101,10 @@ def _declare_core(L):
         "dc_huff_decode_status": ([vp], i32),
         "dc_huff_decode_redo_count": ([vp, C.POINTER(u64)], i32),
         "dc_huff_base64url": ([vp, P, u64, u64, P], i32),
+        "dc_huff_text_bits": ([i32, i32], i32),
+        "dc_huff_text": ([vp, P, u64, u64, i32, i32, P, C.POINTER(u64)], i32),
+        "dc_huff_text_parse": ([vp, P, u64, i32, i32, u64, P], i32),
+        "dc_huff_text_parse_status": ([vp], i32),
         "dc_huff_default_sync": ([u64], u32),
         "dc_huff_choose_sync": ([u64, u64], u32),
         "dc_nyb_compress": ([vp, P, u64, i32, P, C.POINTER(u64)], i32),

@@ -2079,6 +2079,144 @@ __global__ void k_base64url(const uint32_t *__restrict__ words, uint64_t bit_bas
 }
 
 // ------------------------------------------------------------------------------------
+// Digit text of a bit range, and its inverse (the reference's intent:
+// n_ary_huffman.c:46-78 "base64url / base16 / base3 / base9 ... digits", int2digit /
+// digit2int :371-455, the Z85 table :389-407 for 2 base-9 or 4 base-3 digits per char, and
+// "5 trits per octet, 1..243" :745-748). One character per b-bit field, MSB-first:
+//   DC_TEXT_BASE64URL b=6 | DC_TEXT_BASE16 b=4 | DC_TEXT_DIGITS b=w (one base-n digit) |
+//   DC_TEXT_Z85 b=8 (n=3: 4 trits, n=9: 2 digits) | DC_TEXT_TRITS5 b=10 (n=3, byte 1..243)
+// A field holding a digit >= n (never written by the encoder) renders as '~' (byte 0 in
+// TRITS5), which the parser rejects. Restated on the CPU by orc_text / orc_text_parse.
+// ------------------------------------------------------------------------------------
+__constant__ char c_b64[65] = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789-_";
+__constant__ char c_hex[17] = "0123456789ABCDEF";
+__constant__ char c_dig[17] = "0123456789abcdef";
+__constant__ char c_z85[86] = "0123456789abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ.-:+=^!/*?&<>()[]{}@%$#";
+
+static __host__ __device__ int text_bits(int format, int n)
+{
+    int w = 0;
+    while ((1 << w) < n) ++w;
+    switch (format) {
+    case DC_TEXT_BASE64URL: return 6;
+    case DC_TEXT_BASE16: return 4;
+    case DC_TEXT_DIGITS: return (n >= 2 && n <= 16) ? w : 0;
+    case DC_TEXT_Z85: return (n == 3 || n == 9) ? 8 : 0;
+    case DC_TEXT_TRITS5: return n == 3 ? 10 : 0;
+    default: return 0;
+    }
+}
+
+// the digits of a field (dw bits each, MSB-first) as one base-n number; -1 if one is >= n
+static __device__ __forceinline__ int text_digits_value(uint32_t f, int nd, int dw, int n)
+{
+    int v = 0;
+    for (int k = nd - 1; k >= 0; --k) {
+        const int d = (int)((f >> (k * dw)) & ((1u << dw) - 1));
+        if (d >= n) return -1;
+        v = v * n + d;
+    }
+    return v;
+}
+
+__global__ void k_text(const uint32_t *__restrict__ words, uint64_t bit_base, uint64_t bits, int format, int n,
+                       int b, char *__restrict__ text)
+{
+    const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t nchar = (bits + b - 1) / b;
+    if (c >= nchar) return;
+    const uint64_t rel0 = (bit_base & 31) + c * b;
+    const uint64_t wi = rel0 >> 5;   // d_words holds the word of bit_base first (as pack writes it)
+    const uint32_t sh = (uint32_t)(rel0 & 31);
+    const uint64_t valid = bits - c * b;   // >= 1
+    const uint32_t need = valid < (uint64_t)b ? (uint32_t)valid : (uint32_t)b;   // never read past the range
+    const uint64_t pair = ((uint64_t)bswap32(words[wi]) << 32) | ((sh + need > 32) ? bswap32(words[wi + 1]) : 0u);
+    uint32_t f = (uint32_t)((pair << sh) >> (64 - b));
+    if (valid < (uint64_t)b) f &= ~((1u << (b - valid)) - 1);
+    int ch;
+    switch (format) {
+    case DC_TEXT_BASE64URL: ch = c_b64[f]; break;
+    case DC_TEXT_BASE16: ch = c_hex[f]; break;
+    case DC_TEXT_DIGITS: ch = (int)f < n ? c_dig[f] : '~'; break;
+    case DC_TEXT_Z85: {
+        const int v = n == 3 ? text_digits_value(f, 4, 2, 3) : text_digits_value(f, 2, 4, 9);
+        ch = v < 0 ? '~' : c_z85[v];
+        break;
+    }
+    default: {   // DC_TEXT_TRITS5
+        const int v = text_digits_value(f, 5, 2, 3);
+        ch = v < 0 ? 0 : 1 + v;
+    }
+    }
+    text[c] = (char)ch;
+}
+
+// character -> field (or -1), per workgroup in LDS
+static __device__ int text_field(int ch, int format, int n)
+{
+    switch (format) {
+    case DC_TEXT_BASE64URL:
+        if (ch >= 'A' && ch <= 'Z') return ch - 'A';
+        if (ch >= 'a' && ch <= 'z') return ch - 'a' + 26;
+        if (ch >= '0' && ch <= '9') return ch - '0' + 52;
+        if (ch == '-' || ch == '+') return 62;   // digit2int takes both sets, n_ary_huffman.c:443-446
+        if (ch == '_' || ch == '/') return 63;
+        return -1;
+    case DC_TEXT_BASE16:
+    case DC_TEXT_DIGITS: {
+        int d = -1;
+        if (ch >= '0' && ch <= '9') d = ch - '0';
+        else if (ch >= 'a' && ch <= 'f') d = ch - 'a' + 10;
+        else if (format == DC_TEXT_BASE16 && ch >= 'A' && ch <= 'F') d = ch - 'A' + 10;
+        return (format == DC_TEXT_DIGITS && d >= n) ? -1 : d;
+    }
+    case DC_TEXT_Z85: {
+        int v = -1;
+        for (int i = 0; i < 81; ++i)
+            if (c_z85[i] == ch) v = i;
+        if (v < 0) return -1;
+        return n == 3 ? ((v / 27) << 6) | ((v / 9 % 3) << 4) | ((v / 3 % 3) << 2) | (v % 3) : ((v / 9) << 4) | (v % 9);
+    }
+    default: {   // DC_TEXT_TRITS5
+        if (ch < 1 || ch > 243) return -1;
+        int v = ch - 1, f = 0;
+        for (int k = 0; k < 5; ++k) {
+            f |= (v % 3) << (2 * k);
+            v /= 3;
+        }
+        return f;
+    }
+    }
+}
+
+// one output word per thread from the <= 33 characters that cover it; bits past `bits` 0
+__global__ __launch_bounds__(256) void k_text_parse(const uint8_t *__restrict__ text, uint64_t nchar, int format, int n,
+                                                    int b, uint64_t bits, uint32_t *__restrict__ words,
+                                                    int *__restrict__ err)
+{
+    __shared__ int16_t s_inv[256];
+    s_inv[threadIdx.x] = (int16_t)text_field((int)threadIdx.x, format, n);
+    __syncthreads();
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t nwords = (bits + 31) / 32;
+    if (j >= nwords) return;
+    const uint64_t lo = 32 * j, c0 = lo / b, c1 = min((lo + 31) / b, nchar - 1);
+    uint32_t acc = 0;
+    int bad = 0;
+    for (uint64_t c = c0; c <= c1; ++c) {
+        const int f = s_inv[text[c]];
+        bad |= f < 0;
+        const int sh = 32 - (int)((int64_t)(c * b) - (int64_t)lo) - b;   // left shift of the field
+        const uint32_t fu = (uint32_t)(f & 1023);
+        acc |= sh >= 0 ? (uint32_t)((uint64_t)fu << sh) : fu >> (-sh);
+    }
+    const uint64_t valid = bits - lo;   // >= 1
+    if (valid < 32) acc &= ~(0xFFFFFFFFu >> valid);
+    words[j] = bswap32(acc);
+    if (bad) atomicOr(err, 1);
+}
+
+// ------------------------------------------------------------------------------------
 // Byte-stream codecs with a 2-state transducer: nybble static encode/decode
 // (nybble_compression.c:734-1038 with modify=false) and the small front-end
 // (small_compression.c:582-665) plus its inverse. Each element (input byte) maps the
@@ -2871,6 +3009,42 @@ int dc_huff_decode_status(dc_ctx *c)
 {
     int v = 0;
     HIPCHK(hipMemcpyAsync(&v, c->d_err + 1, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return v ? DC_E_STREAM : DC_OK;
+}
+
+int dc_huff_text_bits(int format, int n_ary) { return text_bits(format, n_ary); }
+
+int dc_huff_text(dc_ctx *c, const uint32_t *d_words, uint64_t bit_base, uint64_t bits, int format, int n_ary,
+                 char *d_text, uint64_t *nchar)
+{
+    const int b = text_bits(format, n_ary);
+    if (!c || b == 0 || (bits && (!d_words || !d_text))) return DC_E_ARG;
+    const uint64_t nc = (bits + b - 1) / b;
+    if (nchar) *nchar = nc;
+    if (nc == 0) return DC_OK;
+    LAUNCH(c, "text", k_text, (nc + 255) / 256, 256, d_words, bit_base, bits, format, n_ary, b, d_text);
+    return DC_OK;
+}
+
+int dc_huff_text_parse(dc_ctx *c, const char *d_text, uint64_t nchar, int format, int n_ary, uint64_t bits,
+                       uint32_t *d_words)
+{
+    const int b = text_bits(format, n_ary);
+    if (!c || b == 0 || nchar * (uint64_t)b < bits || (bits && (!d_text || !d_words))) return DC_E_ARG;
+    HIPCHK(hipMemsetAsync(c->d_err + 8, 0, sizeof(int), c->stream));
+    const uint64_t nw = (bits + 31) / 32;
+    if (nw == 0) return DC_OK;
+    LAUNCH(c, "text_parse", k_text_parse, (nw + 255) / 256, 256, (const uint8_t *)d_text, nchar, format, n_ary, b,
+           bits, d_words, c->d_err + 8);
+    return DC_OK;
+}
+
+int dc_huff_text_parse_status(dc_ctx *c)
+{
+    if (!c) return DC_E_ARG;
+    int v = 0;
+    HIPCHK(hipMemcpyAsync(&v, c->d_err + 8, sizeof(int), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return v ? DC_E_STREAM : DC_OK;
 }

@@ -164,6 +164,35 @@ class Codec:
         check("dc_huff_decode_redo_count", self.L.dc_huff_decode_redo_count(self.ctx, C.byref(v)))
         return int(v.value)
 
+    # ---- digit text: formats as dc_gpu.h DC_TEXT_* ------------------------
+    TEXT_FORMATS = {"base64url": 0, "base16": 1, "digits": 2, "z85": 3, "trits5": 4}
+
+    def text_bits(self, fmt, n_ary: int) -> int:
+        """Bits per character of a text format (0: unsupported for this n)."""
+        return int(self.L.dc_huff_text_bits(self.TEXT_FORMATS.get(fmt, fmt), n_ary))
+
+    def text(self, words, bit_base: int, bits: int, fmt, n_ary: int):
+        """Digit text of bits [bit_base, bit_base+bits) of `words` -> uint8 device tensor."""
+        f = self.TEXT_FORMATS.get(fmt, fmt)
+        b = self.text_bits(f, n_ary)
+        if b == 0:
+            raise ValueError(f"text format {fmt} does not support n={n_ary}")
+        out = self._t(max((bits + b - 1) // b, 1))
+        nc = C.c_uint64(0)
+        check("dc_huff_text", self.L.dc_huff_text(self.ctx, _ptr(words), bit_base, bits, f, n_ary, _ptr(out),
+                                                  C.byref(nc)))
+        return out[: nc.value]
+
+    def text_parse(self, text, fmt, n_ary: int, bits: int):
+        """Inverse of text(): uint8 device tensor of characters -> int32 words holding the
+        first `bits` bits. Raises DcError on an invalid character."""
+        f = self.TEXT_FORMATS.get(fmt, fmt)
+        words = self._t(max((bits + 31) // 32, 1), torch.int32)
+        check("dc_huff_text_parse", self.L.dc_huff_text_parse(self.ctx, _ptr(text), text.numel(), f, n_ary, bits,
+                                                              _ptr(words)))
+        check("dc_huff_text_parse_status", self.L.dc_huff_text_parse_status(self.ctx))
+        return words
+
     def default_sync(self, n: int) -> int:
         return int(self.L.dc_huff_default_sync(n))
 

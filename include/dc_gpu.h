@@ -150,6 +150,29 @@ int dc_huff_decode_redo_count(dc_ctx *ctx, uint64_t *count);
 /* base64url text (6 bits per char, MSB-first) of bits [bit_base, bit_base+bits) */
 int dc_huff_base64url(dc_ctx *ctx, const uint32_t *d_words, uint64_t bit_base, uint64_t bits,
                       char *d_text);
+/* Digit text of bits [bit_base, bit_base+bits) (n_ary_huffman.c:46-78,
+ * :371-455, :745-748): one character per b-bit field, MSB-first, the last zero-padded.
+ *   DC_TEXT_BASE64URL  b = 6, the int2digit alphabet (:371-378)
+ *   DC_TEXT_BASE16     b = 4, "0123456789ABCDEF" (RFC 4648)
+ *   DC_TEXT_DIGITS     b = w, one base-n digit per character, "0123456789abcdef" (n <= 16)
+ *   DC_TEXT_Z85        b = 8, 4 trits (n = 3) or 2 base-9 digits (n = 9) -> the first 81
+ *                      characters of Z85 (:379-407)
+ *   DC_TEXT_TRITS5     b = 10, 5 trits (n = 3) -> one byte 1..243 (:745-748)
+ * d_words[0] is the word holding bit bit_base (as dc_huff_pack writes a stream).
+ * A field with a digit >= n (never produced by the encoder) renders as '~' (byte 0 in
+ * TRITS5). dc_huff_text_bits returns b, 0 for an unsupported (format, n). *nchar (host,
+ * may be NULL) receives ceil(bits / b). */
+enum { DC_TEXT_BASE64URL = 0, DC_TEXT_BASE16 = 1, DC_TEXT_DIGITS = 2, DC_TEXT_Z85 = 3, DC_TEXT_TRITS5 = 4 };
+int dc_huff_text_bits(int format, int n_ary);
+int dc_huff_text(dc_ctx *ctx, const uint32_t *d_words, uint64_t bit_base, uint64_t bits, int format, int n_ary,
+                 char *d_text, uint64_t *nchar);
+/* inverse: nchar characters -> the first `bits` bits at bit 0 of d_words (ceil(bits/32)
+ * words; bits past `bits` zeroed). base64url also takes '+' '/' (digit2int :443-446),
+ * base16 lowercase. An invalid character: dc_huff_text_parse_status (synchronising)
+ * returns DC_E_STREAM. */
+int dc_huff_text_parse(dc_ctx *ctx, const char *d_text, uint64_t nchar, int format, int n_ary, uint64_t bits,
+                       uint32_t *d_words);
+int dc_huff_text_parse_status(dc_ctx *ctx);
 /* sync granularity (symbols per chunk): a fixed default, and the choice from the
  * planned payload (keeps a 64-chunk group within the decoder's LDS stage) */
 uint32_t dc_huff_default_sync(uint64_t n);

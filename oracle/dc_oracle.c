@@ -253,6 +253,109 @@ uint64_t orc_base64url(const uint8_t *in, uint64_t bits, char *out)
     return nchar;
 }
 
+/* ---- digit text -------------------------------------------------- */
+static const char orc_b64[] = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789-_";
+static const char orc_hex[] = "0123456789ABCDEF";
+static const char orc_dig[] = "0123456789abcdef";
+/* Z85 (rfc.zeromq.org/spec/32), the table n_ary_huffman.c:389-396 names; first 81 used */
+static const char orc_z85[] = "0123456789abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ.-:+=^!/*?&<>()[]{}@%$#";
+
+static int orc_text_w(int n)
+{
+    int w = 0;
+    while ((1 << w) < n) w++;
+    return w;
+}
+
+/* bits per character, 0 for an unsupported (format, n) */
+static int orc_text_bits(int format, int n)
+{
+    switch (format) {
+    case 0: return 6;
+    case 1: return 4;
+    case 2: return (n >= 2 && n <= 16) ? orc_text_w(n) : 0;
+    case 3: return (n == 3 || n == 9) ? 8 : 0;
+    case 4: return n == 3 ? 10 : 0;
+    default: return 0;
+    }
+}
+
+/* a field of b bits (MSB-first) -> its character; a field holding a digit >= n (never
+ * written by the encoder) renders as '~' (in none of the alphabets), as byte 0 in format 4 */
+static int orc_text_char(unsigned f, int format, int n)
+{
+    switch (format) {
+    case 0: return orc_b64[f];
+    case 1: return orc_hex[f];
+    case 2: return f < (unsigned)n ? orc_dig[f] : '~';
+    case 3: {
+        const int dw = n == 3 ? 2 : 4;
+        unsigned v = 0;
+        for (int k = 8 - dw; k >= 0; k -= dw) {
+            const unsigned d = (f >> k) & ((1u << dw) - 1);
+            if (d >= (unsigned)n) return '~';
+            v = v * (unsigned)n + d;
+        }
+        return orc_z85[v];
+    }
+    case 4: {
+        unsigned v = 0;
+        for (int k = 8; k >= 0; k -= 2) {
+            const unsigned d = (f >> k) & 3u;
+            if (d >= 3) return 0;
+            v = v * 3 + d;
+        }
+        return (int)(1 + v);
+    }
+    }
+    return '~';
+}
+
+uint64_t orc_text(const uint8_t *in, uint64_t bits, int format, int n_ary, char *out)
+{
+    const int b = orc_text_bits(format, n_ary);
+    if (b == 0) return 0;
+    const uint64_t nchar = (bits + (uint64_t)b - 1) / (uint64_t)b;
+    for (uint64_t c = 0; c < nchar; c++) {
+        unsigned f = 0;
+        for (int k = 0; k < b; k++) {
+            const uint64_t p = c * (uint64_t)b + (uint64_t)k;
+            f = (f << 1) | ((p < bits) ? ((in[p >> 3] >> (7 - (p & 7))) & 1u) : 0u);
+        }
+        out[c] = (char)orc_text_char(f, format, n_ary);
+    }
+    return nchar;
+}
+
+/* a character -> its field, or -1 (brute force over the fields: test infrastructure) */
+static int orc_text_field(unsigned char ch, int format, int n)
+{
+    const int b = orc_text_bits(format, n);
+    if (format == 4 ? ch == 0 : ch == '~') return -1;
+    for (unsigned f = 0; f < (1u << b); f++)
+        if ((unsigned char)orc_text_char(f, format, n) == ch) return (int)f;
+    if (format == 0 && ch == '+') return 62;   /* digit2int, n_ary_huffman.c:443-446 */
+    if (format == 0 && ch == '/') return 63;
+    if (format == 1 && ch >= 'a' && ch <= 'f') return ch - 'a' + 10;
+    return -1;
+}
+
+int orc_text_parse(const char *text, uint64_t nchar, int format, int n_ary, uint8_t *out, uint64_t bits)
+{
+    const int b = orc_text_bits(format, n_ary);
+    if (b == 0 || nchar * (uint64_t)b < bits) return -1;
+    memset(out, 0, (size_t)((bits + 7) / 8));
+    for (uint64_t c = 0; c < nchar; c++) {
+        const int f = orc_text_field((unsigned char)text[c], format, n_ary);
+        if (f < 0) return -1;
+        for (int k = 0; k < b; k++) {
+            const uint64_t p = c * (uint64_t)b + (uint64_t)k;
+            if (p < bits && ((f >> (b - 1 - k)) & 1)) out[p >> 3] |= (uint8_t)(0x80u >> (p & 7));
+        }
+    }
+    return 0;
+}
+
 /* ================================================================================== */
 /* nybble codec  (nybble_compression.c:517-1137)                                       */
 /* ================================================================================== */

@@ -60,6 +60,18 @@ int orc_huff_unpack(const uint8_t *in, uint64_t in_bits, uint64_t n_out,
 /* base64url text of the first `bits` bits (6 per char, MSB-first, last zero-padded). */
 uint64_t orc_base64url(const uint8_t *in, uint64_t bits, char *out);
 
+/* Digit text of a bit range (intent n_ary_huffman.c:46-78, :371-455,
+ * :745-753). format: 0 base64url (6 bits/char, int2digit :371-378), 1 base16 (4 bits,
+ * RFC 4648 "0-9A-F"), 2 one base-n digit per char (w bits, "0-9a-f", n <= 16), 3 Z85
+ * pairs (8 bits = 4 trits (n=3) or 2 base-9 digits (n=9) -> the first 81 Z85 characters,
+ * :389-407), 4 five trits per byte (n=3, 10 bits -> byte 1..243, :745-748). The last
+ * character's missing bits are zero. Returns the characters written, 0 on a bad format. */
+uint64_t orc_text(const uint8_t *in, uint64_t bits, int format, int n_ary, char *out);
+/* inverse: text -> the first `bits` bits (out zeroed by the callee, ceil(bits/8) bytes);
+ * base64url also takes '+' '/' (digit2int :443-446), base16 lowercase. 0, or -1 on an
+ * invalid character or a text shorter than `bits` needs. */
+int orc_text_parse(const char *text, uint64_t nchar, int format, int n_ary, uint8_t *out, uint64_t bits);
+
 /* ---- nybble codec: nybble_compression.c:517-1137 ----------------------------------- */
 /* Length-based restatement of compress_bytestring(:887-1038) / decompress_bytestring
  * (:734-817). Output excludes the trailing NUL. out capacity >= n+1. */

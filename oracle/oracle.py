@@ -44,6 +44,10 @@ def lib():
         L.orc_huff_unpack.restype = C.c_int
         L.orc_base64url.argtypes = [u8p, C.c_uint64, C.c_char_p]
         L.orc_base64url.restype = C.c_uint64
+        L.orc_text.argtypes = [u8p, C.c_uint64, C.c_int, C.c_int, C.c_char_p]
+        L.orc_text.restype = C.c_uint64
+        L.orc_text_parse.argtypes = [C.c_char_p, C.c_uint64, C.c_int, C.c_int, u8p, C.c_uint64]
+        L.orc_text_parse.restype = C.c_int
         for f in ("orc_nybble_compress", "orc_nybble_decompress"):
             getattr(L, f).argtypes = [u8p, C.c_uint64, u8p, C.c_int]
             getattr(L, f).restype = C.c_uint64
@@ -123,6 +127,31 @@ def base64url(payload, bits) -> bytes:
     out = C.create_string_buffer((bits + 5) // 6 + 1)
     n = lib().orc_base64url(_p(payload, u8p), bits, out)
     return out.raw[:n]
+
+
+TEXT_BITS = {0: 6, 1: 4, 3: 8, 4: 10}
+
+
+def text_bits_per_char(fmt: int, n_ary: int) -> int:
+    if fmt == 2:
+        return max(1, (n_ary - 1).bit_length())
+    return TEXT_BITS[fmt]
+
+
+def text(payload, bits, fmt: int, n_ary: int) -> bytes:
+    """Digit text of the first `bits` bits (orc_text: formats 0..4, see dc_oracle.h)."""
+    payload = np.ascontiguousarray(payload, dtype=np.uint8)
+    b = text_bits_per_char(fmt, n_ary)
+    out = C.create_string_buffer((bits + b - 1) // b + 1)
+    n = lib().orc_text(_p(payload, u8p), bits, fmt, n_ary, out)
+    return out.raw[:n]
+
+
+def text_parse(txt: bytes, fmt: int, n_ary: int, bits: int) -> np.ndarray:
+    out = np.zeros(max((bits + 7) // 8, 1), dtype=np.uint8)
+    if lib().orc_text_parse(txt, len(txt), fmt, n_ary, _p(out, u8p), bits) != 0:
+        raise ValueError("invalid text")
+    return out[: (bits + 7) // 8]
 
 
 def nybble_compress(x: bytes, modify: bool) -> bytes:

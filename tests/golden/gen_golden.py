@@ -15,6 +15,7 @@ Reference functions exercised (file:line in /root/reference):
   compress_bytestring/decompress_bytestring (modify false/true)
                                      nybble_compression.c:734-1038
   compress_bytestring (front-end)    small_compression.c:582-665
+  digit2int                          n_ary_huffman.c:430-455
 """
 from __future__ import annotations
 
@@ -224,11 +225,28 @@ def gen_small(rng):
     print("small inputs:", len(ins))
 
 
+def gen_digits():
+    """digit2int (n_ary_huffman.c:430-455) for every 7-bit character: it pins the int2digit
+    base64url alphabet (:371-378) and the RFC 4648 '+' '/' extras (:443-446); -1 = not a
+    digit (the NDEBUG build returns r[d] where the debug build asserts)."""
+    lib = load("libref_huffman.so")
+    lib.digit2int.argtypes = [C.c_char]
+    lib.digit2int.restype = C.c_int
+    chars = np.arange(1, 128, dtype=np.uint8)
+    vals = np.array([lib.digit2int(bytes([int(c)])) for c in chars], dtype=np.int32)
+    np.savez_compressed(os.path.join(HERE, "digits.npz"), chars=chars, digit2int=vals)
+    print("digit2int: %d digits" % int((vals >= 0).sum()))
+
+
 def main():
     rng = np.random.default_rng(20250808)
+    if sys.argv[1:] == ["digits"]:   # regenerate only this fixture
+        gen_digits()
+        return
     gen_huffman(rng)
     gen_nybble(rng)
     gen_small(rng)
+    gen_digits()
 
 
 if __name__ == "__main__":

@@ -414,3 +414,33 @@ def test_decode_corrupt_stream_reports(torch_cuda, codec):
     codec.decode_into(enc, out)
     codec.decode_status()   # 0 or DC_E_STREAM; it must return
     torch.cuda.synchronize()
+
+
+TEXT_CASES = [("base64url", 2), ("base16", 2), ("digits", 2), ("digits", 3), ("digits", 9), ("digits", 16),
+              ("z85", 3), ("z85", 9), ("trits5", 3)]
+
+
+@pytest.mark.parametrize("fmt,n_ary", TEXT_CASES)
+def test_text_vs_oracle_and_roundtrip(torch_cuda, codec, fmt, n_ary):
+    """Digit text of a real Huffman stream at bit offsets, byte-identical to
+    the oracle's orc_text; text -> bits round trip; an invalid character is reported."""
+    from data_compression_amd import synth
+    from data_compression_amd._lib import DcError
+    torch = torch_cuda
+    fnum = codec.TEXT_FORMATS[fmt]
+    x = synth.english_like(30011, seed=21)
+    L, el, ev, code, nb, mx = _oracle_encode(x, n_ary)
+    for bit_base in (0, 5, 32, 77):
+        payload, bits, _ = orc.huff_pack(x, code, nb)
+        enc = codec.encode(torch.from_numpy(x).cuda(), n_ary=n_ary, sync_syms=64, bit_base=bit_base)
+        assert enc["bits"] == bits
+        txt = codec.text(enc["words"], bit_base, bits, fmt, n_ary)
+        want = orc.text(payload, bits, fnum, n_ary)
+        assert txt.cpu().numpy().tobytes() == want, (fmt, n_ary, bit_base)
+        back = codec.text_parse(txt, fmt, n_ary, bits)
+        got = back.cpu().numpy().view(np.uint8)[: (bits + 7) // 8]
+        assert np.array_equal(got, payload), (fmt, n_ary, bit_base)
+    bad = txt.clone()
+    bad[len(bad) // 2] = 0 if fmt == "trits5" else ord("~")
+    with pytest.raises(DcError):
+        codec.text_parse(bad, fmt, n_ary, bits)

@@ -130,3 +130,59 @@ def test_bitstream_roundtrip_all_nary():
         back = orc.huff_unpack(payload, bits, x.size, el, ev, n)
         assert np.array_equal(back, x)
         assert idx[0] == 0 and len(idx) == (x.size + 1023) // 1024
+
+
+# ---- digit text -----------------------------------------------------
+TEXT_CASES = [(0, 2), (1, 2), (2, 2), (2, 3), (2, 4), (2, 9), (2, 10), (2, 16), (3, 3), (3, 9), (4, 3)]
+
+
+def _digit_stream(rng, n, bits):
+    """A packed MSB-first stream of random base-n digits (w bits each), cut at `bits`."""
+    w = max(1, (n - 1).bit_length())
+    d = rng.integers(0, n, size=(bits + w - 1) // w)
+    b = ((d[:, None] >> np.arange(w - 1, -1, -1)) & 1).astype(np.uint8).ravel()[:bits]
+    return np.packbits(b)
+
+
+def test_text_base64url_alphabet_matches_reference_digit2int():
+    """The parser's base64url map equals the reference's digit2int for every 7-bit character
+    (tests/golden/digits.npz, generated by running the reference)."""
+    g = _load("digits.npz")
+    for ch, want in zip(g["chars"], g["digit2int"]):
+        try:
+            got = int(orc.text_parse(bytes([int(ch)]), 0, 2, 6)[0]) >> 2
+        except ValueError:
+            got = -1
+        assert got == want, chr(ch)
+    # and rendering uses int2digit's order (the inverse of digit2int on 0..63)
+    inv = {int(v): chr(c) for c, v in zip(g["chars"], g["digit2int"]) if v >= 0 and chr(c) not in "+/"}
+    six = ((np.arange(64)[:, None] >> np.arange(5, -1, -1)) & 1).astype(np.uint8).ravel()
+    alphabet = orc.text(np.packbits(six), 64 * 6, 0, 2)
+    assert alphabet == "".join(inv[i] for i in range(64)).encode()
+
+
+@pytest.mark.parametrize("fmt,n", TEXT_CASES)
+def test_text_roundtrip(fmt, n):
+    rng = np.random.default_rng(100 + 10 * fmt + n)
+    for bits in (1, 5, 6, 7, 10, 31, 32, 33, 64, 999, 4096 + 3):
+        p = _digit_stream(rng, n, bits)
+        t = orc.text(p, bits, fmt, n)
+        b = orc.text_bits_per_char(fmt, n)
+        assert len(t) == (bits + b - 1) // b
+        assert np.array_equal(orc.text_parse(t, fmt, n, bits), p), (fmt, n, bits)
+
+
+def test_text_known_answers():
+    # 5 trits 0,1,2,0,1 -> 1 + 46 = '/', then trit 2 padded with zeros -> 1 + 162
+    p = np.array([0b00011000, 0b01100000], np.uint8)
+    assert orc.text(p, 16, 4, 3) == b"/\xa3"
+    # Z85 pairs: n=9 digits (8, 8) -> 80 = '}' ; n=3 trits (2,2,2,2) -> 80
+    assert orc.text(np.array([0x88], np.uint8), 8, 3, 9) == b"}"
+    assert orc.text(np.array([0xAA], np.uint8), 8, 3, 3) == b"}"
+    assert orc.text(np.array([0xAB], np.uint8), 8, 3, 3) == b"~"      # digit 3: not base 3
+    assert orc.text(np.array([0x1B, 0x8F], np.uint8), 16, 1, 2) == b"1B8F"
+    assert orc.text(np.array([0x1B], np.uint8), 8, 2, 16) == b"1b"
+    assert orc.text(np.array([0b01101100], np.uint8), 8, 2, 3) == b"12~0"
+    for bad, fmt, n in ((b"~", 2, 3), (b"@", 3, 9), (b"\x00", 4, 3), (b"\xf4", 4, 3), (b"G", 1, 2)):
+        with pytest.raises(ValueError):
+            orc.text_parse(bad, fmt, n, 1)
