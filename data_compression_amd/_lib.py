@@ -111,6 +111,8 @@ def _declare_core(L):
         "dc_nyb_decompress": ([vp, P, u64, i32, P, C.POINTER(u64)], i32),
         "dc_small_compress": ([vp, P, u64, P, C.POINTER(u64)], i32),
         "dc_small_decompress": ([vp, P, u64, P, C.POINTER(u64)], i32),
+        "dc_small_compress_body": ([vp, P, u64, i32, u64, P, C.POINTER(u64)], i32),
+        "dc_small_decompress_body": ([vp, P, u64, P, C.POINTER(u64)], i32),
         "dc_host_ctx": ([], vp),
         "dc_huff_compress_bound": ([u64, u32], u64),
         "dc_huff_compress_host": ([u8p, u64, i32, C.POINTER(C.c_int32), i32, u32, u8p, u64, C.POINTER(u64)], i32),

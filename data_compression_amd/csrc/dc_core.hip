@@ -2227,7 +2227,19 @@ __global__ __launch_bounds__(256) void k_text_parse(const uint8_t *__restrict__ 
 //   nybble decode, state = "start at the low nybble" (nybble_offset, :753-795)
 //   small encode / decode: stateless counts
 // ------------------------------------------------------------------------------------
-enum { M_NYB_ENC = 0, M_NYB_DEC = 1, M_SMALL_ENC = 2, M_SMALL_DEC = 3 };
+// Shard bodies of the small front-end (dist.ShardedSmall): no header, no
+// LITERAL fallback (decided over all ranks). BODY0: element j = byte j+1 of the stream
+// (rank 0; its byte 0 is the raw first byte); BODY1: element j = byte j+1 of a shard whose
+// byte 0 is the previous shard's last byte (the 1-byte left halo); both read one byte of
+// right halo for a pair that starts on the shard's last byte. DBODY: decode of a body,
+// element j = byte j.
+enum { M_NYB_ENC = 0, M_NYB_DEC = 1, M_SMALL_ENC = 2, M_SMALL_DEC = 3, M_SMALL_BODY0 = 4, M_SMALL_BODY1 = 5,
+       M_SMALL_DBODY = 6 };
+template <int M> struct FsmMode {
+    static constexpr bool small_enc = M == M_SMALL_ENC || M == M_SMALL_BODY0 || M == M_SMALL_BODY1;
+    static constexpr bool body = M >= M_SMALL_BODY0;
+    static constexpr bool enc = M == M_NYB_ENC || M == M_SMALL_ENC;   // header + LITERAL fallback
+};
 #define FSM_TILE 4096
 
 struct Fsm {
@@ -2265,14 +2277,14 @@ static __device__ __forceinline__ Fsm elem_fsm(const uint8_t *__restrict__ in, u
         else { f.c0 = 1; f.s0 = 0; }
         f.c1 = 1;
         f.s1 = (l & 8) ? 0 : 1;
-    } else if (M == M_SMALL_ENC) {       // byte i = j+1
+    } else if (FsmMode<M>::small_enc) {   // byte i = j+1
         const uint64_t i = j + 1;
         const uint32_t x = in[i];
-        const bool second = (i >= 2) && in[i - 1] == ' ' && is_lower(x);
+        const bool second = (M == M_SMALL_BODY1 || i >= 2) && in[i - 1] == ' ' && is_lower(x);
         f.c0 = f.c1 = second ? 0 : 1;
         f.s0 = f.s1 = 0;
-    } else {                             // small decode, byte k = j+2
-        const uint32_t b = in[j + 2];
+    } else {                             // small decode, byte k = j+2 (a body: byte j)
+        const uint32_t b = in[M == M_SMALL_DBODY ? j : j + 2];
         f.c0 = f.c1 = (b >= 0x80) ? 2 : 1;
         f.s0 = f.s1 = 0;
     }
@@ -2375,7 +2387,7 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
     __shared__ uint64_t s_base[256];
     __shared__ uint32_t s_st[256];
     const int t = threadIdx.x;
-    const bool enc = (M == M_NYB_ENC || M == M_SMALL_ENC);
+    const bool enc = FsmMode<M>::enc;
     const uint64_t body = (M == M_NYB_ENC) ? meta[0] + meta[1] : meta[0];
     const uint64_t total = enc ? 2 + body : 1 + body;
     const bool literal = enc && total >= len;
@@ -2386,7 +2398,7 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
         if (blockIdx.x == 0 && t == 0) out[0] = ' ';
         return;
     }
-    if (blockIdx.x == 0 && t == 0) {
+    if (blockIdx.x == 0 && t == 0 && !FsmMode<M>::body) {
         if (M == M_NYB_ENC) { out[0] = 0xAF; out[1] = in[0]; }
         else if (M == M_SMALL_ENC) { out[0] = 8; out[1] = in[0]; }
         else { out[0] = in[1]; }
@@ -2424,7 +2436,7 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
         s = s ? p.w : p.z;
     }
     (void)s_base; (void)s_st;
-    const uint64_t head = enc ? 2 : 1;
+    const uint64_t head = FsmMode<M>::body ? 0 : enc ? 2 : 1;
     o += head;
     for (int k = 0; k < 16; ++k) {
         const uint64_t j = j0 + k;
@@ -2466,16 +2478,16 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
                 if (l & 8) { out[o++] = tbl[l & 7]; s = 0; }
                 else { out[o++] = (uint8_t)(((l & 7) << 4) + nxt); s = 1; }
             }
-        } else if (M == M_SMALL_ENC) {
+        } else if (FsmMode<M>::small_enc) {
             const uint64_t i = j + 1;
             const uint32_t x = in[i];
-            const bool second = (i >= 2) && in[i - 1] == ' ' && is_lower(x);
+            const bool second = (M == M_SMALL_BODY1 || i >= 2) && in[i - 1] == ' ' && is_lower(x);
             if (!second) {
                 if (x == ' ' && i + 1 < len && is_lower(in[i + 1])) out[o++] = (uint8_t)(0x80 + in[i + 1]);
                 else out[o++] = (uint8_t)x;
             }
         } else {
-            const uint32_t b = in[j + 2];
+            const uint32_t b = in[M == M_SMALL_DBODY ? j : j + 2];
             if (b >= 0x80) { out[o++] = ' '; out[o++] = (uint8_t)(b - 0x80); }
             else out[o++] = (uint8_t)b;
         }
@@ -3081,9 +3093,9 @@ static int fsm_run(dc_ctx *c, const uint8_t *d_in, uint64_t len, uint64_t nelem,
            (const uint64_t *)c->d_meta, d_out);
     HIPCHK(hipMemcpyAsync(c->h_pinned, c->d_meta, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
-    const bool enc = (M == M_NYB_ENC || M == M_SMALL_ENC);
+    const bool enc = FsmMode<M>::enc;
     const uint64_t body = (M == M_NYB_ENC) ? c->h_pinned[0] + c->h_pinned[1] : c->h_pinned[0];
-    uint64_t total = enc ? 2 + body : 1 + body;
+    uint64_t total = FsmMode<M>::body ? body : enc ? 2 + body : 1 + body;
     if (enc && total >= len) total = len + 1;
     *h_len = total;
     return DC_OK;
@@ -3162,6 +3174,22 @@ int dc_small_compress(dc_ctx *c, const uint8_t *d_in, uint64_t n, uint8_t *d_out
     if (!c || !d_out || !h_len || (n && !d_in)) return DC_E_ARG;
     if (n == 0) { int r = write_byte(c, d_out, ' '); if (r) return r; HIPCHK(hipStreamSynchronize(c->stream)); *h_len = 1; return DC_OK; }
     return fsm_run<M_SMALL_ENC>(c, d_in, n, n - 1, d_out, h_len, "small_enc_tiles");
+}
+
+int dc_small_compress_body(dc_ctx *c, const uint8_t *d_in, uint64_t len, int left_halo, uint64_t nelem,
+                           uint8_t *d_out, uint64_t *h_len)
+{
+    if (!c || !d_out || !h_len || (len && !d_in) || (nelem && nelem + 1 > len)) return DC_E_ARG;
+    if (nelem == 0) { *h_len = 0; return DC_OK; }
+    return left_halo ? fsm_run<M_SMALL_BODY1>(c, d_in, len, nelem, d_out, h_len, "small_body_tiles")
+                     : fsm_run<M_SMALL_BODY0>(c, d_in, len, nelem, d_out, h_len, "small_body_tiles");
+}
+
+int dc_small_decompress_body(dc_ctx *c, const uint8_t *d_in, uint64_t m, uint8_t *d_out, uint64_t *h_len)
+{
+    if (!c || !d_out || !h_len || (m && !d_in)) return DC_E_ARG;
+    if (m == 0) { *h_len = 0; return DC_OK; }
+    return fsm_run<M_SMALL_DBODY>(c, d_in, m, m, d_out, h_len, "small_dbody_tiles");
 }
 
 int dc_small_decompress(dc_ctx *c, const uint8_t *d_in, uint64_t m, uint8_t *d_out, uint64_t *h_len)

@@ -164,6 +164,31 @@ class Codec:
         check("dc_huff_decode_redo_count", self.L.dc_huff_decode_redo_count(self.ctx, C.byref(v)))
         return int(v.value)
 
+    # ---- small front-end shard bodies (dist.ShardedSmall) --------------------
+    def small_body(self, y, left_halo: bool, nelem: int):
+        """Front-end body of stream bytes y[1..nelem] (y[0]: left context; y[nelem+1], when
+        present, the right halo) -> uint8 device tensor."""
+        out = self._t(max(nelem, 1))
+        n = C.c_uint64(0)
+        check("dc_small_compress_body", self.L.dc_small_compress_body(self.ctx, _ptr(y), y.numel(), int(left_halo),
+                                                                      nelem, _ptr(out), C.byref(n)))
+        return out[: n.value]
+
+    def small_decompress(self, seg):
+        """A front-end stream that starts with its type byte (rank 0's segment)."""
+        out = self._t(max(2 * seg.numel(), 1))
+        n = C.c_uint64(0)
+        check("dc_small_decompress", self.L.dc_small_decompress(self.ctx, _ptr(seg), seg.numel(), _ptr(out),
+                                                                C.byref(n)))
+        return out[: n.value]
+
+    def small_decompress_body(self, seg):
+        out = self._t(max(2 * seg.numel(), 1))
+        n = C.c_uint64(0)
+        check("dc_small_decompress_body", self.L.dc_small_decompress_body(self.ctx, _ptr(seg), seg.numel(),
+                                                                          _ptr(out), C.byref(n)))
+        return out[: n.value]
+
     # ---- digit text (SURVEY §8(f)3): formats as dc_gpu.h DC_TEXT_* ------------------------
     TEXT_FORMATS = {"base64url": 0, "base16": 1, "digits": 2, "z85": 3, "trits5": 4}
 

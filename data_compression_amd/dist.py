@@ -141,3 +141,101 @@ class ShardedHuffman:
         bases = torch.cat([Gs[r][: allm[r][3]] for r in range(self.world)])
         lens = torch.cat([Cs[r][: allm[r][4]] for r in range(self.world)]).to(torch.int16)
         return out, total_bits, bases, lens
+
+
+class ShardedSmall:
+    """C5 (BASELINE configs[4]): small_compression.c front-end + n-ary Huffman, sharded.
+
+    SURVEY.md §8(e) "Small front-end: pairs never overlap (' ' is never the second byte of
+    a pair), so the only halo is one byte at the shard start" (and one at its end, for a
+    pair that starts on a shard's last byte). Steps:
+      1. all_gather of every rank's (first byte, last byte): the 1-byte halos
+      2. each rank's front-end body (dc_small_compress_body); rank 0 prefixes the header
+         (type byte 8, raw first byte, small_compression.c:582-665)
+      3. all_gather of the body lengths: the LITERAL fallback (output >= input, :655-662)
+         is decided over the whole stream, as the single-stream encoder decides it
+      4. the front-end stream is re-cut at multiples of 64 * sync_syms (each rank sends its
+         < 64 * sync_syms tail bytes to the next rank: one point-to-point exchange), so the
+         Huffman stage (ShardedHuffman) sees the layout it needs
+      5. ShardedHuffman encodes the front-end stream: bit-identical to the single-GPU
+         encoding of the whole front-end output
+    Decode: Huffman decode of the rank's segment, then the front-end inverse (per byte,
+    stateless); the ranks' decoded segments concatenate to the input.
+    """
+
+    def __init__(self, engine, group=None):
+        self.e = engine
+        self.h = ShardedHuffman(engine, group)
+        self.group = group
+        self.world, self.rank = self.h.world, self.h.rank
+
+    def _gather_i64(self, vals):
+        t = torch.tensor(vals, dtype=torch.int64, device=self._dev)
+        if self.world == 1:
+            return [vals]
+        out = [torch.empty_like(t) for _ in range(self.world)]
+        dist.all_gather(out, t, group=self.group)
+        return [o.cpu().tolist() for o in out]
+
+    def frontend(self, x, sync_syms: int = 64):
+        """Steps 1-4: this rank's segment of the global front-end stream (device bytes),
+        its global start, and whether the stream fell back to LITERAL."""
+        self._dev = x.device
+        n = x.numel()
+        if n < 2:
+            raise ValueError("each shard needs >= 2 bytes")
+        ends = self._gather_i64([int(x[0]), int(x[-1]), n])
+        left = ends[self.rank - 1][1] if self.rank > 0 else None
+        right = ends[self.rank + 1][0] if self.rank < self.world - 1 else None
+        n_total = sum(e[2] for e in ends)
+        parts = ([torch.tensor([left], dtype=torch.uint8, device=x.device)] if left is not None else []) + [x] + \
+                ([torch.tensor([right], dtype=torch.uint8, device=x.device)] if right is not None else [])
+        y = torch.cat(parts) if len(parts) > 1 else x
+        # body of stream bytes: rank 0 -> x[1..n-1] (x[0] is the raw first byte); rank r ->
+        # all of x (y[0] is the left halo)
+        nelem = n - 1 if self.rank == 0 else n
+        body = self.e.small_body(y, self.rank > 0, nelem)
+        lens = self._gather_i64([body.numel()])
+        total = 2 + sum(v[0] for v in lens)
+        literal = total >= n_total
+        if literal:   # ' ' + raw input, as the single-stream encoder falls back
+            seg = torch.cat([torch.tensor([ord(" ")], dtype=torch.uint8, device=x.device), x]) if self.rank == 0 else x
+        else:
+            seg = torch.cat([torch.tensor([8, int(x[0])], dtype=torch.uint8, device=x.device), body]) \
+                if self.rank == 0 else body
+        sizes = [v[0] for v in self._gather_i64([seg.numel()])]
+        return self._recut(seg, sizes, 64 * sync_syms), literal
+
+    def _recut(self, seg, sizes, q):
+        """Move each rank's bytes past the next multiple of q (global position) to the next
+        rank, so every segment but the last starts and ends on a multiple of q."""
+        off = [sum(sizes[:r]) for r in range(self.world + 1)]
+        cut = [0] + [(off[r] // q) * q for r in range(1, self.world)] + [off[self.world]]
+        if any(cut[r] < off[r - 1] for r in range(1, self.world)):
+            raise ValueError("front-end segments too short to re-cut at 64 * sync_syms")
+        r = self.rank
+        send = seg[cut[r + 1] - off[r]:] if r < self.world - 1 else seg[:0]
+        keep = seg[: cut[r + 1] - off[r]] if r < self.world - 1 else seg
+        recv = torch.empty(off[r] - cut[r], dtype=torch.uint8, device=seg.device)
+        if self.world > 1:   # < q bytes to the next rank (gloo: even ranks send first)
+            ops = []
+            if r < self.world - 1 and send.numel():
+                ops.append(dist.P2POp(dist.isend, send.contiguous(), r + 1, group=self.group))
+            if r > 0 and recv.numel():
+                ops.append(dist.P2POp(dist.irecv, recv, r - 1, group=self.group))
+            if ops:
+                for w in dist.batch_isend_irecv(ops):
+                    w.wait()
+        return torch.cat([recv, keep]) if recv.numel() else keep
+
+    def encode(self, x, n_ary: int = 16, sync_syms: int = 64):
+        seg, literal = self.frontend(x, sync_syms)
+        s = self.h.encode(seg, n_ary=n_ary, sync_syms=sync_syms)
+        s.literal = literal
+        return s
+
+    def decode(self, s):
+        seg = self.h.decode(s)[: s.n]
+        if self.rank == 0:
+            return self.e.small_decompress(seg)
+        return seg if s.literal else self.e.small_decompress_body(seg)

@@ -192,6 +192,16 @@ int dc_small_compress(dc_ctx *ctx, const uint8_t *d_in, uint64_t n, uint8_t *d_o
                       uint64_t *h_out_len);
 int dc_small_decompress(dc_ctx *ctx, const uint8_t *d_in, uint64_t m, uint8_t *d_out,
                         uint64_t *h_out_len);
+/* Shard bodies (data_compression_amd/dist.py ShardedSmall): the front-end
+ * output of stream bytes d_in[1 .. nelem] (no header, no LITERAL fallback), reading d_in[0]
+ * as left context when left_halo (a shard after the first: d_in[0] = the previous shard's
+ * last byte; else d_in[0] is the stream's raw first byte) and d_in[nelem + 1] (when
+ * nelem + 1 < len) as the right halo. Pairs never overlap, so the bodies of consecutive
+ * shards concatenate to the whole stream's body. d_out capacity >= nelem. */
+int dc_small_compress_body(dc_ctx *ctx, const uint8_t *d_in, uint64_t len, int left_halo, uint64_t nelem,
+                           uint8_t *d_out, uint64_t *h_out_len);
+/* decode of a body (every byte: >= 0x80 -> ' ' + byte - 0x80); d_out capacity >= 2*m */
+int dc_small_decompress_body(dc_ctx *ctx, const uint8_t *d_in, uint64_t m, uint8_t *d_out, uint64_t *h_out_len);
 
 #ifdef __cplusplus
 }

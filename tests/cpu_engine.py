@@ -61,3 +61,30 @@ class CpuEngine:
         total = int(sync[1][: (n + S - 1) // S].numpy().view(np.uint16).astype(np.int64).sum())
         y = orc.huff_unpack(stream, total, n, tab["el"], tab["ev"], tab["n_ary"])
         out[:n] = torch.from_numpy(y)
+
+    # ---- small front-end shard bodies (dist.ShardedSmall), restated with numpy ------------
+    def small_body(self, y, left_halo, nelem):
+        """small_compression.c:582-665 body of y[1..nelem] (dc_small_compress_body)."""
+        a = y.numpy()
+        i = np.arange(1, nelem + 1)
+        low = (a >= ord("a")) & (a <= ord("z"))
+        sp = a == ord(" ")
+        second = sp[i - 1] & low[i] & ((i >= 2) | bool(left_halo))
+        nxt_low = np.zeros(nelem, bool)
+        has = i + 1 < a.size
+        nxt_low[has] = low[i[has] + 1]
+        start = sp[i] & nxt_low
+        vals = np.where(start, 0x80 + a[np.minimum(i + 1, a.size - 1)].astype(np.int64), a[i]).astype(np.uint8)
+        return torch.from_numpy(vals[~second].copy())
+
+    def small_decompress(self, seg):
+        return torch.from_numpy(np.frombuffer(orc.small_decompress(seg.numpy().tobytes()), np.uint8).copy())
+
+    def small_decompress_body(self, seg):
+        a = seg.numpy()
+        pair = a >= 0x80
+        out = np.empty(a.size + int(pair.sum()), np.uint8)
+        pos = np.arange(a.size) + np.concatenate([[0], np.cumsum(pair)[:-1]])
+        out[pos] = np.where(pair, ord(" "), a)
+        out[pos[pair] + 1] = a[pair] - 0x80
+        return torch.from_numpy(out)

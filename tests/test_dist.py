@@ -81,3 +81,75 @@ def test_sharded_stream_is_bit_identical(world, n_ary):
     assert np.array_equal(got, payload)
     assert np.array_equal(bases.astype(np.uint64), rbase)
     assert np.array_equal(lens.view(np.uint16), rlens)
+
+
+def _small_worker(rank, world, port, cuts, kind, n_ary, S, q):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from data_compression_amd.dist import ShardedSmall
+    from tests.cpu_engine import CpuEngine
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        x = _small_input(kind, cuts[-1])
+        xs = torch.from_numpy(x[cuts[rank]: cuts[rank + 1]].copy())
+        sm = ShardedSmall(CpuEngine())
+        s = sm.encode(xs, n_ary=n_ary, sync_syms=S)
+        y = sm.decode(s)
+        g = sm.h.gather(s, dst=0)
+        q.put(("dec", rank, y.numpy().copy(), s.literal))
+        if rank == 0:
+            words, bits, bases, lens = g
+            q.put(("merged", words.numpy().copy(), bits))
+    finally:
+        dist.destroy_process_group()
+
+
+def _small_input(kind, n):
+    from data_compression_amd import synth
+    if kind == "log":
+        return synth.log_like(n, seed=33)
+    rng = np.random.default_rng(4)
+    return rng.integers(ord("A"), ord("Z") + 1, size=n, dtype=np.uint8)   # no pairs: LITERAL
+
+
+@pytest.mark.parametrize("world,kind", [(2, "log"), (3, "log"), (2, "upper")])
+def test_sharded_small_frontend_huffman(world, kind):
+    """C5 orchestration (dist.ShardedSmall): halo exchange, body per rank, global LITERAL
+    decision, re-cut at 64*S, sharded Huffman. The gathered stream equals the oracle's
+    single-stream Huffman encoding of the single-stream front-end output, and the ranks'
+    decoded segments concatenate to the input."""
+    from oracle import oracle as orc
+    S, n_ary = 64, 16
+    total = 64 * S * 4 * world + 777
+    x = _small_input(kind, total)
+    # cuts that land on pair halves (' ' then a letter across the boundary) where possible
+    cuts = [0]
+    for r in range(1, world):
+        c = r * total // world
+        if kind == "log":
+            while not (x[c - 1] == ord(" ") and ord("a") <= x[c] <= ord("z")):
+                c += 1
+        cuts.append(c)
+    cuts.append(total)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_small_worker, args=(r, world, port, cuts, kind, n_ary, S, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in range(world + 1)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    decs = sorted((r for r in res if r[0] == "dec"), key=lambda r: r[1])
+    assert np.array_equal(np.concatenate([d[2] for d in decs]), x)
+    fe = np.frombuffer(orc.small_compress(x.tobytes()), np.uint8)
+    assert all(d[3] == (fe[0] == ord(" ")) for d in decs)
+    _, words, bits = next(r for r in res if r[0] == "merged")
+    h = orc.histogram(fe)
+    L = orc.huffman_lengths(h, n_ary)
+    el, ev = orc.canonical(L, n_ary)
+    code, nb, _ = orc.bitcodes(el, ev, n_ary)
+    payload, rbits, _ = orc.huff_pack(fe, code, nb, sync_syms=S)
+    assert bits == rbits
+    assert np.array_equal(words.view(np.uint8)[: len(payload)], payload)

@@ -444,3 +444,53 @@ def test_text_vs_oracle_and_roundtrip(torch_cuda, codec, fmt, n_ary):
     bad[len(bad) // 2] = 0 if fmt == "trits5" else ord("~")
     with pytest.raises(DcError):
         codec.text_parse(bad, fmt, n_ary, bits)
+
+
+def test_small_shard_bodies_concatenate_to_stream(torch_cuda, codec):
+    """dc_small_compress_body on shards with 1-byte halos (dist.ShardedSmall's per-rank
+    step): header + bodies == the reference front-end output of the whole stream; the
+    body decoder inverts each body."""
+    from data_compression_amd import synth
+    torch = torch_cuda
+    x = synth.log_like(300_001, seed=12)
+    want = orc.small_compress(x.tobytes())
+    cuts = [0, 1000, 1001, 77_777, 200_000, x.size]
+    # a cut between ' ' and a letter (a pair straddling two shards)
+    j = next(i for i in range(150_000, x.size) if x[i - 1] == ord(" ") and ord("a") <= x[i] <= ord("z"))
+    cuts = sorted(set(cuts + [j]))
+    xt = torch.from_numpy(x).cuda()
+    parts = [bytes([8, x[0]])]
+    for r in range(len(cuts) - 1):
+        lo, hi = cuts[r], cuts[r + 1]
+        y = xt[max(lo - 1, 0): min(hi + 1, x.size)]
+        nelem = hi - lo - (1 if lo == 0 else 0)
+        body = codec.small_body(y, lo > 0, nelem)
+        parts.append(body.cpu().numpy().tobytes())
+        back = codec.small_decompress_body(body).cpu().numpy()
+        assert back.tobytes() == _small_body_decode_ref(body.cpu().numpy())
+    assert b"".join(parts) == want
+
+
+def _small_body_decode_ref(b):
+    out = bytearray()
+    for v in b.tolist():
+        out += bytes([32, v - 0x80]) if v >= 0x80 else bytes([v])
+    return bytes(out)
+
+
+def test_sharded_small_single_rank_on_device(torch_cuda, codec):
+    """dist.ShardedSmall with the device engine (world size 1): C5 front-end + n=16
+    Huffman equals the oracle's encoding of the reference front-end output; round trip."""
+    from data_compression_amd import synth
+    from data_compression_amd.dist import ShardedSmall
+    torch = torch_cuda
+    x = synth.log_like(1 << 20, seed=13)
+    sm = ShardedSmall(codec)
+    s = sm.encode(torch.from_numpy(x).cuda(), n_ary=16, sync_syms=64)
+    fe = np.frombuffer(orc.small_compress(x.tobytes()), np.uint8)
+    L, el, ev, code, nb, mx = _oracle_encode(fe, 16)
+    payload, bits, _ = orc.huff_pack(fe, code, nb, sync_syms=64)
+    sm.h.finalize(s)
+    assert s.bits == bits
+    assert np.array_equal(s.words.cpu().numpy().view(np.uint8)[: len(payload)], payload)
+    assert np.array_equal(sm.decode(s).cpu().numpy(), x)
