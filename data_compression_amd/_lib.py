@@ -109,6 +109,11 @@ def _declare_core(L):
         "dc_huff_choose_sync": ([u64, u64], u32),
         "dc_nyb_compress": ([vp, P, u64, i32, P, C.POINTER(u64)], i32),
         "dc_nyb_decompress": ([vp, P, u64, i32, P, C.POINTER(u64)], i32),
+        "dc_nyb_mtf_summary": ([vp, P, u64, P, P], i32),
+        "dc_nyb_body_plan": ([vp, P, u64, i32, P, P], i32),
+        "dc_nyb_body_write": ([vp, P, u64, i32, i32, i32, P, C.POINTER(u64), C.POINTER(i32)], i32),
+        "dc_nyb_dbody_plan": ([vp, P, u64, u64, P], i32),
+        "dc_nyb_dbody_write": ([vp, P, u64, u64, i32, P, C.POINTER(u64), C.POINTER(i32)], i32),
         "dc_small_compress": ([vp, P, u64, P, C.POINTER(u64)], i32),
         "dc_small_decompress": ([vp, P, u64, P, C.POINTER(u64)], i32),
         "dc_small_compress_body": ([vp, P, u64, i32, u64, P, C.POINTER(u64)], i32),

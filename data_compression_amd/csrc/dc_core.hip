@@ -2233,12 +2233,25 @@ __global__ __launch_bounds__(256) void k_text_parse(const uint8_t *__restrict__ 
 // byte 0 is the previous shard's last byte (the 1-byte left halo); both read one byte of
 // right halo for a pair that starts on the shard's last byte. DBODY: decode of a body,
 // element j = byte j.
+// Nybble encode (M_NYB_ENC) is driven by a per-element rank: the static dictionary rank
+// (c_static_rank) or, when FsmAux.rk is set, the adaptive move-to-front rank computed by the
+// k_mtf_* pipeline below. The same mode writes a whole stream (FsmAux.whole: header + LITERAL
+// fallback) or a shard body (dist.ShardedNybble: entry state s_init, the rank of a pending
+// byte carried from the previous shard, odd-tail byte only on the last shard). M_NYB_DBODY is
+// the static decode of a shard of the compressed stream (no header; one byte of right halo).
 enum { M_NYB_ENC = 0, M_NYB_DEC = 1, M_SMALL_ENC = 2, M_SMALL_DEC = 3, M_SMALL_BODY0 = 4, M_SMALL_BODY1 = 5,
-       M_SMALL_DBODY = 6 };
+       M_SMALL_DBODY = 6, M_NYB_DBODY = 7 };
 template <int M> struct FsmMode {
     static constexpr bool small_enc = M == M_SMALL_ENC || M == M_SMALL_BODY0 || M == M_SMALL_BODY1;
-    static constexpr bool body = M >= M_SMALL_BODY0;
-    static constexpr bool enc = M == M_NYB_ENC || M == M_SMALL_ENC;   // header + LITERAL fallback
+    static constexpr bool body = M == M_SMALL_BODY0 || M == M_SMALL_BODY1 || M == M_SMALL_DBODY || M == M_NYB_DBODY;
+    static constexpr bool enc = M == M_SMALL_ENC;   // header + LITERAL fallback (nybble: FsmAux.whole)
+};
+struct FsmAux {
+    const uint8_t *rk;    // M_NYB_ENC: rank per element (0..7, 0xFF = miss); null = static dictionary
+    uint32_t pend_rank;   // M_NYB_ENC body: rank of the byte before element 0 when s_init = 1
+    uint32_t s_init;      // entry state of element 0
+    uint32_t is_last;     // M_NYB_ENC: the shard ends the stream (odd-tail byte, :1000-1009)
+    uint32_t whole;       // M_NYB_ENC: whole stream (header 0xAF x[0], LITERAL fallback)
 };
 #define FSM_TILE 4096
 
@@ -2261,17 +2274,22 @@ __constant__ uint8_t c_static_rank[256];   // " etaoins" -> 0..7, else 0xFF (ini
 
 static __device__ __forceinline__ bool is_lower(uint32_t b) { return b >= 'a' && b <= 'z'; }
 
+static __device__ __forceinline__ uint32_t nyb_rank(const uint8_t *__restrict__ in, const FsmAux &a, uint64_t j)
+{
+    return a.rk ? (uint32_t)a.rk[j] : (uint32_t)c_static_rank[in[j + 1]];
+}
+
 // element j of mode M: transducer entry
 template <int M>
-static __device__ __forceinline__ Fsm elem_fsm(const uint8_t *__restrict__ in, uint64_t len, uint64_t j)
+static __device__ __forceinline__ Fsm elem_fsm(const uint8_t *__restrict__ in, uint64_t len, uint64_t j,
+                                               const FsmAux &a)
 {
     Fsm f;
     if (M == M_NYB_ENC) {                // byte i = j+1
-        const uint32_t x = in[j + 1];
-        if (c_static_rank[x] != 0xFF) { f.c0 = 0; f.c1 = 1; f.s0 = 1; f.s1 = 0; }
+        if (nyb_rank(in, a, j) != 0xFF) { f.c0 = 0; f.c1 = 1; f.s0 = 1; f.s1 = 0; }
         else { f.c0 = 1; f.c1 = 2; f.s0 = 0; f.s1 = 0; }
-    } else if (M == M_NYB_DEC) {         // compressed byte k = j+2
-        const uint32_t b = in[j + 2];
+    } else if (M == M_NYB_DEC || M == M_NYB_DBODY) {   // compressed byte k = j+2 (a body: byte j)
+        const uint32_t b = in[M == M_NYB_DBODY ? j : j + 2];
         const uint32_t h = b >> 4, l = b & 15;
         if (h & 8) { f.c0 = 2; f.s0 = (l & 8) ? 0 : 1; }
         else { f.c0 = 1; f.s0 = 0; }
@@ -2294,7 +2312,7 @@ static __device__ __forceinline__ Fsm elem_fsm(const uint8_t *__restrict__ in, u
 
 template <int M>
 __global__ __launch_bounds__(256) void k_fsm_tiles(const uint8_t *__restrict__ in, uint64_t len,
-                                                   uint64_t nelem, uint4 *__restrict__ summ)
+                                                   uint64_t nelem, uint4 *__restrict__ summ, FsmAux aux)
 {
     __shared__ uint4 s_f[256];
     const int t = threadIdx.x;
@@ -2302,7 +2320,7 @@ __global__ __launch_bounds__(256) void k_fsm_tiles(const uint8_t *__restrict__ i
     Fsm f = fsm_id();
     for (int k = 0; k < 16; ++k) {
         const uint64_t j = j0 + k;
-        if (j < nelem) f = fsm_then(f, elem_fsm<M>(in, len, j));
+        if (j < nelem) f = fsm_then(f, elem_fsm<M>(in, len, j, aux));
     }
     s_f[t] = make_uint4(f.c0, f.c1, f.s0, f.s1);
     __syncthreads();
@@ -2323,10 +2341,12 @@ __global__ __launch_bounds__(256) void k_fsm_tiles(const uint8_t *__restrict__ i
     if (t == 0) summ[blockIdx.x] = s_f[0];
 }
 
-// single workgroup: tile entry (offset, state) from the summaries; meta[0] = total count,
-// meta[1] = final state (starting from state 0)
+// single workgroup: tile entry (offset, state) from the summaries, starting in state s_init;
+// meta[0] = total count, meta[1] = final state (from s_init); meta[2..5] = the whole
+// composition (c0, c1, s0, s1) for shard plans
 __global__ __launch_bounds__(1024) void k_fsm_scan(const uint4 *__restrict__ summ, uint64_t ntiles,
-                                                   uint64_t *__restrict__ entry, uint64_t *__restrict__ meta)
+                                                   uint64_t *__restrict__ entry, uint64_t *__restrict__ meta,
+                                                   uint32_t s_init)
 {
     __shared__ uint64_t s_c0[1024], s_c1[1024];
     __shared__ uint32_t s_s0[1024], s_s1[1024];
@@ -2363,15 +2383,19 @@ __global__ __launch_bounds__(1024) void k_fsm_scan(const uint4 *__restrict__ sum
     }
     // exclusive prefix applied to the initial state 0
     uint64_t off = 0;
-    uint32_t st = 0;
-    if (t > 0) { off = s_c0[t - 1]; st = s_s0[t - 1]; }
+    uint32_t st = s_init;
+    if (t > 0) { off = s_init ? s_c1[t - 1] : s_c0[t - 1]; st = s_init ? s_s1[t - 1] : s_s0[t - 1]; }
     for (uint64_t k = a0; k < a1; ++k) {
         entry[k] = (off << 1) | st;
         const uint4 b = summ[k];
         off += st ? b.y : b.x;
         st = st ? b.w : b.z;
     }
-    if (t == 1023) { meta[0] = s_c0[1023]; meta[1] = s_s0[1023]; }
+    if (t == 1023) {
+        meta[0] = s_init ? s_c1[1023] : s_c0[1023];
+        meta[1] = s_init ? s_s1[1023] : s_s0[1023];
+        meta[2] = s_c0[1023]; meta[3] = s_c1[1023]; meta[4] = s_s0[1023]; meta[5] = s_s1[1023];
+    }
 }
 
 // Re-walk each tile with its entry state and write the output bytes.
@@ -2381,14 +2405,14 @@ __global__ __launch_bounds__(1024) void k_fsm_scan(const uint4 *__restrict__ sum
 template <int M>
 __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ in, uint64_t len, uint64_t nelem,
                                                    const uint64_t *__restrict__ entry,
-                                                   const uint64_t *__restrict__ meta, uint8_t *__restrict__ out)
+                                                   const uint64_t *__restrict__ meta, uint8_t *__restrict__ out,
+                                                   FsmAux aux)
 {
     __shared__ uint4 s_f[256];
-    __shared__ uint64_t s_base[256];
-    __shared__ uint32_t s_st[256];
     const int t = threadIdx.x;
-    const bool enc = FsmMode<M>::enc;
-    const uint64_t body = (M == M_NYB_ENC) ? meta[0] + meta[1] : meta[0];
+    const bool nyb_whole = M == M_NYB_ENC && aux.whole;
+    const bool enc = FsmMode<M>::enc || nyb_whole;
+    const uint64_t body = (M == M_NYB_ENC) ? meta[0] + (aux.is_last ? meta[1] : 0) : meta[0];
     const uint64_t total = enc ? 2 + body : 1 + body;
     const bool literal = enc && total >= len;
     if (literal) {
@@ -2398,7 +2422,8 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
         if (blockIdx.x == 0 && t == 0) out[0] = ' ';
         return;
     }
-    if (blockIdx.x == 0 && t == 0 && !FsmMode<M>::body) {
+    const bool headed = M == M_NYB_ENC ? nyb_whole : !FsmMode<M>::body;
+    if (blockIdx.x == 0 && t == 0 && headed) {
         if (M == M_NYB_ENC) { out[0] = 0xAF; out[1] = in[0]; }
         else if (M == M_SMALL_ENC) { out[0] = 8; out[1] = in[0]; }
         else { out[0] = in[1]; }
@@ -2407,7 +2432,7 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
     Fsm f = fsm_id();
     for (int k = 0; k < 16; ++k) {
         const uint64_t j = j0 + k;
-        if (j < nelem) f = fsm_then(f, elem_fsm<M>(in, len, j));
+        if (j < nelem) f = fsm_then(f, elem_fsm<M>(in, len, j, aux));
     }
     // workgroup exclusive scan of compositions (Hillis-Steele on the 256 thread maps)
     s_f[t] = make_uint4(f.c0, f.c1, f.s0, f.s1);
@@ -2435,32 +2460,30 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
         o += s ? p.y : p.x;
         s = s ? p.w : p.z;
     }
-    (void)s_base; (void)s_st;
-    const uint64_t head = FsmMode<M>::body ? 0 : enc ? 2 : 1;
-    o += head;
+    o += headed ? (enc ? 2 : 1) : 0;
     for (int k = 0; k < 16; ++k) {
         const uint64_t j = j0 + k;
         if (j >= nelem) break;
         if (M == M_NYB_ENC) {
             const uint64_t i = j + 1;
             const uint32_t x = in[i];
-            const uint32_t r = c_static_rank[x];
+            const uint32_t r = nyb_rank(in, aux, j);
             if (r != 0xFF) {
                 if (s == 1) {
-                    const uint32_t rp = c_static_rank[in[i - 1]];
+                    const uint32_t rp = j ? nyb_rank(in, aux, j - 1) : aux.pend_rank;
                     out[o++] = (uint8_t)(((8u | rp) << 4) | (8u | r));
                     s = 0;
                 } else {
                     s = 1;
-                    if (i == len - 1) out[o] = (uint8_t)x;   // odd tail (:1000-1009)
+                    if (aux.is_last && i == len - 1) out[o] = (uint8_t)x;   // odd tail (:1000-1009)
                 }
             } else {
                 if (s == 1) { out[o++] = in[i - 1]; out[o++] = (uint8_t)x; }
                 else out[o++] = (uint8_t)x;
                 s = 0;
             }
-        } else if (M == M_NYB_DEC) {
-            const uint64_t kk = j + 2;
+        } else if (M == M_NYB_DEC || M == M_NYB_DBODY) {
+            const uint64_t kk = M == M_NYB_DBODY ? j : j + 2;
             const uint32_t b = in[kk];
             const uint32_t h = b >> 4, l = b & 15;
             const uint32_t nxt = (kk + 1 < len) ? (uint32_t)(in[kk + 1] >> 4) : 0u;
@@ -2566,6 +2589,144 @@ __global__ void k_nyb_seq(const uint8_t *__restrict__ in, uint64_t len, int enc,
     meta[0] = o;
 }
 
+// ------------------------------------------------------------------------------------
+// Adaptive nybble encode, in parallel (SURVEY.md N4 [verified P6]). The move-to-front list of
+// context c after a stretch of input is the first 8 distinct of (that stretch's context-c
+// bytes, newest first) followed by the list before it. So "the list state after a tile,
+// started empty" is a summary, and summaries compose associatively:
+//     after(A then B)_c = first-8-distinct(B_c ++ A_c)
+// = touching B_c's entries, oldest first, on top of A_c. The encoder's rank of byte i is its
+// position in the list before the touch (compress_byte_index :833-839, update_context
+// :665-687). Pipeline: k_mtf_walk<0> summarises 4096-element tiles (one lane per tile, the
+// 16 lists as u64 words in LDS); k_mtf_reduce composes 64 summaries per group, level by
+// level; k_mtf_down hands each child its entry lists from the top (the initial " etaoins"
+// lists, or a shard's entry lists); k_mtf_walk<1> re-walks every tile from its entry lists
+// and writes the per-element rank (0..7, 0xFF = miss) that drives k_fsm_*<M_NYB_ENC>.
+// ------------------------------------------------------------------------------------
+#define MTF_TILE 4096
+#define MTF_FAN 64
+struct MtfSum {
+    uint64_t L[16];    // list of context c: byte k = entry k (most recent first)
+    uint8_t cnt[16];   // valid entries per list (0..8)
+};
+
+// move v to the front of (L, cnt); returns v's rank before the touch, or -1 (miss)
+static __device__ __forceinline__ int mtf_touch64(uint64_t &L, uint32_t &cnt, uint32_t v)
+{
+    const uint64_t ones = 0x0101010101010101ull;
+    const uint64_t t = L ^ (ones * v);
+    const uint64_t z = (t - ones) & ~t & (ones << 7);   // lowest flagged byte is the first match
+    const int pos = z ? (int)(__builtin_ctzll(z) >> 3) : 8;
+    const bool hit = pos < (int)cnt;
+    const int p = hit ? pos : (cnt < 7 ? (int)cnt : 7);   // entry dropped: the match, or the last slot
+    const uint64_t low = (1ull << (8 * p)) - 1;           // entries above p stay, [0, p) move up
+    const uint64_t high = p == 7 ? 0ull : ~((1ull << (8 * (p + 1))) - 1);
+    L = (L & high) | ((L & low) << 8) | (uint64_t)v;
+    if (!hit && cnt < 8) ++cnt;
+    return hit ? pos : -1;
+}
+
+// apply a summary list (newest first, n entries) on top of (L, cnt)
+static __device__ __forceinline__ void mtf_apply(uint64_t &L, uint32_t &cnt, uint64_t S, uint32_t n)
+{
+    for (int k = (int)n - 1; k >= 0; --k) (void)mtf_touch64(L, cnt, (uint32_t)(S >> (8 * k)) & 255u);
+}
+
+// MODE 0: tile summaries from empty lists -> summ[tile]; MODE 1: ranks from entry[tile].
+// Elements are bytes 1..len-1 of `in` (element e = byte e+1; its context is byte e).
+template <int MODE>
+__global__ __launch_bounds__(256) void k_mtf_walk(const uint8_t *__restrict__ in, uint64_t len, uint64_t ntiles,
+                                                  const MtfSum *__restrict__ entry, MtfSum *__restrict__ summ,
+                                                  uint8_t *__restrict__ rk)
+{
+    __shared__ uint64_t s_L[16][256];
+    const int t = threadIdx.x;
+    const uint64_t tile = (uint64_t)blockIdx.x * 256 + t;
+    if (tile >= ntiles) return;   // no barriers below
+    const uint64_t e0 = tile * MTF_TILE;
+    const uint64_t e1 = (e0 + MTF_TILE < len - 1) ? e0 + MTF_TILE : len - 1;   // elements [e0, e1)
+    uint64_t cnts = 0;   // nibble c = valid entries of list c
+    for (int c = 0; c < 16; ++c) {
+        s_L[c][t] = MODE ? entry[tile].L[c] : 0ull;
+        if (MODE) cnts |= (uint64_t)entry[tile].cnt[c] << (4 * c);
+    }
+    // bytes [e0, e1] in aligned 16-B pieces: byte e0 is the first context
+    const uintptr_t a0 = (uintptr_t)(in + e0), a1 = (uintptr_t)(in + e1);
+    uint32_t prev = in[e0];
+    uint32_t acc = 0;   // MODE 1: ranks of the current 4-element group
+    for (uintptr_t q = a0 & ~(uintptr_t)15; q <= a1; q += 16) {
+        const uint4 v = *(const uint4 *)q;
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const uintptr_t a = q + k;
+            if (a <= a0 || a > a1) continue;
+            const uint32_t x = (w[k >> 2] >> (8 * (k & 3))) & 255u;
+            const uint32_t c = (prev >> 3) & 15u;
+            uint64_t L = s_L[c][t];
+            uint32_t n = (uint32_t)(cnts >> (4 * c)) & 15u;
+            const int r = mtf_touch64(L, n, x);
+            s_L[c][t] = L;
+            cnts = (cnts & ~(15ull << (4 * c))) | ((uint64_t)n << (4 * c));
+            prev = x;
+            if (MODE) {
+                const uint64_t e = (uint64_t)(a - (uintptr_t)in) - 1;
+                acc |= (uint32_t)(r < 0 ? 0xFF : r) << (8 * (e & 3));
+                if ((e & 3) == 3) { *(uint32_t *)(rk + e - 3) = acc; acc = 0; }
+                else if (e + 1 == e1) {   // ragged end of the stream (tiles are multiples of 4)
+                    for (uint64_t u = e & ~3ull; u <= e; ++u) rk[u] = (uint8_t)(acc >> (8 * (u & 3)));
+                }
+            }
+        }
+    }
+    if (!MODE) {
+        for (int c = 0; c < 16; ++c) {
+            summ[tile].L[c] = s_L[c][t];
+            summ[tile].cnt[c] = (uint8_t)((cnts >> (4 * c)) & 15u);
+        }
+    }
+}
+
+// parent[g] = composition of child summaries [64 g, 64 g + 64); one lane per (group, context)
+__global__ __launch_bounds__(256) void k_mtf_reduce(const MtfSum *__restrict__ child, uint64_t nchild,
+                                                    MtfSum *__restrict__ parent)
+{
+    const uint64_t id = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint64_t g = id >> 4;
+    const int c = (int)(id & 15);
+    if (g * MTF_FAN >= nchild) return;
+    uint64_t L = 0;
+    uint32_t n = 0;
+    const uint64_t k1 = (g + 1) * MTF_FAN < nchild ? (g + 1) * MTF_FAN : nchild;
+    for (uint64_t k = g * MTF_FAN; k < k1; ++k) mtf_apply(L, n, child[k].L[c], child[k].cnt[c]);
+    parent[g].L[c] = L;
+    parent[g].cnt[c] = (uint8_t)n;
+}
+
+// child_entry[k] for the children of group g, from parent_entry[g]; the state after the
+// last child of the last group goes to *final (optional)
+__global__ __launch_bounds__(256) void k_mtf_down(const MtfSum *__restrict__ child, uint64_t nchild,
+                                                  const MtfSum *__restrict__ parent_entry,
+                                                  MtfSum *__restrict__ child_entry, MtfSum *__restrict__ final_state)
+{
+    const uint64_t id = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint64_t g = id >> 4;
+    const int c = (int)(id & 15);
+    if (g * MTF_FAN >= nchild) return;
+    uint64_t L = parent_entry[g].L[c];
+    uint32_t n = parent_entry[g].cnt[c];
+    const uint64_t k1 = (g + 1) * MTF_FAN < nchild ? (g + 1) * MTF_FAN : nchild;
+    for (uint64_t k = g * MTF_FAN; k < k1; ++k) {
+        child_entry[k].L[c] = L;
+        child_entry[k].cnt[c] = (uint8_t)n;
+        mtf_apply(L, n, child[k].L[c], child[k].cnt[c]);
+    }
+    if (final_state && k1 == nchild) {
+        final_state->L[c] = L;
+        final_state->cnt[c] = (uint8_t)n;
+    }
+}
+
 // =====================================================================================
 // host side
 // =====================================================================================
@@ -2590,6 +2751,9 @@ struct dc_ctx {
     uint64_t *d_meta;                             // small device scalars
     uint4 *d_summ;          size_t summ_cap;
     uint64_t *d_entry;      size_t entry_cap;
+    MtfSum *d_mtf;          size_t mtf_cap;       // adaptive nybble: tile summaries + entries, all levels
+    uint8_t *d_rk;          size_t rk_cap;        // adaptive nybble: rank per element
+    const uint8_t *rk_in; uint64_t rk_len;        // identity of the input the ranks belong to
     uint64_t *h_pinned;                           // pinned host scalars
     const uint8_t *hist_in; uint64_t hist_n;      // identity of the last dc_huff_hist input
     bool plan_ok;
@@ -2704,6 +2868,8 @@ void dc_ctx_destroy(dc_ctx *c)
     if (c->d_meta) (void)hipFree(c->d_meta);
     if (c->d_summ) (void)hipFree(c->d_summ);
     if (c->d_entry) (void)hipFree(c->d_entry);
+    if (c->d_mtf) (void)hipFree(c->d_mtf);
+    if (c->d_rk) (void)hipFree(c->d_rk);
     if (c->h_pinned) (void)hipHostFree(c->h_pinned);
     if (c->events_made)
         for (int i = 0; i < DC_MAX_EVENTS; ++i) { (void)hipEventDestroy(c->ev0[i]); (void)hipEventDestroy(c->ev1[i]); }
@@ -3073,32 +3239,99 @@ int dc_huff_base64url(dc_ctx *c, const uint32_t *d_words, uint64_t bit_base, uin
 }  // extern "C"
 
 // ---- byte-stream transducer codecs --------------------------------------------------
+// tiles + scan (from state aux.s_init) + write; h_plan (optional) gets the whole composition
+// (c0, c1, s0, s1) for shard plans; write = false stops after the scan
 template <int M>
 static int fsm_run(dc_ctx *c, const uint8_t *d_in, uint64_t len, uint64_t nelem, uint8_t *d_out, uint64_t *h_len,
-                   const char *name)
+                   const char *name, FsmAux aux = FsmAux{nullptr, 0, 0, 1, 1}, uint64_t *h_plan = nullptr,
+                   bool write = true)
 {
     const uint64_t ntiles = (nelem + FSM_TILE - 1) / FSM_TILE;
     const uint64_t nt = ntiles ? ntiles : 1;
     if (ensure((void **)&c->d_summ, &c->summ_cap, nt * sizeof(uint4))) return DC_E_HIP;
     if (ensure((void **)&c->d_entry, &c->entry_cap, nt * sizeof(uint64_t))) return DC_E_HIP;
     if (ntiles == 0) {
-        HIPCHK(hipMemsetAsync(c->d_meta, 0, 2 * sizeof(uint64_t), c->stream));
-        HIPCHK(hipMemsetAsync(c->d_entry, 0, sizeof(uint64_t), c->stream));
+        // empty: count 0, state unchanged; composition = identity
+        c->h_pinned[0] = 0; c->h_pinned[1] = aux.s_init;
+        c->h_pinned[2] = 0; c->h_pinned[3] = 0; c->h_pinned[4] = 0; c->h_pinned[5] = 1;
+        HIPCHK(hipMemcpyAsync(c->d_meta, c->h_pinned, 6 * sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
+        c->h_pinned[6] = aux.s_init;
+        HIPCHK(hipMemcpyAsync(c->d_entry, c->h_pinned + 6, sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
     } else {
-        LAUNCH(c, name, k_fsm_tiles<M>, ntiles, 256, d_in, len, nelem, c->d_summ);
-        LAUNCH(c, "fsm_scan", k_fsm_scan, 1, 1024, (const uint4 *)c->d_summ, ntiles, c->d_entry, c->d_meta);
+        LAUNCH(c, name, k_fsm_tiles<M>, ntiles, 256, d_in, len, nelem, c->d_summ, aux);
+        LAUNCH(c, "fsm_scan", k_fsm_scan, 1, 1024, (const uint4 *)c->d_summ, ntiles, c->d_entry, c->d_meta,
+               aux.s_init);
     }
-    const uint64_t wgrid = ntiles ? ntiles : 1;
-    LAUNCH(c, "fsm_write", k_fsm_write<M>, wgrid, 256, d_in, len, nelem, (const uint64_t *)c->d_entry,
-           (const uint64_t *)c->d_meta, d_out);
-    HIPCHK(hipMemcpyAsync(c->h_pinned, c->d_meta, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+    if (write) {
+        const uint64_t wgrid = ntiles ? ntiles : 1;
+        LAUNCH(c, "fsm_write", k_fsm_write<M>, wgrid, 256, d_in, len, nelem, (const uint64_t *)c->d_entry,
+               (const uint64_t *)c->d_meta, d_out, aux);
+    }
+    HIPCHK(hipMemcpyAsync(c->h_pinned, c->d_meta, 6 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
-    const bool enc = FsmMode<M>::enc;
-    const uint64_t body = (M == M_NYB_ENC) ? c->h_pinned[0] + c->h_pinned[1] : c->h_pinned[0];
-    uint64_t total = FsmMode<M>::body ? body : enc ? 2 + body : 1 + body;
+    if (h_plan) for (int k = 0; k < 4; ++k) h_plan[k] = c->h_pinned[2 + k];
+    const bool nyb = M == M_NYB_ENC;
+    const bool enc = FsmMode<M>::enc || (nyb && aux.whole);
+    const uint64_t body = nyb ? c->h_pinned[0] + (aux.is_last ? c->h_pinned[1] : 0) : c->h_pinned[0];
+    uint64_t total = (FsmMode<M>::body || (nyb && !aux.whole)) ? body : enc ? 2 + body : 1 + body;
     if (enc && total >= len) total = len + 1;
-    *h_len = total;
+    if (h_len) *h_len = total;
     return DC_OK;
+}
+
+// Adaptive nybble ranks (k_mtf_* pipeline) of elements 1..len-1 of d_in into c->d_rk, from the
+// entry lists h_init. ranks = false: only the composition of the whole input from h_init
+// into *h_final (a shard summary when h_init is empty).
+static int mtf_run(dc_ctx *c, const uint8_t *d_in, uint64_t len, const MtfSum *h_init, bool ranks, MtfSum *h_final)
+{
+    const uint64_t n0 = len > 1 ? (len - 2) / MTF_TILE + 1 : 0;
+    if (n0 == 0) {
+        if (h_final) *h_final = *h_init;
+        c->rk_in = d_in; c->rk_len = len;
+        return DC_OK;
+    }
+    uint64_t nl[8], off[8];
+    int levels = 0;
+    uint64_t tot = 0;
+    for (uint64_t n = n0;; n = (n + MTF_FAN - 1) / MTF_FAN) {
+        nl[levels] = n; off[levels] = tot; tot += n; ++levels;
+        if (n <= MTF_FAN) break;
+    }
+    // layout: [summaries, all levels][entries, all levels][init][final]
+    if (ensure((void **)&c->d_mtf, &c->mtf_cap, (2 * tot + 2) * sizeof(MtfSum))) return DC_E_HIP;
+    MtfSum *S = c->d_mtf, *E = c->d_mtf + tot, *init = c->d_mtf + 2 * tot, *fin = init + 1;
+    HIPCHK(hipMemcpyAsync(init, h_init, sizeof(MtfSum), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));   // h_init is pageable
+    if (ranks && ensure((void **)&c->d_rk, &c->rk_cap, ((len + 3) & ~3ull))) return DC_E_HIP;
+    LAUNCH(c, "mtf_tiles", k_mtf_walk<0>, (n0 + 255) / 256, 256, d_in, len, n0, (const MtfSum *)nullptr, S,
+           (uint8_t *)nullptr);
+    for (int l = 0; l + 1 < levels; ++l)
+        LAUNCH(c, "mtf_reduce", k_mtf_reduce, (nl[l + 1] * 16 + 255) / 256, 256, (const MtfSum *)(S + off[l]), nl[l],
+               S + off[l + 1]);
+    for (int l = levels - 1; l >= 0; --l) {
+        const MtfSum *pe = (l == levels - 1) ? init : E + off[l + 1];
+        const uint64_t groups = (nl[l] + MTF_FAN - 1) / MTF_FAN;
+        LAUNCH(c, "mtf_down", k_mtf_down, (groups * 16 + 255) / 256, 256, (const MtfSum *)(S + off[l]), nl[l], pe,
+               E + off[l], l == levels - 1 ? fin : (MtfSum *)nullptr);
+    }
+    if (ranks)
+        LAUNCH(c, "mtf_ranks", k_mtf_walk<1>, (n0 + 255) / 256, 256, d_in, len, n0, (const MtfSum *)E,
+               (MtfSum *)nullptr, c->d_rk);
+    if (h_final) HIPCHK(hipMemcpyAsync(h_final, fin, sizeof(MtfSum), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->rk_in = ranks ? d_in : nullptr; c->rk_len = len;
+    return DC_OK;
+}
+
+static MtfSum mtf_initial()   // initialize_dictionary (nybble_compression.c:546-562)
+{
+    MtfSum s;
+    uint64_t L = 0;
+    const char *init = " etaoins";
+    for (int k = 0; k < 8; ++k) L |= (uint64_t)(uint8_t)init[k] << (8 * k);
+    for (int q = 0; q < 16; ++q) { s.L[q] = L; s.cnt[q] = 8; }
+    return s;
 }
 
 static int read_byte(dc_ctx *c, const uint8_t *d, uint8_t *v)
@@ -3137,10 +3370,93 @@ int dc_nyb_compress(dc_ctx *c, const uint8_t *d_in, uint64_t n, int modify, uint
     if (!c || !d_out || !h_len || (n && !d_in)) return DC_E_ARG;
     if (n == 0) { int r = write_byte(c, d_out, ' '); if (r) return r; HIPCHK(hipStreamSynchronize(c->stream)); *h_len = 1; return DC_OK; }
     if (!modify) return fsm_run<M_NYB_ENC>(c, d_in, n, n - 1, d_out, h_len, "nyb_enc_tiles");
-    LAUNCH(c, "nyb_seq_enc", k_nyb_seq, 1, 64, d_in, n, 1, 1, d_out, c->d_meta);
-    HIPCHK(hipMemcpyAsync(c->h_pinned, c->d_meta, sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
-    *h_len = c->h_pinned[0];
+    const MtfSum init = mtf_initial();
+    int r = mtf_run(c, d_in, n, &init, true, nullptr);
+    if (r) return r;
+    return fsm_run<M_NYB_ENC>(c, d_in, n, n - 1, d_out, h_len, "nyb_enca_tiles",
+                              FsmAux{n > 1 ? c->d_rk : nullptr, 0, 0, 1, 1});
+}
+
+// ---- nybble shard bodies (dist.ShardedNybble) ---------------------------
+int dc_nyb_mtf_summary(dc_ctx *c, const uint8_t *d_in, uint64_t len, uint8_t *h_lists, uint8_t *h_cnt)
+{
+    if (!c || !h_lists || !h_cnt || (len && !d_in)) return DC_E_ARG;
+    MtfSum empty, fin;
+    memset(&empty, 0, sizeof(empty));
+    int r = mtf_run(c, d_in, len, &empty, false, &fin);
+    if (r) return r;
+    memcpy(h_lists, fin.L, 128);
+    memcpy(h_cnt, fin.cnt, 16);
+    return DC_OK;
+}
+
+static int lists_in(const uint8_t *h_lists, MtfSum *s)
+{
+    memcpy(s->L, h_lists, 128);
+    for (int q = 0; q < 16; ++q) s->cnt[q] = 8;
+    return DC_OK;
+}
+
+int dc_nyb_body_plan(dc_ctx *c, const uint8_t *d_in, uint64_t len, int modify, const uint8_t *h_lists,
+                     uint64_t *h_plan)
+{
+    if (!c || !h_plan || !d_in || len < 1 || (modify && !h_lists)) return DC_E_ARG;
+    FsmAux aux{nullptr, 0, 0, 0, 0};
+    if (modify) {
+        MtfSum init;
+        lists_in(h_lists, &init);
+        int r = mtf_run(c, d_in, len, &init, true, nullptr);
+        if (r) return r;
+        aux.rk = len > 1 ? c->d_rk : nullptr;
+    }
+    int r = fsm_run<M_NYB_ENC>(c, d_in, len, len - 1, nullptr, nullptr, "nyb_body_tiles", aux, h_plan, false);
+    if (r) return r;
+    // rank of the last element (the byte a pending nybble of this shard belongs to)
+    uint8_t last = 0xFF;
+    if (len > 1) {
+        if (modify) HIPCHK(hipMemcpyAsync(c->h_pinned, c->d_rk + (len - 2), 1, hipMemcpyDeviceToHost, c->stream));
+        else HIPCHK(hipMemcpyAsync(c->h_pinned, d_in + (len - 1), 1, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        last = *(uint8_t *)c->h_pinned;
+        if (!modify) {
+            const char *t = " etaoins";
+            const uint8_t b = last;
+            last = 0xFF;
+            for (int k = 0; k < 8; ++k) if ((uint8_t)t[k] == b) { last = (uint8_t)k; break; }
+        }
+    }
+    h_plan[4] = last;
+    return DC_OK;
+}
+
+int dc_nyb_body_write(dc_ctx *c, const uint8_t *d_in, uint64_t len, int modify, int pend_rank, int is_last,
+                      uint8_t *d_out, uint64_t *h_len, int *h_state_out)
+{
+    if (!c || !d_out || !h_len || !d_in || len < 1 || pend_rank > 7) return DC_E_ARG;
+    if (modify && len > 1 && (c->rk_in != d_in || c->rk_len != len)) return DC_E_ARG;   // plan this input first
+    FsmAux aux{modify && len > 1 ? c->d_rk : nullptr, pend_rank < 0 ? 0u : (uint32_t)pend_rank,
+               pend_rank < 0 ? 0u : 1u, is_last ? 1u : 0u, 0};
+    int r = fsm_run<M_NYB_ENC>(c, d_in, len, len - 1, d_out, h_len, "nyb_body_tiles", aux);
+    if (r) return r;
+    if (h_state_out) *h_state_out = (int)c->h_pinned[1];
+    return DC_OK;
+}
+
+int dc_nyb_dbody_plan(dc_ctx *c, const uint8_t *d_in, uint64_t len, uint64_t m, uint64_t *h_plan)
+{
+    if (!c || !h_plan || (m && !d_in) || m > len || len > m + 1) return DC_E_ARG;
+    return fsm_run<M_NYB_DBODY>(c, d_in, len, m, nullptr, nullptr, "nyb_dbody_tiles", FsmAux{nullptr, 0, 0, 0, 0},
+                                h_plan, false);
+}
+
+int dc_nyb_dbody_write(dc_ctx *c, const uint8_t *d_in, uint64_t len, uint64_t m, int s_in, uint8_t *d_out,
+                       uint64_t *h_len, int *h_state_out)
+{
+    if (!c || !d_out || !h_len || (m && !d_in) || m > len || len > m + 1 || (s_in & ~1)) return DC_E_ARG;
+    int r = fsm_run<M_NYB_DBODY>(c, d_in, len, m, d_out, h_len, "nyb_dbody_tiles",
+                                 FsmAux{nullptr, 0, (uint32_t)s_in, 0, 0});
+    if (r) return r;
+    if (h_state_out) *h_state_out = (int)c->h_pinned[1];
     return DC_OK;
 }
 

@@ -189,6 +189,60 @@ class Codec:
                                                                           _ptr(out), C.byref(n)))
         return out[: n.value]
 
+    # ---- nybble codec, whole streams and shard bodies (dist.ShardedNybble) -----
+    def nyb_compress(self, x, modify: bool):
+        """compress_bytestring (nybble_compression.c:887-1038) of device bytes x."""
+        out = self._t(x.numel() + 2)
+        n = C.c_uint64(0)
+        check("dc_nyb_compress", self.L.dc_nyb_compress(self.ctx, _ptr(x), x.numel(), int(modify), _ptr(out),
+                                                        C.byref(n)))
+        return out[: n.value]
+
+    def nyb_decompress(self, comp, modify: bool):
+        """decompress_bytestring (nybble_compression.c:734-817) of device bytes comp."""
+        out = self._t(max(2 * comp.numel(), 1))
+        n = C.c_uint64(0)
+        check("dc_nyb_decompress", self.L.dc_nyb_decompress(self.ctx, _ptr(comp), comp.numel(), int(modify),
+                                                            _ptr(out), C.byref(n)))
+        return out[: n.value]
+
+    def nyb_mtf_summary(self, y):
+        """Move-to-front lists after elements y[1..] from empty lists: (lists[16][8], cnt[16])."""
+        lists = np.zeros(128, np.uint8)
+        cnt = np.zeros(16, np.uint8)
+        check("dc_nyb_mtf_summary", self.L.dc_nyb_mtf_summary(self.ctx, _ptr(y), y.numel(), lists.ctypes.data,
+                                                              cnt.ctypes.data))
+        return lists.reshape(16, 8), cnt
+
+    def nyb_body_plan(self, y, modify: bool, lists=None):
+        """(c0, c1, s0, s1, last_rank) of the shard's elements y[1..] (dc_nyb_body_plan)."""
+        plan = np.zeros(5, np.uint64)
+        la = np.ascontiguousarray(lists, dtype=np.uint8) if modify else None
+        check("dc_nyb_body_plan", self.L.dc_nyb_body_plan(self.ctx, _ptr(y), y.numel(), int(modify),
+                                                          la.ctypes.data if modify else None, plan.ctypes.data))
+        return [int(v) for v in plan]
+
+    def nyb_body_write(self, y, modify: bool, pend_rank: int, is_last: bool):
+        out = self._t(max(2 * y.numel(), 1))
+        n = C.c_uint64(0)
+        st = C.c_int32(0)
+        check("dc_nyb_body_write", self.L.dc_nyb_body_write(self.ctx, _ptr(y), y.numel(), int(modify), pend_rank,
+                                                            int(is_last), _ptr(out), C.byref(n), C.byref(st)))
+        return out[: n.value]
+
+    def nyb_dbody_plan(self, y, m: int):
+        plan = np.zeros(4, np.uint64)
+        check("dc_nyb_dbody_plan", self.L.dc_nyb_dbody_plan(self.ctx, _ptr(y), y.numel(), m, plan.ctypes.data))
+        return [int(v) for v in plan]
+
+    def nyb_dbody_write(self, y, m: int, s_in: int):
+        out = self._t(max(2 * m, 1))
+        n = C.c_uint64(0)
+        st = C.c_int32(0)
+        check("dc_nyb_dbody_write", self.L.dc_nyb_dbody_write(self.ctx, _ptr(y), y.numel(), m, s_in, _ptr(out),
+                                                              C.byref(n), C.byref(st)))
+        return out[: n.value]
+
     # ---- digit text (SURVEY §8(f)3): formats as dc_gpu.h DC_TEXT_* ------------------------
     TEXT_FORMATS = {"base64url": 0, "base16": 1, "digits": 2, "z85": 3, "trits5": 4}
 

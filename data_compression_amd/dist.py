@@ -25,6 +25,7 @@ from __future__ import annotations
 
 from dataclasses import dataclass
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -239,3 +240,141 @@ class ShardedSmall:
         if self.rank == 0:
             return self.e.small_decompress(seg)
         return seg if s.literal else self.e.small_decompress_body(seg)
+
+
+INITIAL_LISTS = np.frombuffer(b" etaoins" * 16, np.uint8).reshape(16, 8)   # initialize_dictionary
+
+
+def compose_lists(lists, summ, cnt):
+    """Move-to-front lists after a shard whose summary (started empty) is (summ, cnt):
+    first 8 distinct of (summary list, lists) per context (update_context,
+    nybble_compression.c:665-687). Host side of the adaptive shard exchange."""
+    out = np.empty_like(lists)
+    for c in range(16):
+        seen = []
+        for v in list(summ[c][: int(cnt[c])]) + list(lists[c]):
+            if v not in seen:
+                seen.append(v)
+            if len(seen) == 8:
+                break
+        out[c] = seen
+    return out
+
+
+class ShardedNybble:
+    """nybble_compression.c's compress_bytestring / decompress_bytestring, sharded.
+
+    SURVEY.md §8(e): "Nybble static: shards need a 1-byte halo (x[start-1] for the seed and
+    context) and the carried run parity of the previous shard's trailing hit-run"; "Nybble
+    adaptive: encode can be sharded with a halo of context history; decode: replicas only".
+    Encode (both modes), per rank:
+      1. all_gather of (first byte, last byte, n): the 1-byte left halo and the stream size
+      2. adaptive only: the rank's move-to-front summary (dc_nyb_mtf_summary, 144 B) is
+         all-gathered and each rank composes its entry lists from the initial " etaoins"
+         lists and the summaries of the ranks before it
+      3. the rank's transducer plan (dc_nyb_body_plan: bytes out and exit state from either
+         entry state, the rank of its last element) is all-gathered; each rank derives its
+         entry state (is a hit nybble pending, and that byte's rank) and the stream total
+      4. LITERAL fallback (output >= input, :1018-1037) decided over the whole stream
+      5. each rank writes its body (dc_nyb_body_write); rank 0 prefixes 0xAF, x[0]
+    The ranks' segments concatenate to the single-stream compress_bytestring output.
+    Decode (static): the compressed stream is cut anywhere; each rank's segment needs one
+    byte of right halo and the entry state "start at the low nybble", found the same way
+    (dc_nyb_dbody_plan, all_gather, dc_nyb_dbody_write). The decoded segments concatenate
+    to the input. Adaptive decode is sequential by definition (each byte's list depends on
+    every byte before it): decode_replica gathers the stream and decodes it whole.
+    """
+
+    def __init__(self, engine, group=None):
+        self.e = engine
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+
+    def _gather(self, vals, dev):
+        if self.world == 1:
+            return [list(vals)]
+        t = torch.tensor(vals, dtype=torch.int64, device=dev)
+        out = [torch.empty_like(t) for _ in range(self.world)]
+        dist.all_gather(out, t, group=self.group)
+        return [o.cpu().tolist() for o in out]
+
+    def _u8(self, vals, dev):
+        return torch.tensor(vals, dtype=torch.uint8, device=dev)
+
+    def compress(self, x, modify: bool):
+        """This rank's segment of the compressed stream, and whether it is LITERAL."""
+        dev, n = x.device, x.numel()
+        if n < 1 or (self.rank == 0 and n < 2):
+            raise ValueError("shards need >= 1 byte (rank 0: >= 2)")
+        ends = self._gather([int(x[0]), int(x[-1]), n], dev)
+        n_total = sum(e[2] for e in ends)
+        y = torch.cat([self._u8([ends[self.rank - 1][1]], dev), x]) if self.rank > 0 else x
+        lists = None
+        if modify:
+            summ, cnt = self.e.nyb_mtf_summary(y)
+            allsum = self._gather(list(summ.reshape(-1)) + list(cnt), dev)
+            lists = INITIAL_LISTS.copy()
+            for q in range(self.rank):
+                a = np.asarray(allsum[q], np.uint8)
+                lists = compose_lists(lists, a[:128].reshape(16, 8), a[128:])
+        plan = self.e.nyb_body_plan(y, modify, lists)
+        plans = self._gather(plan, dev)
+        s, pend, total = 0, -1, 2
+        for q in range(self.world):
+            c0, c1, s0, s1, last = plans[q]
+            if q == self.rank:
+                my_s, my_pend = s, pend
+            total += c1 if s else c0
+            s = s1 if s else s0
+            pend = last if s else -1
+        total += s                      # odd tail: the last pending byte is written raw
+        literal = total >= n_total
+        if literal:
+            seg = torch.cat([self._u8([ord(" ")], dev), x]) if self.rank == 0 else x
+            return seg, True
+        body = self.e.nyb_body_write(y, modify, my_pend if my_s else -1, self.rank == self.world - 1)
+        if self.rank == 0:
+            body = torch.cat([self._u8([0xAF, int(x[0])], dev), body])
+        return body, False
+
+    def decompress(self, seg):
+        """Static-mode decode of this rank's segment of a compressed stream (as compress
+        cut it, or cut anywhere) -> this rank's decoded bytes."""
+        dev, m = seg.device, seg.numel()
+        info = self._gather([m, int(seg[0]) if m else -1], dev)
+        typ = info[0][1]
+        if typ == ord(" "):
+            return seg[1:] if self.rank == 0 else seg
+        if typ != 0xAF:
+            raise ValueError("not a nybble stream (type byte %r)" % typ)
+        body = seg[2:] if self.rank == 0 else seg
+        if self.rank == 0 and m < 2:
+            raise ValueError("rank 0's segment must hold the 2-byte header")
+        right = next((info[q][1] for q in range(self.rank + 1, self.world) if info[q][0] > 0), None)
+        y = torch.cat([body, self._u8([right], dev)]) if right is not None else body
+        mb = body.numel()
+        plans = self._gather(self.e.nyb_dbody_plan(y, mb), dev)
+        s = 0
+        for q in range(self.rank):
+            c0, c1, s0, s1 = plans[q]
+            s = s1 if s else s0
+        out = self.e.nyb_dbody_write(y, mb, s)
+        return torch.cat([seg[1:2], out]) if self.rank == 0 else out
+
+    def decode_replica(self, seg, sizes, modify: bool):
+        """Adaptive (or any) decode by replicas: every rank gathers the whole stream, decodes
+        it, and keeps its own byte range (sizes = the ranks' input sizes)."""
+        dev, m = seg.device, seg.numel()
+        ms = [v[0] for v in self._gather([m], dev)]
+        if self.world > 1:
+            buf = torch.zeros(max(ms), dtype=torch.uint8, device=dev)
+            buf[:m] = seg
+            parts = [torch.empty_like(buf) for _ in range(self.world)]
+            dist.all_gather(parts, buf, group=self.group)
+            whole = torch.cat([p[:k] for p, k in zip(parts, ms)])
+        else:
+            whole = seg
+        out = self.e.nyb_decompress(whole, modify)
+        a = sum(sizes[: self.rank])
+        return out[a: a + sizes[self.rank]]

@@ -186,6 +186,34 @@ int dc_nyb_compress(dc_ctx *ctx, const uint8_t *d_in, uint64_t n, int modify, ui
 /* Decode m compressed bytes; d_out capacity >= 2*m. *h_out_len as above. */
 int dc_nyb_decompress(dc_ctx *ctx, const uint8_t *d_in, uint64_t m, int modify, uint8_t *d_out,
                       uint64_t *h_out_len);
+/* Shard bodies (data_compression_amd/dist.py ShardedNybble). A shard buffer is
+ * d_in[0 .. len): d_in[0] is the context byte (the stream's first byte on the first shard, the
+ * previous shard's last byte after it) and the shard's elements are bytes 1 .. len-1, as in
+ * compress_bytestring's loop (nybble_compression.c:908-996).
+ * Adaptive (modify) move-to-front lists: 16 contexts x 8 bytes, most recent first.
+ *   dc_nyb_mtf_summary: the lists after the shard's elements, started empty (h_cnt[c] valid
+ *     entries of list c); summaries compose: lists after A then B = first 8 distinct of
+ *     (B's list, A's list) per context.
+ *   dc_nyb_body_plan: with the shard's entry lists h_lists (adaptive; ignored when static),
+ *     h_plan[0..3] = the shard's transducer (bytes out from state 0, from state 1, exit state
+ *     from 0, from 1; state 1 = the previous element's hit nybble is pending) and h_plan[4] =
+ *     the rank of the shard's last element (0xFF = miss).
+ *   dc_nyb_body_write: the shard's body from the entry state (pend_rank = the pending byte's
+ *     rank, or -1), the odd-tail byte when is_last; no header and no LITERAL fallback (decided
+ *     over the whole stream). The adaptive ranks come from the preceding dc_nyb_body_plan on
+ *     the same d_in/len. d_out capacity >= 2*len. *h_state_out = exit state.
+ * Static decode of a shard of the compressed stream after its 2-byte header: m bytes, plus
+ * one byte of right halo (the next shard's first byte) when len = m + 1:
+ *   dc_nyb_dbody_plan: h_plan[0..3] as above (state 1 = start at the low nybble);
+ *   dc_nyb_dbody_write: decoded bytes from entry state s_in; d_out capacity >= 2*m. */
+int dc_nyb_mtf_summary(dc_ctx *ctx, const uint8_t *d_in, uint64_t len, uint8_t *h_lists, uint8_t *h_cnt);
+int dc_nyb_body_plan(dc_ctx *ctx, const uint8_t *d_in, uint64_t len, int modify, const uint8_t *h_lists,
+                     uint64_t *h_plan);
+int dc_nyb_body_write(dc_ctx *ctx, const uint8_t *d_in, uint64_t len, int modify, int pend_rank, int is_last,
+                      uint8_t *d_out, uint64_t *h_out_len, int *h_state_out);
+int dc_nyb_dbody_plan(dc_ctx *ctx, const uint8_t *d_in, uint64_t len, uint64_t m, uint64_t *h_plan);
+int dc_nyb_dbody_write(dc_ctx *ctx, const uint8_t *d_in, uint64_t len, uint64_t m, int s_in, uint8_t *d_out,
+                       uint64_t *h_out_len, int *h_state_out);
 
 /* ---- small front-end (small_compression.c:507-665), device-resident ----------------- */
 int dc_small_compress(dc_ctx *ctx, const uint8_t *d_in, uint64_t n, uint8_t *d_out,

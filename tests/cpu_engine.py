@@ -88,3 +88,105 @@ class CpuEngine:
         out[pos] = np.where(pair, ord(" "), a)
         out[pos[pair] + 1] = a[pair] - 0x80
         return torch.from_numpy(out)
+
+    # ---- nybble shard bodies (dist.ShardedNybble), restated in plain Python ----------------
+    # nybble_compression.c: context byte_to_context :517-523, compress_byte_index :819-884,
+    # update_context :665-687, compress_bytestring :887-1038, decompress_nybble :643-663.
+    _STATIC = b" etaoins"
+
+    @staticmethod
+    def _touch(lst, v):
+        if v in lst:
+            lst.remove(v)
+        lst.insert(0, v)
+        del lst[8:]
+
+    def _ranks(self, a, modify, lists):
+        L = [list(r) for r in lists] if modify else None
+        rk = []
+        for i in range(1, len(a)):
+            x = a[i]
+            if modify:
+                c = (a[i - 1] >> 3) & 15
+                rk.append(L[c].index(x) if x in L[c] else 0xFF)
+                self._touch(L[c], x)
+            else:
+                rk.append(self._STATIC.index(x) if x in self._STATIC else 0xFF)
+        return rk
+
+    def nyb_mtf_summary(self, y):
+        a = bytes(y.numpy())
+        L = [[] for _ in range(16)]
+        for i in range(1, len(a)):
+            self._touch(L[(a[i - 1] >> 3) & 15], a[i])
+        lists = np.zeros((16, 8), np.uint8)
+        cnt = np.zeros(16, np.uint8)
+        for c in range(16):
+            lists[c, : len(L[c])] = L[c]
+            cnt[c] = len(L[c])
+        return lists, cnt
+
+    @staticmethod
+    def _walk(a, rk, s, pend, is_last):
+        out = bytearray()
+        for j, r in enumerate(rk):
+            i = j + 1
+            if r != 0xFF:
+                if s:
+                    rp = rk[j - 1] if j else pend
+                    out.append(((8 | rp) << 4) | (8 | r))
+                    s = 0
+                else:
+                    s = 1
+            else:
+                out += bytes([a[i - 1], a[i]]) if s else bytes([a[i]])
+                s = 0
+        if is_last and s:
+            out.append(a[-1])
+        return bytes(out), s
+
+    def nyb_body_plan(self, y, modify, lists=None):
+        a = bytes(y.numpy())
+        rk = self._ranks(a, modify, lists)
+        self._plan = (a, rk)
+        o0, s0 = self._walk(a, rk, 0, 0, False)
+        o1, s1 = self._walk(a, rk, 1, 0, False)
+        return [len(o0), len(o1), s0, s1, rk[-1] if rk else 0xFF]
+
+    def nyb_body_write(self, y, modify, pend_rank, is_last):
+        a, rk = self._plan
+        assert a == bytes(y.numpy())
+        out, _ = self._walk(a, rk, 1 if pend_rank >= 0 else 0, pend_rank, is_last)
+        return torch.from_numpy(np.frombuffer(out, np.uint8).copy())
+
+    def _dwalk(self, a, m, s):
+        out = bytearray()
+        for k in range(m):
+            b = a[k]
+            h, l = b >> 4, b & 15
+            nxt = a[k + 1] >> 4 if k + 1 < len(a) else 0
+            if s == 0 and not (h & 8):
+                out.append(b)
+                continue
+            if s == 0:
+                out.append(self._STATIC[h & 7])
+            if l & 8:
+                out.append(self._STATIC[l & 7])
+                s = 0
+            else:
+                out.append(((l & 7) << 4) + nxt)
+                s = 1
+        return bytes(out), s
+
+    def nyb_dbody_plan(self, y, m):
+        a = bytes(y.numpy())
+        o0, s0 = self._dwalk(a, m, 0)
+        o1, s1 = self._dwalk(a, m, 1)
+        return [len(o0), len(o1), s0, s1]
+
+    def nyb_dbody_write(self, y, m, s_in):
+        out, _ = self._dwalk(bytes(y.numpy()), m, s_in)
+        return torch.from_numpy(np.frombuffer(out, np.uint8).copy())
+
+    def nyb_decompress(self, comp, modify):
+        return torch.from_numpy(np.frombuffer(orc.nybble_decompress(bytes(comp.numpy()), modify), np.uint8).copy())

@@ -153,3 +153,70 @@ def test_sharded_small_frontend_huffman(world, kind):
     payload, rbits, _ = orc.huff_pack(fe, code, nb, sync_syms=S)
     assert bits == rbits
     assert np.array_equal(words.view(np.uint8)[: len(payload)], payload)
+
+
+def _nyb_worker(rank, world, port, cuts, kind, modify, dcuts, q):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from data_compression_amd.dist import ShardedNybble
+    from tests.cpu_engine import CpuEngine
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        x = _nyb_input(kind, cuts[-1])
+        xs = torch.from_numpy(x[cuts[rank]: cuts[rank + 1]].copy())
+        sn = ShardedNybble(CpuEngine())
+        seg, literal = sn.compress(xs, modify)
+        sizes = [cuts[r + 1] - cuts[r] for r in range(world)]
+        if modify:
+            y = sn.decode_replica(seg, sizes, True)
+            yd = None
+        else:
+            y = sn.decompress(seg)
+            # the same stream re-cut at arbitrary byte positions (dcuts), decoded again
+            from oracle import oracle as orc
+            whole = np.frombuffer(orc.nybble_compress(x.tobytes(), False), np.uint8)
+            lo, hi = int(dcuts[rank] * whole.size), int(dcuts[rank + 1] * whole.size)
+            yd = sn.decompress(torch.from_numpy(whole[lo:hi].copy())).numpy().copy()
+        q.put(("r", rank, seg.numpy().copy(), literal, y.numpy().copy(), yd))
+    finally:
+        dist.destroy_process_group()
+
+
+def _nyb_input(kind, n):
+    from data_compression_amd import synth
+    if kind == "text":
+        return synth.english_like(n, seed=12)
+    rng = np.random.default_rng(5)
+    return rng.integers(ord("A"), ord("Z") + 1, size=n, dtype=np.uint8)   # all misses: LITERAL
+
+
+@pytest.mark.parametrize("world,kind,modify", [(2, "text", False), (3, "text", False), (4, "text", True),
+                                               (2, "text", True), (2, "upper", False), (3, "upper", True)])
+def test_sharded_nybble(world, kind, modify):
+    """SURVEY §8(e) nybble rows (dist.ShardedNybble): 1-byte halos, carried run parity (and,
+    adaptive, the composed move-to-front lists). The ranks' segments concatenate to the
+    reference's single-stream compress_bytestring output; decoding gives the input back,
+    also when the compressed stream is cut at arbitrary bytes (static)."""
+    from oracle import oracle as orc
+    total = 3000 * world + 123
+    x = _nyb_input(kind, total)
+    rng = np.random.default_rng(world * 7 + modify)
+    cuts = [0] + sorted(int(v) for v in rng.choice(np.arange(2, total - 1), world - 1, replace=False)) + [total]
+    dcuts = [0.0] + sorted(float(v) for v in rng.uniform(0.05, 0.95, world - 1)) + [1.0]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_nyb_worker, args=(r, world, port, cuts, kind, modify, dcuts, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=180) for _ in range(world)), key=lambda r: r[1])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ref = orc.nybble_compress(x.tobytes(), modify)
+    assert b"".join(r[2].tobytes() for r in res) == ref
+    assert all(r[3] == (ref[:1] == b" ") for r in res)
+    assert np.array_equal(np.concatenate([r[4] for r in res]), x)
+    if not modify:
+        assert np.array_equal(np.concatenate([r[5] for r in res]), x)
