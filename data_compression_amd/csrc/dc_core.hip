@@ -2727,6 +2727,154 @@ __global__ __launch_bounds__(256) void k_mtf_down(const MtfSum *__restrict__ chi
     }
 }
 
+// ------------------------------------------------------------------------------------
+// Chunked nybble container "DCNK" (SURVEY.md §8(e) "adaptive decode needs independent-chunk
+// framing", §8(f)4): the input is cut into chunks of K bytes and each chunk is stored as the
+// reference's own stream of that chunk (compress_bytestring on the chunk: header, packed
+// nybbles, LITERAL fallback), so every chunk decodes alone with decompress_bytestring.
+// Layout: u32 magic 'DCNK', u32 version 1, u32 modify, u32 K, u64 n, u64 nchunks,
+// u64 off[nchunks + 1] (chunk streams, relative to the payload), payload.
+// One lane walks one chunk (the adaptive lists are sequential within a chunk); the lists
+// live in LDS as u64 words, one column per lane.
+// ------------------------------------------------------------------------------------
+#define NYBK_MAGIC 0x4B4E4344u   // "DCNK"
+#define NYBK_HEAD 32
+
+static __device__ __forceinline__ uint64_t mtf_init_word()
+{
+    return 0x736E696F61746520ull;   // " etaoins", byte k = entry k
+}
+
+__global__ __launch_bounds__(64) void k_nyb_chunk_enc(const uint8_t *__restrict__ in, uint64_t n, uint32_t K,
+                                                      uint64_t nchunks, int modify, uint8_t *__restrict__ scr,
+                                                      uint64_t *__restrict__ lens)
+{
+    __shared__ uint64_t s_L[16][64];
+    const int t = threadIdx.x;
+    const uint64_t ch = (uint64_t)blockIdx.x * 64 + t;
+    if (ch >= nchunks) return;
+    const uint8_t *x = in + ch * K;
+    const uint64_t len = (n - ch * K < K) ? n - ch * K : K;
+    uint8_t *out = scr + ch * ((uint64_t)K + 2);
+    for (int c = 0; c < 16; ++c) s_L[c][t] = mtf_init_word();
+    uint64_t o = 0;
+    out[o++] = 0xAF;
+    uint32_t prev = x[0];
+    out[o++] = (uint8_t)prev;
+    int half = 0;
+    uint32_t hi = 0;   // pending high nybble (with its byte's value, for a later rewrite)
+    for (uint64_t i = 1; i < len; ++i) {
+        const uint32_t v = x[i];
+        const uint32_t c = (prev >> 3) & 15u;
+        uint64_t L = s_L[c][t];
+        uint32_t cnt = 8;
+        const int r = mtf_touch64(L, cnt, v);   // compress_byte_index :833-839 (rank before the touch)
+        if (modify) s_L[c][t] = L;              // update_context :665-687
+        if (r < 0) {
+            if (half) { out[o++] = (uint8_t)prev; half = 0; }   // miss at offset 1 (:855-857)
+            out[o++] = (uint8_t)v;
+        } else if (!half) {
+            hi = (8u | (uint32_t)r) << 4;
+            half = 1;
+        } else {
+            out[o++] = (uint8_t)(hi | 8u | (uint32_t)r);
+            half = 0;
+        }
+        prev = v;
+    }
+    if (half) out[o++] = x[len - 1];   // odd tail (:1000-1009)
+    if (o >= len) {                    // LITERAL fallback (:1018-1037)
+        out[0] = ' ';
+        for (uint64_t i = 0; i < len; ++i) out[1 + i] = x[i];
+        o = len + 1;
+    }
+    lens[ch] = o;
+}
+
+// single workgroup: off[0..nchunks] = exclusive scan of lens (off[nchunks] = total)
+__global__ __launch_bounds__(1024) void k_scan_u64(const uint64_t *__restrict__ lens, uint64_t count,
+                                                   uint64_t *__restrict__ off)
+{
+    __shared__ uint64_t s[1024];
+    const int t = threadIdx.x;
+    const uint64_t per = (count + 1023) / 1024;
+    const uint64_t a0 = (uint64_t)t * per, a1 = (a0 + per < count) ? a0 + per : count;
+    uint64_t sum = 0;
+    for (uint64_t k = a0; k < a1; ++k) sum += lens[k];
+    s[t] = sum;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {
+        const uint64_t v = t >= d ? s[t - d] : 0;
+        __syncthreads();
+        s[t] += v;
+        __syncthreads();
+    }
+    uint64_t o = t ? s[t - 1] : 0;
+    for (uint64_t k = a0; k < a1; ++k) { off[k] = o; o += lens[k]; }
+    if (t == 1023) off[count] = s[1023];
+}
+
+// one workgroup per chunk: scratch stream -> payload
+__global__ __launch_bounds__(256) void k_nyb_chunk_copy(const uint8_t *__restrict__ scr, uint32_t K,
+                                                        const uint64_t *__restrict__ off, uint8_t *__restrict__ payload)
+{
+    const uint64_t ch = blockIdx.x;
+    const uint8_t *src = scr + ch * ((uint64_t)K + 2);
+    const uint64_t a = off[ch], len = off[ch + 1] - a;
+    for (uint64_t i = threadIdx.x; i < len; i += 256) payload[a + i] = src[i];
+}
+
+// one lane per chunk: decompress_bytestring (nybble_compression.c:734-817) of the chunk's
+// stream into out + ch*K; a stream that is not a nybble/LITERAL stream of exactly the chunk's
+// length sets *err (bytes >= 0x80 do not round-trip through the reference codec, P8)
+__global__ __launch_bounds__(64) void k_nyb_chunk_dec(const uint8_t *__restrict__ payload,
+                                                      const uint64_t *__restrict__ off, uint64_t total, uint64_t n,
+                                                      uint32_t K, uint64_t nchunks, int modify,
+                                                      uint8_t *__restrict__ out, uint64_t *__restrict__ err)
+{
+    __shared__ uint64_t s_L[16][64];
+    const int t = threadIdx.x;
+    const uint64_t ch = (uint64_t)blockIdx.x * 64 + t;
+    if (ch >= nchunks) return;
+    const uint64_t a = off[ch], b = off[ch + 1];
+    const uint64_t expect = (n - ch * K < K) ? n - ch * K : K;
+    uint8_t *o = out + ch * K;
+    if (b < a || b > total || b - a < 1) { *err = 1; return; }
+    const uint8_t *src = payload + a;
+    const uint64_t m = b - a;
+    const uint32_t type = src[0];
+    if (type == ' ') {
+        if (m - 1 != expect) { *err = 1; return; }
+        for (uint64_t i = 1; i < m; ++i) o[i - 1] = src[i];
+        return;
+    }
+    if (type != 0xAF || m < 2) { *err = 1; return; }
+    for (int c = 0; c < 16; ++c) s_L[c][t] = mtf_init_word();
+    uint32_t prev = src[1];
+    o[0] = (uint8_t)prev;
+    uint64_t q = 1, pos = 2;
+    int offn = 0;
+    while (pos < m) {
+        const uint32_t bb = src[pos];
+        uint32_t nyb, nxt;
+        if (offn == 0) { nyb = bb >> 4; nxt = bb & 15; }
+        else { nyb = bb & 15; nxt = (pos + 1 < m) ? (uint32_t)(src[pos + 1] >> 4) : 0u; }
+        const uint32_t c = (prev >> 3) & 15u;
+        uint64_t L = s_L[c][t];
+        uint32_t v;
+        int used;
+        if (nyb & 8) { v = (uint32_t)(L >> (8 * (nyb & 7))) & 255u; used = 1; }
+        else { v = ((nyb & 7) << 4) + nxt; used = 2; }
+        if (modify) { uint32_t cnt = 8; (void)mtf_touch64(L, cnt, v); s_L[c][t] = L; }
+        if (q >= expect) { *err = 1; return; }
+        o[q++] = (uint8_t)v;
+        prev = v;
+        offn += used;
+        if (offn >= 2) { ++pos; offn -= 2; }
+    }
+    if (q != expect) *err = 1;
+}
+
 // =====================================================================================
 // host side
 // =====================================================================================
@@ -2754,6 +2902,8 @@ struct dc_ctx {
     MtfSum *d_mtf;          size_t mtf_cap;       // adaptive nybble: tile summaries + entries, all levels
     uint8_t *d_rk;          size_t rk_cap;        // adaptive nybble: rank per element
     const uint8_t *rk_in; uint64_t rk_len;        // identity of the input the ranks belong to
+    uint8_t *d_kscr;        size_t kscr_cap;      // chunked nybble: per-chunk streams before packing
+    uint64_t *d_klens;      size_t klens_cap;     // chunked nybble: stream length per chunk
     uint64_t *h_pinned;                           // pinned host scalars
     const uint8_t *hist_in; uint64_t hist_n;      // identity of the last dc_huff_hist input
     bool plan_ok;
@@ -2870,6 +3020,8 @@ void dc_ctx_destroy(dc_ctx *c)
     if (c->d_entry) (void)hipFree(c->d_entry);
     if (c->d_mtf) (void)hipFree(c->d_mtf);
     if (c->d_rk) (void)hipFree(c->d_rk);
+    if (c->d_kscr) (void)hipFree(c->d_kscr);
+    if (c->d_klens) (void)hipFree(c->d_klens);
     if (c->h_pinned) (void)hipHostFree(c->h_pinned);
     if (c->events_made)
         for (int i = 0; i < DC_MAX_EVENTS; ++i) { (void)hipEventDestroy(c->ev0[i]); (void)hipEventDestroy(c->ev1[i]); }
@@ -3375,6 +3527,84 @@ int dc_nyb_compress(dc_ctx *c, const uint8_t *d_in, uint64_t n, int modify, uint
     if (r) return r;
     return fsm_run<M_NYB_ENC>(c, d_in, n, n - 1, d_out, h_len, "nyb_enca_tiles",
                               FsmAux{n > 1 ? c->d_rk : nullptr, 0, 0, 1, 1});
+}
+
+// ---- chunked nybble container (DCNK) ---------------------------------------------------
+uint64_t dc_nyb_chunked_bound(uint64_t n, uint32_t K)
+{
+    const uint64_t nch = (n && K) ? (n + K - 1) / K : 0;
+    return NYBK_HEAD + 8 * (nch + 1) + n + 2 * nch;
+}
+
+int dc_nyb_compress_chunked(dc_ctx *c, const uint8_t *d_in, uint64_t n, int modify, uint32_t K, uint8_t *d_out,
+                            uint64_t out_cap, uint64_t *h_len)
+{
+    if (!c || !d_out || !h_len || (n && !d_in) || K < 16 || ((uintptr_t)d_out & 7)) return DC_E_ARG;
+    const uint64_t nch = n ? (n + K - 1) / K : 0;
+    const uint64_t head = NYBK_HEAD + 8 * (nch + 1);
+    if (out_cap < head) return DC_E_CAPACITY;
+    uint32_t *h = (uint32_t *)c->h_pinned;
+    h[0] = NYBK_MAGIC; h[1] = 1; h[2] = modify ? 1 : 0; h[3] = K;
+    c->h_pinned[2] = n; c->h_pinned[3] = nch;
+    HIPCHK(hipMemcpyAsync(d_out, c->h_pinned, NYBK_HEAD, hipMemcpyHostToDevice, c->stream));
+    uint64_t *off = (uint64_t *)(d_out + NYBK_HEAD);
+    if (nch == 0) {
+        HIPCHK(hipMemsetAsync(off, 0, 8, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        *h_len = head;
+        return DC_OK;
+    }
+    if (ensure((void **)&c->d_kscr, &c->kscr_cap, nch * ((uint64_t)K + 2))) return DC_E_HIP;
+    if (ensure((void **)&c->d_klens, &c->klens_cap, nch * sizeof(uint64_t))) return DC_E_HIP;
+    LAUNCH(c, "nyb_chunk_enc", k_nyb_chunk_enc, (nch + 63) / 64, 64, d_in, n, K, nch, modify ? 1 : 0, c->d_kscr,
+           c->d_klens);
+    LAUNCH(c, "nyb_chunk_scan", k_scan_u64, 1, 1024, (const uint64_t *)c->d_klens, nch, off);
+    HIPCHK(hipMemcpyAsync(c->h_pinned, off + nch, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    const uint64_t total = c->h_pinned[0];
+    if (out_cap < head + total) return DC_E_CAPACITY;
+    LAUNCH(c, "nyb_chunk_copy", k_nyb_chunk_copy, nch, 256, (const uint8_t *)c->d_kscr, K, (const uint64_t *)off,
+           d_out + head);
+    HIPCHK(hipStreamSynchronize(c->stream));
+    *h_len = head + total;
+    return DC_OK;
+}
+
+int dc_nyb_chunked_info(dc_ctx *c, const uint8_t *d_in, uint64_t m, uint64_t *h_n, int *h_modify, uint32_t *h_K)
+{
+    if (!c || !d_in || m < NYBK_HEAD) return DC_E_ARG;
+    HIPCHK(hipMemcpyAsync(c->h_pinned, d_in, NYBK_HEAD, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    const uint32_t *h = (const uint32_t *)c->h_pinned;
+    if (h[0] != NYBK_MAGIC || h[1] != 1 || h[3] < 16) return DC_E_STREAM;
+    if (h_n) *h_n = c->h_pinned[2];
+    if (h_modify) *h_modify = (int)h[2];
+    if (h_K) *h_K = h[3];
+    return DC_OK;
+}
+
+int dc_nyb_decompress_chunked(dc_ctx *c, const uint8_t *d_in, uint64_t m, uint8_t *d_out, uint64_t out_cap,
+                              uint64_t *h_len)
+{
+    if (!c || !d_out || !h_len || !d_in || ((uintptr_t)d_in & 7)) return DC_E_ARG;
+    uint64_t n = 0;
+    int modify = 0;
+    uint32_t K = 0;
+    int r = dc_nyb_chunked_info(c, d_in, m, &n, &modify, &K);
+    if (r) return r;
+    const uint64_t nch = c->h_pinned[3];
+    if (nch != (n ? (n + K - 1) / K : 0) || m < NYBK_HEAD + 8 * (nch + 1)) return DC_E_STREAM;
+    if (out_cap < n) return DC_E_CAPACITY;
+    *h_len = n;
+    if (nch == 0) return DC_OK;
+    const uint64_t head = NYBK_HEAD + 8 * (nch + 1);
+    uint64_t *err = c->d_meta + 8;
+    HIPCHK(hipMemsetAsync(err, 0, 8, c->stream));
+    LAUNCH(c, "nyb_chunk_dec", k_nyb_chunk_dec, (nch + 63) / 64, 64, d_in + head,
+           (const uint64_t *)(d_in + NYBK_HEAD), m - head, n, K, nch, modify, d_out, err);
+    HIPCHK(hipMemcpyAsync(c->h_pinned, err, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return c->h_pinned[0] ? DC_E_STREAM : DC_OK;
 }
 
 // ---- nybble shard bodies (dist.ShardedNybble) ---------------------------

@@ -206,6 +206,25 @@ class Codec:
                                                             _ptr(out), C.byref(n)))
         return out[: n.value]
 
+    def nyb_compress_chunked(self, x, modify: bool, chunk: int = 1 << 16):
+        """DCNK container: chunks of `chunk` bytes, each the reference stream of that chunk."""
+        cap = int(self.L.dc_nyb_chunked_bound(x.numel(), chunk))
+        out = self._t(cap)
+        n = C.c_uint64(0)
+        check("dc_nyb_compress_chunked", self.L.dc_nyb_compress_chunked(self.ctx, _ptr(x), x.numel(), int(modify),
+                                                                        chunk, _ptr(out), cap, C.byref(n)))
+        return out[: n.value]
+
+    def nyb_decompress_chunked(self, comp):
+        n, mod, K = C.c_uint64(0), C.c_int32(0), C.c_uint32(0)
+        check("dc_nyb_chunked_info", self.L.dc_nyb_chunked_info(self.ctx, _ptr(comp), comp.numel(), C.byref(n),
+                                                                C.byref(mod), C.byref(K)))
+        out = self._t(max(n.value, 1))
+        got = C.c_uint64(0)
+        check("dc_nyb_decompress_chunked", self.L.dc_nyb_decompress_chunked(self.ctx, _ptr(comp), comp.numel(),
+                                                                            _ptr(out), n.value, C.byref(got)))
+        return out[: got.value]
+
     def nyb_mtf_summary(self, y):
         """Move-to-front lists after elements y[1..] from empty lists: (lists[16][8], cnt[16])."""
         lists = np.zeros(128, np.uint8)

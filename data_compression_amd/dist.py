@@ -378,3 +378,32 @@ class ShardedNybble:
         out = self.e.nyb_decompress(whole, modify)
         a = sum(sizes[: self.rank])
         return out[a: a + sizes[self.rank]]
+
+    # ---- independent-chunk framing (DCNK): the adaptive decode that shards -------------------
+    def compress_chunked(self, x, modify: bool, chunk: int = 1 << 16):
+        """This rank's DCNK container (no exchange: chunks are independent). With every shard
+        but the last a multiple of `chunk` bytes, merge_chunked of the ranks' containers is
+        byte-identical to the single-GPU container of the whole input."""
+        return self.e.nyb_compress_chunked(x, modify, chunk)
+
+    def decompress_chunked(self, comp):
+        return self.e.nyb_decompress_chunked(comp)
+
+
+def merge_chunked(containers):
+    """Concatenate per-rank DCNK containers (host bytes, in rank order) into one."""
+    import struct
+    heads = [struct.unpack_from("<IIIIQQ", c) for c in containers]
+    magic, ver, mod, K = heads[0][:4]
+    offs, pays, base = [], [], 0
+    for c, h in zip(containers, heads):
+        assert h[:4] == (magic, ver, mod, K), "containers differ in format"
+        nch = h[5]
+        o = np.frombuffer(c, np.uint64, nch + 1, 32)
+        offs.append(o[:-1] + np.uint64(base))
+        pays.append(c[32 + 8 * (nch + 1): 32 + 8 * (nch + 1) + int(o[-1])])
+        base += int(o[-1])
+    n = sum(h[4] for h in heads)
+    nch = sum(h[5] for h in heads)
+    head = struct.pack("<IIIIQQ", magic, ver, mod, K, n, nch)
+    return head + np.concatenate(offs + [np.array([base], np.uint64)]).astype(np.uint64).tobytes() + b"".join(pays)

@@ -186,6 +186,19 @@ int dc_nyb_compress(dc_ctx *ctx, const uint8_t *d_in, uint64_t n, int modify, ui
 /* Decode m compressed bytes; d_out capacity >= 2*m. *h_out_len as above. */
 int dc_nyb_decompress(dc_ctx *ctx, const uint8_t *d_in, uint64_t m, int modify, uint8_t *d_out,
                       uint64_t *h_out_len);
+/* Chunked container "DCNK" (build-defined; SURVEY §8(e)/(f)4: adaptive streams decode in
+ * parallel only with independent chunks). Chunk k = bytes [kK, kK+K) stored as the
+ * reference's own stream of that chunk (compress_bytestring on it), so each chunk decodes
+ * alone. Layout: u32 'DCNK', u32 version 1, u32 modify, u32 K, u64 n, u64 nchunks,
+ * u64 off[nchunks+1] (relative to the payload), payload. K >= 16; d_out / d_in 8-B aligned.
+ * Decode returns DC_E_STREAM when a chunk does not decode to exactly its length (a corrupt
+ * container, or input bytes >= 0x80, which the reference codec does not round-trip). */
+uint64_t dc_nyb_chunked_bound(uint64_t n, uint32_t K);
+int dc_nyb_compress_chunked(dc_ctx *ctx, const uint8_t *d_in, uint64_t n, int modify, uint32_t K, uint8_t *d_out,
+                            uint64_t out_cap, uint64_t *h_out_len);
+int dc_nyb_chunked_info(dc_ctx *ctx, const uint8_t *d_in, uint64_t m, uint64_t *h_n, int *h_modify, uint32_t *h_K);
+int dc_nyb_decompress_chunked(dc_ctx *ctx, const uint8_t *d_in, uint64_t m, uint8_t *d_out, uint64_t out_cap,
+                              uint64_t *h_out_len);
 /* Shard bodies (data_compression_amd/dist.py ShardedNybble). A shard buffer is
  * d_in[0 .. len): d_in[0] is the context byte (the stream's first byte on the first shard, the
  * previous shard's last byte after it) and the shard's elements are bytes 1 .. len-1, as in

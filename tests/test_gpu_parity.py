@@ -589,3 +589,43 @@ def test_sharded_nybble_on_device(torch_cuda, world, modify):
     assert b"".join(r[0] for r in res) == ref
     if not modify:
         assert np.array_equal(np.concatenate([r[2] for r in res]), x)
+
+
+@pytest.mark.parametrize("modify", [True, False])
+def test_nybble_chunked_container(torch_cuda, codec, modify):
+    """DCNK: every chunk is the reference's stream of that chunk (so it decodes alone), the
+    container decodes chunk-parallel back to the input, and damage is reported."""
+    import struct
+
+    from data_compression_amd import synth
+    from data_compression_amd._lib import DcError
+    torch = torch_cuda
+    for n, K in ((0, 64), (1, 16), (17, 16), (5000, 4096), (300_007, 4096), (3 << 20, 1 << 16)):
+        x = synth.english_like(n, seed=n + 1) if n else np.zeros(0, np.uint8)
+        xt = torch.from_numpy(x).cuda() if n else torch.zeros(0, dtype=torch.uint8, device="cuda")
+        comp = codec.nyb_compress_chunked(xt, modify, K)
+        c = comp.cpu().numpy().tobytes()
+        magic, ver, mod, k, nn, nch = struct.unpack_from("<IIIIQQ", c)
+        assert (magic, ver, mod, k, nn) == (0x4B4E4344, 1, int(modify), K, n)
+        assert nch == (n + K - 1) // K
+        off = np.frombuffer(c, np.uint64, nch + 1, 32)
+        pay = c[32 + 8 * (nch + 1):]
+        assert len(pay) == int(off[-1])
+        for i in range(0, nch, max(1, nch // 7)):
+            chunk = x[i * K: (i + 1) * K].tobytes()
+            assert pay[int(off[i]): int(off[i + 1])] == orc.nybble_compress(chunk, modify), (n, K, i)
+        if n:
+            back = codec.nyb_decompress_chunked(comp)
+            assert np.array_equal(back.cpu().numpy(), x), (n, K)
+    bad = comp.clone()
+    bad[32 + 8] = bad[32 + 8] + 1   # chunk 1 starts one byte late
+    with pytest.raises(DcError):
+        codec.nyb_decompress_chunked(bad)
+    # shards that are multiples of K: the merged per-shard containers equal the whole one
+    from data_compression_amd.dist import merge_chunked
+    x = synth.log_like(5 * 65536 + 999, seed=3)
+    parts = [x[:2 * 65536], x[2 * 65536: 4 * 65536], x[4 * 65536:]]
+    per = [codec.nyb_compress_chunked(torch.from_numpy(p.copy()).cuda(), modify, 65536).cpu().numpy().tobytes()
+           for p in parts]
+    whole = codec.nyb_compress_chunked(torch.from_numpy(x).cuda(), modify, 65536).cpu().numpy().tobytes()
+    assert merge_chunked(per) == whole
