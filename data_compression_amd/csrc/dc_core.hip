@@ -60,7 +60,8 @@ static __device__ __forceinline__ uint32_t wg_scan_excl_u32(uint32_t v, uint32_t
 // index so it is conflict free as well.
 // ------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_hist_blocks(const uint8_t *__restrict__ in, uint64_t n,
-                                                     uint64_t nblocks, uint16_t *__restrict__ bh)
+                                                     uint64_t nblocks, uint16_t *__restrict__ bh,
+                                                     uint32_t *__restrict__ partial)
 {
     __shared__ __attribute__((aligned(16))) uint32_t cnt[256 * 64];
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -69,16 +70,30 @@ __global__ __launch_bounds__(256) void k_hist_blocks(const uint8_t *__restrict__
     char *const cbase = reinterpret_cast<char *>(cnt);
     for (int i = t; i < 256 * 16; i += 256) reinterpret_cast<uint4 *>(cnt)[i] = make_uint4(0u, 0u, 0u, 0u);
     __syncthreads();
-    for (uint64_t b = blockIdx.x; b < nblocks; b += gridDim.x) {
-        const uint64_t base = b * (uint64_t)DC_BLOCK_BYTES;
-        if (base + DC_BLOCK_BYTES <= n) {
-            const uint4 *p = reinterpret_cast<const uint4 *>(in + base) + t;
-            uint4 v[8];
+    const uint64_t nfull = n / DC_BLOCK_BYTES;   // blocks read as 8 x 16 B per thread
+    uint32_t total = 0;                           // bin t over this workgroup's blocks
+    // software pipeline: the next full block's 8 loads are in flight while this block counts
+    uint4 v[8];
+    uint64_t b = blockIdx.x;
+    if (b < nfull) {
+        const uint4 *p = reinterpret_cast<const uint4 *>(in + b * (uint64_t)DC_BLOCK_BYTES) + t;
 #pragma unroll
-            for (int k = 0; k < 8; ++k) v[k] = p[k * 256];
+        for (int k = 0; k < 8; ++k) v[k] = p[k * 256];
+    }
+    for (; b < nblocks; b += gridDim.x) {
+        if (b < nfull) {
+            uint4 cur[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) cur[k] = v[k];
+            const uint64_t nb = b + gridDim.x;
+            if (nb < nfull) {
+                const uint4 *p = reinterpret_cast<const uint4 *>(in + nb * (uint64_t)DC_BLOCK_BYTES) + t;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) v[k] = p[k * 256];
+            }
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
-                const uint32_t w4[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+                const uint32_t w4[4] = {cur[k].x, cur[k].y, cur[k].z, cur[k].w};
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
 #pragma unroll
@@ -91,8 +106,8 @@ __global__ __launch_bounds__(256) void k_hist_blocks(const uint8_t *__restrict__
                 }
             }
         } else {
-            const uint64_t end = n;
-            for (uint64_t i = base + t; i < end; i += 256) atomicAdd(&cnt[in[i] * 64 + lane], inc);
+            const uint64_t base = b * (uint64_t)DC_BLOCK_BYTES;
+            for (uint64_t i = base + t; i < n; i += 256) atomicAdd(&cnt[in[i] * 64 + lane], inc);
         }
         __syncthreads();
         // bin t: its 64 lane columns (16-B reads, rotated so a wave's reads spread over all
@@ -110,28 +125,30 @@ __global__ __launch_bounds__(256) void k_hist_blocks(const uint8_t *__restrict__
             acc = __builtin_amdgcn_udot4(d.w, 0x01010101u, acc, false);
         }
         bh[b * 256 + t] = (uint16_t)acc;
+        total += acc;
         __syncthreads();
     }
+    partial[blockIdx.x * 256 + t] = total;
 }
 
-// sum of the block histograms: each workgroup sums a range of blocks per bin and adds
-// it into hist[256] (zeroed by the host launcher) with one u64 atomic per bin
-__global__ __launch_bounds__(256) void k_hist_reduce(const uint16_t *__restrict__ bh, uint64_t nblocks,
+// hist[256] (zeroed by the host launcher) += the workgroup partials of k_hist_blocks: each
+// workgroup sums a range of partial rows per bin, then one u64 atomic per bin
+__global__ __launch_bounds__(256) void k_hist_reduce(const uint32_t *__restrict__ partial, uint64_t rows,
                                                      uint64_t *__restrict__ hist)
 {
     const int t = threadIdx.x;
-    const uint64_t per = (nblocks + gridDim.x - 1) / gridDim.x;
-    const uint64_t b0 = (uint64_t)blockIdx.x * per;
-    const uint64_t b1 = (b0 + per < nblocks) ? b0 + per : nblocks;
+    const uint64_t per = (rows + gridDim.x - 1) / gridDim.x;
+    const uint64_t r0 = (uint64_t)blockIdx.x * per;
+    const uint64_t r1 = (r0 + per < rows) ? r0 + per : rows;
     uint64_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
-    uint64_t b = b0;
-    for (; b + 4 <= b1; b += 4) {
-        a0 += bh[(b + 0) * 256 + t];
-        a1 += bh[(b + 1) * 256 + t];
-        a2 += bh[(b + 2) * 256 + t];
-        a3 += bh[(b + 3) * 256 + t];
+    uint64_t r = r0;
+    for (; r + 4 <= r1; r += 4) {
+        a0 += partial[(r + 0) * 256 + t];
+        a1 += partial[(r + 1) * 256 + t];
+        a2 += partial[(r + 2) * 256 + t];
+        a3 += partial[(r + 3) * 256 + t];
     }
-    for (; b < b1; ++b) a0 += bh[b * 256 + t];
+    for (; r < r1; ++r) a0 += partial[r * 256 + t];
     const uint64_t sum = a0 + a1 + a2 + a3;
     if (sum) atomicAdd((unsigned long long *)&hist[t], (unsigned long long)sum);
 }
@@ -1908,6 +1925,19 @@ __global__ __launch_bounds__(D8F_WAVES * 64) void k_huff_decode8_fix(const uint3
     D8_STAMP(f0);
     unsigned long long f_dec = 0, f_rounds = 0, f_wait = 0, f_first = 0;
 #endif
+    // rounds of 64 list items: wave wid takes rounds wid, wid + P, ...; the first two rounds'
+    // chunks and positions are requested before the table copy, so their latency overlaps it
+    // written by k_huff_fix_list (an earlier launch): a plain scalar load
+    const uint32_t total = ((const __attribute__((address_space(4))) uint32_t *)queue)[D8_FIX_CNT];
+    const uint32_t nrounds = (total + 63) / 64;
+    const uint32_t wstride = gridDim.x * D8F_WAVES;
+    uint32_t ra = blockIdx.x * D8F_WAVES + wv;   // round of A; B and C follow by the stride
+    auto item_ok = [&](uint32_t r) -> bool { return r < nrounds && r * 64 + (uint32_t)lane < total; };
+    auto chunk_of = [&](uint32_t r) -> uint32_t { return item_ok(r) ? list[r * 64 + lane] : ~0u; };
+    uint32_t cha = chunk_of(ra);
+    uint32_t chb = chunk_of(ra + wstride);
+    uint64_t posa = fix_pos[cha != ~0u ? cha : 0u];
+    uint64_t posb = fix_pos[chb != ~0u ? chb : 0u];
     const uint32_t K2 = (uint32_t)T->dlut2_k, kmask = (1u << K2) - 1;
     for (int i = t; i < (1 << D8_LUT_BITS) / 8; i += D8F_WAVES * 64)
         reinterpret_cast<uint4 *>(F.lut)[i] = reinterpret_cast<const uint4 *>(T->dlut14)[i];
@@ -1923,22 +1953,12 @@ __global__ __launch_bounds__(D8F_WAVES * 64) void k_huff_decode8_fix(const uint3
     __syncthreads();
     const int nary = T->n_ary, w = T->w;
     const bool pow2 = (nary & (nary - 1)) == 0;
-    // rounds of 64 list items: wave wid takes rounds wid, wid + P, ...
-    // written by k_huff_fix_list (an earlier launch): a plain scalar load
-    const uint32_t total = ((const __attribute__((address_space(4))) uint32_t *)queue)[D8_FIX_CNT];
-    const uint32_t nrounds = (total + 63) / 64;
-    const uint32_t wstride = gridDim.x * D8F_WAVES;
     uint32_t *row = F.rows[wv] + lane * (D8F_ROW + 1);
     int bad = 0;
 
 #ifdef DC_DIAG
     D8_STAMP(f1);
 #endif
-    uint32_t ra = blockIdx.x * D8F_WAVES + wv;   // round of A; B and C follow by the stride
-    auto chunk_of = [&](uint32_t r) -> uint32_t {
-        const uint32_t item = r * 64 + (uint32_t)lane;
-        return (r < nrounds && item < total) ? list[item] : ~0u;
-    };
     // a span's 16-B aligned first word (clamped so that a whole row can be read)
     auto row_base = [&](uint64_t pos) -> uint64_t {
         const uint64_t lim = nwords > D8F_ROW ? (nwords - D8F_ROW) & ~3ull : 0ull;
@@ -1959,10 +1979,6 @@ __global__ __launch_bounds__(D8F_WAVES * 64) void k_huff_decode8_fix(const uint3
             row[4 * k + 3] = brev8(v[k].w);
         }
     };
-    uint32_t cha = chunk_of(ra);
-    uint64_t posa = fix_pos[cha != ~0u ? cha : 0u];
-    uint32_t chb = chunk_of(ra + wstride);
-    uint64_t posb = fix_pos[chb != ~0u ? chb : 0u];
     uint4 sv[D8F_ROW / 4];
 #ifdef DC_DIAG
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -3100,11 +3116,11 @@ int dc_huff_hist(dc_ctx *c, const uint8_t *d_in, uint64_t n, uint64_t *d_hist)
         HIPCHK(hipMemsetAsync(d_hist, 0, 256 * sizeof(uint64_t), c->stream));
         return DC_OK;
     }
-    const uint64_t grid = nb < 2048 ? nb : 2048;
-    LAUNCH(c, "hist_blocks", k_hist_blocks, grid, 256, d_in, n, nb, c->d_bh);
-    const int G = (int)(nb < 256 ? nb : 256);
+    const uint64_t grid = nb < 512 ? nb : 512;   // 2 resident per CU (64 KiB LDS each); <= 1024 partial rows
+    LAUNCH(c, "hist_blocks", k_hist_blocks, grid, 256, d_in, n, nb, c->d_bh, (uint32_t *)c->d_partials);
+    const int G = (int)(grid < 32 ? grid : 32);
     HIPCHK(hipMemsetAsync(d_hist, 0, 256 * sizeof(uint64_t), c->stream));
-    LAUNCH(c, "hist_reduce", k_hist_reduce, G, 256, (const uint16_t *)c->d_bh, nb, d_hist);
+    LAUNCH(c, "hist_reduce", k_hist_reduce, G, 256, (const uint32_t *)c->d_partials, grid, d_hist);
     return DC_OK;
 }
 
