@@ -803,7 +803,8 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
         const uint64_t blk_first_word = blk_abs >> 5;
         uint64_t tile_abs = blk_abs;
         if (t == 0) s_stage[0] = 0u;
-        // the whole 32 KiB block: 8 independent 16-B loads per lane in flight at once
+        // the whole 32 KiB block: 8 independent 16-B loads per lane in flight at once (loading
+        // the next block ahead in registers measured 8% slower: 147 VGPRs, 3 waves/SIMD)
         uint4 blkv[DC_BLOCK_BYTES / PACK_TILE];
         const bool full = (blk_start + DC_BLOCK_BYTES <= n);
         if (full) {
@@ -877,6 +878,8 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
                 if (Hk[k] <= 64u && Tk[k] - Hk[k] <= 64u) {
 #pragma unroll
                     for (int h = 0; h < 2; ++h) {
+                        // (a packed 32-bit code|length table measured 4% slower: the
+                        // extraction VALU costs more than the uint2 reads' bank conflicts)
                         uint64_t acc = 0;
 #pragma unroll
                         for (int i = 8 * h; i < 8 * h + 8; ++i) {
