@@ -662,8 +662,8 @@ __global__ __launch_bounds__(1024) void k_block_scan(uint64_t *__restrict__ bits
 
 // Plan in two launches (k_block_bits + the single-workgroup k_block_scan read 32768
 // offsets with strided, uncoalesced loads: 40 us on 1 GiB): (1) a workgroup per 64 blocks
-// computes their bit counts and scans them locally; (2) one workgroup scans the workgroup
-// totals and writes every block's absolute offset, coalesced.
+// computes their bit counts and scans them locally; (2) a workgroup per 64 blocks adds the
+// workgroup totals before it and writes its blocks' absolute offsets.
 #define PLAN_WG_BLOCKS 64
 #define PLAN_MAX_WG 16384   /* workgroup bases in LDS (128 KiB): streams up to 32 GiB per call */
 __global__ __launch_bounds__(256) void k_block_local(const uint16_t *__restrict__ bh, uint64_t nblocks,
@@ -677,12 +677,20 @@ __global__ __launch_bounds__(256) void k_block_local(const uint16_t *__restrict_
     __syncthreads();
     const uint64_t b0 = (uint64_t)blockIdx.x * PLAN_WG_BLOCKS;
     int missing = 0;
+    // all 16 of the wave's block-histogram loads in flight at once
+    uint2 hv[PLAN_WG_BLOCKS / 4];
+#pragma unroll
+    for (int k = 0; k < PLAN_WG_BLOCKS / 4; ++k) {
+        const uint64_t b = b0 + wv * (PLAN_WG_BLOCKS / 4) + k;
+        hv[k] = b < nblocks ? *reinterpret_cast<const uint2 *>(bh + b * 256 + lane * 4) : make_uint2(0u, 0u);
+    }
+#pragma unroll
     for (int k = 0; k < PLAN_WG_BLOCKS / 4; ++k) {
         const int j = wv * (PLAN_WG_BLOCKS / 4) + k;
         const uint64_t b = b0 + j;
         uint32_t acc = 0;
         if (b < nblocks) {
-            const uint2 h = *reinterpret_cast<const uint2 *>(bh + b * 256 + lane * 4);
+            const uint2 h = hv[k];
             const uint32_t c[4] = {h.x & 0xFFFFu, h.x >> 16, h.y & 0xFFFFu, h.y >> 16};
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -704,40 +712,46 @@ __global__ __launch_bounds__(256) void k_block_local(const uint16_t *__restrict_
     }
 }
 
-__global__ __launch_bounds__(1024) void k_block_final(const uint32_t *__restrict__ local,
-                                                      const uint32_t *__restrict__ wgtot, uint64_t nblocks,
-                                                      uint32_t nwg, uint64_t *__restrict__ off,
-                                                      uint64_t *__restrict__ d_total)
+// (2), one workgroup per PLAN_WG_BLOCKS blocks: its base = the sum of the workgroup totals
+// before it (every workgroup re-reads the <= PLAN_MAX_WG totals: 2 KiB on 1 GiB), then its
+// blocks' absolute offsets; the last workgroup writes the stream total
+__global__ __launch_bounds__(256) void k_block_final_wide(const uint32_t *__restrict__ local,
+                                                          const uint32_t *__restrict__ wgtot, uint64_t nblocks,
+                                                          uint32_t nwg, uint64_t *__restrict__ off,
+                                                          uint64_t *__restrict__ d_total)
 {
-    __shared__ uint64_t s_base[PLAN_MAX_WG];
-    __shared__ uint64_t s_w[16];
+    __shared__ uint64_t s_w[4];
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-    uint64_t run = 0;
-    for (uint32_t c0 = 0; c0 < nwg; c0 += 1024) {
-        const uint32_t i = c0 + t;
-        const uint64_t v = i < nwg ? wgtot[i] : 0ull;
-        uint64_t incl = v;   // 64-bit wave scan (a small kernel: shuffles are fine)
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint64_t y = __shfl_up(incl, d, 64);
-            if (lane >= d) incl += y;
-        }
-        if (lane == 63) s_w[wv] = incl;
-        __syncthreads();
-        uint64_t before = 0, all = 0;
-        for (int q = 0; q < 16; ++q) {
-            const uint64_t x = s_w[q];
-            before += (q < wv) ? x : 0ull;
-            all += x;
-        }
-        if (i < nwg) s_base[i] = run + before + incl - v;
-        run += all;
-        __syncthreads();
+    const uint32_t g = blockIdx.x;
+    const bool last = g + 1 == nwg;
+    const uint32_t lim = last ? nwg : g;   // the last workgroup sums everything (the total)
+    uint64_t before = 0, all = 0;
+    for (uint32_t i = t; i < lim; i += 256) {
+        const uint64_t v = wgtot[i];
+        all += v;
+        before += i < g ? v : 0ull;
     }
-    for (uint64_t b = t; b < nblocks; b += 1024) off[b] = s_base[b / PLAN_WG_BLOCKS] + local[b];
-    if (t == 0) {
-        off[nblocks] = run;
-        *d_total = run;
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) {
+        before += __shfl_xor(before, d, 64);
+        all += __shfl_xor(all, d, 64);
+    }
+    if (lane == 0) s_w[wv] = before;
+    __syncthreads();
+    const uint64_t base = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+    __syncthreads();
+    if (last) {
+        if (lane == 0) s_w[wv] = all;
+        __syncthreads();
+        if (t == 0) {
+            const uint64_t tot = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+            off[nblocks] = tot;
+            *d_total = tot;
+        }
+    }
+    if (t < PLAN_WG_BLOCKS) {
+        const uint64_t b = (uint64_t)g * PLAN_WG_BLOCKS + t;
+        if (b < nblocks) off[b] = base + local[b];
     }
 }
 
@@ -3179,7 +3193,7 @@ int dc_huff_plan(dc_ctx *c, const dc_dtable *d_table, uint64_t *d_total_bits)
         if (ensure((void **)&c->d_plan, &c->plan_cap, (nb + nwg + 64) * sizeof(uint32_t))) return DC_E_HIP;
         uint32_t *loc = c->d_plan, *tot = c->d_plan + nb + 32;
         LAUNCH(c, "block_bits", k_block_local, nwg, 256, (const uint16_t *)c->d_bh, nb, d_table, loc, tot, c->d_err);
-        LAUNCH(c, "block_scan", k_block_final, 1, 1024, (const uint32_t *)loc, (const uint32_t *)tot, nb,
+        LAUNCH(c, "block_scan", k_block_final_wide, nwg, 256, (const uint32_t *)loc, (const uint32_t *)tot, nb,
                (uint32_t)nwg, c->d_off, d_total_bits);
     } else {
         LAUNCH(c, "block_bits", k_block_bits, (nb + 3) / 4, 256, (const uint16_t *)c->d_bh, nb, d_table, c->d_off,
