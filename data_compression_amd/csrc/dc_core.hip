@@ -255,7 +255,62 @@ __global__ __launch_bounds__(256) void k_huff_table(const uint64_t *__restrict__
             }
         }
         TBL_STAMP(8);
-        if (t == 0) {
+        if (nary <= 32 && t < 64) {
+            // two-queue merge by wave 0 in rounds, no LDS access inside a round: at the start
+            // of a round lanes 0-31 load the next 32 leaf keys and lanes 32-63 the next 32
+            // internal sums; every pick reads both queue heads from that window register
+            // (v_readlane at a uniform index), a new internal node is written back into the
+            // window (one lane's select) so the same round can pick it, and the round's picks get
+            // their parents in one parallel LDS store at its end. A round makes 32/n merges
+            // (<= 32 picks), so the window never runs out. (The one-lane loop this replaces
+            // waited an LDS round trip per pick: 95k of the kernel's 203k cycles.)
+            const int lane = t;
+            const int first_internal = leaves + dummies;
+            const int mpr = 32 / nary;
+            int h1 = 0, h2 = 0, t2 = 0, active = items, next = first_internal;
+            while (active > 1) {
+                const int li0 = h1, qi0 = h2, next0 = next;
+                const int lj = li0 + lane, qj = qi0 + lane - 32;
+                uint64_t win = lane < 32 ? (lj < items ? s_key[lj] : ~0ull) : (qj < t2 ? s_q2[qj] : ~0ull);
+                uint32_t wlo = (uint32_t)win, whi = (uint32_t)(win >> 32);
+                int picked = 0, npick = 0;   // lane p: node index of the round's p-th pick
+                uint32_t slo = 0, shi = 0;    // lane m: the round's m-th sum (stored at its end)
+                int nmerge = 0;
+                // one pick, branch-free (leaf on ties: c1 <= c2, as the reference's stable order)
+                auto pick = [&](uint64_t &sum) {
+                    const int i1 = h1 - li0, i2 = 32 + h2 - qi0;
+                    const uint64_t k1 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)whi, i1) << 32) |
+                                        (uint32_t)__builtin_amdgcn_readlane((int)wlo, i1);
+                    const uint64_t c2 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)whi, i2) << 32) |
+                                        (uint32_t)__builtin_amdgcn_readlane((int)wlo, i2);
+                    const uint64_t c1 = k1 >> 11;
+                    const bool tl = (h1 < items) & ((h2 == t2) | (c1 <= c2));
+                    const int idx = tl ? (int)(k1 & 2047u) : first_internal + h2;
+                    sum += tl ? c1 : c2;
+                    h1 += tl ? 1 : 0;
+                    h2 += tl ? 0 : 1;
+                    picked = lane == npick ? idx : picked;
+                    ++npick;
+                };
+                for (int m = 0; m < mpr && active > 1; ++m) {
+                    uint64_t sum = 0;
+                    if (nary == 2) { pick(sum); pick(sum); }
+                    else for (int q = 0; q < nary; ++q) pick(sum);
+                    if (lane == 32 + t2 - qi0) {   // (t2 - qi0 >= 32: not reachable this round)
+                        wlo = (uint32_t)sum;
+                        whi = (uint32_t)(sum >> 32);
+                    }
+                    if (lane == m) { slo = (uint32_t)sum; shi = (uint32_t)(sum >> 32); }
+                    ++nmerge;
+                    ++t2;
+                    ++next;
+                    active -= nary - 1;
+                }
+                if (lane < nmerge) s_q2[t2 - nmerge + lane] = ((uint64_t)shi << 32) | slo;
+                if (lane < npick && picked < TBL_NODES) s_parent[picked] = (int16_t)(next0 + lane / nary);
+            }
+            if (lane == 0 && next >= TBL_NODES) s_bad = 1;
+        } else if (t == 0) {
             // two-queue merge; both queues' heads and next elements held in registers, the
             // element after them prefetched from LDS when a head is consumed, so no pick
             // waits for an LDS round trip (the internal queue's next element may not exist
