@@ -2362,40 +2362,86 @@ __constant__ uint8_t c_static_rank[256];   // " etaoins" -> 0..7, else 0xFF (ini
 
 static __device__ __forceinline__ bool is_lower(uint32_t b) { return b >= 'a' && b <= 'z'; }
 
-static __device__ __forceinline__ uint32_t nyb_rank(const uint8_t *__restrict__ in, const FsmAux &a, uint64_t j)
+// A lane's 16 elements read their bytes from one window of 20 bytes: window byte r = stream
+// byte g0 - 1 + r, g0 = the byte of the lane's first element (element j <-> byte j + FSM_OFF).
+// Six aligned dword loads (only granules holding a byte of [0, len): no access outside the
+// buffer) and five v_alignbyte replace 16-48 single-byte loads.
+template <int M> struct FsmOff {
+    static constexpr int v = (M == M_NYB_DEC || M == M_SMALL_DEC) ? 2 : (FsmMode<M>::body && !FsmMode<M>::small_enc) ? 0 : 1;
+};
+struct FsmWin {
+    uint32_t w[5];
+    __device__ __forceinline__ uint32_t b(int r) const { return (w[r >> 2] >> (8 * (r & 3))) & 255u; }
+};
+static __device__ __forceinline__ FsmWin fsm_window(const uint8_t *__restrict__ in, uint64_t len, int64_t g0)
 {
-    return a.rk ? (uint32_t)a.rk[j] : (uint32_t)c_static_rank[in[j + 1]];
+    const uintptr_t lo = (uintptr_t)in, hi = (uintptr_t)(in + len);
+    const uintptr_t s = (uintptr_t)(in + g0 - 1);
+    const uintptr_t a = s & ~(uintptr_t)3;
+    const uint32_t m = (uint32_t)(s & 3);
+    uint32_t d[6];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+        const uintptr_t ad = a + 4 * q;
+        d[q] = (ad + 4 > lo && ad < hi) ? *reinterpret_cast<const uint32_t *>(ad) : 0u;
+    }
+    FsmWin f;
+#pragma unroll
+    for (int q = 0; q < 5; ++q) f.w[q] = __builtin_amdgcn_alignbyte(d[q + 1], d[q], m);
+    return f;
 }
 
-// element j of mode M: transducer entry
+// element j (lane-local k: window bytes prev = b(k), cur = b(k+1), next = b(k+2)) of mode M
 template <int M>
-static __device__ __forceinline__ Fsm elem_fsm(const uint8_t *__restrict__ in, uint64_t len, uint64_t j,
-                                               const FsmAux &a)
+static __device__ __forceinline__ Fsm elem_fsm(const FsmWin &W, int k, uint64_t len, uint64_t j, uint32_t rk)
 {
     Fsm f;
-    if (M == M_NYB_ENC) {                // byte i = j+1
-        if (nyb_rank(in, a, j) != 0xFF) { f.c0 = 0; f.c1 = 1; f.s0 = 1; f.s1 = 0; }
+    const uint32_t x = W.b(k + 1);
+    if (M == M_NYB_ENC) {                // byte i = j+1; rk = its rank (0xFF = miss)
+        if (rk != 0xFF) { f.c0 = 0; f.c1 = 1; f.s0 = 1; f.s1 = 0; }
         else { f.c0 = 1; f.c1 = 2; f.s0 = 0; f.s1 = 0; }
     } else if (M == M_NYB_DEC || M == M_NYB_DBODY) {   // compressed byte k = j+2 (a body: byte j)
-        const uint32_t b = in[M == M_NYB_DBODY ? j : j + 2];
-        const uint32_t h = b >> 4, l = b & 15;
+        const uint32_t h = x >> 4, l = x & 15;
         if (h & 8) { f.c0 = 2; f.s0 = (l & 8) ? 0 : 1; }
         else { f.c0 = 1; f.s0 = 0; }
         f.c1 = 1;
         f.s1 = (l & 8) ? 0 : 1;
     } else if (FsmMode<M>::small_enc) {   // byte i = j+1
         const uint64_t i = j + 1;
-        const uint32_t x = in[i];
-        const bool second = (M == M_SMALL_BODY1 || i >= 2) && in[i - 1] == ' ' && is_lower(x);
+        const bool second = (M == M_SMALL_BODY1 || i >= 2) && W.b(k) == ' ' && is_lower(x);
         f.c0 = f.c1 = second ? 0 : 1;
         f.s0 = f.s1 = 0;
     } else {                             // small decode, byte k = j+2 (a body: byte j)
-        const uint32_t b = in[M == M_SMALL_DBODY ? j : j + 2];
-        f.c0 = f.c1 = (b >= 0x80) ? 2 : 1;
+        f.c0 = f.c1 = (x >= 0x80) ? 2 : 1;
         f.s0 = f.s1 = 0;
     }
     (void)len;
     return f;
+}
+
+// the lane's 16 ranks (adaptive nybble: aux.rk, element-indexed and 16-B aligned at j0), or
+// the static dictionary's ranks of the window bytes
+template <int M>
+static __device__ __forceinline__ void fsm_ranks(const FsmWin &W, const FsmAux &aux, uint64_t j0, uint64_t nelem,
+                                                 uint32_t (&rk)[16])
+{
+    if (M != M_NYB_ENC) return;
+    if (aux.rk) {
+        uint4 v = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+        if (j0 + 16 <= nelem) v = *reinterpret_cast<const uint4 *>(aux.rk + j0);
+        else for (uint64_t q = 0; j0 + q < nelem; ++q) {
+            const uint32_t r = aux.rk[j0 + q];
+            const uint32_t sh = 8 * (q & 3), msk = ~(255u << sh);
+            if (q < 4) v.x = (v.x & msk) | (r << sh); else if (q < 8) v.y = (v.y & msk) | (r << sh);
+            else if (q < 12) v.z = (v.z & msk) | (r << sh); else v.w = (v.w & msk) | (r << sh);
+        }
+        const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 16; ++k) rk[k] = (w4[k >> 2] >> (8 * (k & 3))) & 255u;
+    } else {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) rk[k] = c_static_rank[W.b(k + 1)];
+    }
 }
 
 template <int M>
@@ -2406,9 +2452,13 @@ __global__ __launch_bounds__(256) void k_fsm_tiles(const uint8_t *__restrict__ i
     const int t = threadIdx.x;
     const uint64_t j0 = (uint64_t)blockIdx.x * FSM_TILE + (uint64_t)t * 16;
     Fsm f = fsm_id();
-    for (int k = 0; k < 16; ++k) {
-        const uint64_t j = j0 + k;
-        if (j < nelem) f = fsm_then(f, elem_fsm<M>(in, len, j, aux));
+    if (j0 < nelem) {
+        const FsmWin W = fsm_window(in, len, (int64_t)j0 + FsmOff<M>::v);
+        uint32_t rk[16];
+        fsm_ranks<M>(W, aux, j0, nelem, rk);
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            if (j0 + k < nelem) f = fsm_then(f, elem_fsm<M>(W, k, len, j0 + k, M == M_NYB_ENC ? rk[k] : 0u));
     }
     s_f[t] = make_uint4(f.c0, f.c1, f.s0, f.s1);
     __syncthreads();
@@ -2429,6 +2479,40 @@ __global__ __launch_bounds__(256) void k_fsm_tiles(const uint8_t *__restrict__ i
     if (t == 0) summ[blockIdx.x] = s_f[0];
 }
 
+// Scan of the tile summaries in two levels, all accesses coalesced: k_fsm_scan_up turns each
+// group of 1024 tile summaries into local exclusive compositions (in place) and one group
+// summary; k_fsm_scan (below) then scans the group summaries; a tile's entry is its group's
+// entry followed by its local composition (k_fsm_write). (One workgroup walking 262144
+// tile summaries with 4-KiB-strided lanes took 0.6 ms on 1 GiB.)
+#define FSM_GROUP 1024
+__global__ __launch_bounds__(FSM_GROUP) void k_fsm_scan_up(uint4 *__restrict__ summ, uint64_t ntiles,
+                                                           uint4 *__restrict__ gsum)
+{
+    __shared__ uint4 s_f[FSM_GROUP];
+    const int t = threadIdx.x;
+    const uint64_t k = (uint64_t)blockIdx.x * FSM_GROUP + t;
+    const uint4 mine = k < ntiles ? summ[k] : make_uint4(0u, 0u, 0u, 1u);
+    s_f[t] = mine;
+    __syncthreads();
+    for (int d = 1; d < FSM_GROUP; d <<= 1) {
+        uint4 p = make_uint4(0u, 0u, 0u, 1u);
+        const bool has = t >= d;
+        if (has) p = s_f[t - d];
+        const uint4 me = s_f[t];
+        __syncthreads();
+        if (has) {
+            Fsm fa, fb;
+            fa.c0 = p.x; fa.c1 = p.y; fa.s0 = p.z; fa.s1 = p.w;
+            fb.c0 = me.x; fb.c1 = me.y; fb.s0 = me.z; fb.s1 = me.w;
+            const Fsm r = fsm_then(fa, fb);
+            s_f[t] = make_uint4(r.c0, r.c1, r.s0, r.s1);
+        }
+        __syncthreads();
+    }
+    if (k < ntiles) summ[k] = t ? s_f[t - 1] : make_uint4(0u, 0u, 0u, 1u);
+    if (t == FSM_GROUP - 1) gsum[blockIdx.x] = s_f[FSM_GROUP - 1];
+}
+
 // single workgroup: tile entry (offset, state) from the summaries, starting in state s_init;
 // meta[0] = total count, meta[1] = final state (from s_init); meta[2..5] = the whole
 // composition (c0, c1, s0, s1) for shard plans
@@ -2444,11 +2528,17 @@ __global__ __launch_bounds__(1024) void k_fsm_scan(const uint4 *__restrict__ sum
     const uint64_t a1 = (a0 + per < ntiles) ? a0 + per : ntiles;
     uint64_t c0 = 0, c1 = 0;
     uint32_t s0 = 0, s1 = 1;
-    for (uint64_t k = a0; k < a1; ++k) {
-        const uint4 b = summ[k];
-        const uint64_t n0 = c0 + (s0 ? b.y : b.x), n1 = c1 + (s1 ? b.y : b.x);
-        const uint32_t m0 = s0 ? b.w : b.z, m1 = s1 ? b.w : b.z;
-        c0 = n0; c1 = n1; s0 = m0; s1 = m1;
+    for (uint64_t k0 = a0; k0 < a1; k0 += 8) {   // 8 summaries in flight per lane
+        uint4 bb[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) bb[q] = k0 + q < a1 ? summ[k0 + q] : make_uint4(0u, 0u, 0u, 1u);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const uint4 b = bb[q];
+            const uint64_t n0 = c0 + (s0 ? b.y : b.x), n1 = c1 + (s1 ? b.y : b.x);
+            const uint32_t m0 = s0 ? b.w : b.z, m1 = s1 ? b.w : b.z;
+            c0 = n0; c1 = n1; s0 = m0; s1 = m1;
+        }
     }
     s_c0[t] = c0; s_c1[t] = c1; s_s0[t] = s0; s_s1[t] = s1;
     __syncthreads();
@@ -2473,11 +2563,17 @@ __global__ __launch_bounds__(1024) void k_fsm_scan(const uint4 *__restrict__ sum
     uint64_t off = 0;
     uint32_t st = s_init;
     if (t > 0) { off = s_init ? s_c1[t - 1] : s_c0[t - 1]; st = s_init ? s_s1[t - 1] : s_s0[t - 1]; }
-    for (uint64_t k = a0; k < a1; ++k) {
-        entry[k] = (off << 1) | st;
-        const uint4 b = summ[k];
-        off += st ? b.y : b.x;
-        st = st ? b.w : b.z;
+    for (uint64_t k0 = a0; k0 < a1; k0 += 8) {
+        uint4 bb[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) bb[q] = k0 + q < a1 ? summ[k0 + q] : make_uint4(0u, 0u, 0u, 1u);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            if (k0 + q < a1) entry[k0 + q] = (off << 1) | st;
+            const uint4 b = bb[q];
+            off += st ? b.y : b.x;
+            st = st ? b.w : b.z;
+        }
     }
     if (t == 1023) {
         meta[0] = s_init ? s_c1[1023] : s_c0[1023];
@@ -2492,11 +2588,16 @@ __global__ __launch_bounds__(1024) void k_fsm_scan(const uint4 *__restrict__ sum
 //           LITERAL (' ' + raw, :1018-1037) when the stream is not shorter than n.
 template <int M>
 __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ in, uint64_t len, uint64_t nelem,
-                                                   const uint64_t *__restrict__ entry,
+                                                   const uint64_t *__restrict__ entry, const uint4 *__restrict__ loc,
                                                    const uint64_t *__restrict__ meta, uint8_t *__restrict__ out,
                                                    FsmAux aux)
 {
+    // the tile's output (<= 2 bytes per element) is staged in LDS, s_out[x] = out[o_al + x]
+    // with o_al the 16-B granule of its first byte, then stored as whole uint4s (bytes only in
+    // the two granules shared with the neighbouring tiles)
     __shared__ uint4 s_f[256];
+    __shared__ __attribute__((aligned(16))) uint8_t s_out[2 * FSM_TILE + 32];
+    __shared__ uint64_t s_end;
     const int t = threadIdx.x;
     const bool nyb_whole = M == M_NYB_ENC && aux.whole;
     const bool enc = FsmMode<M>::enc || nyb_whole;
@@ -2517,10 +2618,15 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
         else { out[0] = in[1]; }
     }
     const uint64_t j0 = (uint64_t)blockIdx.x * FSM_TILE + (uint64_t)t * 16;
+    FsmWin W;
+    uint32_t rk[16];
     Fsm f = fsm_id();
-    for (int k = 0; k < 16; ++k) {
-        const uint64_t j = j0 + k;
-        if (j < nelem) f = fsm_then(f, elem_fsm<M>(in, len, j, aux));
+    if (j0 < nelem) {
+        W = fsm_window(in, len, (int64_t)j0 + FsmOff<M>::v);
+        fsm_ranks<M>(W, aux, j0, nelem, rk);
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            if (j0 + k < nelem) f = fsm_then(f, elem_fsm<M>(W, k, len, j0 + k, M == M_NYB_ENC ? rk[k] : 0u));
     }
     // workgroup exclusive scan of compositions (Hillis-Steele on the 256 thread maps)
     s_f[t] = make_uint4(f.c0, f.c1, f.s0, f.s1);
@@ -2540,67 +2646,100 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
         }
         __syncthreads();
     }
-    const uint64_t e = entry[blockIdx.x];
-    uint64_t o = e >> 1;
-    uint32_t s = (uint32_t)(e & 1);
+    // entry = the group's entry, then the tile's local exclusive composition (k_fsm_scan_up)
+    const uint64_t e = entry[blockIdx.x / FSM_GROUP];
+    const uint4 lc = loc[blockIdx.x];
+    const uint32_t s_g = (uint32_t)(e & 1);
+    const uint64_t o_tile = (e >> 1) + (s_g ? lc.y : lc.x) + (headed ? (enc ? 2 : 1) : 0);   // first output byte
+    const uint32_t s_tile = s_g ? lc.w : lc.z;
+    uint64_t o = o_tile;
+    uint32_t s = s_tile;
     if (t > 0) {
         const uint4 p = s_f[t - 1];
         o += s ? p.y : p.x;
         s = s ? p.w : p.z;
     }
-    o += headed ? (enc ? 2 : 1) : 0;
-    for (int k = 0; k < 16; ++k) {
-        const uint64_t j = j0 + k;
-        if (j >= nelem) break;
-        if (M == M_NYB_ENC) {
-            const uint64_t i = j + 1;
-            const uint32_t x = in[i];
-            const uint32_t r = nyb_rank(in, aux, j);
-            if (r != 0xFF) {
-                if (s == 1) {
-                    const uint32_t rp = j ? nyb_rank(in, aux, j - 1) : aux.pend_rank;
-                    out[o++] = (uint8_t)(((8u | rp) << 4) | (8u | r));
-                    s = 0;
+    if (t == 255) {   // the tile's end: inclusive composition from the entry state
+        const uint4 p = s_f[255];
+        s_end = o_tile + (s_tile ? p.y : p.x);
+    }
+    // granule of the tile's first byte, relative to out (negative when out is unaligned and
+    // the tile starts in out's first granule)
+    const int64_t o_al = (int64_t)((((uintptr_t)(out + o_tile)) & ~(uintptr_t)15) - (uintptr_t)out);
+#define so(o) s_out[(uint32_t)((int64_t)(o) - o_al)]   /* staged out[o] */
+    const uint8_t *tbl = (const uint8_t *)" etaoins";
+    if (j0 < nelem) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const uint64_t j = j0 + k;
+            if (j >= nelem) break;
+            const uint32_t x = W.b(k + 1);
+            if (M == M_NYB_ENC) {
+                const uint64_t i = j + 1;
+                const uint32_t r = rk[k];
+                if (r != 0xFF) {
+                    if (s == 1) {
+                        const uint32_t rp = k ? rk[k - 1] : (j ? (aux.rk ? (uint32_t)aux.rk[j - 1]
+                                                                        : (uint32_t)c_static_rank[W.b(0)])
+                                                               : aux.pend_rank);
+                        so(o++) = (uint8_t)(((8u | rp) << 4) | (8u | r));
+                        s = 0;
+                    } else {
+                        s = 1;
+                        if (aux.is_last && i == len - 1) out[o] = (uint8_t)x;   // odd tail (:1000-1009)
+                    }
                 } else {
-                    s = 1;
-                    if (aux.is_last && i == len - 1) out[o] = (uint8_t)x;   // odd tail (:1000-1009)
-                }
-            } else {
-                if (s == 1) { out[o++] = in[i - 1]; out[o++] = (uint8_t)x; }
-                else out[o++] = (uint8_t)x;
-                s = 0;
-            }
-        } else if (M == M_NYB_DEC || M == M_NYB_DBODY) {
-            const uint64_t kk = M == M_NYB_DBODY ? j : j + 2;
-            const uint32_t b = in[kk];
-            const uint32_t h = b >> 4, l = b & 15;
-            const uint32_t nxt = (kk + 1 < len) ? (uint32_t)(in[kk + 1] >> 4) : 0u;
-            const uint8_t *tbl = (const uint8_t *)" etaoins";
-            if (s == 0) {
-                if (h & 8) {
-                    out[o++] = tbl[h & 7];
-                    if (l & 8) { out[o++] = tbl[l & 7]; s = 0; }
-                    else { out[o++] = (uint8_t)(((l & 7) << 4) + nxt); s = 1; }
-                } else {
-                    out[o++] = (uint8_t)b;
+                    if (s == 1) { so(o++) = (uint8_t)W.b(k); so(o++) = (uint8_t)x; }
+                    else so(o++) = (uint8_t)x;
                     s = 0;
                 }
+            } else if (M == M_NYB_DEC || M == M_NYB_DBODY) {
+                const uint64_t kk = M == M_NYB_DBODY ? j : j + 2;
+                const uint32_t h = x >> 4, l = x & 15;
+                const uint32_t nxt = (kk + 1 < len) ? (W.b(k + 2) >> 4) : 0u;
+                if (s == 0) {
+                    if (h & 8) {
+                        so(o++) = tbl[h & 7];
+                        if (l & 8) { so(o++) = tbl[l & 7]; s = 0; }
+                        else { so(o++) = (uint8_t)(((l & 7) << 4) + nxt); s = 1; }
+                    } else {
+                        so(o++) = (uint8_t)x;
+                        s = 0;
+                    }
+                } else {
+                    if (l & 8) { so(o++) = tbl[l & 7]; s = 0; }
+                    else { so(o++) = (uint8_t)(((l & 7) << 4) + nxt); s = 1; }
+                }
+            } else if (FsmMode<M>::small_enc) {
+                const uint64_t i = j + 1;
+                const bool second = (M == M_SMALL_BODY1 || i >= 2) && W.b(k) == ' ' && is_lower(x);
+                if (!second) {
+                    const uint32_t nx = W.b(k + 2);
+                    if (x == ' ' && i + 1 < len && is_lower(nx)) so(o++) = (uint8_t)(0x80 + nx);
+                    else so(o++) = (uint8_t)x;
+                }
             } else {
-                if (l & 8) { out[o++] = tbl[l & 7]; s = 0; }
-                else { out[o++] = (uint8_t)(((l & 7) << 4) + nxt); s = 1; }
+                if (x >= 0x80) { so(o++) = ' '; so(o++) = (uint8_t)(x - 0x80); }
+                else so(o++) = (uint8_t)x;
             }
-        } else if (FsmMode<M>::small_enc) {
-            const uint64_t i = j + 1;
-            const uint32_t x = in[i];
-            const bool second = (M == M_SMALL_BODY1 || i >= 2) && in[i - 1] == ' ' && is_lower(x);
-            if (!second) {
-                if (x == ' ' && i + 1 < len && is_lower(in[i + 1])) out[o++] = (uint8_t)(0x80 + in[i + 1]);
-                else out[o++] = (uint8_t)x;
+        }
+    }
+    __syncthreads();
+    // store [o_tile, end): whole granules as uint4, the first and last granule bytewise
+#undef so
+    const int64_t end = (int64_t)s_end, beg = (int64_t)o_tile;
+    if (end > beg) {
+        const int64_t ng = (end - o_al + 15) / 16;
+        for (int64_t g = t; g < ng; g += 256) {
+            const int64_t b0 = o_al + 16 * g;
+            if (b0 >= beg && b0 + 16 <= end) {
+                *reinterpret_cast<uint4 *>(out + b0) = *reinterpret_cast<const uint4 *>(s_out + 16 * g);
+            } else {
+                for (int q = 0; q < 16; ++q) {
+                    const int64_t bq = b0 + q;
+                    if (bq >= beg && bq < end) out[bq] = s_out[16 * g + q];
+                }
             }
-        } else {
-            const uint32_t b = in[M == M_SMALL_DBODY ? j : j + 2];
-            if (b >= 0x80) { out[o++] = ' '; out[o++] = (uint8_t)(b - 0x80); }
-            else out[o++] = (uint8_t)b;
         }
     }
 }
@@ -3488,8 +3627,10 @@ static int fsm_run(dc_ctx *c, const uint8_t *d_in, uint64_t len, uint64_t nelem,
 {
     const uint64_t ntiles = (nelem + FSM_TILE - 1) / FSM_TILE;
     const uint64_t nt = ntiles ? ntiles : 1;
-    if (ensure((void **)&c->d_summ, &c->summ_cap, nt * sizeof(uint4))) return DC_E_HIP;
-    if (ensure((void **)&c->d_entry, &c->entry_cap, nt * sizeof(uint64_t))) return DC_E_HIP;
+    const uint64_t ng = (nt + FSM_GROUP - 1) / FSM_GROUP;
+    if (ensure((void **)&c->d_summ, &c->summ_cap, (nt + ng) * sizeof(uint4))) return DC_E_HIP;
+    if (ensure((void **)&c->d_entry, &c->entry_cap, ng * sizeof(uint64_t))) return DC_E_HIP;
+    uint4 *gsum = c->d_summ + nt;
     if (ntiles == 0) {
         // empty: count 0, state unchanged; composition = identity
         c->h_pinned[0] = 0; c->h_pinned[1] = aux.s_init;
@@ -3497,16 +3638,19 @@ static int fsm_run(dc_ctx *c, const uint8_t *d_in, uint64_t len, uint64_t nelem,
         HIPCHK(hipMemcpyAsync(c->d_meta, c->h_pinned, 6 * sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
         c->h_pinned[6] = aux.s_init;
         HIPCHK(hipMemcpyAsync(c->d_entry, c->h_pinned + 6, sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
+        uint32_t *idn = reinterpret_cast<uint32_t *>(c->h_pinned + 8);   // identity local composition
+        idn[0] = 0; idn[1] = 0; idn[2] = 0; idn[3] = 1;
+        HIPCHK(hipMemcpyAsync(c->d_summ, idn, sizeof(uint4), hipMemcpyHostToDevice, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
     } else {
         LAUNCH(c, name, k_fsm_tiles<M>, ntiles, 256, d_in, len, nelem, c->d_summ, aux);
-        LAUNCH(c, "fsm_scan", k_fsm_scan, 1, 1024, (const uint4 *)c->d_summ, ntiles, c->d_entry, c->d_meta,
-               aux.s_init);
+        LAUNCH(c, "fsm_scan_up", k_fsm_scan_up, ng, FSM_GROUP, c->d_summ, ntiles, gsum);
+        LAUNCH(c, "fsm_scan", k_fsm_scan, 1, 1024, (const uint4 *)gsum, ng, c->d_entry, c->d_meta, aux.s_init);
     }
     if (write) {
         const uint64_t wgrid = ntiles ? ntiles : 1;
         LAUNCH(c, "fsm_write", k_fsm_write<M>, wgrid, 256, d_in, len, nelem, (const uint64_t *)c->d_entry,
-               (const uint64_t *)c->d_meta, d_out, aux);
+               (const uint4 *)c->d_summ, (const uint64_t *)c->d_meta, d_out, aux);
     }
     HIPCHK(hipMemcpyAsync(c->h_pinned, c->d_meta, 6 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
