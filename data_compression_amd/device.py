@@ -165,14 +165,18 @@ class Codec:
         return int(v.value)
 
     # ---- small front-end shard bodies (dist.ShardedSmall) --------------------
-    def small_body(self, y, left_halo: bool, nelem: int):
+    def small_body(self, y, left_halo: bool, nelem: int, head: bytes = b""):
         """Front-end body of stream bytes y[1..nelem] (y[0]: left context; y[nelem+1], when
-        present, the right halo) -> uint8 device tensor."""
-        out = self._t(max(nelem, 1))
+        present, the right halo) -> uint8 device tensor, after the bytes `head` (the stream
+        header on rank 0: written in place, no copy of the body)."""
+        h = len(head)
+        out = self._t(max(nelem + h, 1))
+        if h:
+            out[:h] = torch.tensor(list(head), dtype=torch.uint8, device=out.device)
         n = C.c_uint64(0)
         check("dc_small_compress_body", self.L.dc_small_compress_body(self.ctx, _ptr(y), y.numel(), int(left_halo),
-                                                                      nelem, _ptr(out), C.byref(n)))
-        return out[: n.value]
+                                                                      nelem, _ptr(out) + h, C.byref(n)))
+        return out[: h + n.value]
 
     def small_decompress(self, seg):
         """A front-end stream that starts with its type byte (rank 0's segment)."""

@@ -195,15 +195,15 @@ class ShardedSmall:
         # body of stream bytes: rank 0 -> x[1..n-1] (x[0] is the raw first byte); rank r ->
         # all of x (y[0] is the left halo)
         nelem = n - 1 if self.rank == 0 else n
-        body = self.e.small_body(y, self.rank > 0, nelem)
-        lens = self._gather_i64([body.numel()])
+        head = bytes([8, ends[0][0]]) if self.rank == 0 else b""   # type byte, raw first byte
+        body = self.e.small_body(y, self.rank > 0, nelem, head=head)
+        lens = self._gather_i64([body.numel() - len(head)])
         total = 2 + sum(v[0] for v in lens)
         literal = total >= n_total
         if literal:   # ' ' + raw input, as the single-stream encoder falls back
             seg = torch.cat([torch.tensor([ord(" ")], dtype=torch.uint8, device=x.device), x]) if self.rank == 0 else x
         else:
-            seg = torch.cat([torch.tensor([8, int(x[0])], dtype=torch.uint8, device=x.device), body]) \
-                if self.rank == 0 else body
+            seg = body   # rank 0's already starts with the header
         sizes = [v[0] for v in self._gather_i64([seg.numel()])]
         return self._recut(seg, sizes, 64 * sync_syms), literal
 

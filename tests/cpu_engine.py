@@ -63,8 +63,8 @@ class CpuEngine:
         out[:n] = torch.from_numpy(y)
 
     # ---- small front-end shard bodies (dist.ShardedSmall), restated with numpy ------------
-    def small_body(self, y, left_halo, nelem):
-        """small_compression.c:582-665 body of y[1..nelem] (dc_small_compress_body)."""
+    def small_body(self, y, left_halo, nelem, head=b""):
+        """small_compression.c:582-665 body of y[1..nelem] (dc_small_compress_body), after `head`."""
         a = y.numpy()
         i = np.arange(1, nelem + 1)
         low = (a >= ord("a")) & (a <= ord("z"))
@@ -75,7 +75,7 @@ class CpuEngine:
         nxt_low[has] = low[i[has] + 1]
         start = sp[i] & nxt_low
         vals = np.where(start, 0x80 + a[np.minimum(i + 1, a.size - 1)].astype(np.int64), a[i]).astype(np.uint8)
-        return torch.from_numpy(vals[~second].copy())
+        return torch.from_numpy(np.concatenate([np.frombuffer(head, np.uint8), vals[~second]]))
 
     def small_decompress(self, seg):
         return torch.from_numpy(np.frombuffer(orc.small_decompress(seg.numpy().tobytes()), np.uint8).copy())
