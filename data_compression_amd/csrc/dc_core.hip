@@ -944,9 +944,19 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
                 // opaque copy: stops the compiler from keeping pass A's lookup addresses live
                 asm volatile("" : "+v"(w4[0]), "+v"(w4[1]), "+v"(w4[2]), "+v"(w4[3]));
                 const uint32_t rel = (uint32_t)(As - org);
-                if (Hk[k] <= 64u && Tk[k] - Hk[k] <= 64u) {
+                // OR a right-justified run of nb <= 64 bits into the stage at bit pos (<= 3 words)
+                auto emit = [&](uint64_t acc, uint32_t nb, uint32_t pos) {
+                    const uint64_t al = nb ? acc << (64u - nb) : 0ull;
+                    const uint32_t hi = (uint32_t)(al >> 32), lo = (uint32_t)al, r = pos & 31u, wi = pos >> 5;
+                    atomicOr(&s_stage[wi], hi >> r);
+                    if (r + nb > 32u) atomicOr(&s_stage[wi + 1], __builtin_amdgcn_alignbit(hi, lo, r));
+                    if (r + nb > 64u) atomicOr(&s_stage[wi + 2], __builtin_amdgcn_alignbit(lo, 0u, r));
+                };
 #pragma unroll
-                    for (int h = 0; h < 2; ++h) {
+                for (int h = 0; h < 2; ++h) {
+                    const uint32_t Th = h ? Tk[k] - Hk[k] : Hk[k];
+                    const uint32_t pos = h ? rel + Hk[k] : rel;
+                    if (Th <= 64u) {
                         // (a packed 32-bit code|length table measured 4% slower: the
                         // extraction VALU costs more than the uint2 reads' bank conflicts)
                         uint64_t acc = 0;
@@ -955,31 +965,35 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
                             const uint2 e = s_tab[(w4[i >> 2] >> (8 * (i & 3))) & 255u];
                             acc = (acc << e.y) | e.x;
                         }
-                        const uint32_t Th = h ? Tk[k] - Hk[k] : Hk[k];
-                        const uint32_t pos = h ? rel + Hk[k] : rel;
-                        // left-justify, then split over the (up to) 3 stage words it touches
-                        const uint64_t al = Th ? acc << (64u - Th) : 0ull;
-                        const uint32_t hi = (uint32_t)(al >> 32), lo = (uint32_t)al, r = pos & 31u, wi = pos >> 5;
-                        atomicOr(&s_stage[wi], hi >> r);
-                        if (r + Th > 32u) atomicOr(&s_stage[wi + 1], __builtin_amdgcn_alignbit(hi, lo, r));
-                        if (r + Th > 64u) atomicOr(&s_stage[wi + 2], __builtin_amdgcn_alignbit(lo, 0u, r));
-                    }
-                } else {
-                    uint64_t acc = 0;
-                    uint32_t nacc = rel & 31u;
-                    uint32_t wi = rel >> 5;
+                        emit(acc, Th, pos);
+                    } else {
+                        // a half of more than 64 bits (skewed or long codes, e.g. C4's Zipf
+                        // bytes): two quarters of 4 codes, each <= 64 bits unless codes exceed
+                        // 16 bits, then code by code
+                        uint32_t p = pos;
 #pragma unroll 1
-                    for (int i = 0; i < 16; ++i) {
-                        const uint2 e = s_tab[(w4[i >> 2] >> (8 * (i & 3))) & 255u];
-                        acc = (acc << e.y) | e.x;
-                        nacc += e.y;
-                        if (nacc >= 32) {
-                            nacc -= 32;
-                            atomicOr(&s_stage[wi], (uint32_t)(acc >> nacc));
-                            ++wi;
+                        for (int qq = 0; qq < 2; ++qq) {
+                            uint2 e[4];
+                            uint32_t nq = 0;
+#pragma unroll
+                            for (int i = 0; i < 4; ++i) {
+                                const int bi = 8 * h + 4 * qq + i;
+                                const uint32_t wv = qq ? w4[2 * h + 1] : w4[2 * h];
+                                e[i] = s_tab[(wv >> (8 * (bi & 3))) & 255u];
+                                nq += e[i].y;
+                            }
+                            if (nq <= 64u) {
+                                uint64_t acc = 0;
+#pragma unroll
+                                for (int i = 0; i < 4; ++i) acc = (acc << e[i].y) | e[i].x;
+                                emit(acc, nq, p);
+                                p += nq;
+                            } else {
+#pragma unroll
+                                for (int i = 0; i < 4; ++i) { emit(e[i].x, e[i].y, p); p += e[i].y; }
+                            }
                         }
                     }
-                    if (nacc > 0) atomicOr(&s_stage[wi], (uint32_t)(acc << (32 - nacc)));
                 }
                 __builtin_amdgcn_sched_barrier(0);   // keep the pieces' lookups from being hoisted
             }
