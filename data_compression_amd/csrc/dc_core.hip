@@ -72,6 +72,9 @@ __global__ __launch_bounds__(256) void k_hist_blocks(const uint8_t *__restrict__
     __syncthreads();
     const uint64_t nfull = n / DC_BLOCK_BYTES;   // blocks read as 8 x 16 B per thread
     uint32_t total = 0;                           // bin t over this workgroup's blocks
+    uint32_t prevc[64];                           // bin t's 64 counter dwords after the last block
+#pragma unroll
+    for (int q = 0; q < 64; ++q) prevc[q] = 0u;
     // software pipeline: the next full block's 8 loads are in flight while this block counts
     uint4 v[8];
     uint64_t b = blockIdx.x;
@@ -111,18 +114,25 @@ __global__ __launch_bounds__(256) void k_hist_blocks(const uint8_t *__restrict__
         }
         __syncthreads();
         // bin t: its 64 lane columns (16-B reads, rotated so a wave's reads spread over all
-        // banks); v_dot4_u32_u8 with 0x01010101 adds the four wave counters of a dword
-        uint4 *row = reinterpret_cast<uint4 *>(&cnt[t * 64]);
+        // banks). The counters are never cleared: the block's counts are the difference to
+        // the previous values, kept in this thread's registers; v_dot4_u32_u8 with
+        // 0x01010101 adds the four wave fields. (Clearing them cost a 64 KiB LDS write per
+        // 32 KiB block.)
+        const uint4 *row = reinterpret_cast<const uint4 *>(&cnt[t * 64]);
         uint32_t acc = 0;
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
-            const int c = (k + t) & 15;
-            const uint4 d = row[c];
-            row[c] = make_uint4(0u, 0u, 0u, 0u);
-            acc = __builtin_amdgcn_udot4(d.x, 0x01010101u, acc, false);
-            acc = __builtin_amdgcn_udot4(d.y, 0x01010101u, acc, false);
-            acc = __builtin_amdgcn_udot4(d.z, 0x01010101u, acc, false);
-            acc = __builtin_amdgcn_udot4(d.w, 0x01010101u, acc, false);
+            const uint4 d = row[(k + t) & 15];
+            const uint32_t dn[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                // a dword is c0 + 256 c1 + 65536 c2 + 2^24 c3 (mod 2^32) of the four waves'
+                // running counts (field carries included), and each c_f grows by <= 128 per
+                // block, so the plain 32-bit difference holds the block's four counts as bytes
+                const uint32_t x = dn[q], diff = x - prevc[4 * k + q];
+                acc = __builtin_amdgcn_udot4(diff, 0x01010101u, acc, false);
+                prevc[4 * k + q] = x;
+            }
         }
         bh[b * 256 + t] = (uint16_t)acc;
         total += acc;

@@ -689,3 +689,15 @@ def test_sharded_huffman_on_device(torch_cuda, world, n_ary):
     assert enc["bits"] == total
     ref = enc["words"].cpu().numpy().view(np.uint32)[: merged.size]
     assert np.array_equal(merged, ref)
+
+
+def test_histogram_running_counters_skewed(torch_cuda, codec):
+    """k_hist_blocks keeps running 8-bit wave counters across a workgroup's blocks (the
+    block's counts are 32-bit differences): a single repeated byte makes every field wrap
+    and carry many times; ragged tails and every bin value."""
+    torch = torch_cuda
+    for n, fill in ((64 << 20, 0x20), (64 << 20, 0xFF), ((48 << 20) + 12345, 0x00)):
+        x = torch.full((n,), fill, dtype=torch.uint8, device="cuda")
+        x[::4099] = torch.arange(256, device="cuda", dtype=torch.int64).repeat(n // 4099 // 256 + 1)[: x[::4099].numel()].to(torch.uint8)
+        h = codec.hist(x)
+        assert torch.equal(h, torch.bincount(x.to(torch.int64), minlength=256)), (n, fill)
