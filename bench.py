@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--sync", type=int, default=0, help="sync-index granularity (0 = default)")
     ap.add_argument("--cpu-sample", type=int, default=256 << 20)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--table-mode", default="replicate", choices=["replicate", "broadcast"],
+                    help="multi-GPU code table: built on every rank, or on rank 0 and broadcast")
     ap.add_argument("--profile-steps", type=int, default=5)
     return ap.parse_args()
 
@@ -81,7 +83,7 @@ def main():
     ngroups, nchunks = c.sync_sizes(n, S)
 
     from data_compression_amd.dist import ShardedHuffman
-    sh = ShardedHuffman(c)
+    sh = ShardedHuffman(c, table_mode=a.table_mode)
     hist = torch.empty(256, dtype=torch.int64, device=dev)
     tab = torch.empty(c.table_bytes, dtype=torch.uint8, device=dev)
     total = torch.empty(1, dtype=torch.int64, device=dev)

@@ -97,6 +97,10 @@ class Codec:
         check("dc_huff_table", self.L.dc_huff_table(self.ctx, _ptr(hist), max_symbol_value, n_ary, _ptr(out)))
         return out
 
+    def alloc_table(self):
+        """An uninitialised device table (dc_dtable bytes), e.g. a broadcast target."""
+        return self._t(self.table_bytes)
+
     def table_freq(self, freq, n_ary: int, max_symbol_value: int, out=None):
         out = out if out is not None else self._t(self.table_bytes)
         check("dc_huff_table_freq",

@@ -4,7 +4,11 @@ SURVEY.md §8(e): the stream is split into contiguous shards, one per rank. The 
 exchange steps are the ones the single global bitstream needs:
 
   1. local 256-bin histogram  -> all_reduce(SUM)           (2 KiB, RCCL over xGMI)
-  2. every rank builds the same code table from the global histogram (deterministic)
+  2. every rank builds the same code table from the global histogram (deterministic;
+     table_mode="replicate", the default), or rank table_src builds it from a reduce(SUM)
+     of the histograms and broadcasts the table bytes to the others (table_mode="broadcast",
+     the north star's "RCCL broadcast of the shared code table": one 2 KiB reduce and one
+     table-sized broadcast instead of an all_reduce and a table build on every rank)
   3. local payload bit count  -> all_gather                 (8 B per rank)
      rank r's stream starts at bit_base_r = sum of the bit counts of ranks < r
   4. each rank packs its shard at bit_base_r: the shard boundaries fall inside 32-bit
@@ -42,16 +46,31 @@ class ShardStream:
 
 
 class ShardedHuffman:
-    def __init__(self, engine, group=None):
+    def __init__(self, engine, group=None, table_mode: str = "replicate", table_src: int = 0):
+        if table_mode not in ("replicate", "broadcast"):
+            raise ValueError(f"table_mode must be 'replicate' or 'broadcast', not {table_mode!r}")
         self.e = engine
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        if not 0 <= table_src < self.world:
+            raise ValueError(f"table_src {table_src} outside the group of {self.world} ranks")
+        self.table_mode = table_mode
+        self.table_src = table_src
 
     # ---- collectives (no-ops at world size 1) -------------------------------------------
     def _all_reduce(self, t):
         if self.world > 1:
             dist.all_reduce(t, group=self.group)
+
+    def _src_global(self):
+        return self.table_src if self.group is None else dist.get_global_rank(self.group, self.table_src)
+
+    def _reduce_to_src(self, t):
+        dist.reduce(t, dst=self._src_global(), group=self.group)
+
+    def _broadcast_table(self, t):
+        dist.broadcast(t, src=self._src_global(), group=self.group)
 
     def _all_gather_scalar(self, t):
         if self.world == 1:
@@ -65,8 +84,16 @@ class ShardedHuffman:
         """Steps 1-3: global table and this rank's payload bit count (device tensors), and
         the gathered per-rank bit counts (device tensor; None at world size 1)."""
         hist = self.e.hist(x, out=hist) if hist is not None else self.e.hist(x)
-        self._all_reduce(hist)
-        tab = self.e.table(hist, n_ary, out=table) if table is not None else self.e.table(hist, n_ary)
+        if self.table_mode == "broadcast" and self.world > 1:
+            self._reduce_to_src(hist)
+            if self.rank == self.table_src:
+                tab = self.e.table(hist, n_ary, out=table) if table is not None else self.e.table(hist, n_ary)
+            else:
+                tab = table if table is not None else self.e.alloc_table()
+            self._broadcast_table(tab)
+        else:
+            self._all_reduce(hist)
+            tab = self.e.table(hist, n_ary, out=table) if table is not None else self.e.table(hist, n_ary)
         total = self.e.plan(tab, total=total) if total is not None else self.e.plan(tab)
         totals = self._all_gather_scalar(total) if self.world > 1 else None
         return tab, total, totals
@@ -285,11 +312,17 @@ class ShardedNybble:
     every byte before it): decode_replica gathers the stream and decodes it whole.
     """
 
-    def __init__(self, engine, group=None):
+    def __init__(self, engine, group=None, table_mode: str = "replicate", table_src: int = 0):
+        if table_mode not in ("replicate", "broadcast"):
+            raise ValueError(f"table_mode must be 'replicate' or 'broadcast', not {table_mode!r}")
         self.e = engine
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        if not 0 <= table_src < self.world:
+            raise ValueError(f"table_src {table_src} outside the group of {self.world} ranks")
+        self.table_mode = table_mode
+        self.table_src = table_src
 
     def _gather(self, vals, dev):
         if self.world == 1:

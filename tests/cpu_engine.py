@@ -18,15 +18,32 @@ class CpuEngine:
         self._hist_in = x
         return torch.from_numpy(orc.histogram(x.numpy()).astype(np.int64))
 
+    # the table travels as one int64 tensor (dist broadcast): n_ary, lengths[259],
+    # enc_len[259], enc_val[259], code[256], nbits[256]
+    _TAB_LEN = 1 + 3 * 259 + 2 * 256
+
     def table(self, hist, n_ary, out=None):
         h = hist.numpy().astype(np.uint64)
         L = orc.huffman_lengths(h, n_ary)
         el, ev = orc.canonical(L, n_ary)
         code, nb, mx = orc.bitcodes(el, ev, n_ary)
         assert 0 < mx <= 32
-        return {"L": L, "el": el, "ev": ev, "code": code, "nb": nb, "n_ary": n_ary}
+        t = np.concatenate([[n_ary], L, el, ev, code, nb]).astype(np.int64)
+        assert t.size == self._TAB_LEN
+        return torch.from_numpy(t)
+
+    def alloc_table(self):
+        return torch.zeros(self._TAB_LEN, dtype=torch.int64)
+
+    @staticmethod
+    def _tab(t):
+        a = t.numpy()
+        L, el, ev = a[1:260].astype(np.int32), a[260:519].astype(np.int32), a[519:778].astype(np.uint32)
+        return {"n_ary": int(a[0]), "L": L, "el": el, "ev": ev, "code": a[778:1034].astype(np.uint32),
+                "nb": a[1034:1290].astype(np.uint8)}
 
     def plan(self, tab, total=None):
+        tab = self._tab(tab)
         h = orc.histogram(self._hist_in.numpy()).astype(np.int64)
         self._total = int((h * tab["nb"].astype(np.int64)).sum())
         return torch.tensor([self._total], dtype=torch.int64)
@@ -45,6 +62,7 @@ class CpuEngine:
         return torch.zeros(max(n, 1), dtype=torch.uint8)
 
     def pack_async(self, x, tab, bit_base, words, sync, S):
+        tab = self._tab(tab)
         xs = x.numpy()
         payload, bits, idx = orc.huff_pack(xs, tab["code"], tab["nb"], bit_base=bit_base, sync_syms=S)
         w = words.numpy().view(np.uint8)
@@ -56,6 +74,7 @@ class CpuEngine:
         sync[1][: len(lens)] = torch.from_numpy(lens.view(np.int16))
 
     def decode(self, words, bit_base, sync, S, n, tab, out):
+        tab = self._tab(tab)
         bits_all = np.unpackbits(words.numpy().view(np.uint8))
         stream = np.packbits(bits_all[bit_base & 31:])
         total = int(sync[1][: (n + S - 1) // S].numpy().view(np.uint16).astype(np.int64).sum())

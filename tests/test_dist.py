@@ -23,7 +23,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, n_ary, S, shard, total, q):
+def _worker(rank, world, port, n_ary, S, shard, total, q, table_mode="replicate"):
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     from data_compression_amd import synth
@@ -35,7 +35,7 @@ def _worker(rank, world, port, n_ary, S, shard, total, q):
         lo = rank * shard
         hi = total if rank == world - 1 else lo + shard
         xs = torch.from_numpy(x[lo:hi].copy())
-        sh = ShardedHuffman(CpuEngine())
+        sh = ShardedHuffman(CpuEngine(), table_mode=table_mode, table_src=world - 1)
         s = sh.encode(xs, n_ary=n_ary, sync_syms=S)
         y = sh.decode(s)
         ok = bool(torch.equal(y[: xs.numel()], xs))
@@ -48,8 +48,9 @@ def _worker(rank, world, port, n_ary, S, shard, total, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,n_ary", [(2, 2), (3, 16), (2, 3)])
-def test_sharded_stream_is_bit_identical(world, n_ary):
+@pytest.mark.parametrize("world,n_ary,table_mode", [(2, 2, "replicate"), (3, 16, "replicate"), (2, 3, "replicate"),
+                                                    (2, 2, "broadcast"), (3, 16, "broadcast")])
+def test_sharded_stream_is_bit_identical(world, n_ary, table_mode):
     from data_compression_amd import synth
     from oracle import oracle as orc
     S = 64
@@ -58,7 +59,7 @@ def test_sharded_stream_is_bit_identical(world, n_ary):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n_ary, S, shard, total, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_ary, S, shard, total, q, table_mode)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in range(world + 1)]

@@ -631,11 +631,12 @@ def test_nybble_chunked_container(torch_cuda, codec, modify):
     assert merge_chunked(per) == whole
 
 
-@pytest.mark.parametrize("world,n_ary", [(2, 2), (3, 16)])
-def test_sharded_huffman_on_device(torch_cuda, world, n_ary):
+@pytest.mark.parametrize("world,n_ary,table_mode", [(2, 2, "replicate"), (3, 16, "replicate"), (3, 2, "broadcast")])
+def test_sharded_huffman_on_device(torch_cuda, world, n_ary, table_mode):
     """dist.ShardedHuffman on the device engine (thread ranks, collectives by a barrier):
     each rank packs at its global bit offset; the OR-merged shards equal the single-GPU
-    stream of the whole input bit for bit, and every rank decodes its own shard."""
+    stream of the whole input bit for bit, and every rank decodes its own shard. In
+    broadcast mode the table bytes one rank's context built drive every other context."""
     import threading
 
     from data_compression_amd import synth
@@ -651,8 +652,9 @@ def test_sharded_huffman_on_device(torch_cuda, world, n_ary):
     def run(r):
         try:
             torch.cuda.set_device(0)
-            sh = ShardedHuffman(Codec(0))
+            sh = ShardedHuffman(Codec(0), table_mode=table_mode)
             sh.world, sh.rank = world, r
+            sh.table_src = world - 1
 
             def all_reduce(t):
                 tot = np.sum(np.array(tr.gather(r, t.cpu().tolist()), dtype=np.int64), axis=0)
@@ -661,7 +663,14 @@ def test_sharded_huffman_on_device(torch_cuda, world, n_ary):
             def all_gather_scalar(t):
                 v = tr.gather(r, [int(t.item())])
                 return torch.tensor([q[0] for q in v], dtype=t.dtype, device=t.device)
+            def reduce_to_src(t):   # the sum is only read by the table rank
+                all_reduce(t)
+
+            def broadcast_table(t):
+                v = tr.gather(r, t.cpu().numpy().tobytes())[world - 1]
+                t.copy_(torch.from_numpy(np.array(v, dtype=np.uint8)).to(t.device))
             sh._all_reduce, sh._all_gather_scalar = all_reduce, all_gather_scalar
+            sh._reduce_to_src, sh._broadcast_table = reduce_to_src, broadcast_table
             lo = r * shard
             xs = torch.from_numpy(x[lo: x.size if r == world - 1 else lo + shard].copy()).cuda()
             s = sh.encode(xs, n_ary=n_ary, sync_syms=S)
