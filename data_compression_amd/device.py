@@ -182,16 +182,24 @@ class Codec:
                                                                       nelem, _ptr(out) + h, C.byref(n)))
         return out[: h + n.value]
 
-    def small_decompress(self, seg):
-        """A front-end stream that starts with its type byte (rank 0's segment)."""
-        out = self._t(max(2 * seg.numel(), 1))
+    def _dec_out(self, seg, out):
+        if out is None:
+            return self._t(max(2 * seg.numel(), 1))
+        if out.numel() < 2 * seg.numel() or out.dtype != torch.uint8 or not out.is_contiguous():
+            raise ValueError("front-end decode output: contiguous uint8 of >= 2 * input bytes")
+        return out
+
+    def small_decompress(self, seg, out=None):
+        """A front-end stream that starts with its type byte (rank 0's segment). out: an
+        optional preallocated buffer of >= 2 * seg.numel() bytes (the result is a view)."""
+        out = self._dec_out(seg, out)
         n = C.c_uint64(0)
         check("dc_small_decompress", self.L.dc_small_decompress(self.ctx, _ptr(seg), seg.numel(), _ptr(out),
                                                                 C.byref(n)))
         return out[: n.value]
 
-    def small_decompress_body(self, seg):
-        out = self._t(max(2 * seg.numel(), 1))
+    def small_decompress_body(self, seg, out=None):
+        out = self._dec_out(seg, out)
         n = C.c_uint64(0)
         check("dc_small_decompress_body", self.L.dc_small_decompress_body(self.ctx, _ptr(seg), seg.numel(),
                                                                           _ptr(out), C.byref(n)))

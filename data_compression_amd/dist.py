@@ -262,11 +262,14 @@ class ShardedSmall:
         s.literal = literal
         return s
 
-    def decode(self, s):
+    def decode(self, s, out=None):
+        """out: optional buffer of >= 2 * s.n bytes for the front-end inverse (the result is a
+        view of it, or of the Huffman output when a later rank's segment is LITERAL)."""
         seg = self.h.decode(s)[: s.n]
+        kw = {} if out is None else {"out": out}
         if self.rank == 0:
-            return self.e.small_decompress(seg)
-        return seg if s.literal else self.e.small_decompress_body(seg)
+            return self.e.small_decompress(seg, **kw)
+        return seg if s.literal else self.e.small_decompress_body(seg, **kw)
 
 
 INITIAL_LISTS = np.frombuffer(b" etaoins" * 16, np.uint8).reshape(16, 8)   # initialize_dictionary
