@@ -6,7 +6,7 @@ import sys
 from collections import defaultdict
 
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
-want = ("k_hist_blocks", "k_huff_pack", "k_huff_decode", "k_huff_decode_fix", "k_huff_table", "k_hist_reduce",
+want = ("k_hist_blocks", "k_huff_pack", "k_huff_decode", "k_huff_decode_fix", "k_huff_table",
         "k_block_local", "k_block_final", "k_huff_fix_list", "k_zero_bounds")
 vals = defaultdict(lambda: defaultdict(list))
 for f in sorted(glob.glob(os.path.join(root, "p*", "run_counter_collection.csv"))):
