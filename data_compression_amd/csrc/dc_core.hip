@@ -3332,7 +3332,9 @@ int dc_huff_hist(dc_ctx *c, const uint8_t *d_in, uint64_t n, uint64_t *d_hist)
         HIPCHK(hipMemsetAsync(d_hist, 0, 256 * sizeof(uint64_t), c->stream));
         return DC_OK;
     }
-    const uint64_t grid = nb < 512 ? nb : 512;   // 2 resident per CU (64 KiB LDS each)
+    const char *hg = getenv("DC_HIST_GRID");   // A/B of the grid (tools/ab_env.sh)
+    const uint64_t hmax = hg && atoll(hg) > 0 ? (uint64_t)atoll(hg) : 512u;
+    const uint64_t grid = nb < hmax ? nb : hmax;   // 512: 2 resident per CU (64 KiB LDS each)
     HIPCHK(hipMemsetAsync(d_hist, 0, 256 * sizeof(uint64_t), c->stream));
     LAUNCH(c, "hist_blocks", k_hist_blocks, grid, 256, d_in, n, nb, c->d_bh, d_hist);
     return DC_OK;
