@@ -181,6 +181,11 @@ def main():
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
     traffic, traffic_src = pmc_traffic("k_" + dom, a, n)
 
+    # whole-pipeline rooflines (SURVEY §8(d) bytes over the whole encode / whole decode time:
+    # extra passes such as the histogram's read of the input count against them)
+    enc_alg = nh + payload + sync_bytes
+    enc_frac = enc_alg / (enc_ms * 1e-3) / HBM_PEAK
+    dec_frac = enc_alg / (dec_ms * 1e-3) / HBM_PEAK
     value = world * n / (ms_step * 1e-3) / 1e9
     res = {
         "metric": METRIC,
@@ -205,7 +210,10 @@ def main():
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK / 1e9,
                      "unit": "GB/s", "frac": round(achieved * 1e9 / HBM_PEAK, 4), "traffic": traffic,
                      "traffic_source": traffic_src,
-                     "alg_bytes_per_launch": dom_bytes, "mean_ms": round(dom_ms, 4)},
+                     "alg_bytes_per_launch": dom_bytes, "mean_ms": round(dom_ms, 4),
+                     "encode_frac": round(enc_frac, 4), "decode_frac": round(dec_frac, 4),
+                     "encode_ms": round(enc_ms, 4), "decode_ms": round(dec_ms, 4),
+                     "pipeline_alg_bytes": enc_alg},
         "encode_GBps": round(n / (enc_ms * 1e-3) / 1e9, 2),
         "decode_GBps": round(n / (dec_ms * 1e-3) / 1e9, 2),
         "ratio": round(payload / n, 4),
@@ -247,10 +255,21 @@ def pmc_traffic(kernel, a, n):
 
 
 def cpu_baseline(x, a):
-    """Oracle (single-threaded C restatement, oracle/dc_oracle.c) on a bounded sample."""
+    """Oracle (single-threaded C restatement, oracle/dc_oracle.c) on a bounded sample, pinned
+    to one host core (taskset -c 0 equivalent) for the timed part."""
     from oracle import oracle as orc
     m = min(a.cpu_sample, x.numel())
     s = x[:m].cpu().numpy()
+    old = os.sched_getaffinity(0)
+    core = min(old)
+    os.sched_setaffinity(0, {core})
+    try:
+        return _cpu_timed(orc, s, m, a, core)
+    finally:
+        os.sched_setaffinity(0, old)
+
+
+def _cpu_timed(orc, s, m, a, core):
     t0 = time.perf_counter()
     h = orc.histogram(s)
     L = orc.huffman_lengths(h, a.nary)
@@ -267,7 +286,7 @@ def cpu_baseline(x, a):
         cpu = "unknown"
     return {"value": round(m / (t2 - t0) / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
             "sample": f"first {m >> 20} MiB of the rank-0 stream; encode {t1 - t0:.2f} s + decode "
-                      f"{t2 - t1:.2f} s; {cpu}; nproc={os.cpu_count()}"}
+                      f"{t2 - t1:.2f} s; pinned to cpu {core}; {cpu}; nproc={os.cpu_count()}"}
 
 
 if __name__ == "__main__":

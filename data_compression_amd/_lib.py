@@ -75,6 +75,7 @@ def _declare_core(L):
         "dc_ctx_sync": ([vp], i32),
         "dc_ctx_stream": ([vp], vp),
         "dc_ctx_set_timing": ([vp, i32], i32),
+        "dc_ctx_set_option": ([vp, i32, C.c_int64], i32),
         "dc_ctx_timings": ([vp, C.POINTER(C.c_char_p), C.POINTER(C.c_float), i32], i32),
         "dc_version": ([], C.c_char_p),
         "dc_dtable_size": ([], C.c_size_t),

@@ -71,7 +71,7 @@ __global__ __launch_bounds__(256) void k_hist_blocks(const uint8_t *__restrict__
     for (int i = t; i < 256 * 16; i += 256) reinterpret_cast<uint4 *>(cnt)[i] = make_uint4(0u, 0u, 0u, 0u);
     __syncthreads();
     const uint64_t nfull = n / DC_BLOCK_BYTES;   // blocks read as 8 x 16 B per thread
-    uint32_t total = 0;                           // bin t over this workgroup's blocks
+    uint64_t total = 0;                           // bin t over this workgroup's blocks (u64: any grid)
     uint32_t prevc[64];                           // bin t's 64 counter dwords after the last block
 #pragma unroll
     for (int q = 0; q < 64; ++q) prevc[q] = 0u;
@@ -140,7 +140,7 @@ __global__ __launch_bounds__(256) void k_hist_blocks(const uint8_t *__restrict__
     }
     // this workgroup's bin totals straight into hist[] (zeroed by the launcher): 512 u64
     // atomics per bin at the end, no reduce launch (A/B r1 v14: step 1.379 -> 1.368 ms)
-    if (total) atomicAdd(reinterpret_cast<unsigned long long *>(&hist[t]), (unsigned long long)total);
+    if (total) atomicAdd(reinterpret_cast<unsigned long long *>(&hist[t]), total);
 }
 
 // ------------------------------------------------------------------------------------
@@ -3113,7 +3113,7 @@ __global__ __launch_bounds__(64) void k_nyb_chunk_dec(const uint8_t *__restrict_
 // =====================================================================================
 // host side
 // =====================================================================================
-#define DC_MAX_EVENTS 64
+#define DC_MAX_EVENTS 1024   /* HIP-event pairs per timing window (a C5 step launches ~40 kernels) */
 
 struct dc_ctx {
     int device;
@@ -3141,6 +3141,11 @@ struct dc_ctx {
     uint64_t *h_pinned;                           // pinned host scalars
     const uint8_t *hist_in; uint64_t hist_n;      // identity of the last dc_huff_hist input
     bool plan_ok;
+    // tuning options (dc_ctx_set_option; initial values from the environment, read once here)
+    uint32_t opt_hist_grid;       // histogram workgroups (0: default 512)
+    uint32_t opt_pack_grid;       // pack workgroups (0: default, two blocks per workgroup)
+    uint32_t opt_d8_static;       // decoder: static share of the tuples, percent (0..100)
+    uint32_t opt_decode_general;  // 1: always the general decoder (k_huff_decode)
     // timing
     int timing;
     int nev;
@@ -3221,6 +3226,14 @@ static int ctx_create(dc_ctx **out, int device, void *stream, bool own)
         free(c);
         return DC_E_HIP;
     }
+    c->opt_d8_static = D8_STATIC_PCT;
+    {   // A/B knobs of tools/ab_env.sh and tools/dec_ab.py, read once per context and clamped
+        const char *e;
+        if ((e = getenv("DC_HIST_GRID"))) (void)dc_ctx_set_option(c, DC_OPT_HIST_GRID, atoll(e));
+        if ((e = getenv("DC_PACK_GRID"))) (void)dc_ctx_set_option(c, DC_OPT_PACK_GRID, atoll(e));
+        if ((e = getenv("DC_D8_STATIC"))) (void)dc_ctx_set_option(c, DC_OPT_DECODE_STATIC_PCT, atoll(e));
+        if ((e = getenv("DC_DECODE_V7"))) (void)dc_ctx_set_option(c, DC_OPT_DECODE_GENERAL, atoll(e) != 0);
+    }
     if (g_rank_uploaded != device) {
         uint8_t rank[256];
         memset(rank, 0xFF, sizeof(rank));
@@ -3259,6 +3272,31 @@ void dc_ctx_destroy(dc_ctx *c)
         for (int i = 0; i < DC_MAX_EVENTS; ++i) { (void)hipEventDestroy(c->ev0[i]); (void)hipEventDestroy(c->ev1[i]); }
     if (c->own_stream) (void)hipStreamDestroy(c->stream);
     free(c);
+}
+
+int dc_ctx_set_option(dc_ctx *c, int option, int64_t value)
+{
+    if (!c) return DC_E_ARG;
+    switch (option) {
+    case DC_OPT_HIST_GRID:   // 0 = default; the kernel's per-workgroup bin totals are u64
+        if (value < 0 || value > (1 << 20)) return DC_E_ARG;
+        c->opt_hist_grid = (uint32_t)value;
+        return DC_OK;
+    case DC_OPT_PACK_GRID:
+        if (value < 0 || value > (1 << 24)) return DC_E_ARG;
+        c->opt_pack_grid = (uint32_t)value;
+        return DC_OK;
+    case DC_OPT_DECODE_STATIC_PCT:
+        if (value < 0 || value > 100) return DC_E_ARG;
+        c->opt_d8_static = (uint32_t)value;
+        return DC_OK;
+    case DC_OPT_DECODE_GENERAL:
+        if (value != 0 && value != 1) return DC_E_ARG;
+        c->opt_decode_general = (uint32_t)value;
+        return DC_OK;
+    default:
+        return DC_E_ARG;
+    }
 }
 
 int dc_ctx_sync(dc_ctx *c) { return (c && hipStreamSynchronize(c->stream) == hipSuccess) ? DC_OK : DC_E_HIP; }
@@ -3332,8 +3370,7 @@ int dc_huff_hist(dc_ctx *c, const uint8_t *d_in, uint64_t n, uint64_t *d_hist)
         HIPCHK(hipMemsetAsync(d_hist, 0, 256 * sizeof(uint64_t), c->stream));
         return DC_OK;
     }
-    const char *hg = getenv("DC_HIST_GRID");   // A/B of the grid (tools/ab_env.sh)
-    const uint64_t hmax = hg && atoll(hg) > 0 ? (uint64_t)atoll(hg) : 512u;
+    const uint64_t hmax = c->opt_hist_grid ? c->opt_hist_grid : 512u;
     const uint64_t grid = nb < hmax ? nb : hmax;   // 512: 2 resident per CU (64 KiB LDS each)
     HIPCHK(hipMemsetAsync(d_hist, 0, 256 * sizeof(uint64_t), c->stream));
     LAUNCH(c, "hist_blocks", k_hist_blocks, grid, 256, d_in, n, nb, c->d_bh, d_hist);
@@ -3450,9 +3487,8 @@ int dc_huff_pack_async(dc_ctx *c, const uint8_t *d_in, uint64_t n, const dc_dtab
            d_words, words_cap, c->d_err);
     // two blocks per workgroup (grid-stride): on 1 GiB C2, 16384 workgroups ran pack in
     // 0.452 ms against 0.481 at 4096, 0.469 at 32768, 0.504 at 1024 (r1 v15 A/B)
-    const char *pg = getenv("DC_PACK_GRID");   // A/B of the grid (tools/ab_env.sh)
-    const uint64_t gmax = pg ? (uint64_t)atoll(pg) : (nb + 1) / 2;
-    const uint64_t grid = nb < gmax ? nb : (gmax ? gmax : 1u);
+    const uint64_t gmax = c->opt_pack_grid ? c->opt_pack_grid : (nb + 1) / 2;
+    const uint64_t grid = nb < gmax ? nb : gmax;
     LAUNCH(c, "huff_pack", k_huff_pack, grid, 256, d_in, n, d_table, (const uint64_t *)c->d_off, bit_base, d_words,
            d_sync_base, d_sync_len, sync_syms, nb, words_cap, (const int *)c->d_err);
     return DC_OK;
@@ -3521,20 +3557,17 @@ int dc_huff_decode(dc_ctx *c, const uint32_t *d_words, uint64_t bit_base, uint64
     if (words < 4) return DC_E_ARG;
     const uint64_t groups = dc_huff_sync_groups(n, S);
     HIPCHK(hipMemsetAsync(c->d_err + 1, 0, sizeof(int), c->stream));
-    if (S == 64 && n < (1ull << 37) && words < (1ull << 31) && !getenv("DC_DECODE_V7")) {
-        // 16 waves x 2 chains (one workgroup per CU): the 8 x 4 split measured 0.89 vs
-        // 0.70 ms on 1 GiB C2 (fewer waves to cover the LDS round trips, spills)
-        const char *sp = getenv("DC_D8_STATIC");   // A/B of the static share (tools/dec_ab.py)
-        const uint32_t spct = sp ? (uint32_t)atoi(sp) : D8_STATIC_PCT;
-        const char *nwe = getenv("DC_D8_WAVES");   // A/B of the waves per CU (tools/dec_ab.py)
-        const int nw = nwe ? atoi(nwe) : 12;
+    if (S == 64 && n < (1ull << 37) && words < (1ull << 31) && !c->opt_decode_general) {
+        // 12 waves x 2 chains, one workgroup per CU: the stage and the 14-bit table fill the
+        // LDS (the 8 x 4 split measured 0.89 vs 0.70 ms on 1 GiB C2: spills)
+        const uint32_t spct = c->opt_d8_static;   // clamped to 0..100 by dc_ctx_set_option
+        constexpr int nw = 12;
         const uint64_t tuples = (groups + 1) / 2;
         const uint64_t wgs = (tuples + nw - 1) / nw;
         const uint64_t grid = wgs < 256 ? wgs : 256;   // persistent: one workgroup per CU
         if (ensure((void **)&c->d_fix, &c->fix_cap, (groups + 64) * sizeof(uint64_t)) ||
             ensure((void **)&c->d_fixpos, &c->fixpos_cap, (groups * 64 + 64) * sizeof(uint64_t)))
             return DC_E_HIP;
-        (void)nw;   // 12 waves x 2 chains: the stage and the 14-bit table fill the LDS
         if (ensure((void **)&c->d_scr, &c->scr_cap, (size_t)D8_SCRATCH_WAVES * D8_WSCR)) return DC_E_HIP;
         LAUNCH(c, "huff_decode", (k_huff_decode8<12, 2>), grid, 12 * 64, d_words, bit_base, d_sync_base, d_sync_len,
                n, words, d_table, d_out, c->d_err + 1, c->d_queue, spct, (uint64_t *)c->d_fix,

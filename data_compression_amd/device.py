@@ -75,7 +75,13 @@ class Codec:
     def timing(self, enable: bool):
         check("dc_ctx_set_timing", self.L.dc_ctx_set_timing(self.ctx, int(enable)))
 
-    def timings(self, max_n: int = 64):
+    OPTIONS = {"hist_grid": 1, "pack_grid": 2, "decode_static_pct": 3, "decode_general": 4}
+
+    def set_option(self, name, value: int):
+        """dc_ctx_set_option (dc_gpu.h DC_OPT_*): tuning knobs of this context."""
+        check("dc_ctx_set_option", self.L.dc_ctx_set_option(self.ctx, self.OPTIONS.get(name, name), int(value)))
+
+    def timings(self, max_n: int = 1024):
         names = (C.c_char_p * max_n)()
         ms = (C.c_float * max_n)()
         n = self.L.dc_ctx_timings(self.ctx, names, ms, max_n)

@@ -87,6 +87,16 @@ void *dc_ctx_stream(dc_ctx *ctx);
  * recording; dc_ctx_timings() synchronises and returns up to max stages. */
 int dc_ctx_set_timing(dc_ctx *ctx, int enable);
 int dc_ctx_timings(dc_ctx *ctx, const char **names, float *ms, int max);
+/* Tuning options of a context (defaults suit MI355X; each is also read once from the
+ * environment at context creation, for A/B runs: DC_HIST_GRID, DC_PACK_GRID, DC_D8_STATIC,
+ * DC_DECODE_V7). Out-of-range values return DC_E_ARG and leave the option unchanged. */
+enum {
+    DC_OPT_HIST_GRID = 1,         /* histogram workgroups, 0 = default (512)              */
+    DC_OPT_PACK_GRID = 2,         /* pack workgroups, 0 = default (two blocks each)        */
+    DC_OPT_DECODE_STATIC_PCT = 3, /* fast decoder: statically dealt share of work, 0..100  */
+    DC_OPT_DECODE_GENERAL = 4     /* 1: decode with the general (any-S) decoder            */
+};
+int dc_ctx_set_option(dc_ctx *ctx, int option, int64_t value);
 const char *dc_version(void);
 size_t dc_dtable_size(void);
 

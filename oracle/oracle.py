@@ -98,7 +98,8 @@ def bitcodes(enc_len, enc_val, n_ary):
 
 def huff_pack(x, code, nbits, bit_base=0, sync_syms=0):
     x = np.ascontiguousarray(x, dtype=np.uint8)
-    total = int((nbits[x].astype(np.uint64)).sum()) if x.size else 0
+    # payload bits from the histogram (no per-byte temporary: GiB-sized inputs)
+    total = int((histogram(x) * np.asarray(nbits, dtype=np.uint64)[:256]).sum()) if x.size else 0
     out = np.zeros((total + (bit_base & 7) + 7) // 8 + 8, dtype=np.uint8)
     nidx = (x.size + sync_syms - 1) // sync_syms if sync_syms else 0
     idx = np.zeros(max(nidx, 1), dtype=np.uint64)

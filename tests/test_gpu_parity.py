@@ -383,7 +383,7 @@ def test_decode_fast_path_rare_codes(torch_cuda, codec, case):
 
 
 @pytest.mark.parametrize("n_ary", [2, 3, 16])
-def test_decode_v8_equals_v7(torch_cuda, codec, n_ary, monkeypatch):
+def test_decode_v8_equals_v7(torch_cuda, codec, n_ary):
     """The S = 64 fast decoder and the general decoder give identical bytes."""
     torch = torch_cuda
     from data_compression_amd import synth
@@ -393,10 +393,13 @@ def test_decode_v8_equals_v7(torch_cuda, codec, n_ary, monkeypatch):
     a = torch.empty_like(xt)
     codec.decode_into(enc, a)
     assert codec.decode_status() == 0
-    monkeypatch.setenv("DC_DECODE_V7", "1")
-    b = torch.empty_like(xt)
-    codec.decode_into(enc, b)
-    assert codec.decode_status() == 0
+    codec.set_option("decode_general", 1)
+    try:
+        b = torch.empty_like(xt)
+        codec.decode_into(enc, b)
+        assert codec.decode_status() == 0
+    finally:
+        codec.set_option("decode_general", 0)
     assert torch.equal(a, b) and torch.equal(a, xt)
 
 

@@ -1,7 +1,8 @@
 """A/B timing of decode kernels on one encoded stream (same process, interleaved rounds).
 
     python tools/dec_ab.py [--cfg C2] [--size BYTES] [--nary 2] [--rounds 5] [--iters 10]
-Prints per-variant HIP-event mean ms of the huff_decode launch (v8 default vs DC_DECODE_V7).
+Prints per-variant HIP-event mean ms of the huff_decode launch (fast default "v8" vs the
+general decoder "v7"; "sNN": the fast decoder with a static share of NN %).
 """
 import argparse
 import os
@@ -32,20 +33,8 @@ res = {v: [] for v in a.variants.split(",")}
 fix = {}
 for r in range(a.rounds):
     for v in res:
-        os.environ.pop("DC_DECODE_V7", None)
-        os.environ.pop("DC_D8_CFG", None)
-        os.environ.pop("DC_D8_STATIC", None)
-        os.environ.pop("DC_D8_WAVES", None)
-        if v.startswith("w"):   # e.g. w12: 12 waves per CU
-            os.environ["DC_D8_WAVES"] = v[1:]
-        elif "s" in v:   # e.g. 16x2s80: static share 80 %
-            v0, sp = v.split("s")
-            os.environ["DC_D8_STATIC"] = sp
-            os.environ["DC_D8_CFG"] = v0
-        elif v == "v7":
-            os.environ["DC_DECODE_V7"] = "1"
-        elif v != "v8":
-            os.environ["DC_D8_CFG"] = v
+        c.set_option("decode_general", 1 if v == "v7" else 0)
+        c.set_option("decode_static_pct", int(v[1:]) if v.startswith("s") else 60)
         c.decode_into(enc, out)
         torch.cuda.synchronize()
         c.timing(True)
