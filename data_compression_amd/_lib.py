@@ -127,6 +127,10 @@ def _declare_core(L):
         "dc_huff_compress_bound": ([u64, u32], u64),
         "dc_huff_compress_host": ([u8p, u64, i32, C.POINTER(C.c_int32), i32, u32, u8p, u64, C.POINTER(u64)], i32),
         "dc_huff_decompress_host": ([u8p, u64, u8p, u64, C.POINTER(u64)], i32),
+        "dc_huff_netstring_bound": ([u64], u64),
+        "dc_huff_compress_netstring": ([u8p, u64, i32, C.POINTER(C.c_int32), i32, u32, u8p, u64, C.POINTER(u64)], i32),
+        "dc_huff_decompress_netstring": ([u8p, u64, u8p, u64, C.POINTER(u64)], i32),
+        "dc_huff_netstring_info": ([u8p, u64, C.POINTER(u64)], i32),
         "dc_huff_container_info": ([u8p, u64, C.POINTER(u64), C.POINTER(i32), C.POINTER(u64)], i32),
         "dc_nyb_compress_host": ([u8p, u64, i32, u8p, u64, C.POINTER(u64)], i32),
         "dc_nyb_decompress_host": ([u8p, u64, i32, u8p, u64, C.POINTER(u64)], i32),

@@ -127,19 +127,26 @@ int represent_items_with_codes(const int max_symbol_value, int canonical_lengths
     return (int)nchar;
 }
 
-// same parameters as the static compress() (n_ary_huffman.c:1688-1697); DCH1 container
+// same parameters as the static compress() (n_ary_huffman.c:1688-1697): the reference's
+// netstring blocks (dc_host.h "netstring container"); the output is NUL-terminated when it
+// fits, as the reference's sprintf leaves it (:1811)
 int dc_huff_compress(const int max_symbol_value, int canonical_lengths[], const int compressed_symbols,
                      const int bufsize, const int original_length, char original_text[], char compressed_text[])
 {
     if (original_length < 0 || bufsize < 0) return DC_E_ARG;
     uint64_t len = 0;
-    const int r = dc_huff_compress_host((const uint8_t *)original_text, (uint64_t)original_length,
-                                        compressed_symbols, canonical_lengths, max_symbol_value, 0,
-                                        (uint8_t *)compressed_text, (uint64_t)bufsize + 1, &len);
-    return r ? r : (int)len;
+    const int r = dc_huff_compress_netstring((const uint8_t *)original_text, (uint64_t)original_length,
+                                             compressed_symbols, canonical_lengths, max_symbol_value, 0,
+                                             (uint8_t *)compressed_text, (uint64_t)bufsize + 1, &len);
+    if (r) return r;
+    if (len < (uint64_t)bufsize + 1) compressed_text[len] = 0;
+    return (int)len;
 }
 
-// same parameters as the static decompress() (n_ary_huffman.c:2014-2020)
+// same parameters as the static decompress() (n_ary_huffman.c:2014-2020): every block of a
+// netstring container (or a DCH1 container), not only the first; returns the decompressed
+// length (the reference returns the first block's netstring length and copies two bytes too
+// many of a raw block, :2071-2076)
 int dc_huff_decompress(const int max_compressed_size, const char compressed_text[], const int max_decompressed_size,
                        char decompressed_text[])
 {

@@ -89,7 +89,8 @@ def represent_items_with_codes(max_symbol_value: int, canonical_lengths, compres
 
 
 def compress(data: bytes, n_ary: int = 2, lengths=None, max_symbol_value: int = 258) -> bytes:
-    """dc_huff_compress (same parameters as the reference's static compress) -> DCH1 bytes.
+    """dc_huff_compress (same parameters as the reference's static compress,
+    n_ary_huffman.c:1688) -> netstring blocks (raw, or #dc1 + X + #dcidx + Z).
     lengths None: the input's own Huffman lengths (histogram -> huffman on the GPU)."""
     data = bytes(data)
     n = len(data)
@@ -97,7 +98,7 @@ def compress(data: bytes, n_ary: int = 2, lengths=None, max_symbol_value: int = 
         lengths = huffman(max_symbol_value, histogram_bytes(data, max_symbol_value), n_ary)
     L = np.zeros(max_symbol_value + 1, dtype=np.int32)
     L[: len(lengths)] = np.asarray(lengths, dtype=np.int32)
-    cap = int(core().dc_huff_compress_bound(n, 0))
+    cap = int(core().dc_huff_netstring_bound(n)) + 1
     out = C.create_string_buffer(cap)
     r = lib().dc_huff_compress(max_symbol_value, _ip(L), n_ary, cap - 1, n, C.create_string_buffer(data, n + 1), out)
     if r < 0:
@@ -105,7 +106,23 @@ def compress(data: bytes, n_ary: int = 2, lengths=None, max_symbol_value: int = 
     return out.raw[:r]
 
 
+def compress_dch1(data: bytes, n_ary: int = 2, sync_syms: int = 0) -> bytes:
+    """The binary "DCH1" container (dc_huff_compress_host; dc_host.h)."""
+    data = bytes(data)
+    n = len(data)
+    cap = int(core().dc_huff_compress_bound(n, sync_syms))
+    out = (C.c_uint8 * cap)()
+    got = C.c_uint64(0)
+    src = (C.c_uint8 * max(n, 1)).from_buffer_copy(data + b"\0")
+    rc = core().dc_huff_compress_host(src, n, n_ary, None, 258, sync_syms, out, cap, C.byref(got))
+    if rc:
+        raise DcError("dc_huff_compress_host", rc)
+    return bytes(out[: got.value])
+
+
 def decompress(blob: bytes, max_decompressed_size: int | None = None) -> bytes:
+    """dc_huff_decompress: a netstring container (this build's or the reference compress()'s
+    raw blocks) or a DCH1 container."""
     blob = bytes(blob)
     if max_decompressed_size is None:
         nn = C.c_uint64(0)

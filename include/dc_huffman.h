@@ -26,8 +26,13 @@
  *    compressed_text[start] and returns the characters written, or -1 when a byte has no
  *    code, a code exceeds 32 bits, or the text would not fit in bufsize+1 bytes.
  *  - compress/decompress are `static` in the reference; the same-parameter functions
- *    are exported as dc_huff_compress/dc_huff_decompress and use the binary "DCH1"
- *    container (dc_host.h) instead of the reference's always-raw netstring block.
+ *    are exported as dc_huff_compress/dc_huff_decompress and read/write the reference's
+ *    netstring blocks (n_ary_huffman.c:1866-1943; layout in dc_host.h): the raw block is
+ *    byte-identical to the reference's compress() output for inputs < 32767 bytes, and a
+ *    Huffman stream is "#dc1" metadata + "X" table + "#dcidx" sync index + "Z" base64url
+ *    data blocks, written when smaller than the raw form. dc_huff_decompress decodes every
+ *    block and returns the decompressed length (the reference's returns the first block's
+ *    netstring length and copies 2 bytes too many, :2071-2076). It also reads "DCH1".
  *  - On a HIP failure (no GPU) the void functions abort with a message, as the
  *    reference's asserts do; they never fall back to CPU compute.
  */

@@ -20,3 +20,20 @@
 #define putchar(c) ((int)0)
 #define main ref_main
 #include REF_SRC
+
+#ifdef REF_EXPORT_CONTAINER
+/* n_ary_huffman.c's compress() and decompress() are `static` (:1688, :2014): these two
+ * wrappers, in the same translation unit, make them callable for the container golden
+ * vectors (tests/golden/gen_golden.py gen_container). They only forward the arguments. */
+void ref_compress(const int max_symbol_value, int canonical_lengths[], const int compressed_symbols,
+                  const int bufsize, const int original_length, char original_text[], char compressed_text[])
+{
+    compress(max_symbol_value, canonical_lengths, compressed_symbols, bufsize, original_length, original_text,
+             compressed_text);
+}
+int ref_decompress(const int max_compressed_size, const char compressed_text[], const int max_decompressed_size,
+                   char decompressed_text[])
+{
+    return decompress(max_compressed_size, compressed_text, max_decompressed_size, decompressed_text);
+}
+#endif

@@ -16,6 +16,8 @@ Reference functions exercised (file:line in /root/reference):
                                      nybble_compression.c:734-1038
   compress_bytestring (front-end)    small_compression.c:582-665
   digit2int                          n_ary_huffman.c:430-455
+  compress / decompress (static; via oracle/ref_shim.c wrappers)
+                                     n_ary_huffman.c:1688-1815, :2014-2094
 """
 from __future__ import annotations
 
@@ -238,15 +240,59 @@ def gen_digits():
     print("digit2int: %d digits" % int((vals >= 0).sum()))
 
 
+def gen_container(rng):
+    """compress() / decompress() (n_ary_huffman.c:1688-1815, :2014-2094; static, reached
+    through ref_compress / ref_decompress in oracle/ref_shim.c). The reference always writes
+    its raw pass-through block "<N+2>:\n\n<data>," (:1806-1814); n = 2 skips the table path
+    (whose NDEBUG build writes out of bounds, :1760-1792). ref_back: what its decompress()
+    writes for that block (data, ',', then the NUL its sprintf left: the off-by-2 copy,
+    :2071-2076) and its return value (the netstring length)."""
+    lib = load("libref_huffman.so")
+    lib.ref_compress.argtypes = [C.c_int, C.POINTER(C.c_int), C.c_int, C.c_int, C.c_int, C.c_char_p, C.c_char_p]
+    lib.ref_compress.restype = None
+    lib.ref_decompress.argtypes = [C.c_int, C.c_char_p, C.c_int, C.c_char_p]
+    lib.ref_decompress.restype = C.c_int
+    ins = [SENTENCE, b"a", b"ab", synth.english_like(4096, seed=21).tobytes(),
+           synth.enwik_like(20000, seed=22).tobytes(), synth.log_like(30000, seed=23).tobytes(),
+           bytes(rng.integers(1, 256, size=32766, dtype=np.uint8))]
+    rec = {}
+    lens = (C.c_int * (MAXSYM + 1))()
+    for i, x in enumerate(ins):
+        assert 0 not in x
+        size = len(x) + 64
+        dst = C.create_string_buffer(size)
+        lib.ref_compress(MAXSYM, lens, 2, size - 1, len(x), C.create_string_buffer(x, len(x) + 1), dst)
+        blob = dst.value
+        assert blob == b"%d:\n\n" % (len(x) + 2) + x + b","
+        outs = []
+        for fill in (0x11, 0xEE):
+            buf = C.create_string_buffer(bytes([fill]) * (len(x) + 64), len(x) + 64)
+            src = C.create_string_buffer(blob + b"\n", len(blob) + 2)   # its reader wants "," then "\n" (:2050)
+            ret = lib.ref_decompress(len(blob) + 2, src, len(x) + 64, buf)
+            outs.append(np.frombuffer(buf.raw, dtype=np.uint8))
+        differ = np.nonzero(outs[0] != outs[1])[0]   # first byte the reader left untouched
+        rec[f"in_{i}"] = np.frombuffer(x, dtype=np.uint8)
+        rec[f"comp_{i}"] = np.frombuffer(blob, dtype=np.uint8)
+        rec[f"back_{i}"] = outs[0][: int(differ[0])].copy()
+        rec[f"ret_{i}"] = np.array([ret])
+    rec["n_inputs"] = np.array([len(ins)])
+    np.savez_compressed(os.path.join(HERE, "container.npz"), **rec)
+    print("container inputs:", len(ins))
+
+
 def main():
     rng = np.random.default_rng(20250808)
     if sys.argv[1:] == ["digits"]:   # regenerate only this fixture
         gen_digits()
         return
+    if sys.argv[1:] == ["container"]:
+        gen_container(np.random.default_rng(20251016))
+        return
     gen_huffman(rng)
     gen_nybble(rng)
     gen_small(rng)
     gen_digits()
+    gen_container(np.random.default_rng(20251016))
 
 
 if __name__ == "__main__":
