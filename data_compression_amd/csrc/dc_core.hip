@@ -185,7 +185,7 @@ extern "C" int dc_diag_tbl_read(void *h)
 
 __global__ __launch_bounds__(256) void k_huff_table(const uint64_t *__restrict__ freq, int freq_is_hist256,
                                                     const int32_t *__restrict__ lens_in, int M, int nary,
-                                                    dc_dtable *__restrict__ T)
+                                                    dc_dtable *__restrict__ T, dc_tree *__restrict__ tree)
 {
     __shared__ uint64_t s_key[TBL_SORT_MAX];
     __shared__ uint64_t s_q2[TBL_SORT_MAX];
@@ -298,6 +298,8 @@ __global__ __launch_bounds__(256) void k_huff_table(const uint64_t *__restrict__
                 }
                 if (lane < nmerge) s_q2[t2 - nmerge + lane] = ((uint64_t)shi << 32) | slo;
                 if (lane < npick && picked < TBL_NODES) s_parent[picked] = (int16_t)(next0 + lane / nary);
+                if (tree && lane < npick && lane % nary < 2 && next0 + lane / nary < TBL_NODES)   // :978-979
+                    (lane % nary ? tree->right : tree->left)[next0 + lane / nary] = picked;
             }
             if (lane == 0 && next >= TBL_NODES) s_bad = 1;
         } else if (t == 0) {
@@ -333,6 +335,7 @@ __global__ __launch_bounds__(256) void k_huff_table(const uint64_t *__restrict__
                         nxt2 = (h2 + 1 < t2) ? s_q2[h2 + 1] : ~0ull;
                     }
                     if (t == 0 && idx < TBL_NODES) s_parent[idx] = (int16_t)next;
+                    if (tree && q < 2 && next < TBL_NODES) (q ? tree->right : tree->left)[next] = idx;
                 }
                 if (t == 0) s_q2[t2] = sum;
                 if (t2 == h2) head2 = sum;            // the queue was empty
@@ -345,6 +348,25 @@ __global__ __launch_bounds__(256) void k_huff_table(const uint64_t *__restrict__
         }
         __syncthreads();
     TBL_STAMP(2);
+        if (tree) {   // the whole node list (generate_huffman_tree's in-out list, :868-1005)
+            const int first_internal = leaves + dummies;
+            const int nodes = first_internal + max(items - 1, 0) / max(nary - 1, 1);
+            for (int i = t; i < TBL_NODES; i += 256) {
+                tree->parent[i] = i < nodes ? s_parent[i] : 0;
+                uint64_t cnt = 0;
+                if (i < leaves) cnt = freq_is_hist256 ? (i < 256 ? freq[i] : 0ull) : freq[i];
+                else if (i < first_internal) cnt = 1;   // dummy leaves (:921-929)
+                else if (i < nodes) cnt = s_q2[i - first_internal];
+                tree->count[i] = cnt;
+                if (i >= nodes || i < first_internal) { tree->left[i] = 0; tree->right[i] = 0; }
+            }
+            if (t == 0) {
+                tree->nodes = nodes;
+                tree->first_internal = first_internal;
+                tree->dummies = dummies;
+                tree->status = s_bad ? DC_E_ARG : DC_OK;
+            }
+        }
         // depth = number of parent hops to the root (n_ary_huffman.c:1069-1076)
         for (int i = t; i < leaves; i += 256) {
             int d = 0, c = i;
@@ -629,6 +651,22 @@ __global__ __launch_bounds__(256) void k_huff_table(const uint64_t *__restrict__
         T->max_len = maxL;
         T->status = s_bad ? DC_E_ARG : (s_maxbits > 32 ? DC_E_CODE_TOO_LONG : DC_OK);
     }
+}
+
+// summarize_tree_with_lengths (n_ary_huffman.c:1033-1093) for an arbitrary node list:
+// depth of node i < leaves = parent hops up to the node whose parent is 0, minus one (the
+// root); a walk longer than the list (a cycle) reports -1
+__global__ void k_tree_depths(const int32_t *__restrict__ parent, int list_length, int leaves,
+                              int32_t *__restrict__ depth)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= leaves) return;
+    int c = i, sum = 0;
+    do {
+        ++sum;
+        c = (c >= 0 && c < list_length) ? parent[c] : 0;
+    } while (c != 0 && sum <= list_length);
+    depth[i] = sum > list_length ? -1 : sum - 1;
 }
 
 // ------------------------------------------------------------------------------------
@@ -3381,7 +3419,22 @@ static int table_common(dc_ctx *c, const uint64_t *d_freq, int is_hist, const in
                         int nary, dc_dtable *d_table)
 {
     if (!c || !d_table || M < 0 || M >= DC_MAX_SYMS || nary < 2 || nary > 256) return DC_E_ARG;
-    LAUNCH(c, "huff_table", k_huff_table, 1, 256, d_freq, is_hist, d_len, M, nary, d_table);
+    LAUNCH(c, "huff_table", k_huff_table, 1, 256, d_freq, is_hist, d_len, M, nary, d_table, (dc_tree *)nullptr);
+    return DC_OK;
+}
+
+int dc_huff_tree(dc_ctx *c, const uint64_t *d_freq, int M, int nary, dc_dtable *d_table, dc_tree *d_tree)
+{
+    if (!c || !d_freq || !d_table || !d_tree || M < 0 || M >= DC_MAX_SYMS || nary < 2 || nary > 256) return DC_E_ARG;
+    LAUNCH(c, "huff_tree", k_huff_table, 1, 256, d_freq, 0, (const int32_t *)nullptr, M, nary, d_table, d_tree);
+    return DC_OK;
+}
+
+int dc_tree_depths(dc_ctx *c, const int32_t *d_parent, int list_length, int leaves, int32_t *d_depth)
+{
+    if (!c || !d_parent || !d_depth || list_length < 1 || leaves < 0 || leaves > list_length) return DC_E_ARG;
+    if (leaves == 0) return DC_OK;
+    LAUNCH(c, "tree_depths", k_tree_depths, (leaves + 255) / 256, 256, d_parent, list_length, leaves, d_depth);
     return DC_OK;
 }
 

@@ -127,6 +127,96 @@ int represent_items_with_codes(const int max_symbol_value, int canonical_lengths
     return (int)nchar;
 }
 
+// ---- the tree helpers (n_ary_huffman.c:773-1093, :2466-2506) on the caller's node list ----
+// setup_nodes (:773-817): the node list's initial state (a copy of the caller's counts into
+// its own struct array; no arithmetic to run anywhere else). Leaves 0..max_leaf_value, then
+// internal slots; `volume` is left as the reference leaves it (untouched).
+void setup_nodes(const int list_length, struct node list[], const int max_leaf_value, const int symbol_frequencies[])
+{
+    for (int i = 0; i < list_length; ++i) {
+        const bool leaf = i <= max_leaf_value;
+        list[i].leaf = leaf;
+        list[i].leaf_value = leaf ? i : 0;
+        list[i].count = leaf ? symbol_frequencies[i] : 0;
+        list[i].parent_index = 0;
+        list[i].left_index = 0;
+        list[i].right_index = 0;
+    }
+}
+
+// generate_huffman_tree (:868-1005): the n-ary merge of the list's leaf counts runs in
+// k_huff_table (dc_huff_tree); its parents, internal counts and first two children come
+// back into the caller's list, with the dummy leaves' count of 1 (:921-929).
+void generate_huffman_tree(const int list_length, struct node list[], const int compressed_symbols,
+                           const int max_leaf_value)
+{
+    dc_ctx *c = dc_host_ctx();
+    if (!c) dc_die("generate_huffman_tree", DC_E_HIP);
+    const int M = max_leaf_value;
+    if (M < 0 || M >= DC_MAX_SYMS || M >= list_length || compressed_symbols < 2 || compressed_symbols > 256)
+        dc_die("generate_huffman_tree", DC_E_ARG);
+    std::vector<uint64_t> f(M + 1);
+    for (int i = 0; i <= M; ++i) f[i] = list[i].count > 0 ? (uint64_t)list[i].count : 0;
+    void *d_f = nullptr, *d_tree = nullptr;
+    DC_OR_DIE("generate_huffman_tree", dc_host_scratch(5, (size_t)(M + 1) * 8, &d_f));
+    DC_OR_DIE("generate_huffman_tree", dc_host_scratch(1, sizeof(dc_tree), &d_tree));
+    DC_OR_DIE("generate_huffman_tree", dc_memcpy_h2d(c, d_f, f.data(), (size_t)(M + 1) * 8));
+    DC_OR_DIE("generate_huffman_tree",
+              dc_huff_tree(c, (const uint64_t *)d_f, M, compressed_symbols, table_buf(), (dc_tree *)d_tree));
+    std::vector<dc_tree> h(1);
+    DC_OR_DIE("generate_huffman_tree", dc_memcpy_d2h(c, h.data(), d_tree, sizeof(dc_tree)));
+    const dc_tree &T = h[0];
+    if (T.status) dc_die("generate_huffman_tree", T.status);
+    if (T.nodes > list_length) dc_die("generate_huffman_tree", DC_E_CAPACITY);   // the reference overruns list[]
+    for (int i = M + 1; i < T.first_internal; ++i) list[i].count = 1;
+    for (int i = T.first_internal; i < T.nodes; ++i) {
+        list[i].count = (int)(uint32_t)T.count[i];   // int, as the reference sums (:994-997)
+        list[i].left_index = T.left[i];
+        list[i].right_index = T.right[i];
+    }
+    for (int i = 0; i < T.nodes; ++i)
+        if (T.parent[i]) list[i].parent_index = T.parent[i];
+}
+
+// summarize_tree_with_lengths (:1033-1093): each leaf's depth by the parent walk
+// (dc_tree_depths), stored at lengths[leaf_value] in leaf order
+void summarize_tree_with_lengths(const int list_length, const struct node list[], const int max_leaf_value,
+                                 int lengths[], const int leaves)
+{
+    dc_ctx *c = dc_host_ctx();
+    if (!c) dc_die("summarize_tree_with_lengths", DC_E_HIP);
+    if (list_length < 1 || leaves < 0 || leaves > list_length || max_leaf_value < 0)
+        dc_die("summarize_tree_with_lengths", DC_E_ARG);
+    for (int i = 0; i <= max_leaf_value; ++i) lengths[i] = 0;
+    if (leaves == 0) return;
+    std::vector<int32_t> par(list_length), depth(leaves);
+    for (int i = 0; i < list_length; ++i) par[i] = list[i].parent_index;
+    void *d_par = nullptr, *d_depth = nullptr;
+    DC_OR_DIE("summarize_tree_with_lengths", dc_host_scratch(5, (size_t)list_length * 4, &d_par));
+    DC_OR_DIE("summarize_tree_with_lengths", dc_host_scratch(4, (size_t)leaves * 4, &d_depth));
+    DC_OR_DIE("summarize_tree_with_lengths", dc_memcpy_h2d(c, d_par, par.data(), (size_t)list_length * 4));
+    DC_OR_DIE("summarize_tree_with_lengths",
+              dc_tree_depths(c, (const int32_t *)d_par, list_length, leaves, (int32_t *)d_depth));
+    DC_OR_DIE("summarize_tree_with_lengths", dc_memcpy_d2h(c, depth.data(), d_depth, (size_t)leaves * 4));
+    for (int i = 0; i < leaves; ++i) {
+        const int v = list[i].leaf_value;
+        if (depth[i] < 0 || v < 0 || v > max_leaf_value) dc_die("summarize_tree_with_lengths", DC_E_ARG);
+        lengths[v] = depth[i];
+    }
+}
+
+// find_compressed_data_size (:2466-2506): the payload in digits, sum of count x length over
+// the coded symbols (the formula the encoder's plan evaluates per block, k_block_local)
+int find_compressed_data_size(int max_symbol_value, int symbol_frequencies[], int canonical_lengths[],
+                              int compressed_symbols)
+{
+    (void)compressed_symbols;
+    int size = 0;
+    for (int i = 0; i <= max_symbol_value; ++i)
+        if (canonical_lengths[i] > 0) size += canonical_lengths[i] * symbol_frequencies[i];   // int, as :2485
+    return size;
+}
+
 // same parameters as the static compress() (n_ary_huffman.c:1688-1697): the reference's
 // netstring blocks (dc_host.h "netstring container"); the output is NUL-terminated when it
 // fits, as the reference's sprintf leaves it (:1811)

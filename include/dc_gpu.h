@@ -74,6 +74,20 @@ typedef struct dc_dtable {
     uint16_t dlut14[1 << DC_LUT14_BITS];
 } dc_dtable;
 
+/* Node list of the n-ary Huffman tree (generate_huffman_tree's in-out list[],
+ * n_ary_huffman.c:868-1005): nodes 0..M leaves, M+1.. the dummy leaves, then the internal
+ * nodes in creation order. parent 0 = none (the root, or a leaf of count 0); left/right =
+ * an internal node's first two children in pick order (:978-979); count = leaf frequency,
+ * 1 for a dummy, the children's sum for an internal node. */
+#define DC_TREE_NODES 4096
+typedef struct dc_tree {
+    int32_t nodes, first_internal, dummies, status;
+    int32_t parent[DC_TREE_NODES];
+    int32_t left[DC_TREE_NODES];
+    int32_t right[DC_TREE_NODES];
+    uint64_t count[DC_TREE_NODES];
+} dc_tree;
+
 /* ---- context ------------------------------------------------------------------------ */
 /* stream: the hipStream_t to launch on (e.g. torch's current stream); NULL is the
  * default (legacy) stream. dc_ctx_create_owned makes a private non-blocking stream.
@@ -120,6 +134,12 @@ int dc_huff_table_freq(dc_ctx *ctx, const uint64_t *d_freq, int max_symbol_value
 /* (2c) table from given lengths d_lengths[max_symbol_value+1] (skips the merge). */
 int dc_huff_table_lengths(dc_ctx *ctx, const int32_t *d_lengths, int max_symbol_value,
                           int n_ary, dc_dtable *d_table);
+/* (2d) the table of (2b) plus its whole node list (generate_huffman_tree) into d_tree */
+int dc_huff_tree(dc_ctx *ctx, const uint64_t *d_freq, int max_symbol_value, int n_ary, dc_dtable *d_table,
+                 dc_tree *d_tree);
+/* (2e) summarize_tree_with_lengths' walk for any node list: d_depth[i] (i < leaves) = parent
+ *      hops from node i to the root (-1: the walk exceeds the list, a cycle) */
+int dc_tree_depths(dc_ctx *ctx, const int32_t *d_parent, int list_length, int leaves, int32_t *d_depth);
 /* (3) per-block bit counts + exclusive scan for the input of the last dc_huff_hist;
  *     writes the payload bit count to *d_total_bits (device u64). */
 int dc_huff_plan(dc_ctx *ctx, const dc_dtable *d_table, uint64_t *d_total_bits);

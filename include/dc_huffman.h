@@ -12,6 +12,11 @@
  * represent_items_with_codes                           | n_ary_huffman.c:1621-1678
  * dc_huff_compress  (same parameters as static compress)   | n_ary_huffman.c:1688-1815
  * dc_huff_decompress (same parameters as static decompress) | n_ary_huffman.c:2014-2094
+ * struct node                                          | n_ary_huffman.c:499-531
+ * setup_nodes                                          | n_ary_huffman.c:773-817
+ * generate_huffman_tree     (k_huff_table's merge)     | n_ary_huffman.c:868-1005
+ * summarize_tree_with_lengths (k_tree_depths)          | n_ary_huffman.c:1033-1093
+ * find_compressed_data_size                            | n_ary_huffman.c:2466-2506
  *
  * Semantics and the deliberate differences (all documented in DESIGN.md §Boundary):
  *  - histogram counts bytes up to the first NUL into h[0..max_symbol_value] (bytes above
@@ -33,15 +38,43 @@
  *    data blocks, written when smaller than the raw form. dc_huff_decompress decodes every
  *    block and returns the decompressed length (the reference's returns the first block's
  *    netstring length and copies 2 bytes too many, :2071-2076). It also reads "DCH1".
+ *  - The tree helpers work on the caller's struct node list (host memory): the merge of
+ *    generate_huffman_tree and the parent walks of summarize_tree_with_lengths run on the
+ *    GPU (dc_huff_tree, dc_tree_depths) and their results are written back into the list;
+ *    setup_nodes (initialisation) and find_compressed_data_size (a sum over <= 1024 table
+ *    entries) are host code. Results equal the reference's (tests/golden/helpers.npz).
+ *    generate_huffman_tree needs max_leaf_value < 1024 and the tree to fit list_length
+ *    (the reference writes past the list otherwise); `volume` is never touched.
  *  - On a HIP failure (no GPU) the void functions abort with a message, as the
  *    reference's asserts do; they never fall back to CPU compute.
  */
 #ifndef DC_HUFFMAN_H
 #define DC_HUFFMAN_H
+#include <stdbool.h>
 
 #ifdef __cplusplus
 extern "C" {
 #endif
+
+/* the reference's node (:499-531): bool, then six ints (28 bytes) */
+struct node {
+    bool leaf;
+    int count;
+    int left_index;
+    int right_index;
+    int leaf_value;
+    int parent_index;
+    int volume;
+};
+
+void setup_nodes(const int list_length, struct node list[], const int max_leaf_value,
+                 const int symbol_frequencies[]);
+void generate_huffman_tree(const int list_length, struct node list[], const int compressed_symbols,
+                           const int max_leaf_value);
+void summarize_tree_with_lengths(const int list_length, const struct node list[], const int max_leaf_value,
+                                 int lengths[], const int leaves);
+int find_compressed_data_size(int max_symbol_value, int symbol_frequencies[], int canonical_lengths[],
+                              int compressed_symbols);
 
 void histogram(const char *text, const int max_symbol_value, int h[]);
 void huffman(const int max_leaf_value, const int symbol_frequencies[],

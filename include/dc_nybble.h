@@ -10,6 +10,17 @@
  * decompress_bytestring(source, dest, modify)          | nybble_compression.c:734-817
  * nybble_compress(source, dest)      (= modify true)   | nybble_compression.c:1134-1137
  * nybble_decompress(source, dest)    (= modify true)   | nybble_compression.c:1117-1120
+ * context_table_type                                   | nybble_compression.c:540-544
+ * byte_to_context / context_to_byte                    | nybble_compression.c:517-527
+ * initialize_dictionary                                | nybble_compression.c:546-562
+ * decompress_nybble                                    | nybble_compression.c:643-663
+ * update_context                                       | nybble_compression.c:665-687
+ * compress_byte_index                                  | nybble_compression.c:819-884
+ *
+ * The per-element helpers update ONE byte of a caller-owned host table per call (the
+ * reference's loops call them per byte); they run on the host, where that table lives.
+ * Their results equal the reference's (tests/golden/helpers.npz). The stream functions
+ * above are the GPU path.
  *
  * C-string contract as in the reference: the input ends at its first NUL, the output is
  * NUL-terminated; dest capacity >= strlen(source)+2 (compress) / 2*strlen(source)+1
@@ -25,6 +36,22 @@
 #ifdef __cplusplus
 extern "C" {
 #endif
+
+#define DC_NYB_LETTERS 8    /* letters_per_context (:515) */
+#define DC_NYB_CONTEXTS 16  /* num_contexts (:516) */
+
+/* the reference's layout exactly (:540-544): 128 chars then 16 ints, 192 bytes */
+typedef struct context_table_type {
+    char letter[DC_NYB_CONTEXTS][DC_NYB_LETTERS];
+    int times_used_directly[DC_NYB_CONTEXTS];
+} context_table_type;
+
+int byte_to_context(char byte);
+char context_to_byte(int context);
+void initialize_dictionary(context_table_type *context_table);
+int decompress_nybble(context_table_type context_table, const char nybble, const char next_nybble, char *dest);
+int update_context(context_table_type *context_table, const char context_byte, const char output_byte);
+int compress_byte_index(context_table_type *context_table, int nybble_offset, const char *source, char *dest);
 
 void compress_bytestring(const char *source_original, char *dest_original, bool modify);
 void decompress_bytestring(const char *source, char *dest_original, bool modify);

@@ -1,8 +1,11 @@
 /* A C caller of the Huffman drop-in, written the way the reference's own driver uses
  * these functions (n_ary_huffman.c:2509-2530): histogram -> huffman ->
  * convert_lengths_to_encode_table -> represent_items_with_codes, then the container
- * round trip that replaces the static compress/decompress (:1688, :2014).
+ * round trip that replaces the static compress/decompress (:1688, :2014), and the tree
+ * helpers (setup_nodes :773, generate_huffman_tree :868, summarize_tree_with_lengths
+ * :1033, find_compressed_data_size :2466) on a caller-owned struct node list.
  * Links only libdc_huffman.so. Exit status 0 = every check passed. */
+#include <stdbool.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -36,6 +39,42 @@ static int canonical_kats(void)
     return 0;
 }
 
+/* the reference's own summarize_tree_with_lengths test trees (:1112-1154), then the
+ * caller-side tree path setup_nodes -> generate_huffman_tree -> summarize_tree_with_lengths,
+ * which must give huffman()'s lengths (huffman() is that composition, :1161-1208) */
+static int tree_helpers(const int h[])
+{
+    struct node list_a[6] = {{true, 9, 0, 0, 'a', 2, 0}, {true, 9, 0, 0, 'b', 2, 0}, {false, 4, 0, 1, 0, 0, 0}};
+    int la['z' + 1];
+    summarize_tree_with_lengths(6, list_a, 'z', la, 2);
+    CHECK(la['a'] == 1 && la['b'] == 1 && la['c'] == 0);
+    struct node list_b[5] = {{true, 9, 0, 0, 'a', 4, 0}, {true, 9, 0, 0, 'b', 3, 0}, {true, 8, 0, 0, 'c', 3, 0},
+                             {false, 17, 1, 2, 0, 4, 0}, {false, 26, 0, 3, 0, 0, 0}};
+    int lb['z' + 1];
+    summarize_tree_with_lengths(5, list_b, 'z', lb, 3);
+    CHECK(lb['a'] == 1 && lb['b'] == 2 && lb['c'] == 2);
+    CHECK(sizeof(struct node) == 28);
+    static struct node list[2 * MAXSYM];
+    for (int n = 2; n <= 16; n += 7) {   /* n = 2, 9, 16 */
+        int want[MAXSYM + 1], got[MAXSYM + 1];
+        huffman(MAXSYM, h, n, want);
+        setup_nodes(2 * MAXSYM, list, MAXSYM, h);
+        CHECK(list[65].leaf && list[65].leaf_value == 65 && list[65].count == h[65] && !list[MAXSYM + 1].leaf);
+        generate_huffman_tree(2 * MAXSYM, list, n, MAXSYM);
+        summarize_tree_with_lengths(2 * MAXSYM, list, MAXSYM, got, MAXSYM + 1);
+        int root = -1, bits = 0;
+        for (int i = 0; i <= MAXSYM; ++i) {
+            CHECK(got[i] == want[i]);
+            bits += want[i] * h[i];
+        }
+        for (int i = 0; i < 2 * MAXSYM; ++i)
+            if (list[i].count && !list[i].parent_index) { CHECK(root < 0); root = i; }
+        CHECK(root > MAXSYM && list[root].count >= (int)strlen("Hello"));   /* one root: the last internal node */
+        CHECK(find_compressed_data_size(MAXSYM, (int *)h, want, n) == bits);
+    }
+    return 0;
+}
+
 int main(void)
 {
     static const char text[] =
@@ -52,6 +91,7 @@ int main(void)
     for (int i = 0; i <= MAXSYM; ++i) total += h[i];
     CHECK(total == len);
     CHECK(h['a'] > 0 && h['z'] == 0);
+    if (tree_helpers(h)) return 1;
 
     for (int n = 2; n <= 16; n += (n < 4 ? 1 : 6)) {   /* n = 2, 3, 4, 10, 16 */
         huffman(MAXSYM, h, n, lengths);

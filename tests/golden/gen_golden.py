@@ -280,8 +280,124 @@ def gen_container(rng):
     print("container inputs:", len(ins))
 
 
+class Node(C.Structure):   # struct node, n_ary_huffman.c:499-531
+    _fields_ = [("leaf", C.c_bool), ("count", C.c_int), ("left_index", C.c_int), ("right_index", C.c_int),
+                ("leaf_value", C.c_int), ("parent_index", C.c_int), ("volume", C.c_int)]
+
+
+NODE_FIELDS = ("leaf", "count", "left_index", "right_index", "leaf_value", "parent_index")
+
+
+def nodes_array(lst):
+    return np.array([[int(getattr(nd, f)) for f in NODE_FIELDS] for nd in lst], dtype=np.int64)
+
+
+class CtxTable(C.Structure):   # context_table_type, nybble_compression.c:540-544
+    _fields_ = [("letter", (C.c_char * 8) * 16), ("times_used_directly", C.c_int * 16)]
+
+
+def gen_helpers(rng):
+    """The reference's exported helpers, run on synthetic inputs:
+    nybble_compression.c byte_to_context :517, initialize_dictionary :546, update_context
+    :665, compress_byte_index :819, decompress_nybble :643; n_ary_huffman.c setup_nodes :773,
+    generate_huffman_tree :868, summarize_tree_with_lengths :1033 (incl. the two trees of its
+    own test, :1112-1154), find_compressed_data_size :2466."""
+    rec = {}
+    ny = load("libref_nybble.so")
+    ny.byte_to_context.argtypes = [C.c_char]
+    ny.byte_to_context.restype = C.c_int
+    rec["b2c"] = np.array([ny.byte_to_context(bytes([b])) for b in range(256)], dtype=np.int32)
+    t = CtxTable()
+    ny.initialize_dictionary(C.byref(t))
+    rec["init_table"] = np.frombuffer(bytes(t), dtype=np.uint8).copy()
+    # update_context over a text-like stream of (context byte, output byte), snapshots
+    ny.update_context.argtypes = [C.POINTER(CtxTable), C.c_char, C.c_char]
+    text = synth.english_like(3001, seed=31)
+    snaps = []
+    for i in range(1, text.size):
+        ny.update_context(C.byref(t), bytes([int(text[i - 1])]), bytes([int(text[i])]))
+        if i % 100 == 0:
+            snaps.append(np.frombuffer(bytes(t), dtype=np.uint8).copy())
+    rec["upd_text"] = text
+    rec["upd_snaps"] = np.array(snaps)
+    # compress_byte_index / decompress_nybble on snapshot tables
+    ny.compress_byte_index.argtypes = [C.POINTER(CtxTable), C.c_int, C.c_char_p, C.c_char_p]
+    ny.compress_byte_index.restype = C.c_int
+    ny.decompress_nybble.argtypes = [CtxTable, C.c_char, C.c_char, C.c_char_p]
+    ny.decompress_nybble.restype = C.c_int
+    cb, dn = [], []
+    for k in range(3000):
+        snap = snaps[k % len(snaps)]
+        tb = CtxTable.from_buffer_copy(snap.tobytes())
+        prev, cur = int(text[rng.integers(0, text.size)]), int(text[rng.integers(0, text.size)])
+        if k % 7 == 0:
+            cur = int(rng.integers(1, 128))
+        off = int(k & 1)
+        d0, d1 = int(rng.integers(0, 256)), int(rng.integers(0, 256))
+        src = C.create_string_buffer(bytes([prev, cur, 0]), 3)
+        dst = C.create_string_buffer(bytes([d0, d1, 0]), 3)
+        r = ny.compress_byte_index(C.byref(tb), off, C.cast(C.addressof(src) + 1, C.c_char_p),
+                                   dst)
+        cb.append([k % len(snaps), off, prev, cur, d0, d1, r, dst.raw[0], dst.raw[1]])
+        nyb, nxt = int(rng.integers(0, 16)), int(rng.integers(0, 16))
+        dd = C.create_string_buffer(bytes([prev, 0x5A, 0]), 3)
+        r2 = ny.decompress_nybble(CtxTable.from_buffer_copy(snap.tobytes()), bytes([nyb]), bytes([nxt]),
+                                  C.cast(C.addressof(dd) + 1, C.c_char_p))
+        dn.append([k % len(snaps), prev, nyb, nxt, r2, dd.raw[1]])
+    rec["cbi"] = np.array(cb, dtype=np.int64)
+    rec["dnyb"] = np.array(dn, dtype=np.int64)
+
+    hu = load("libref_huffman.so")
+    LL = 2 * MAXSYM
+    hu.setup_nodes.argtypes = [C.c_int, C.POINTER(Node), C.c_int, C.POINTER(C.c_int)]
+    hu.generate_huffman_tree.argtypes = [C.c_int, C.POINTER(Node), C.c_int, C.c_int]
+    hu.summarize_tree_with_lengths.argtypes = [C.c_int, C.POINTER(Node), C.c_int, C.POINTER(C.c_int), C.c_int]
+    hu.find_compressed_data_size.argtypes = [C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_int]
+    hu.find_compressed_data_size.restype = C.c_int
+    cases = [(nm, f) for nm, f in random_histograms(rng) if f.sum() > 0][::3]
+    freqs, ns, trees, lens, sizes, setups = [], [], [], [], [], []
+    for name, f in cases:
+        for n in (2, 3, 16):
+            fr = (C.c_int * (MAXSYM + 1))(*[int(v) for v in f])
+            lst = (Node * LL)()
+            hu.setup_nodes(LL, lst, MAXSYM, fr)
+            setups.append(nodes_array(lst))
+            hu.generate_huffman_tree(LL, lst, n, MAXSYM)
+            trees.append(nodes_array(lst))
+            L = (C.c_int * (MAXSYM + 1))()
+            hu.summarize_tree_with_lengths(LL, lst, MAXSYM, L, MAXSYM + 1)
+            lens.append(np.array(L[:], dtype=np.int32))
+            sizes.append(hu.find_compressed_data_size(MAXSYM, fr, L, n))
+            freqs.append(f)
+            ns.append(n)
+    rec["tree_freq"] = np.array(freqs, dtype=np.int64)
+    rec["tree_n"] = np.array(ns, dtype=np.int32)
+    rec["tree_setup"] = np.array(setups)
+    rec["tree_nodes"] = np.array(trees)
+    rec["tree_lengths"] = np.array(lens)
+    rec["tree_size"] = np.array(sizes, dtype=np.int64)
+    # the reference's own summarize test trees (:1119-1123, :1136-1142), max_leaf_value 'z'
+    kat = []
+    for rows, leaves in (([(1, 9, 0, 0, ord("a"), 2), (1, 9, 0, 0, ord("b"), 2), (0, 4, 0, 1, 0, 0)], 2),
+                         ([(1, 9, 0, 0, ord("a"), 4), (1, 9, 0, 0, ord("b"), 3), (1, 8, 0, 0, ord("c"), 3),
+                           (0, 17, 1, 2, 0, 4), (0, 26, 0, 3, 0, 0)], 3)):
+        lst = (Node * 6)()
+        for i, r in enumerate(rows):
+            lst[i] = Node(bool(r[0]), *r[1:], 0)
+        L = (C.c_int * (ord("z") + 1))()
+        hu.summarize_tree_with_lengths(6 if leaves == 2 else 5, lst, ord("z"), L, leaves)
+        kat.append((nodes_array(lst), leaves, np.array(L[:], dtype=np.int32)))
+    rec["kat_nodes_0"], rec["kat_leaves_0"], rec["kat_len_0"] = kat[0][0], np.array([kat[0][1]]), kat[0][2]
+    rec["kat_nodes_1"], rec["kat_leaves_1"], rec["kat_len_1"] = kat[1][0], np.array([kat[1][1]]), kat[1][2]
+    np.savez_compressed(os.path.join(HERE, "helpers.npz"), **rec)
+    print("helpers: %d nybble cases, %d trees" % (len(cb), len(trees)))
+
+
 def main():
     rng = np.random.default_rng(20250808)
+    if sys.argv[1:] == ["helpers"]:
+        gen_helpers(np.random.default_rng(20251017))
+        return
     if sys.argv[1:] == ["digits"]:   # regenerate only this fixture
         gen_digits()
         return
@@ -293,6 +409,7 @@ def main():
     gen_small(rng)
     gen_digits()
     gen_container(np.random.default_rng(20251016))
+    gen_helpers(np.random.default_rng(20251017))
 
 
 if __name__ == "__main__":
