@@ -1473,6 +1473,29 @@ static __device__ uint32_t d8_long(uint32_t lo, uint32_t hi, const dc_dtable *__
     return 0u;
 }
 
+// Multi-symbol lookup table of k_huff_decode9 (built into its LDS by every workgroup): up to
+// 3 whole codes at the start of a DC_MULTI_BITS-bit LSB-first window, by the canonical search
+// of d8_long repeated after each code while the window holds it. Symbols in bytes 0..2 (the
+// first code in byte 0, unused bytes 0), bits 24..27 = their total bit length, bits 28..29 =
+// how many (0: the first code is longer than the window, or invalid).
+#define DC_MULTI_BITS 13
+static __device__ __forceinline__ uint32_t multi_entry(uint32_t x, const dc_dtable *__restrict__ T, int nary, int w,
+                                                       bool pow2)
+{
+    constexpr uint32_t K = DC_MULTI_BITS;
+    uint32_t syms = 0, used = 0, cnt = 0;
+    while (cnt < 3) {
+        int bad = 0;
+        const uint32_t e = d8_long(x >> used, 0u, T, nary, w, pow2, &bad);
+        const uint32_t L = e & 255u;
+        if (bad || L == 0 || used + L > K) break;
+        syms |= ((e >> 8) & 255u) << (8 * cnt);
+        used += L;
+        ++cnt;
+    }
+    return cnt ? syms | (used << 24) | (cnt << 28) : 0u;
+}
+
 // any chunk, any count, exact: words read from HBM (MSB-first bytes; reads clamped to the
 // nwords of the buffer), bytes written one by one
 static __device__ void d8_chunk_hbm(const uint32_t *__restrict__ in, uint64_t nwords, uint64_t pos, uint32_t cnt,
@@ -1947,6 +1970,202 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode8(const uint32_t *__rest
 #endif
 }
 
+// ------------------------------------------------------------------------------------
+// (H8) fast decoder, multi-symbol form (S = 64; same schedule, staging, sync index, output
+// layout and redo protocol as k_huff_decode8, one chain per wave). A lookup in the 13-bit
+// multi-symbol table (multi_entry) yields up to 3 whole codes (2.44 per lookup on C2 text, against 1),
+// so a chunk takes ~26 lookups instead of 64: half the LDS table reads, which bound
+// k_huff_decode8 (random 16-bit reads, ~3.5-way bank conflicts). The symbols of a lookup
+// are appended to a 64-bit byte accumulator; its low dword is stored to the lane's LDS
+// output row every lookup (aligned, conflict-free: rows are 17 dwords apart) and the
+// accumulator moves on a dword when one is complete. A code longer than 13 bits (a lookup
+// with no code: ~0.1% of C2 symbols) is taken after the batch through the 12-bit table and
+// its second level (dlut / dlut2, also in LDS); only a code longer than 12 + dlut2_k bits,
+// or a tuple that is not staged, goes to the exact redo (k_huff_decode8_fix).
+// Measured (r2, 1 GiB C2): 0.569 ms + 0.013 redo against k_huff_decode8's 0.454 + 0.099: a
+// wave runs until its slowest lane has its 64 symbols (max ~38 lookups against a mean of 26),
+// and each lookup carries ~20 VALU of output bookkeeping. Kept as DC_OPT_DECODE_VARIANT 1.
+// ------------------------------------------------------------------------------------
+#define D9_ROW 17   /* dwords per output row: 64 bytes + one dword the last lookup may spill into */
+template <int NW>
+struct Dec9Lds {
+    __attribute__((aligned(16))) uint32_t lut[1 << DC_MULTI_BITS];
+    uint16_t dlut[1 << DC_LUT_BITS];
+    uint16_t dlut2[DC_LUT2_CAP];
+    uint32_t exhausted;
+    __attribute__((aligned(16))) uint32_t stage[NW][D8_STAGE_WORDS];
+    uint32_t rows[NW][64 * D9_ROW];
+    uint32_t tail_pad[64];
+};
+
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void k_huff_decode9(const uint32_t *__restrict__ in, uint64_t bit_base,
+                                                          const uint64_t *__restrict__ sync_base,
+                                                          const uint16_t *__restrict__ sync_len, uint64_t n,
+                                                          uint64_t nwords, const dc_dtable *__restrict__ T,
+                                                          uint8_t *__restrict__ out, int *__restrict__ err,
+                                                          uint32_t *__restrict__ queue, uint32_t static_pct,
+                                                          uint64_t *__restrict__ fix_mask, uint64_t *__restrict__ fix_pos,
+                                                          uint8_t *__restrict__ scratch)
+{
+    constexpr int NC = 1;
+    constexpr uint32_t S = 64;
+    constexpr int NT = NW * 64;
+    constexpr uint32_t MB = (1u << DC_MULTI_BITS) - 1;
+    __shared__ Dec9Lds<NW> L;
+    const int t = threadIdx.x, lane = t & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
+    {
+        const int nary = T->n_ary, w = T->w;
+        const bool pow2 = (nary & (nary - 1)) == 0, ok = T->status == DC_OK;
+        for (int x = t; x < (1 << DC_MULTI_BITS); x += NT) L.lut[x] = ok ? multi_entry((uint32_t)x, T, nary, w, pow2) : 0u;
+    }
+    for (int i = t; i < (1 << DC_LUT_BITS) / 8; i += NT)
+        reinterpret_cast<uint4 *>(L.dlut)[i] = reinterpret_cast<const uint4 *>(T->dlut)[i];
+    for (int i = t; i < DC_LUT2_CAP / 4; i += NT)   // dlut2 is 8-B aligned
+        reinterpret_cast<uint2 *>(L.dlut2)[i] = reinterpret_cast<const uint2 *>(T->dlut2)[i];
+    const uint32_t K2 = (uint32_t)T->dlut2_k, kmask = (1u << K2) - 1;
+    if (t == 0) L.exhausted = 0;
+    if (blockIdx.x == 0 && t == 0) queue[D8_FIX_CNT] = 0u;   // k_huff_fix_list's counter (runs after)
+    __syncthreads();
+
+    const uint32_t nchunks = (uint32_t)((n + S - 1) / S);
+    const uint32_t ngroups = (nchunks + DC_SYNC_GROUP - 1) / DC_SYNC_GROUP;
+    const uint32_t ntuples = ngroups;   // one group per tuple
+    const uint64_t word_base = bit_base >> 5;
+    uint32_t *const stw = L.stage[wv];
+    const uint32_t *st[1] = {stw};
+    uint32_t *stws[1] = {stw};
+    uint32_t *const row = L.rows[wv] + lane * D9_ROW;   // this lane's output row
+    const uint32_t stride = gridDim.x * NW;
+    D8Geo<NC> g, cur;
+    D8Meta<NC> m1, m2;
+    uint4 v[NC][5];
+    D8Sched sc;
+    sc.ntuples = ntuples;
+    sc.P = stride;
+    sc.wid = blockIdx.x * NW + wv;
+    sc.Ks = (uint32_t)((uint64_t)ntuples * static_pct / 100 / stride);
+    sc.Ts = sc.Ks * stride;
+    sc.Dh = (ntuples - sc.Ts + 7) / 8;
+    sc.k = 0;
+    sc.head = blockIdx.x & 7;
+    sc.tried = 0;
+    sc.pend = 0;
+    d8_fetch(sc, queue, lane);
+    uint32_t tp = d8_resolve(sc, queue, &L.exhausted, lane);
+    d8_fetch(sc, queue, lane);
+    uint32_t t1 = d8_resolve(sc, queue, &L.exhausted, lane);
+    d8_fetch(sc, queue, lane);
+    uint8_t *const wscr = scratch + (size_t)(blockIdx.x * NW + wv) * D8_WSCR;
+    uint4 *const trash = reinterpret_cast<uint4 *>(wscr);
+    uint32_t *const dummy = reinterpret_cast<uint32_t *>(wscr + 2 * 4096);
+    d8_load_meta<NC>(m2, tp, ngroups, nchunks, lane, sync_len, sync_base);
+    d8_geometry<NC>(g, m2, tp, ntuples, n, nchunks, nwords, word_base, lane);
+    d8_issue<NC>(v, g, in, lane);
+    d8_load_meta<NC>(m1, t1, ngroups, nchunks, lane, sync_len, sync_base);
+    cur = g;
+    d8_stage<NC>(cur, v, stws, lane);
+    d8_geometry<NC>(g, m1, t1, ntuples, n, nchunks, nwords, word_base, lane);
+    uint32_t t2 = d8_resolve(sc, queue, &L.exhausted, lane);
+    d8_load_meta<NC>(m1, t2, ngroups, nchunks, lane, sync_len, sync_base);
+    d8_fetch(sc, queue, lane);
+    d8_issue<NC>(v, g, in, lane);
+    while (tp < ntuples) {
+        __builtin_amdgcn_wave_barrier();
+        // ---- decode this lane's chunk of the staged group into its LDS row ----
+        uint32_t c = cur.fast ? cur.lead[0] + cur.off[0] : 0u;   // stage bit of the next code
+        uint32_t wi = 0;                                       // row dword the accumulator starts at
+        uint64_t acc = 0;                                      // pending output bytes (low = next)
+        uint32_t fill = 0;                                     // pending bits in acc (< 32 between lookups)
+        bool redo = !cur.fast;                                 // not staged: every chunk is redone
+        uint32_t wend = redo ? 0u : 16u;                       // dword 16 = the row's spill dword
+        while (__builtin_amdgcn_ballot_w64(wi < wend)) {   // a batch: 4 lookups in one 64-bit window
+            const bool live = wi < wend;
+            const uint32_t a = c >> 5;
+            const uint32_t w0 = stw[a], w1 = stw[a + 1], w2 = stw[a + 2];
+            const uint64_t win = ((uint64_t)__builtin_amdgcn_alignbit(w2, w1, c) << 32) | __builtin_amdgcn_alignbit(w1, w0, c);
+            uint32_t off = 0, e = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {   // 4 x <= 13 bits fit the window
+                e = L.lut[(uint32_t)(win >> off) & MB];
+                acc |= (uint64_t)(e & 0xFFFFFFu) << fill;
+                row[wi] = (uint32_t)acc;
+                fill += (e >> 25) & 0x18u;          // 8 x codes
+                off += (e >> 24) & 15u;             // their bits
+                const uint32_t k32 = fill & 32u;     // a dword is complete
+                acc >>= k32;
+                fill ^= k32;
+                wi = min(wi + (k32 >> 5), wend);
+            }
+            c = live ? c + off : c;
+            // a code longer than 13 bits stops the lane (no code, no bits): take it through the
+            // 12-bit table's escape and its second level (rare: ~0.1% of C2 symbols)
+            const bool esc = live && wi < wend && (e >> 28) == 0u;
+            if (__builtin_amdgcn_ballot_w64(esc)) {
+                if (esc) {
+                    const uint32_t b = c >> 5;
+                    const uint32_t x = __builtin_amdgcn_alignbit(stw[b + 1], stw[b], c);
+                    const uint32_t d = L.dlut[x & ((1u << DC_LUT_BITS) - 1)];
+                    const uint32_t e2 = (K2 && (d & 255u) == 0u)
+                                            ? L.dlut2[min((((d >> 8) & 255u) << K2) | ((x >> DC_LUT_BITS) & kmask),
+                                                          (uint32_t)DC_LUT2_CAP - 1)]
+                                            : 0u;
+                    if ((e2 & 255u) == 0u) {   // longer still, or invalid: the exact redo
+                        redo = true;
+                        wend = wi;
+                    } else {
+                        acc |= (uint64_t)(e2 >> 8) << fill;
+                        row[wi] = (uint32_t)acc;
+                        fill += 8;
+                        c += e2 & 255u;
+                        const uint32_t k32 = fill & 32u;
+                        acc >>= k32;
+                        fill ^= k32;
+                        wi = min(wi + (k32 >> 5), wend);
+                    }
+                }
+            }
+        }
+        // ---- the group's 64 rows -> 4 KiB of contiguous output (16 B per lane per store) ----
+        __builtin_amdgcn_wave_barrier();
+        {
+            uint4 *dst = cur.fast ? reinterpret_cast<uint4 *>(out + (uint64_t)cur.g0 * DC_SYNC_GROUP * S) : trash;
+            const uint32_t *rows = L.rows[wv];
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4) {
+                const uint32_t ch = 16 * s4 + (lane >> 2), p = lane & 3;
+                const uint32_t *r = rows + ch * D9_ROW + 4 * p;
+                dst[s4 * 64 + lane] = make_uint4(r[0], r[1], r[2], r[3]);
+            }
+        }
+        // chunks to redo exactly (as k_huff_decode8: a bit per chunk + its first bit)
+        {
+            const uint32_t gg = cur.g0;
+            const uint64_t m = __ballot(redo);
+            uint64_t *pp = redo ? fix_pos + (uint64_t)gg * DC_SYNC_GROUP + lane : reinterpret_cast<uint64_t *>(dummy) + lane;
+            *pp = (uint64_t)cur.wo[0] * 32 + cur.lead[0] + cur.off[0];
+            uint64_t *mp = gg < ngroups ? fix_mask + gg : reinterpret_cast<uint64_t *>(dummy) + 64;
+            *mp = m;
+        }
+        tp = t1;
+        t1 = t2;
+        cur = g;
+        __builtin_amdgcn_wave_barrier();   // the stage and the rows are rewritten
+        d8_stage<NC>(cur, v, stws, lane);
+        d8_geometry<NC>(g, m1, t1, ntuples, n, nchunks, nwords, word_base, lane);
+        t2 = d8_resolve(sc, queue, &L.exhausted, lane);
+        d8_load_meta<NC>(m1, t2, ngroups, nchunks, lane, sync_len, sync_base);
+        d8_fetch(sc, queue, lane);
+        d8_issue<NC>(v, g, in, lane);
+    }
+    if (lane == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (atomicAdd(queue + 8 * D8_QSTRIDE, 1u) == gridDim.x * NW - 1)
+            for (int h = 0; h <= 8; ++h) atomicExch(queue + h * D8_QSTRIDE, 0u);
+    }
+}
+
 // Exact decode of the chunks k_huff_decode8 flagged (fix_mask: a bit per chunk, fix_pos: the
 // chunk's first bit), compacted into one list by k_huff_fix_list: one chunk per lane, decoded
 // from its span staged in LDS; the 12-bit table and the canonical tables for longer codes
@@ -2062,22 +2281,36 @@ __global__ __launch_bounds__(D8F_WAVES * 64) void k_huff_decode8_fix(const uint3
     uint32_t ra = blockIdx.x * D8F_WAVES + wv;   // round of A; B and C follow by the stride
     auto item_ok = [&](uint32_t r) -> bool { return r < nrounds && r * 64 + (uint32_t)lane < total; };
     auto chunk_of = [&](uint32_t r) -> uint32_t { return item_ok(r) ? list[r * 64 + lane] : ~0u; };
-    uint32_t cha = chunk_of(ra);
-    uint32_t chb = chunk_of(ra + wstride);
+    const uint32_t K2 = (uint32_t)T->dlut2_k, kmask = (1u << K2) - 1;
+    uint32_t cha, chb;
+    {   // the tables into LDS: their loads first, then the first two rounds' list items (in
+        // flight during the stores); their positions, which depend on them, after the barrier
+        // (the positions' dependent loads issued before the copy held its stores back: 29k of a
+        // wave's 121k cycles, r2 diag)
+        constexpr int NT = D8F_WAVES * 64;
+        static_assert((1 << D8_LUT_BITS) / 8 <= 2 * NT && DC_LUT2_CAP / 4 <= 2 * NT && DC_MAX_SYMS <= NT &&
+                      DC_MAX_DIGITS + 1 <= NT, "one copy pass");
+        const uint4 *l1 = reinterpret_cast<const uint4 *>(T->dlut14);
+        const uint2 *l2 = reinterpret_cast<const uint2 *>(T->dlut2);   // dlut2 is 8-B aligned
+        constexpr int N1 = (1 << D8_LUT_BITS) / 8, N2 = DC_LUT2_CAP / 4;
+        const uint4 a0 = l1[t], a1 = t + NT < N1 ? l1[t + NT] : make_uint4(0u, 0u, 0u, 0u);
+        const uint2 b0 = t < N2 ? l2[t] : make_uint2(0u, 0u), b1 = t + NT < N2 ? l2[t + NT] : make_uint2(0u, 0u);
+        const uint16_t sy = t < DC_MAX_SYMS ? T->syms[t] : (uint16_t)0;
+        const bool cn = t <= DC_MAX_DIGITS;
+        const uint32_t fi = cn ? T->first[t] : 0u, co = cn ? T->count[t] : 0u, sa = cn ? T->start[t] : 0u;
+        const uint64_t li = t < 33 ? T->lim[t] : 0ull;
+        cha = chunk_of(ra);
+        chb = chunk_of(ra + wstride);
+        reinterpret_cast<uint4 *>(F.lut)[t] = a0;
+        if (t + NT < N1) reinterpret_cast<uint4 *>(F.lut)[t + NT] = a1;
+        if (t < N2) reinterpret_cast<uint2 *>(F.lut2)[t] = b0;
+        if (t + NT < N2) reinterpret_cast<uint2 *>(F.lut2)[t + NT] = b1;
+        if (t < DC_MAX_SYMS) F.syms[t] = sy;
+        if (cn) { F.first[t] = fi; F.count[t] = co; F.start[t] = sa; }
+        if (t < 33) F.lim[t] = li;
+    }
     uint64_t posa = fix_pos[cha != ~0u ? cha : 0u];
     uint64_t posb = fix_pos[chb != ~0u ? chb : 0u];
-    const uint32_t K2 = (uint32_t)T->dlut2_k, kmask = (1u << K2) - 1;
-    for (int i = t; i < (1 << D8_LUT_BITS) / 8; i += D8F_WAVES * 64)
-        reinterpret_cast<uint4 *>(F.lut)[i] = reinterpret_cast<const uint4 *>(T->dlut14)[i];
-    for (int i = t; i < DC_LUT2_CAP / 4; i += D8F_WAVES * 64)   // dlut2 is 8-B aligned
-        reinterpret_cast<uint2 *>(F.lut2)[i] = reinterpret_cast<const uint2 *>(T->dlut2)[i];
-    for (int i = t; i < DC_MAX_SYMS; i += D8F_WAVES * 64) F.syms[i] = T->syms[i];
-    for (int i = t; i <= DC_MAX_DIGITS; i += D8F_WAVES * 64) {
-        F.first[i] = T->first[i];
-        F.count[i] = T->count[i];
-        F.start[i] = T->start[i];
-    }
-    if (t < 33) F.lim[t] = T->lim[t];
     __syncthreads();
     const int nary = T->n_ary, w = T->w;
     const bool pow2 = (nary & (nary - 1)) == 0;
@@ -2167,9 +2400,11 @@ __global__ __launch_bounds__(D8F_WAVES * 64) void k_huff_decode8_fix(const uint3
                 const uint32_t a = c >> 5;
                 const uint32_t lo = __builtin_amdgcn_alignbit(row[a + 1], row[a], c);
                 uint32_t e = F.lut[lo & ((1u << D8_LUT_BITS) - 1)];
-                const uint32_t i2 = min(((e >> 8) << K2) | ((lo >> DC_LUT_BITS) & kmask), (uint32_t)DC_LUT2_CAP - 1);
-                const uint32_t e2 = F.lut2[i2];
-                e = (e & 255u) ? e : e2;
+                if (__builtin_amdgcn_ballot_w64((e & 255u) == 0u)) {   // the second level, only when a lane needs it
+                    const uint32_t i2 = min(((e >> 8) << K2) | ((lo >> DC_LUT_BITS) & kmask), (uint32_t)DC_LUT2_CAP - 1);
+                    const uint32_t e2 = F.lut2[(e & 255u) ? 0u : i2];
+                    e = (e & 255u) ? e : e2;
+                }
                 if (e == 0) {   // past the second level (rare): canonical search
                     const uint32_t hi = __builtin_amdgcn_alignbit(row[a + 2], row[a + 1], c);
                     e = d8_long_lds(lo, hi, F, nary, w, pow2);
@@ -3195,6 +3430,7 @@ struct dc_ctx {
     uint32_t opt_d8_static;       // decoder: static share of the tuples, percent (0..100)
     uint32_t opt_decode_general;  // 1: always the general decoder (k_huff_decode)
     uint32_t opt_hist_pf;         // histogram: blocks of loads in flight ahead (1..2, 0 = default 1)
+    uint32_t opt_decode_variant;  // fast decoder: 0 one code per lookup (k_huff_decode8), 1 up to 3 (k_huff_decode9)
     // timing
     int timing;
     int nev;
@@ -3342,6 +3578,10 @@ int dc_ctx_set_option(dc_ctx *c, int option, int64_t value)
     case DC_OPT_DECODE_GENERAL:
         if (value != 0 && value != 1) return DC_E_ARG;
         c->opt_decode_general = (uint32_t)value;
+        return DC_OK;
+    case DC_OPT_DECODE_VARIANT:
+        if (value < 0 || value > 1) return DC_E_ARG;
+        c->opt_decode_variant = (uint32_t)value;
         return DC_OK;
     case DC_OPT_HIST_PREFETCH:
         if (value < 0 || value > 2) return DC_E_ARG;
@@ -3632,17 +3872,23 @@ int dc_huff_decode(dc_ctx *c, const uint32_t *d_words, uint64_t bit_base, uint64
         // 12 waves x 2 chains, one workgroup per CU: the stage and the 14-bit table fill the
         // LDS (the 8 x 4 split measured 0.89 vs 0.70 ms on 1 GiB C2: spills)
         const uint32_t spct = c->opt_d8_static;   // clamped to 0..100 by dc_ctx_set_option
-        constexpr int nw = 12;
-        const uint64_t tuples = (groups + 1) / 2;
-        const uint64_t wgs = (tuples + nw - 1) / nw;
-        const uint64_t grid = wgs < 256 ? wgs : 256;   // persistent: one workgroup per CU
+        const uint64_t tuples = (groups + 1) / 2;   // 2 chains (groups) per wave
         if (ensure((void **)&c->d_fix, &c->fix_cap, (groups + 64) * sizeof(uint64_t)) ||
             ensure((void **)&c->d_fixpos, &c->fixpos_cap, (groups * 64 + 64) * sizeof(uint64_t)))
             return DC_E_HIP;
         if (ensure((void **)&c->d_scr, &c->scr_cap, (size_t)D8_SCRATCH_WAVES * D8_WSCR)) return DC_E_HIP;
-        LAUNCH(c, "huff_decode", (k_huff_decode8<12, 2>), grid, 12 * 64, d_words, bit_base, d_sync_base, d_sync_len,
-               n, words, d_table, d_out, c->d_err + 1, c->d_queue, spct, (uint64_t *)c->d_fix,
-               (uint64_t *)c->d_fixpos, (uint8_t *)c->d_scr);
+#define D8_LAUNCH(NW_, NC_)                                                                                   \
+        LAUNCH(c, "huff_decode", (k_huff_decode8<NW_, NC_>), (tuples + NW_ - 1) / NW_ < 256 ? (tuples + NW_ - 1) / NW_ : 256, \
+               NW_ * 64, d_words, bit_base, d_sync_base, d_sync_len, n, words, d_table, d_out, c->d_err + 1,       \
+               c->d_queue, spct, (uint64_t *)c->d_fix, (uint64_t *)c->d_fixpos, (uint8_t *)c->d_scr)
+        if (c->opt_decode_variant == 1) {   // multi-symbol lookups, one group per wave
+            LAUNCH(c, "huff_decode", k_huff_decode9<12>, groups < 256 * 12 ? (groups + 11) / 12 : 256, 12 * 64,
+                   d_words, bit_base, d_sync_base, d_sync_len, n, words, d_table, d_out, c->d_err + 1, c->d_queue,
+                   spct, (uint64_t *)c->d_fix, (uint64_t *)c->d_fixpos, (uint8_t *)c->d_scr);
+        } else {   // one code per lookup, 12 waves x 2 chains
+            D8_LAUNCH(12, 2);
+        }
+#undef D8_LAUNCH
         c->last_groups = groups;
         if (ensure((void **)&c->d_fixlist, &c->fixlist_cap, (groups * 64 + 64) * sizeof(uint32_t))) return DC_E_HIP;
         const uint64_t nchunks = (n + 63) / 64;

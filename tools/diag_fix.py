@@ -22,7 +22,7 @@ torch.cuda.synchronize()
 L = _lib.load("libdc_core.so")
 buf = np.zeros(256 * 16 * 4, np.uint64)
 assert L.dc_diag_read(buf.ctypes.data_as(C.c_void_p), C.c_size_t(buf.nbytes)) == 0
-raw = buf.reshape(-1, 4)[: 256 * 12]
+raw = buf.reshape(-1, 4)[: 256 * 16]
 d = raw.astype(np.float64)
 tot, _, dec, _ = d.T
 tab = (raw[:, 1] & 0xffffffff).astype(np.float64)
