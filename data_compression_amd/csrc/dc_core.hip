@@ -201,16 +201,14 @@ __global__ __launch_bounds__(256) void k_huff_table(const uint64_t *__restrict__
     __shared__ uint64_t s_q2[TBL_SORT_MAX];
     __shared__ int16_t s_parent[TBL_NODES];
     __shared__ int32_t s_len[DC_MAX_SYMS];
-    __shared__ uint32_t s_cnt[DC_MAX_DIGITS + 2];
+    __shared__ __attribute__((aligned(16))) uint32_t s_cnt[DC_MAX_DIGITS + 2];   // also the merge's 64-key window
     __shared__ uint32_t s_startv[DC_MAX_DIGITS + 2];
     __shared__ uint32_t s_starti[DC_MAX_DIGITS + 2];
     __shared__ uint32_t s_code[256];
     __shared__ uint32_t s_nb[256];
     __shared__ int s_k, s_min, s_max, s_maxbits, s_bad;
-    __shared__ uint32_t s_tot_esc[256];
     __shared__ uint32_t s_rbase[DC_MAX_DIGITS + 1];
     __shared__ uint32_t s_wcnt[4][DC_MAX_DIGITS + 1];
-    __shared__ uint16_t s_syms[DC_MAX_SYMS];
 
     const int t = threadIdx.x;
     const int leaves = M + 1;
@@ -256,62 +254,72 @@ __global__ __launch_bounds__(256) void k_huff_table(const uint64_t *__restrict__
         }
         TBL_STAMP(8);
         if (nary <= 32 && t < 64) {
-            // two-queue merge by wave 0 in rounds, no LDS access inside a round: at the start
-            // of a round lanes 0-31 load the next 32 leaf keys and lanes 32-63 the next 32
-            // internal sums; every pick reads both queue heads from that window register
-            // (v_readlane at a uniform index), a new internal node is written back into the
-            // window (one lane's select) so the same round can pick it, and the round's picks get
-            // their parents in one parallel LDS store at its end. A round makes 32/n merges
-            // (<= 32 picks), so the window never runs out. (The one-lane loop this replaces
-            // waited an LDS round trip per pick: 95k of the kernel's 203k cycles.)
+            // Batched two-queue merge by wave 0. Leaves (and dummies) sit sorted in s_key as
+            // count << 11 | index; internal nodes are created in non-decreasing count order
+            // (queue s_q2), and on equal counts a leaf precedes an internal node and an older
+            // internal node a younger one, as in the reference's stable re-sort (:672-731).
+            // Let smin = the sum of the n smallest live nodes: every node created from now on
+            // has count >= smin and a larger index, so all live nodes of count <= smin are picked
+            // before any new one, n at a time, in sorted order. A round therefore takes a window
+            // of 32 leaves and 32 internal nodes, ranks the 64 by binary search in the other
+            // side, keeps the prefix of count <= smin (cut at a window's last key when more
+            // nodes lie beyond it), and creates floor(prefix / n) nodes at once: ~15-20 rounds
+            // on text or bytes where the one-pick-at-a-time loop took 512 dependent picks.
+            // Key of an internal node: count << 11 | 2047 (ties: after every leaf).
             const int lane = t;
             const int first_internal = leaves + dummies;
-            const int mpr = 32 / nary;
-            int h1 = 0, h2 = 0, t2 = 0, active = items, next = first_internal;
+            const bool isL = lane < 32;
+            const int j = isL ? lane : lane - 32;
+            uint64_t *const s_win = reinterpret_cast<uint64_t *>(s_cnt);   // 64 window keys (reused scratch)
+            uint64_t *const s_B = s_q2 + (TBL_SORT_MAX - 64);               // the round's nodes in rank order
+            int h1 = 0, h2 = 0, t2 = 0, active = items, nxt = first_internal;
+            constexpr uint64_t INF = ~0ull;
             while (active > 1) {
-                const int li0 = h1, qi0 = h2, next0 = next;
-                const int lj = li0 + lane, qj = qi0 + lane - 32;
-                uint64_t win = lane < 32 ? (lj < items ? s_key[lj] : ~0ull) : (qj < t2 ? s_q2[qj] : ~0ull);
-                uint32_t wlo = (uint32_t)win, whi = (uint32_t)(win >> 32);
-                int picked = 0, npick = 0;   // lane p: node index of the round's p-th pick
-                uint32_t slo = 0, shi = 0;    // lane m: the round's m-th sum (stored at its end)
-                int nmerge = 0;
-                // one pick, branch-free (leaf on ties: c1 <= c2, as the reference's stable order)
-                auto pick = [&](uint64_t &sum) {
-                    const int i1 = h1 - li0, i2 = 32 + h2 - qi0;
-                    const uint64_t k1 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)whi, i1) << 32) |
-                                        (uint32_t)__builtin_amdgcn_readlane((int)wlo, i1);
-                    const uint64_t c2 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)whi, i2) << 32) |
-                                        (uint32_t)__builtin_amdgcn_readlane((int)wlo, i2);
-                    const uint64_t c1 = k1 >> 11;
-                    const bool tl = (h1 < items) & ((h2 == t2) | (c1 <= c2));
-                    const int idx = tl ? (int)(k1 & 2047u) : first_internal + h2;
-                    sum += tl ? c1 : c2;
-                    h1 += tl ? 1 : 0;
-                    h2 += tl ? 0 : 1;
-                    picked = lane == npick ? idx : picked;
-                    ++npick;
-                };
-                for (int m = 0; m < mpr && active > 1; ++m) {
+                const uint64_t key = isL ? (h1 + j < items ? s_key[h1 + j] : INF)
+                                         : (h2 + j < t2 ? ((s_q2[h2 + j] << 11) | 2047ull) : INF);
+                s_win[lane] = key;
+                __builtin_amdgcn_wave_barrier();
+                // rank in the window union: own position + nodes of the other side before it
+                const uint64_t *other = isL ? s_win + 32 : s_win;
+                int lo = 0;
+#pragma unroll
+                for (int st = 32; st >= 1; st >>= 1)
+                    if (lo + st <= 32 && other[lo + st - 1] < key) lo += st;
+                const int rank = j + lo;
+                const bool valid = key != INF;
+                if (valid) s_B[rank] = key;
+                __builtin_amdgcn_wave_barrier();
+                uint64_t smin = 0;   // every lane sums the n smallest (broadcast reads, no shuffles)
+                for (int q = 0; q < nary; ++q) smin += s_B[q] >> 11;
+                const uint64_t boundL = h1 + 32 < items ? s_win[31] : INF;
+                const uint64_t boundQ = t2 - h2 > 32 ? s_win[63] : INF;
+                const bool qual = valid && (key >> 11) <= smin && key <= boundL && key <= boundQ;
+                const int cq = __popcll(__ballot(qual));
+                int m = cq / nary;
+                if (m == 0) { m = 1; if (lane == 0) s_bad = 1; }   // cannot happen: n smallest always qualify
+                const int used = m * nary;
+                const bool inB = valid && rank < used;
+                const int na = __popcll(__ballot(inB && isL));
+                if (lane < m) {
                     uint64_t sum = 0;
-                    if (nary == 2) { pick(sum); pick(sum); }
-                    else for (int q = 0; q < nary; ++q) pick(sum);
-                    if (lane == 32 + t2 - qi0) {   // (t2 - qi0 >= 32: not reachable this round)
-                        wlo = (uint32_t)sum;
-                        whi = (uint32_t)(sum >> 32);
-                    }
-                    if (lane == m) { slo = (uint32_t)sum; shi = (uint32_t)(sum >> 32); }
-                    ++nmerge;
-                    ++t2;
-                    ++next;
-                    active -= nary - 1;
+                    for (int q = 0; q < nary; ++q) sum += s_B[lane * nary + q] >> 11;
+                    s_q2[t2 + lane] = sum;
                 }
-                if (lane < nmerge) s_q2[t2 - nmerge + lane] = ((uint64_t)shi << 32) | slo;
-                if (lane < npick && picked < TBL_NODES) s_parent[picked] = (int16_t)(next0 + lane / nary);
-                if (tree && lane < npick && lane % nary < 2 && next0 + lane / nary < TBL_NODES)   // :978-979
-                    (lane % nary ? tree->right : tree->left)[next0 + lane / nary] = picked;
+                if (inB) {
+                    const int node = isL ? (int)(key & 2047u) : first_internal + h2 + j;
+                    const int par = nxt + rank / nary;
+                    if (node < TBL_NODES) s_parent[node] = (int16_t)par;
+                    if (tree && rank % nary < 2 && par < TBL_NODES)   // first two children (:978-979)
+                        (rank % nary ? tree->right : tree->left)[par] = node;
+                }
+                __builtin_amdgcn_wave_barrier();
+                h1 += na;
+                h2 += used - na;
+                t2 += m;
+                nxt += m;
+                active -= m * (nary - 1);
             }
-            if (lane == 0 && next >= TBL_NODES) s_bad = 1;
+            if (lane == 0 && nxt >= TBL_NODES) s_bad = 1;
         } else if (t == 0) {
             // two-queue merge; both queues' heads and next elements held in registers, the
             // element after them prefetched from LDS when a head is consumed, so no pick
@@ -423,25 +431,35 @@ __global__ __launch_bounds__(256) void k_huff_table(const uint64_t *__restrict__
         }
     }
     __syncthreads();
-    if (t == 0) {
-        uint32_t code = 0, acc = 0;   // reference: int arithmetic, wraps mod 2^32
-        for (int L = 0; L <= DC_MAX_DIGITS; ++L) {
-            if (L > maxL) { s_starti[L] = acc; s_startv[L] = 0; continue; }
-            s_starti[L] = acc;
-            if (L >= minL && L <= maxL) {
-                s_startv[L] = code;
-                code = (code + s_cnt[L]) * (uint32_t)nary;
-                acc += s_cnt[L];
-            } else {
-                s_startv[L] = 0;
+    TBL_STAMP(9);
+    if (t < 64) {
+        // first canonical value and first sorted slot per length (:1540-1568; int arithmetic,
+        // wraps mod 2^32): the lengths' counts held one per lane, the recurrence walked by
+        // readlane over [minL, maxL] only (the one-lane loop over every length read LDS per
+        // step: 16k cycles)
+        uint32_t code = 0, acc = 0;
+        for (int base = minL; base <= min(maxL, DC_MAX_DIGITS); base += 64) {
+            const int L = base + t;
+            const uint32_t cl = (L <= maxL && L <= DC_MAX_DIGITS) ? s_cnt[L] : 0u;
+            uint32_t sv = 0, si = 0;
+            const int span = min(64, min(maxL, DC_MAX_DIGITS) - base + 1);
+            for (int q = 0; q < span; ++q) {
+                const uint32_t cq = (uint32_t)__builtin_amdgcn_readlane((int)cl, q);
+                if (t == q) { sv = code; si = acc; }
+                code = (code + cq) * (uint32_t)nary;
+                acc += cq;
             }
+            if (t < span) { s_startv[L] = sv; s_starti[L] = si; }
         }
+        for (int L = t; L < minL && L <= DC_MAX_DIGITS; L += 64) { s_startv[L] = 0; s_starti[L] = 0; }
+        for (int L = maxL + 1 + t; L <= DC_MAX_DIGITS; L += 64) { s_startv[L] = 0; s_starti[L] = acc; }
     }
     for (int s = t; s < 256; s += 256) { s_code[s] = 0; s_nb[s] = 0; }
     __syncthreads();
     for (int L = t; L <= DC_MAX_DIGITS; L += 256) s_rbase[L] = 0;
     for (int q = t; q < 4 * (DC_MAX_DIGITS + 1); q += 256) (&s_wcnt[0][0])[q] = 0;
     __syncthreads();
+    TBL_STAMP(10);
     const int wvt = t >> 6, lnt = t & 63;
     for (int i0 = 0; i0 < leaves; i0 += 256) {
         // canonical rank = symbols of the same length before this one (index order):
@@ -478,7 +496,6 @@ __global__ __launch_bounds__(256) void k_huff_table(const uint64_t *__restrict__
             T->enc_len[i] = L;
             T->enc_val[i] = val;
             T->syms[s_starti[L] + rank] = (uint16_t)i;
-            s_syms[(s_starti[L] + rank) & (DC_MAX_SYMS - 1)] = (uint16_t)i;
             if (i < 256) {
                 // L base-n digits of val, MSB-first, w bits each (n = 2^w: the bits of val)
                 if ((long long)L * w <= 32) {
@@ -505,6 +522,7 @@ __global__ __launch_bounds__(256) void k_huff_table(const uint64_t *__restrict__
             else { T->last_written = 0; T->enc_len[i] = 0; T->enc_val[i] = 0; }
         }
     }
+    TBL_STAMP(11);
     for (int i = leaves + t; i < DC_MAX_SYMS; i += 256) {
         T->lengths[i] = 0; T->enc_len[i] = 0; T->enc_val[i] = 0;
     }
@@ -524,13 +542,56 @@ __global__ __launch_bounds__(256) void k_huff_table(const uint64_t *__restrict__
         else lim = ((uint64_t)s_startv[Ld] + s_cnt[Ld]) << (32 - Ld * w);
         T->lim[t] = lim;
     }
-    TBL_STAMP(4);
-    // one-symbol table in LDS (reuses s_key): window -> sym | nbits<<8, 0 = longer code
-    uint32_t *s_lut1 = reinterpret_cast<uint32_t *>(s_key);
-    for (int e = t; e < (1 << DC_LUT_BITS); e += 256) s_lut1[e] = 0;
-    __syncthreads();
+    __syncthreads();   // s_code, s_nb, s_maxbits
     T->code[t] = s_code[t];
     T->nbits[t] = s_nb[t];
+    if (t == 0) {
+#ifdef DC_DIAG
+        g_tbldiag[4] = g_tbldiag[7] = __builtin_amdgcn_s_memtime();
+#endif
+        T->n_ary = nary;
+        T->w = w;
+        T->max_symbol_value = M;
+        T->max_bits = s_maxbits;
+        T->min_len = minL;
+        T->max_len = maxL;
+        T->dec_ready = 0;   // the decoder tables follow (k_huff_pack's builder, or k_dec_tables)
+        T->status = s_bad ? DC_E_ARG : (s_maxbits > 32 ? DC_E_CODE_TOO_LONG : DC_OK);
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// Decoder tables of a code table (dc_gpu.h: lut, dlut, dlut2, dlut14), built by one
+// 256-thread workgroup from the canonical arrays k_huff_table wrote. Not on the encoder's
+// critical path: k_huff_pack runs it in an extra workgroup beside the pack (its LDS is the
+// pack stage), and dc_huff_decode launches k_dec_tables first, which returns at once when the
+// tables are current (dec_ready). 55k of k_huff_table's 184k cycles moved off the encode (r2).
+// ------------------------------------------------------------------------------------
+struct DecBuildLds {
+    uint32_t lut1[1 << DC_LUT_BITS];   // one-symbol table, MSB-first 12-bit window -> sym | nbits << 8
+    uint16_t esc[1 << DC_LUT_BITS];    // escape id per dlut entry
+    uint32_t code[256], nb[256];
+    uint32_t startv[DC_MAX_DIGITS + 2], cnt[DC_MAX_DIGITS + 2], starti[DC_MAX_DIGITS + 2];
+    uint16_t syms[DC_MAX_SYMS];
+    uint32_t tot_esc[256];
+    int nesc;
+};
+
+static __device__ void dec_tables_build(dc_dtable *__restrict__ T, DecBuildLds &S)
+{
+    const int t = threadIdx.x;
+    const int nary = T->n_ary, w = T->w, minL = T->min_len, maxL = T->max_len, maxbits = T->max_bits;
+    S.code[t] = T->code[t];
+    S.nb[t] = T->nbits[t];
+    for (int L = t; L < DC_MAX_DIGITS + 1; L += 256) {
+        S.startv[L] = T->first[L];
+        S.cnt[L] = T->count[L];
+        S.starti[L] = T->start[L];
+    }
+    for (int i = t; i < DC_MAX_SYMS; i += 256) S.syms[i] = T->syms[i];
+    for (int e = t; e < (1 << DC_LUT_BITS); e += 256) S.lut1[e] = 0;
+    __syncthreads();
+    uint32_t *const s_lut1 = S.lut1;
     if ((nary & (nary - 1)) == 0) {
         // n = 2^w: a 12-bit window's code is the canonical one whose value at its length
         // matches (lengths ascending), decoded per entry
@@ -538,8 +599,8 @@ __global__ __launch_bounds__(256) void k_huff_table(const uint64_t *__restrict__
             uint32_t v1 = 0;
             for (int L = minL; L <= maxL && L * w <= DC_LUT_BITS; ++L) {
                 const uint32_t b = (uint32_t)(L * w), v = (uint32_t)e >> (DC_LUT_BITS - b);
-                if (v - s_startv[L] < s_cnt[L]) {
-                    const uint32_t sym = s_syms[(s_starti[L] + v - s_startv[L]) & (DC_MAX_SYMS - 1)];
+                if (v - S.startv[L] < S.cnt[L]) {
+                    const uint32_t sym = S.syms[(S.starti[L] + v - S.startv[L]) & (DC_MAX_SYMS - 1)];
                     v1 = sym < 256 ? (sym | (b << 8)) : 0u;
                     break;
                 }
@@ -547,15 +608,14 @@ __global__ __launch_bounds__(256) void k_huff_table(const uint64_t *__restrict__
             s_lut1[e] = v1;
         }
     } else {   // thread s fills its own code's span
-        const uint32_t nb = s_nb[t];
+        const uint32_t nb = S.nb[t];
         if (nb != 0 && nb <= DC_LUT_BITS) {
             const uint32_t span = 1u << (DC_LUT_BITS - nb);
-            const uint32_t base = s_code[t] << (DC_LUT_BITS - nb);
+            const uint32_t base = S.code[t] << (DC_LUT_BITS - nb);
             for (uint32_t j = 0; j < span; ++j) s_lut1[base + j] = (uint32_t)t | (nb << 8);
         }
     }
     __syncthreads();
-    TBL_STAMP(5);
     // two-symbol table: a window holding a whole second code after the first yields both
     // (DC_LUT_* layout in dc_gpu.h)
     for (int e = t; e < (1 << DC_LUT_BITS); e += 256) {
@@ -570,12 +630,11 @@ __global__ __launch_bounds__(256) void k_huff_table(const uint64_t *__restrict__
         }
         T->lut[e] = v;
     }
-    TBL_STAMP(6);
     // decoder tables on the LSB-first window (dc_gpu.h): dlut = the one-symbol table at the
     // bit-reversed index; escape prefixes (entries 0) numbered in index order; dlut2 filled
     // per symbol: a code of 12 < b <= 12 + k bits covers 2^(12 + k - b) entries of its
     // prefix's sub-table (no per-entry search)
-    uint16_t *s_esc = reinterpret_cast<uint16_t *>(s_q2);   // escape id per dlut entry
+    uint16_t *const s_esc = S.esc;
     constexpr int PER = (1 << DC_LUT_BITS) / 256;
     uint32_t d1[PER], nesc = 0;
 #pragma unroll
@@ -587,23 +646,23 @@ __global__ __launch_bounds__(256) void k_huff_table(const uint64_t *__restrict__
     }
     {   // exclusive scan of the per-thread escape counts: DPP inside each wave, 4 wave totals
         const uint32_t inc = wave_scan_incl(nesc);
-        if ((t & 63) == 63) s_tot_esc[t >> 6] = inc;
+        if ((t & 63) == 63) S.tot_esc[t >> 6] = inc;
         __syncthreads();
         uint32_t before = 0, all = 0;
         for (int q = 0; q < 4; ++q) {
-            const uint32_t v = s_tot_esc[q];
+            const uint32_t v = S.tot_esc[q];
             before += (q < (t >> 6)) ? v : 0u;
             all += v;
         }
         __syncthreads();
-        s_tot_esc[t] = before + inc - nesc;
-        if (t == 0) s_k = (int)all;   // escape prefixes
+        S.tot_esc[t] = before + inc - nesc;
+        if (t == 0) S.nesc = (int)all;   // escape prefixes
         __syncthreads();
     }
-    const uint32_t E = (uint32_t)s_k;
-    const uint32_t K = (uint32_t)min(max(s_maxbits - DC_LUT_BITS, 1), 8);
-    const bool l2ok = E > 0 && E <= 256 && (E << K) <= DC_LUT2_CAP && s_maxbits <= 32;
-    uint32_t id = s_tot_esc[t];
+    const uint32_t E = (uint32_t)S.nesc;
+    const uint32_t K = (uint32_t)min(max(maxbits - DC_LUT_BITS, 1), 8);
+    const bool l2ok = E > 0 && E <= 256 && (E << K) <= DC_LUT2_CAP && maxbits <= 32;
+    uint32_t id = S.tot_esc[t];
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
         const uint32_t i = (uint32_t)(t * PER + j);
@@ -614,9 +673,9 @@ __global__ __launch_bounds__(256) void k_huff_table(const uint64_t *__restrict__
     for (int q = t; q < DC_LUT2_CAP; q += 256) T->dlut2[q] = 0;
     __syncthreads();   // s_esc complete; dlut2 zeroed (same workgroup: global writes ordered by the barrier)
     if (l2ok) {
-        const uint32_t nb = s_nb[t];
+        const uint32_t nb = S.nb[t];
         if (nb > DC_LUT_BITS && nb <= DC_LUT_BITS + K) {
-            const uint32_t c = s_code[t], tl = nb - DC_LUT_BITS;
+            const uint32_t c = S.code[t], tl = nb - DC_LUT_BITS;
             const uint32_t pre = __builtin_bitreverse32(c >> tl) >> (32 - DC_LUT_BITS);   // first 12 stream bits
             const uint32_t rt = __builtin_bitreverse32(c & ((1u << tl) - 1)) >> (32 - tl);
             const uint32_t base = (uint32_t)s_esc[pre] << K;
@@ -648,19 +707,21 @@ __global__ __launch_bounds__(256) void k_huff_table(const uint64_t *__restrict__
             d14[p] = pr;
         }
     }
-    if (t == 0) {
-        T->dlut2_k = l2ok ? (int32_t)K : 0;
-#ifdef DC_DIAG
-        g_tbldiag[7] = __builtin_amdgcn_s_memtime();
-#endif
-        T->n_ary = nary;
-        T->w = w;
-        T->max_symbol_value = M;
-        T->max_bits = s_maxbits;
-        T->min_len = minL;
-        T->max_len = maxL;
-        T->status = s_bad ? DC_E_ARG : (s_maxbits > 32 ? DC_E_CODE_TOO_LONG : DC_OK);
+    if (t == 0) T->dlut2_k = l2ok ? (int32_t)K : 0;
+    __syncthreads();
+    if (t == 0) {   // every table store of the workgroup before the flag (agent scope)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __hip_atomic_store(&T->dec_ready, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+}
+
+// dc_huff_decode's first launch: the decoder tables unless they are current
+__global__ __launch_bounds__(256) void k_dec_tables(dc_dtable *__restrict__ T, int *__restrict__ err_clear)
+{
+    __shared__ DecBuildLds S;
+    if (threadIdx.x == 0) err_clear[0] = 0;
+    if (__hip_atomic_load(&T->dec_ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) || T->status != DC_OK) return;
+    dec_tables_build(T, S);
 }
 
 // summarize_tree_with_lengths (n_ary_huffman.c:1033-1093) for an arbitrary node list:
@@ -885,14 +946,21 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
                                                    uint32_t *__restrict__ out, uint64_t *__restrict__ sync_base,
                                                    uint16_t *__restrict__ sync_len, uint32_t sync_syms,
                                                    uint64_t nblocks, uint64_t words_cap,
-                                                   const int *__restrict__ err)
+                                                   const int *__restrict__ err, int build_dec)
 {
     __shared__ uint2 s_tab[256];
     __shared__ uint8_t s_nb8[256];   // bit lengths alone: pass A reads 1 byte, not 8
     __shared__ __attribute__((aligned(16))) uint32_t s_stage[PACK_BLK_WORDS];
     __shared__ uint32_t s_scan[4];
     __shared__ uint32_t s_tot[PACK_PIECES][4];
+    static_assert(sizeof(DecBuildLds) <= sizeof(s_stage), "decoder-table builder uses the stage");
     const int t = threadIdx.x;
+    if (build_dec && blockIdx.x == 0) {   // workgroup 0: the decoder tables, beside the pack
+        if (T->status == DC_OK)
+            dec_tables_build(const_cast<dc_dtable *>(T), *reinterpret_cast<DecBuildLds *>(s_stage));
+        return;
+    }
+    const uint64_t bx = blockIdx.x - (uint64_t)build_dec, gstride = gridDim.x - (uint64_t)build_dec;
     // device-side guards (no host round trip): a byte without a code (plan error) or an
     // output buffer smaller than the planned stream -> write nothing
     if (err[0] != 0 || ((bit_base & 31) + block_off[nblocks] + 31) / 32 > words_cap) return;
@@ -903,7 +971,7 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
     const uint32_t slog = sync_syms ? (uint32_t)__builtin_ctz(sync_syms) : 0u;   // S is a power of two
     __syncthreads();
 
-    for (uint64_t b = blockIdx.x; b < nblocks; b += gridDim.x) {
+    for (uint64_t b = bx; b < nblocks; b += gstride) {
         const uint64_t blk_start = b * (uint64_t)DC_BLOCK_BYTES;
         const uint64_t blk_end = (blk_start + DC_BLOCK_BYTES < n) ? blk_start + DC_BLOCK_BYTES : n;
         const uint64_t blk_abs = bit_base + block_off[b];
@@ -1812,7 +1880,7 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode8(const uint32_t *__rest
     // read length 0
     // D8_LUT_BITS first level from the 12-bit one and its second level: 2.9% of C2 chunks hold a
     // code of > 14 bits (to the exact redo), 6.6% one of > 12
-    // the 14-bit first level (dc_dtable.dlut14, built by k_huff_table): 2.5% of C2 chunks
+    // the 14-bit first level (dc_dtable.dlut14, built by dec_tables_build): 2.5% of C2 chunks
     // hold a code of > 14 bits (to the exact redo)
     static_assert(D8_LUT_BITS == DC_LUT14_BITS, "table width");
     for (int i = t; i < (1 << D8_LUT_BITS) / 8; i += NT)
@@ -3800,8 +3868,9 @@ int dc_huff_pack_async(dc_ctx *c, const uint8_t *d_in, uint64_t n, const dc_dtab
     // 0.452 ms against 0.481 at 4096, 0.469 at 32768, 0.504 at 1024 (r1 v15 A/B)
     const uint64_t gmax = c->opt_pack_grid ? c->opt_pack_grid : (nb + 1) / 2;
     const uint64_t grid = nb < gmax ? nb : gmax;
-    LAUNCH(c, "huff_pack", k_huff_pack, grid, 256, d_in, n, d_table, (const uint64_t *)c->d_off, bit_base, d_words,
-           d_sync_base, d_sync_len, sync_syms, nb, words_cap, (const int *)c->d_err);
+    // + workgroup 0: the decoder tables (k_huff_table leaves them to the pack's idle CU time)
+    LAUNCH(c, "huff_pack", k_huff_pack, grid + 1, 256, d_in, n, d_table, (const uint64_t *)c->d_off, bit_base, d_words,
+           d_sync_base, d_sync_len, sync_syms, nb, words_cap, (const int *)c->d_err, 1);
     return DC_OK;
 }
 
@@ -3867,7 +3936,8 @@ int dc_huff_decode(dc_ctx *c, const uint32_t *d_words, uint64_t bit_base, uint64
     if (n == 0) return DC_OK;
     if (words < 4) return DC_E_ARG;
     const uint64_t groups = dc_huff_sync_groups(n, S);
-    HIPCHK(hipMemsetAsync(c->d_err + 1, 0, sizeof(int), c->stream));
+    // decoder tables unless the pack built them (returns at once then); clears the error flag
+    LAUNCH(c, "dec_tables", k_dec_tables, 1, 256, const_cast<dc_dtable *>(d_table), c->d_err + 1);
     if (S == 64 && n < (1ull << 37) && words < (1ull << 31) && !c->opt_decode_general) {
         // 12 waves x 2 chains, one workgroup per CU: the stage and the 14-bit table fill the
         // LDS (the 8 x 4 split measured 0.89 vs 0.70 ms on 1 GiB C2: spills)

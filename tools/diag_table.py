@@ -21,7 +21,9 @@ torch.cuda.synchronize()
 L = _lib.load("libdc_core.so")
 buf = np.zeros(16, np.uint64)
 assert L.dc_diag_tbl_read(buf.ctypes.data_as(C.c_void_p)) == 0
-names = ["keys", "sort", "merge", "depth", "canonical", "lut1", "lut2sym", "dlut"]
-d = np.diff(buf[:8].astype(np.int64))
-print("table phases (cycles):", {n: int(v) for n, v in zip(names[1:], d)}, "total", int(buf[7] - buf[0]),
-      "| sort", int(buf[8] - buf[1]), "merge", int(buf[2] - buf[8]))
+names = ["keys", "sort", "merge", "depth", "canonical"]
+d = np.diff(buf[:5].astype(np.int64))
+print("table phases (cycles):", {n: int(v) for n, v in zip(names[1:], d)}, "total", int(buf[4] - buf[0]),
+      "| sort", int(buf[8] - buf[1]), "merge", int(buf[2] - buf[8]),
+      "| canonical: counts", int(buf[9] - buf[3]), "prefix", int(buf[10] - buf[9]), "ranks", int(buf[11] - buf[10]),
+      "tail", int(buf[4] - buf[11]))
