@@ -100,7 +100,7 @@ def main():
 
     if a.frontend:   # C5: front-end bodies + halo/LITERAL/re-cut exchanges, then sharded Huffman
         from data_compression_amd.dist import ShardedSmall
-        ss = ShardedSmall(c)
+        ss = ShardedSmall(c, table_mode=a.table_mode)
 
         def encode():   # noqa: F811
             state["s"] = ss.encode(x, a.nary, S)
@@ -136,7 +136,13 @@ def main():
     # ---- correctness of the measured configuration (outside the timed region) ----------
     st = c.pack_status(state["s"].table if a.frontend else tab)
     y = state["dec"] if a.frontend else out
-    ok = st == 0 and c.decode_status() == 0 and bool(torch.equal(y, x))
+    if a.frontend and world > 1:
+        # a rank's decoded front-end segment covers a different byte range than its input
+        # shard (the re-cut moves bytes between ranks): compare the concatenations through a
+        # position-weighted checksum over global offsets
+        ok = st == 0 and c.decode_status() == 0 and _concat_equal(y, x, world, dev)
+    else:
+        ok = st == 0 and c.decode_status() == 0 and bool(torch.equal(y, x))
     bits = state["s"].bits if a.frontend else int(total.item())   # this rank's payload bits
     if world > 1:
         okt = torch.tensor([1 if ok else 0], device=dev)
@@ -226,6 +232,32 @@ def main():
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def _pos_checksum(t, off):
+    """sum over i of (t[i] + 1) * w(off + i) mod 2^64, w a 32-bit multiplicative hash of the
+    global position (int64 arithmetic wraps)."""
+    h = torch.zeros((), dtype=torch.int64, device=t.device)
+    step = 1 << 26
+    for a in range(0, t.numel(), step):
+        v = t[a: a + step].to(torch.int64) + 1
+        idx = torch.arange(off + a, off + a + v.numel(), dtype=torch.int64, device=t.device)
+        h += (v * ((idx * 0x9E3779B1) & 0xFFFFFFFF)).sum()
+    return h
+
+
+def _concat_equal(y, x, world, dev):
+    """Whether the ranks' y segments, concatenated in rank order, equal the ranks' x shards
+    concatenated (lengths and position-weighted checksums, summed over ranks)."""
+    n = torch.tensor([y.numel(), x.numel()], dtype=torch.int64, device=dev)
+    alln = [torch.empty_like(n) for _ in range(world)]
+    dist.all_gather(alln, n)
+    alln = [v.tolist() for v in alln]
+    r = dist.get_rank()
+    oy, ox = sum(v[0] for v in alln[:r]), sum(v[1] for v in alln[:r])
+    hs = torch.stack([_pos_checksum(y, oy), _pos_checksum(x, ox)])
+    dist.all_reduce(hs)
+    return sum(v[0] for v in alln) == sum(v[1] for v in alln) and bool(hs[0] == hs[1])
 
 
 CFG_TEXT = {"C2": "enwik-like text", "C3": "uniform random bytes", "C4": "Zipf s=1 bytes",

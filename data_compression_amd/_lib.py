@@ -95,10 +95,12 @@ def _declare_core(L):
         "dc_huff_sync_groups": ([u64, u32], u64),
         "dc_huff_words_needed": ([u64, u64], u64),
         "dc_huff_pack_async": ([vp, P, u64, P, u64, P, u64, P, P, u32], i32),
+        "dc_huff_pack_async_dev": ([vp, P, u64, P, P, P, u64, P, P, u32], i32),
         "dc_huff_pack_status": ([vp, P], i32),
         "dc_huff_plan_offsets": ([vp, P, u64, C.POINTER(u64)], i32),
         "dc_huff_block_hist": ([vp, P, u64], i32),
         "dc_huff_decode": ([vp, P, u64, u64, P, P, u32, u64, P, P], i32),
+        "dc_huff_decode_dev": ([vp, P, P, u64, P, P, u32, u64, P, P], i32),
         "dc_huff_decode_status": ([vp], i32),
         "dc_huff_decode_redo_count": ([vp, C.POINTER(u64)], i32),
         "dc_huff_base64url": ([vp, P, u64, u64, P], i32),
@@ -122,6 +124,8 @@ def _declare_core(L):
         "dc_small_compress": ([vp, P, u64, P, C.POINTER(u64)], i32),
         "dc_small_decompress": ([vp, P, u64, P, C.POINTER(u64)], i32),
         "dc_small_compress_body": ([vp, P, u64, i32, u64, P, C.POINTER(u64)], i32),
+        "dc_small_compress_body_plan": ([vp, P, u64, i32, u64, C.POINTER(u64)], i32),
+        "dc_small_compress_body_write": ([vp, P, u64, i32, u64, P, C.POINTER(u64)], i32),
         "dc_small_decompress_body": ([vp, P, u64, P, C.POINTER(u64)], i32),
         "dc_host_ctx": ([], vp),
         "dc_huff_compress_bound": ([u64, u32], u64),

@@ -912,9 +912,11 @@ __global__ __launch_bounds__(256) void k_block_final_wide(const uint32_t *__rest
 // zero every word that two blocks share (the words holding a block start) before
 // k_huff_pack OR-merges into them
 __global__ void k_zero_bounds(const uint64_t *__restrict__ off, uint64_t nblocks, uint64_t bit_base,
+                              const uint64_t *__restrict__ d_base,
                               uint32_t *__restrict__ words, uint64_t words_cap, int *__restrict__ err)
 {
     const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (d_base) bit_base += *d_base;   // device-resident shard offset (dist: no host read)
     if (b > nblocks || err[0] != 0) return;
     if (((bit_base & 31) + off[nblocks] + 31) / 32 > words_cap) {
         if (b == 0) err[2] = 1;
@@ -943,7 +945,7 @@ __global__ void k_zero_bounds(const uint64_t *__restrict__ off, uint64_t nblocks
 __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ in, uint64_t n,
                                                    const dc_dtable *__restrict__ T,
                                                    const uint64_t *__restrict__ block_off, uint64_t bit_base,
-                                                   uint32_t *__restrict__ out, uint64_t *__restrict__ sync_base,
+                                                   const uint64_t *__restrict__ d_base, uint32_t *__restrict__ out, uint64_t *__restrict__ sync_base,
                                                    uint16_t *__restrict__ sync_len, uint32_t sync_syms,
                                                    uint64_t nblocks, uint64_t words_cap,
                                                    const int *__restrict__ err, int build_dec)
@@ -961,6 +963,7 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
         return;
     }
     const uint64_t bx = blockIdx.x - (uint64_t)build_dec, gstride = gridDim.x - (uint64_t)build_dec;
+    if (d_base) bit_base += *d_base;   // device-resident shard offset (dist: no host read)
     // device-side guards (no host round trip): a byte without a code (plan error) or an
     // output buffer smaller than the planned stream -> write nothing
     if (err[0] != 0 || ((bit_base & 31) + block_off[nblocks] + 31) / 32 > words_cap) return;
@@ -1377,7 +1380,7 @@ static __device__ __forceinline__ void decode_chunk_hbm(R rd, uint32_t sh, uint3
     }
 }
 
-__global__ __launch_bounds__(DEC_WAVES * 64) void k_huff_decode(const uint32_t *__restrict__ in, uint64_t bit_base,
+__global__ __launch_bounds__(DEC_WAVES * 64) void k_huff_decode(const uint32_t *__restrict__ in, uint64_t bit_base, const uint64_t *__restrict__ d_base,
                                                      const uint64_t *__restrict__ sync_base,
                                                      const uint16_t *__restrict__ sync_len, uint32_t S,
                                                      uint64_t n, const dc_dtable *__restrict__ T,
@@ -1385,6 +1388,7 @@ __global__ __launch_bounds__(DEC_WAVES * 64) void k_huff_decode(const uint32_t *
 {
     __shared__ DecLds L;
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    if (d_base) bit_base += *d_base;   // device-resident shard offset (dist: no host read)
     {
         const uint4 *src = reinterpret_cast<const uint4 *>(T->lut);
         uint4 *dst = reinterpret_cast<uint4 *>(L.lut);
@@ -1861,7 +1865,7 @@ static __device__ __forceinline__ void d8_stage(const D8Geo<NC> &cur, const uint
 // NW waves per workgroup (one workgroup per CU), NC chains per wave: wave w of workgroup b
 // decodes the NC consecutive groups of "tuple" b*NW + w (+ grid stride), lane = chunk.
 template <int NW, int NC>
-__global__ __launch_bounds__(NW * 64) void k_huff_decode8(const uint32_t *__restrict__ in, uint64_t bit_base,
+__global__ __launch_bounds__(NW * 64) void k_huff_decode8(const uint32_t *__restrict__ in, uint64_t bit_base, const uint64_t *__restrict__ d_base,
                                                           const uint64_t *__restrict__ sync_base,
                                                           const uint16_t *__restrict__ sync_len, uint64_t n,
                                                           uint64_t nwords, const dc_dtable *__restrict__ T,
@@ -1874,6 +1878,7 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode8(const uint32_t *__rest
     constexpr uint32_t S = 64;
     constexpr int NT = NW * 64;
     __shared__ Dec8Lds L;
+    if (d_base) bit_base += *d_base;   // device-resident shard offset (dist: no host read)
     const int t = threadIdx.x, lane = t & 63;
     const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
     // ---- table: the LSB-first 12-bit table (dc_dtable.dlut); codes longer than 12 bits
@@ -2067,7 +2072,7 @@ struct Dec9Lds {
 };
 
 template <int NW>
-__global__ __launch_bounds__(NW * 64) void k_huff_decode9(const uint32_t *__restrict__ in, uint64_t bit_base,
+__global__ __launch_bounds__(NW * 64) void k_huff_decode9(const uint32_t *__restrict__ in, uint64_t bit_base, const uint64_t *__restrict__ d_base,
                                                           const uint64_t *__restrict__ sync_base,
                                                           const uint16_t *__restrict__ sync_len, uint64_t n,
                                                           uint64_t nwords, const dc_dtable *__restrict__ T,
@@ -2081,6 +2086,7 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode9(const uint32_t *__rest
     constexpr int NT = NW * 64;
     constexpr uint32_t MB = (1u << DC_MULTI_BITS) - 1;
     __shared__ Dec9Lds<NW> L;
+    if (d_base) bit_base += *d_base;   // device-resident shard offset (dist: no host read)
     const int t = threadIdx.x, lane = t & 63;
     const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
     {
@@ -3487,6 +3493,7 @@ struct dc_ctx {
     MtfSum *d_mtf;          size_t mtf_cap;       // adaptive nybble: tile summaries + entries, all levels
     uint8_t *d_rk;          size_t rk_cap;        // adaptive nybble: rank per element
     const uint8_t *rk_in; uint64_t rk_len;        // identity of the input the ranks belong to
+    const uint8_t *fsm_in; uint64_t fsm_len, fsm_nelem; int fsm_mode;   // input of the last transducer plan
     uint8_t *d_kscr;        size_t kscr_cap;      // chunked nybble: per-chunk streams before packing
     uint64_t *d_klens;      size_t klens_cap;     // chunked nybble: stream length per chunk
     uint64_t *h_pinned;                           // pinned host scalars
@@ -3852,9 +3859,9 @@ static bool sync_ok(uint32_t S) { return S >= 16 && S <= DC_SYNC_MAX && (S & (S 
 uint64_t dc_huff_sync_chunks(uint64_t n, uint32_t S) { return S ? (n + S - 1) / S : 0; }
 uint64_t dc_huff_sync_groups(uint64_t n, uint32_t S) { return (dc_huff_sync_chunks(n, S) + DC_SYNC_GROUP - 1) / DC_SYNC_GROUP; }
 
-int dc_huff_pack_async(dc_ctx *c, const uint8_t *d_in, uint64_t n, const dc_dtable *d_table, uint64_t bit_base,
-                       uint32_t *d_words, uint64_t words_cap, uint64_t *d_sync_base, uint16_t *d_sync_len,
-                       uint32_t sync_syms)
+static int pack_impl(dc_ctx *c, const uint8_t *d_in, uint64_t n, const dc_dtable *d_table, uint64_t bit_base,
+                     const uint64_t *d_base, uint32_t *d_words, uint64_t words_cap, uint64_t *d_sync_base,
+                     uint16_t *d_sync_len, uint32_t sync_syms)
 {
     if (!c || !d_table || !d_words) return DC_E_ARG;
     if (d_in != c->hist_in || n != c->hist_n || !c->plan_ok) return DC_E_STATE;
@@ -3863,15 +3870,30 @@ int dc_huff_pack_async(dc_ctx *c, const uint8_t *d_in, uint64_t n, const dc_dtab
     const uint64_t nb = nblocks_of(n);
     if (nb == 0) return DC_OK;
     LAUNCH(c, "zero_bounds", k_zero_bounds, (nb + 1 + 255) / 256, 256, (const uint64_t *)c->d_off, nb, bit_base,
-           d_words, words_cap, c->d_err);
+           d_base, d_words, words_cap, c->d_err);
     // two blocks per workgroup (grid-stride): on 1 GiB C2, 16384 workgroups ran pack in
     // 0.452 ms against 0.481 at 4096, 0.469 at 32768, 0.504 at 1024 (r1 v15 A/B)
     const uint64_t gmax = c->opt_pack_grid ? c->opt_pack_grid : (nb + 1) / 2;
     const uint64_t grid = nb < gmax ? nb : gmax;
     // + workgroup 0: the decoder tables (k_huff_table leaves them to the pack's idle CU time)
-    LAUNCH(c, "huff_pack", k_huff_pack, grid + 1, 256, d_in, n, d_table, (const uint64_t *)c->d_off, bit_base, d_words,
+    LAUNCH(c, "huff_pack", k_huff_pack, grid + 1, 256, d_in, n, d_table, (const uint64_t *)c->d_off, bit_base, d_base, d_words,
            d_sync_base, d_sync_len, sync_syms, nb, words_cap, (const int *)c->d_err, 1);
     return DC_OK;
+}
+
+int dc_huff_pack_async(dc_ctx *c, const uint8_t *d_in, uint64_t n, const dc_dtable *d_table, uint64_t bit_base,
+                       uint32_t *d_words, uint64_t words_cap, uint64_t *d_sync_base, uint16_t *d_sync_len,
+                       uint32_t sync_syms)
+{
+    return pack_impl(c, d_in, n, d_table, bit_base, nullptr, d_words, words_cap, d_sync_base, d_sync_len, sync_syms);
+}
+
+int dc_huff_pack_async_dev(dc_ctx *c, const uint8_t *d_in, uint64_t n, const dc_dtable *d_table,
+                           const uint64_t *d_bit_base, uint32_t *d_words, uint64_t words_cap, uint64_t *d_sync_base,
+                           uint16_t *d_sync_len, uint32_t sync_syms)
+{
+    if (!d_bit_base) return DC_E_ARG;
+    return pack_impl(c, d_in, n, d_table, 0, d_bit_base, d_words, words_cap, d_sync_base, d_sync_len, sync_syms);
 }
 
 int dc_huff_pack_status(dc_ctx *c, const dc_dtable *d_table)
@@ -3925,9 +3947,9 @@ uint32_t dc_huff_choose_sync(uint64_t n, uint64_t total_bits)
     return (64.0 * 64.0 * avg / 8.0 <= 4200.0) ? 64u : 32u;
 }
 
-int dc_huff_decode(dc_ctx *c, const uint32_t *d_words, uint64_t bit_base, uint64_t words,
-                   const uint64_t *d_sync_base, const uint16_t *d_sync_len, uint32_t S, uint64_t n,
-                   const dc_dtable *d_table, uint8_t *d_out)
+static int decode_impl(dc_ctx *c, const uint32_t *d_words, uint64_t bit_base, const uint64_t *d_base, uint64_t words,
+                       const uint64_t *d_sync_base, const uint16_t *d_sync_len, uint32_t S, uint64_t n,
+                       const dc_dtable *d_table, uint8_t *d_out)
 {
     if (!c || !d_table || (n && (!d_words || !d_sync_base || !d_sync_len || !d_out))) return DC_E_ARG;
     if (!sync_ok(S)) return DC_E_ARG;
@@ -3949,11 +3971,11 @@ int dc_huff_decode(dc_ctx *c, const uint32_t *d_words, uint64_t bit_base, uint64
         if (ensure((void **)&c->d_scr, &c->scr_cap, (size_t)D8_SCRATCH_WAVES * D8_WSCR)) return DC_E_HIP;
 #define D8_LAUNCH(NW_, NC_)                                                                                   \
         LAUNCH(c, "huff_decode", (k_huff_decode8<NW_, NC_>), (tuples + NW_ - 1) / NW_ < 256 ? (tuples + NW_ - 1) / NW_ : 256, \
-               NW_ * 64, d_words, bit_base, d_sync_base, d_sync_len, n, words, d_table, d_out, c->d_err + 1,       \
+               NW_ * 64, d_words, bit_base, d_base, d_sync_base, d_sync_len, n, words, d_table, d_out, c->d_err + 1,       \
                c->d_queue, spct, (uint64_t *)c->d_fix, (uint64_t *)c->d_fixpos, (uint8_t *)c->d_scr)
         if (c->opt_decode_variant == 1) {   // multi-symbol lookups, one group per wave
             LAUNCH(c, "huff_decode", k_huff_decode9<12>, groups < 256 * 12 ? (groups + 11) / 12 : 256, 12 * 64,
-                   d_words, bit_base, d_sync_base, d_sync_len, n, words, d_table, d_out, c->d_err + 1, c->d_queue,
+                   d_words, bit_base, d_base, d_sync_base, d_sync_len, n, words, d_table, d_out, c->d_err + 1, c->d_queue,
                    spct, (uint64_t *)c->d_fix, (uint64_t *)c->d_fixpos, (uint8_t *)c->d_scr);
         } else {   // one code per lookup, 12 waves x 2 chains
             D8_LAUNCH(12, 2);
@@ -3970,9 +3992,24 @@ int dc_huff_decode(dc_ctx *c, const uint32_t *d_words, uint64_t bit_base, uint64
     }
     const uint64_t wgs = (groups + DEC_WAVES - 1) / DEC_WAVES;
     const uint64_t grid = wgs < 256 ? wgs : 256;   // persistent: one 16-wave workgroup per CU
-    LAUNCH(c, "huff_decode", k_huff_decode, grid, DEC_WAVES * 64, d_words, bit_base, d_sync_base, d_sync_len, S, n, d_table,
+    LAUNCH(c, "huff_decode", k_huff_decode, grid, DEC_WAVES * 64, d_words, bit_base, d_base, d_sync_base, d_sync_len, S, n, d_table,
            d_out, c->d_err + 1);
     return DC_OK;
+}
+
+int dc_huff_decode(dc_ctx *c, const uint32_t *d_words, uint64_t bit_base, uint64_t words,
+                   const uint64_t *d_sync_base, const uint16_t *d_sync_len, uint32_t S, uint64_t n,
+                   const dc_dtable *d_table, uint8_t *d_out)
+{
+    return decode_impl(c, d_words, bit_base, nullptr, words, d_sync_base, d_sync_len, S, n, d_table, d_out);
+}
+
+int dc_huff_decode_dev(dc_ctx *c, const uint32_t *d_words, const uint64_t *d_bit_base, uint64_t words,
+                       const uint64_t *d_sync_base, const uint16_t *d_sync_len, uint32_t S, uint64_t n,
+                       const dc_dtable *d_table, uint8_t *d_out)
+{
+    if (!d_bit_base) return DC_E_ARG;
+    return decode_impl(c, d_words, 0, d_bit_base, words, d_sync_base, d_sync_len, S, n, d_table, d_out);
 }
 
 int dc_huff_decode_redo_count(dc_ctx *c, uint64_t *count)
@@ -4084,12 +4121,30 @@ static int fsm_run(dc_ctx *c, const uint8_t *d_in, uint64_t len, uint64_t nelem,
     HIPCHK(hipMemcpyAsync(c->h_pinned, c->d_meta, 6 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     if (h_plan) for (int k = 0; k < 4; ++k) h_plan[k] = c->h_pinned[2 + k];
+    c->fsm_in = write ? nullptr : d_in; c->fsm_len = len; c->fsm_nelem = nelem; c->fsm_mode = M;
     const bool nyb = M == M_NYB_ENC;
     const bool enc = FsmMode<M>::enc || (nyb && aux.whole);
     const uint64_t body = nyb ? c->h_pinned[0] + (aux.is_last ? c->h_pinned[1] : 0) : c->h_pinned[0];
     uint64_t total = (FsmMode<M>::body || (nyb && !aux.whole)) ? body : enc ? 2 + body : 1 + body;
     if (enc && total >= len) total = len + 1;
     if (h_len) *h_len = total;
+    return DC_OK;
+}
+
+// the write pass alone, on the tile summaries and entries the last fsm_run(write = false) of
+// the same input left in the context (a shard body sized before its output is placed)
+template <int M>
+static int fsm_write_planned(dc_ctx *c, const uint8_t *d_in, uint64_t len, uint64_t nelem, uint8_t *d_out,
+                             uint64_t *h_len, FsmAux aux = FsmAux{nullptr, 0, 0, 1, 1})
+{
+    if (c->fsm_in != d_in || c->fsm_len != len || c->fsm_nelem != nelem || c->fsm_mode != M) return DC_E_STATE;
+    const uint64_t ntiles = (nelem + FSM_TILE - 1) / FSM_TILE;
+    LAUNCH(c, "fsm_write", k_fsm_write<M>, ntiles ? ntiles : 1, 256, d_in, len, nelem, (const uint64_t *)c->d_entry,
+           (const uint4 *)c->d_summ, (const uint64_t *)c->d_meta, d_out, aux);
+    HIPCHK(hipMemcpyAsync(c->h_pinned, c->d_meta, sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->fsm_in = nullptr;
+    if (h_len) *h_len = c->h_pinned[0];
     return DC_OK;
 }
 
@@ -4390,6 +4445,26 @@ int dc_small_compress_body(dc_ctx *c, const uint8_t *d_in, uint64_t len, int lef
     if (nelem == 0) { *h_len = 0; return DC_OK; }
     return left_halo ? fsm_run<M_SMALL_BODY1>(c, d_in, len, nelem, d_out, h_len, "small_body_tiles")
                      : fsm_run<M_SMALL_BODY0>(c, d_in, len, nelem, d_out, h_len, "small_body_tiles");
+}
+
+int dc_small_compress_body_plan(dc_ctx *c, const uint8_t *d_in, uint64_t len, int left_halo, uint64_t nelem,
+                                uint64_t *h_len)
+{
+    if (!c || !h_len || (len && !d_in) || (nelem && nelem + 1 > len)) return DC_E_ARG;
+    if (nelem == 0) { c->fsm_in = nullptr; *h_len = 0; return DC_OK; }
+    return left_halo ? fsm_run<M_SMALL_BODY1>(c, d_in, len, nelem, nullptr, h_len, "small_body_tiles",
+                                              FsmAux{nullptr, 0, 0, 1, 1}, nullptr, false)
+                     : fsm_run<M_SMALL_BODY0>(c, d_in, len, nelem, nullptr, h_len, "small_body_tiles",
+                                              FsmAux{nullptr, 0, 0, 1, 1}, nullptr, false);
+}
+
+int dc_small_compress_body_write(dc_ctx *c, const uint8_t *d_in, uint64_t len, int left_halo, uint64_t nelem,
+                                 uint8_t *d_out, uint64_t *h_len)
+{
+    if (!c || !d_out || !h_len || (len && !d_in) || (nelem && nelem + 1 > len)) return DC_E_ARG;
+    if (nelem == 0) { *h_len = 0; return DC_OK; }
+    return left_halo ? fsm_write_planned<M_SMALL_BODY1>(c, d_in, len, nelem, d_out, h_len)
+                     : fsm_write_planned<M_SMALL_BODY0>(c, d_in, len, nelem, d_out, h_len);
 }
 
 int dc_small_decompress_body(dc_ctx *c, const uint8_t *d_in, uint64_t m, uint8_t *d_out, uint64_t *h_len)

@@ -152,17 +152,30 @@ class Codec:
                                                   sync_syms if sync is not None else 0))
 
     def pack_async(self, x, tab, bit_base, words, sync, sync_syms):
+        """bit_base: an int, or a one-element int64 device tensor read by the kernels
+        (dc_huff_pack_async_dev: no host read of a gathered offset)."""
         base, lens = sync if sync is not None else (None, None)
+        S = sync_syms if sync is not None else 0
+        if hasattr(bit_base, "data_ptr"):
+            check("dc_huff_pack_async_dev",
+                  self.L.dc_huff_pack_async_dev(self.ctx, _ptr(x), x.numel(), _ptr(tab), _ptr(bit_base), _ptr(words),
+                                                words.numel(), _ptr(base), _ptr(lens), S))
+            return
         check("dc_huff_pack_async",
               self.L.dc_huff_pack_async(self.ctx, _ptr(x), x.numel(), _ptr(tab), bit_base, _ptr(words),
-                                        words.numel(), _ptr(base), _ptr(lens),
-                                        sync_syms if sync is not None else 0))
+                                        words.numel(), _ptr(base), _ptr(lens), S))
 
     def pack_status(self, tab):
         return int(self.L.dc_huff_pack_status(self.ctx, _ptr(tab)))
 
     def decode(self, words, bit_base, sync, sync_syms, n, tab, out):
+        """bit_base: an int, or a one-element int64 device tensor (dc_huff_decode_dev)."""
         base, lens = sync
+        if hasattr(bit_base, "data_ptr"):
+            check("dc_huff_decode_dev", self.L.dc_huff_decode_dev(self.ctx, _ptr(words), _ptr(bit_base), words.numel(),
+                                                                  _ptr(base), _ptr(lens), sync_syms, n, _ptr(tab),
+                                                                  _ptr(out)))
+            return
         check("dc_huff_decode", self.L.dc_huff_decode(self.ctx, _ptr(words), bit_base, words.numel(), _ptr(base),
                                                       _ptr(lens), sync_syms, n, _ptr(tab), _ptr(out)))
 
@@ -176,17 +189,40 @@ class Codec:
         return int(v.value)
 
     # ---- small front-end shard bodies (dist.ShardedSmall) --------------------
-    def small_body(self, y, left_halo: bool, nelem: int, head: bytes = b""):
+    def small_body(self, y, left_halo: bool, nelem: int, head: bytes = b"", out=None):
         """Front-end body of stream bytes y[1..nelem] (y[0]: left context; y[nelem+1], when
-        present, the right halo) -> uint8 device tensor, after the bytes `head` (the stream
-        header on rank 0: written in place, no copy of the body)."""
+        present, the right halo) -> uint8 device tensor, after the bytes `head` (written in
+        place, no copy of the body). out: optional buffer of >= nelem + len(head) bytes."""
         h = len(head)
-        out = self._t(max(nelem + h, 1))
+        if out is None:
+            out = self._t(max(nelem + h, 1))
+        elif out.numel() < nelem + h or out.dtype != torch.uint8 or not out.is_contiguous():
+            raise ValueError("small_body output: contiguous uint8 of >= nelem + len(head) bytes")
         if h:
             out[:h] = torch.tensor(list(head), dtype=torch.uint8, device=out.device)
         n = C.c_uint64(0)
         check("dc_small_compress_body", self.L.dc_small_compress_body(self.ctx, _ptr(y), y.numel(), int(left_halo),
                                                                       nelem, _ptr(out) + h, C.byref(n)))
+        return out[: h + n.value]
+
+    def small_body_plan(self, y, left_halo: bool, nelem: int) -> int:
+        """Length of small_body(y, left_halo, nelem) without writing it (dc_small_compress_body_plan);
+        small_body_write then writes it wherever the caller places it."""
+        n = C.c_uint64(0)
+        check("dc_small_compress_body_plan", self.L.dc_small_compress_body_plan(self.ctx, _ptr(y), y.numel(),
+                                                                                int(left_halo), nelem, C.byref(n)))
+        return n.value
+
+    def small_body_write(self, y, left_halo: bool, nelem: int, out, head: bytes = b""):
+        """The planned body after `head`, into out (>= len(head) + planned bytes) -> view of out."""
+        h = len(head)
+        if out.dtype != torch.uint8 or not out.is_contiguous() or out.numel() < h:
+            raise ValueError("small_body_write output: contiguous uint8")
+        if h:
+            out[:h] = torch.tensor(list(head), dtype=torch.uint8, device=out.device)
+        n = C.c_uint64(0)
+        check("dc_small_compress_body_write", self.L.dc_small_compress_body_write(
+            self.ctx, _ptr(y), y.numel(), int(left_halo), nelem, _ptr(out) + h, C.byref(n)))
         return out[: h + n.value]
 
     def _dec_out(self, seg, out):
@@ -264,26 +300,35 @@ class Codec:
                                                           la.ctypes.data if modify else None, plan.ctypes.data))
         return [int(v) for v in plan]
 
-    def nyb_body_write(self, y, modify: bool, pend_rank: int, is_last: bool):
-        out = self._t(max(2 * y.numel(), 1))
+    def _headed(self, cap, head):
+        out = self._t(max(cap + len(head), 1))
+        if head:
+            out[: len(head)] = torch.tensor(list(head), dtype=torch.uint8, device=out.device)
+        return out
+
+    def nyb_body_write(self, y, modify: bool, pend_rank: int, is_last: bool, head: bytes = b""):
+        """Body of the shard's elements y[1..] after the bytes `head` (written in place)."""
+        h = len(head)
+        out = self._headed(2 * y.numel(), head)
         n = C.c_uint64(0)
         st = C.c_int32(0)
         check("dc_nyb_body_write", self.L.dc_nyb_body_write(self.ctx, _ptr(y), y.numel(), int(modify), pend_rank,
-                                                            int(is_last), _ptr(out), C.byref(n), C.byref(st)))
-        return out[: n.value]
+                                                            int(is_last), _ptr(out) + h, C.byref(n), C.byref(st)))
+        return out[: h + n.value]
 
     def nyb_dbody_plan(self, y, m: int):
         plan = np.zeros(4, np.uint64)
         check("dc_nyb_dbody_plan", self.L.dc_nyb_dbody_plan(self.ctx, _ptr(y), y.numel(), m, plan.ctypes.data))
         return [int(v) for v in plan]
 
-    def nyb_dbody_write(self, y, m: int, s_in: int):
-        out = self._t(max(2 * m, 1))
+    def nyb_dbody_write(self, y, m: int, s_in: int, head: bytes = b""):
+        h = len(head)
+        out = self._headed(2 * m, head)
         n = C.c_uint64(0)
         st = C.c_int32(0)
-        check("dc_nyb_dbody_write", self.L.dc_nyb_dbody_write(self.ctx, _ptr(y), y.numel(), m, s_in, _ptr(out),
+        check("dc_nyb_dbody_write", self.L.dc_nyb_dbody_write(self.ctx, _ptr(y), y.numel(), m, s_in, _ptr(out) + h,
                                                               C.byref(n), C.byref(st)))
-        return out[: n.value]
+        return out[: h + n.value]
 
     # ---- digit text (SURVEY §8(f)3): formats as dc_gpu.h DC_TEXT_* ------------------------
     TEXT_FORMATS = {"base64url": 0, "base16": 1, "digits": 2, "z85": 3, "trits5": 4}

@@ -37,12 +37,15 @@ import torch.distributed as dist
 @dataclass
 class ShardStream:
     words: torch.Tensor      # int32 words; word 0 = global stream word bit_base // 32
-    bit_base: int            # global bit offset of this shard's first code bit
-    bits: int                # payload bits of this shard
+    bit_base: object         # global bit offset of this shard's first code bit: an int, or (an
+                             # encode into preallocated buffers at world size > 1) a one-element
+                             # int64 device tensor the kernels read; finalize() makes it an int
+    bits: int                # payload bits of this shard (-1 until finalize())
     sync: tuple              # (int64 group bases, int16 chunk bit lengths), absolute bits
     sync_syms: int
     n: int                   # symbols in this shard
     table: torch.Tensor      # device code table (identical on every rank)
+    totals: torch.Tensor = None   # the ranks' payload bits (device), when bit_base is a tensor
 
 
 class ShardedHuffman:
@@ -100,27 +103,38 @@ class ShardedHuffman:
 
     def encode(self, x, n_ary: int = 2, sync_syms: int = 64, words=None, sync=None, hist=None, table=None,
                total=None) -> ShardStream:
-        """words/sync/hist/table/total: optional preallocated buffers. At world size 1 with
-        preallocated words the encode issues no host synchronisation."""
+        """words/sync/hist/table/total: optional preallocated buffers. With preallocated words
+        and sync the encode issues no host synchronisation at any world size: the rank's bit
+        offset (the exclusive prefix of the gathered bit counts) stays on the device and the
+        pack kernels read it there (dc_huff_pack_async_dev)."""
         n = x.numel()
         if self.world > 1 and self.rank < self.world - 1 and n % (64 * sync_syms):
             raise ValueError("every shard but the last must hold a multiple of 64*sync_syms symbols")
         tab, tot, totals = self.plan(x, n_ary, hist, table, total)
         base, bits = 0, None
-        if totals is not None:   # the rank's global bit offset: one small host read
-            tv = totals.cpu().tolist()
-            base, bits = int(sum(tv[: self.rank])), int(tv[self.rank])
+        if totals is not None:
+            if words is not None and sync is not None:
+                base = totals[: self.rank].sum().reshape(1)   # device int64, no host read
+                bits = -1
+            else:   # buffers sized here: one small host read
+                tv = totals.cpu().tolist()
+                base, bits = int(sum(tv[: self.rank])), int(tv[self.rank])
         if words is None:
             bits = int(tot.item()) if bits is None else bits
             words = self.e.alloc_words(base, bits)
         if sync is None:
             sync = self.e.alloc_sync(n, sync_syms)
         self.e.pack_async(x, tab, base, words, sync, sync_syms)
-        return ShardStream(words, base, bits if bits is not None else -1, sync, sync_syms, n, tab)
+        return ShardStream(words, base, bits if bits is not None else -1, sync, sync_syms, n, tab,
+                           totals if not isinstance(base, int) else None)
 
     def finalize(self, s: ShardStream):
-        """Fill in the payload bit count (host read) if encode() skipped it."""
-        if s.bits < 0:
+        """Host values of the bit offset and payload bit count (one host read) if encode()
+        left them on the device."""
+        if s.totals is not None:
+            tv = s.totals.cpu().tolist()
+            s.bit_base, s.bits, s.totals = int(sum(tv[: self.rank])), int(tv[self.rank]), None
+        elif s.bits < 0:
             s.bits = int(self.e.plan_total())
         return s
 
@@ -133,41 +147,68 @@ class ShardedHuffman:
     # ---- step 6: gather the whole stream to one rank (timed separately by bench.py) -------
     def gather(self, s: ShardStream, dst: int = 0):
         """Returns (words, bits, bases, lens) of the whole stream on rank dst, None elsewhere.
-        Boundary words shared by two ranks are OR-merged."""
-        nw = (s.bit_base % 32 + s.bits + 31) // 32
-        meta = torch.tensor([s.bit_base, s.bits, nw, s.sync[0].numel(), s.sync[1].numel()],
-                            dtype=torch.int64, device=s.words.device)
+        One small all_gather of the shapes, then point-to-point sends to dst only (grouped
+        send/recv): the interior words of each rank land in place in the merged
+        stream; the two words a rank may share with its neighbours travel separately and are
+        OR-merged."""
+        self.finalize(s)
+        nw = (s.bit_base % 32 + s.bits + 31) // 32 if s.bits > 0 else 0
         if self.world == 1:
             return s.words[:nw], s.bits, s.sync[0], s.sync[1]
+        ng, nc = s.sync[0].numel(), s.sync[1].numel()
+        meta = torch.tensor([s.bit_base, s.bits, nw, ng, nc], dtype=torch.int64, device=s.words.device)
         allm = [torch.empty_like(meta) for _ in range(self.world)]
         dist.all_gather(allm, meta, group=self.group)
         allm = [m.cpu().tolist() for m in allm]
-        mw = max(m[2] for m in allm)
-        mg = max(m[3] for m in allm)
-        mc = max(m[4] for m in allm)
-        dev = s.words.device
-        wpad = torch.zeros(mw, dtype=torch.int32, device=dev)
-        wpad[:nw] = s.words[:nw]
-        gpad = torch.zeros(mg, dtype=torch.int64, device=dev)
-        gpad[: s.sync[0].numel()] = s.sync[0]
-        cpad = torch.zeros(mc, dtype=torch.int32, device=dev)   # int16 is not a gloo dtype
-        cpad[: s.sync[1].numel()] = s.sync[1].to(torch.int32) & 0xFFFF
-        W = [torch.empty_like(wpad) for _ in range(self.world)]
-        Gs = [torch.empty_like(gpad) for _ in range(self.world)]
-        Cs = [torch.empty_like(cpad) for _ in range(self.world)]
-        dist.all_gather(W, wpad, group=self.group)
-        dist.all_gather(Gs, gpad, group=self.group)
-        dist.all_gather(Cs, cpad, group=self.group)
+        dst_g = dst if self.group is None else dist.get_global_rank(self.group, dst)
+
+        def pieces(words, m):   # (head word, interior, tail word) views of a rank's words
+            k = m[2]
+            return (words[0:min(k, 1)], words[1:max(k - 1, 1)], words[max(k - 1, 1):k])
+
         if self.rank != dst:
+            h, body, tl = pieces(s.words, allm[self.rank])
+            lens = s.sync[1].view(torch.uint8)   # int16 travels as bytes (not every backend has it)
+            ops = [dist.P2POp(dist.isend, t.contiguous(), dst_g, group=self.group)
+                   for t in (h, body, tl, s.sync[0], lens) if t.numel()]
+            for w in dist.batch_isend_irecv(ops) if ops else []:
+                w.wait()
             return None
+        dev = s.words.device
         total_bits = allm[-1][0] + allm[-1][1]
         out = torch.zeros((total_bits + 31) // 32, dtype=torch.int32, device=dev)
+        bases = torch.empty(sum(m[3] for m in allm), dtype=torch.int64, device=dev)
+        lens = torch.empty(sum(m[4] for m in allm), dtype=torch.int16, device=dev)
+        lens8 = lens.view(torch.uint8)
+        ops, edges = [], []
+        g0 = c0 = 0
         for r, m in enumerate(allm):
-            w0 = m[0] // 32
-            k = min(m[2], out.numel() - w0)
-            out[w0: w0 + k] |= W[r][:k]
-        bases = torch.cat([Gs[r][: allm[r][3]] for r in range(self.world)])
-        lens = torch.cat([Cs[r][: allm[r][4]] for r in range(self.world)]).to(torch.int16)
+            w0, k = m[0] // 32, m[2]
+            if r == self.rank:
+                h, body, tl = pieces(s.words, m)
+                if body.numel():
+                    out[w0 + 1: w0 + k - 1] = body
+                edges.append((w0, h, w0 + k - 1, tl))
+                bases[g0: g0 + m[3]] = s.sync[0]
+                lens[c0: c0 + m[4]] = s.sync[1]
+            else:
+                e = torch.zeros(2, dtype=torch.int32, device=dev)
+                h, tl = e[0:min(k, 1)], e[1:1 + max(min(k - 1, 1), 0)]
+                body = out[w0 + 1: w0 + max(k - 1, 1)]
+                for t in (h, body, tl, bases[g0: g0 + m[3]], lens8[2 * c0: 2 * (c0 + m[4])]):
+                    if t.numel():
+                        ops.append(dist.P2POp(dist.irecv, t, r if self.group is None else
+                                              dist.get_global_rank(self.group, r), group=self.group))
+                edges.append((w0, h, w0 + k - 1, tl))
+            g0 += m[3]
+            c0 += m[4]
+        for w in dist.batch_isend_irecv(ops) if ops else []:
+            w.wait()
+        for w0, h, wl, tl in edges:   # words shared with a neighbouring rank: OR-merged
+            if h.numel():
+                out[w0: w0 + 1] |= h
+            if tl.numel():
+                out[wl: wl + 1] |= tl
         return out, total_bits, bases, lens
 
 
@@ -191,9 +232,9 @@ class ShardedSmall:
     stateless); the ranks' decoded segments concatenate to the input.
     """
 
-    def __init__(self, engine, group=None):
+    def __init__(self, engine, group=None, table_mode: str = "replicate", table_src: int = 0):
         self.e = engine
-        self.h = ShardedHuffman(engine, group)
+        self.h = ShardedHuffman(engine, group, table_mode=table_mode, table_src=table_src)
         self.group = group
         self.world, self.rank = self.h.world, self.h.rank
 
@@ -205,56 +246,94 @@ class ShardedSmall:
         dist.all_gather(out, t, group=self.group)
         return [o.cpu().tolist() for o in out]
 
+    @staticmethod
+    def _lower(v):
+        return ord("a") <= v <= ord("z")
+
     def frontend(self, x, sync_syms: int = 64):
-        """Steps 1-4: this rank's segment of the global front-end stream (device bytes),
-        its global start, and whether the stream fell back to LITERAL."""
+        """Steps 1-4: this rank's segment of the global front-end stream (device bytes, 16-B
+        aligned) and whether the stream fell back to LITERAL.
+        No copy of the shard: the body kernel reads x itself (elements x[1..], x[0] its left
+        context), and the two elements whose output depends on a neighbour's byte are settled
+        on the host from the gathered halo bytes: x[0] (the second byte of a pair that starts
+        on the previous shard's last byte, or the start of a pair with x[1]) is written as
+        the body's head, and x[-1] (' ' starting a pair with the next shard's first byte)
+        patches the body's last byte. The body is sized first (dc_small_compress_body_plan),
+        so every rank knows the re-cut before writing: it writes its body once, at the offset
+        where the bytes received from the previous rank complete an aligned segment."""
         self._dev = x.device
         n = x.numel()
         if n < 2:
             raise ValueError("each shard needs >= 2 bytes")
-        ends = self._gather_i64([int(x[0]), int(x[-1]), n])
+        x0, x1, xl = x[[0, 1, n - 1]].tolist()
+        ends = self._gather_i64([x0, xl, n])
         left = ends[self.rank - 1][1] if self.rank > 0 else None
         right = ends[self.rank + 1][0] if self.rank < self.world - 1 else None
         n_total = sum(e[2] for e in ends)
-        parts = ([torch.tensor([left], dtype=torch.uint8, device=x.device)] if left is not None else []) + [x] + \
-                ([torch.tensor([right], dtype=torch.uint8, device=x.device)] if right is not None else [])
-        y = torch.cat(parts) if len(parts) > 1 else x
-        # body of stream bytes: rank 0 -> x[1..n-1] (x[0] is the raw first byte); rank r ->
-        # all of x (y[0] is the left halo)
-        nelem = n - 1 if self.rank == 0 else n
-        head = bytes([8, ends[0][0]]) if self.rank == 0 else b""   # type byte, raw first byte
-        body = self.e.small_body(y, self.rank > 0, nelem, head=head)
-        lens = self._gather_i64([body.numel() - len(head)])
+        if self.rank == 0:
+            head = bytes([8, x0])                       # type byte, raw first byte
+        elif left == ord(" ") and self._lower(x0):
+            head = b""                                  # x[0] closes the previous shard's pair
+        elif x0 == ord(" ") and self._lower(x1):
+            head = bytes([0x80 + x1])                   # x[0] x[1] is a pair
+        else:
+            head = bytes([x0])
+        hb = 2 if self.rank == 0 else 0                 # header bytes (not body)
+        nb = len(head) - hb + self.e.small_body_plan(x, self.rank > 0, n - 1)
+        lens = self._gather_i64([nb])
         total = 2 + sum(v[0] for v in lens)
         literal = total >= n_total
+        sizes = [v[0] + 2 for v in lens[:1]] + [v[0] for v in lens[1:]]
         if literal:   # ' ' + raw input, as the single-stream encoder falls back
-            seg = torch.cat([torch.tensor([ord(" ")], dtype=torch.uint8, device=x.device), x]) if self.rank == 0 else x
+            sizes = [e[2] + (1 if r == 0 else 0) for r, e in enumerate(ends)]
+        q = 64 * sync_syms
+        cut, nrecv, keep = self._cuts(sizes, q)
+        m = sizes[self.rank]
+        buf = self.e.alloc_bytes(nrecv + m + 16)        # [received | own segment]
+        if literal:
+            k = 0
+            if self.rank == 0:
+                buf[nrecv: nrecv + 1].fill_(ord(" "))
+                k = 1
+            buf[nrecv + k: nrecv + k + n] = x
         else:
-            seg = body   # rank 0's already starts with the header
-        sizes = [v[0] for v in self._gather_i64([seg.numel()])]
-        return self._recut(seg, sizes, 64 * sync_syms), literal
+            body = self.e.small_body_write(x, self.rank > 0, n - 1, buf[nrecv:], head=head)
+            if right is not None and xl == ord(" ") and self._lower(right):
+                body[-1:].fill_(0x80 + right)           # x[-1] starts a pair with the next shard
+        return self._exchange(buf, nrecv, m, keep), literal
 
-    def _recut(self, seg, sizes, q):
-        """Move each rank's bytes past the next multiple of q (global position) to the next
-        rank, so every segment but the last starts and ends on a multiple of q."""
+    def _cuts(self, sizes, q):
+        """Re-cut of the segments (sizes, in rank order) at multiples of q (global position):
+        each rank's bytes past the next multiple of q move to the next rank, so every segment
+        but the last starts and ends on a multiple of q. Returns (cuts, bytes this rank
+        receives, bytes it keeps of its own)."""
         off = [sum(sizes[:r]) for r in range(self.world + 1)]
         cut = [0] + [(off[r] // q) * q for r in range(1, self.world)] + [off[self.world]]
         if any(cut[r] < off[r - 1] for r in range(1, self.world)):
             raise ValueError("front-end segments too short to re-cut at 64 * sync_syms")
         r = self.rank
-        send = seg[cut[r + 1] - off[r]:] if r < self.world - 1 else seg[:0]
-        keep = seg[: cut[r + 1] - off[r]] if r < self.world - 1 else seg
-        recv = torch.empty(off[r] - cut[r], dtype=torch.uint8, device=seg.device)
-        if self.world > 1:   # < q bytes to the next rank (gloo: even ranks send first)
-            ops = []
-            if r < self.world - 1 and send.numel():
-                ops.append(dist.P2POp(dist.isend, send.contiguous(), r + 1, group=self.group))
-            if r > 0 and recv.numel():
-                ops.append(dist.P2POp(dist.irecv, recv, r - 1, group=self.group))
-            if ops:
-                for w in dist.batch_isend_irecv(ops):
-                    w.wait()
-        return torch.cat([recv, keep]) if recv.numel() else keep
+        keep = cut[r + 1] - off[r] if r < self.world - 1 else sizes[r]
+        return cut, off[r] - cut[r], keep
+
+    def _exchange(self, buf, nrecv, m, keep):
+        """buf = [nrecv bytes to receive | own segment of m bytes]: send own bytes past `keep`
+        to the next rank, receive the previous rank's into the front (in place, no copy).
+        Returns the re-cut segment buf[: nrecv + keep]."""
+        r = self.rank
+        if self.world > 1:   # < q bytes to the next rank
+            self._shift(buf[nrecv + keep: nrecv + m] if r < self.world - 1 else None,
+                        buf[:nrecv] if r > 0 else None)
+        return buf[: nrecv + keep]
+
+    def _shift(self, send, recv):
+        """send (or None) to rank + 1 and recv (or None) from rank - 1, grouped."""
+        ops = []
+        if send is not None and send.numel():
+            ops.append(dist.P2POp(dist.isend, send, self.rank + 1, group=self.group))
+        if recv is not None and recv.numel():
+            ops.append(dist.P2POp(dist.irecv, recv, self.rank - 1, group=self.group))
+        for w in dist.batch_isend_irecv(ops) if ops else []:
+            w.wait()
 
     def encode(self, x, n_ary: int = 16, sync_syms: int = 64):
         seg, literal = self.frontend(x, sync_syms)
@@ -273,6 +352,23 @@ class ShardedSmall:
 
 
 INITIAL_LISTS = np.frombuffer(b" etaoins" * 16, np.uint8).reshape(16, 8)   # initialize_dictionary
+
+
+def compose_summaries(la, ca, lb, cb):
+    """Summary of (stretch A then stretch B) from theirs (each started empty): per context,
+    first 8 distinct of (B's list, A's list)."""
+    out = np.zeros((16, 8), np.uint8)
+    cnt = np.zeros(16, np.uint8)
+    for c in range(16):
+        seen = []
+        for v in list(lb[c][: int(cb[c])]) + list(la[c][: int(ca[c])]):
+            if v not in seen:
+                seen.append(v)
+            if len(seen) == 8:
+                break
+        out[c, : len(seen)] = seen
+        cnt[c] = len(seen)
+    return out, cnt
 
 
 def compose_lists(lists, summ, cnt):
@@ -338,28 +434,70 @@ class ShardedNybble:
     def _u8(self, vals, dev):
         return torch.tensor(vals, dtype=torch.uint8, device=dev)
 
+    _STATIC = b" etaoins"
+
+    @staticmethod
+    def _fsm_elem(hit):
+        """(c0, c1, s0, s1) of one element (dc_core.hip elem_fsm, M_NYB_ENC): a hit flips
+        the pending state and emits 1 byte when it closes a pair; a miss emits itself (and a
+        pending byte raw before it)."""
+        return (0, 1, 1, 0) if hit else (1, 2, 0, 0)
+
+    @staticmethod
+    def _then(a, b):
+        """Composition of transducer plans (a then b), as fsm_then."""
+        c0 = a[0] + (b[1] if a[2] else b[0])
+        s0 = b[3] if a[2] else b[2]
+        c1 = a[1] + (b[1] if a[3] else b[0])
+        s1 = b[3] if a[3] else b[2]
+        return (c0, c1, s0, s1)
+
     def compress(self, x, modify: bool):
-        """This rank's segment of the compressed stream, and whether it is LITERAL."""
+        """This rank's segment of the compressed stream, and whether it is LITERAL.
+        No copy of the shard: the kernels walk x itself (elements x[1..], context x[0]); the
+        element x[0], whose context is the previous shard's last byte (the 1-byte halo), is
+        coded on the host (its rank from the entry lists, its transducer step) and its
+        output written as the body's head."""
         dev, n = x.device, x.numel()
         if n < 1 or (self.rank == 0 and n < 2):
             raise ValueError("shards need >= 1 byte (rank 0: >= 2)")
-        ends = self._gather([int(x[0]), int(x[-1]), n], dev)
+        x0, xl = x[[0, n - 1]].tolist()
+        ends = self._gather([x0, xl, n], dev)
         n_total = sum(e[2] for e in ends)
-        y = torch.cat([self._u8([ends[self.rank - 1][1]], dev), x]) if self.rank > 0 else x
+        r = self.rank
+        left = ends[r - 1][1] if r > 0 else None
         lists = None
         if modify:
-            summ, cnt = self.e.nyb_mtf_summary(y)
+            summ, cnt = self.e.nyb_mtf_summary(x)   # elements x[1..] from empty lists
+            if r > 0:   # x[0] touched into its context's list first: summary = (x0) then (x[1..])
+                first = np.zeros((16, 8), np.uint8)
+                fcnt = np.zeros(16, np.uint8)
+                first[(left >> 3) & 15, 0] = x0
+                fcnt[(left >> 3) & 15] = 1
+                summ, cnt = compose_summaries(first, fcnt, summ, cnt)
             allsum = self._gather(list(summ.reshape(-1)) + list(cnt), dev)
             lists = INITIAL_LISTS.copy()
-            for q in range(self.rank):
+            for q in range(r):
                 a = np.asarray(allsum[q], np.uint8)
                 lists = compose_lists(lists, a[:128].reshape(16, 8), a[128:])
-        plan = self.e.nyb_body_plan(y, modify, lists)
+        r0 = 0xFF
+        if r > 0:   # x[0]: its rank under the entry lists, then touched
+            if modify:
+                c = (left >> 3) & 15
+                row = list(lists[c])
+                r0 = row.index(x0) if x0 in row else 0xFF
+                lists[c] = [x0] + [v for v in row if v != x0][:7]
+            else:
+                r0 = self._STATIC.index(bytes([x0])) if bytes([x0]) in self._STATIC else 0xFF
+        plan = self.e.nyb_body_plan(x, modify, lists)   # (c0, c1, s0, s1, last rank) of x[1..]
+        if r > 0:
+            comp = self._then(self._fsm_elem(r0 != 0xFF), tuple(plan[:4]))
+            plan = list(comp) + [plan[4] if n > 1 else r0]
         plans = self._gather(plan, dev)
         s, pend, total = 0, -1, 2
         for q in range(self.world):
             c0, c1, s0, s1, last = plans[q]
-            if q == self.rank:
+            if q == r:
                 my_s, my_pend = s, pend
             total += c1 if s else c0
             s = s1 if s else s0
@@ -367,36 +505,57 @@ class ShardedNybble:
         total += s                      # odd tail: the last pending byte is written raw
         literal = total >= n_total
         if literal:
-            seg = torch.cat([self._u8([ord(" ")], dev), x]) if self.rank == 0 else x
+            seg = torch.cat([self._u8([ord(" ")], dev), x]) if r == 0 else x
             return seg, True
-        body = self.e.nyb_body_write(y, modify, my_pend if my_s else -1, self.rank == self.world - 1)
-        if self.rank == 0:
-            body = torch.cat([self._u8([0xAF, int(x[0])], dev), body])
+        is_last = r == self.world - 1
+        if r == 0:
+            head, s_in, p_in = bytes([0xAF, x0]), 0, -1
+        else:   # x[0]'s output from the entry state (compress_byte_index, :819-884)
+            s_in, p_in = my_s, my_pend if my_s else -1
+            if r0 != 0xFF:
+                if s_in:
+                    head, s_in, p_in = bytes([((8 | p_in) << 4) | (8 | r0)]), 0, -1
+                else:
+                    head, s_in, p_in = b"", 1, r0
+            else:
+                head = bytes([left, x0]) if s_in else bytes([x0])
+                s_in, p_in = 0, -1
+        if n == 1:   # x[0] alone: its head, and on the last shard a pending byte written raw
+            tail = bytes([x0]) if is_last and s_in else b""
+            return self._u8(list(head + tail), dev), False
+        body = self.e.nyb_body_write(x, modify, p_in if s_in else -1, is_last, head=head)
         return body, False
 
     def decompress(self, seg):
         """Static-mode decode of this rank's segment of a compressed stream (as compress
-        cut it, or cut anywhere) -> this rank's decoded bytes."""
+        cut it, or cut anywhere) -> this rank's decoded bytes. No copy of the segment: the
+        one byte of right halo (the next segment's first byte) only completes this segment's
+        last output byte when the walk ends "at the low nybble" (it supplies that byte's low
+        half), which is patched after the body is written."""
         dev, m = seg.device, seg.numel()
-        info = self._gather([m, int(seg[0]) if m else -1], dev)
+        b0, b1 = (seg[[0, 1]].tolist() if m > 1 else ([int(seg[0]), -1] if m else [-1, -1]))
+        info = self._gather([m, b0, b1], dev)
         typ = info[0][1]
         if typ == ord(" "):
             return seg[1:] if self.rank == 0 else seg
         if typ != 0xAF:
             raise ValueError("not a nybble stream (type byte %r)" % typ)
-        body = seg[2:] if self.rank == 0 else seg
         if self.rank == 0 and m < 2:
             raise ValueError("rank 0's segment must hold the 2-byte header")
+        body = seg[2:] if self.rank == 0 else seg
         right = next((info[q][1] for q in range(self.rank + 1, self.world) if info[q][0] > 0), None)
-        y = torch.cat([body, self._u8([right], dev)]) if right is not None else body
         mb = body.numel()
-        plans = self._gather(self.e.nyb_dbody_plan(y, mb), dev)
+        plans = self._gather(self.e.nyb_dbody_plan(body, mb), dev)
         s = 0
         for q in range(self.rank):
             c0, c1, s0, s1 = plans[q]
             s = s1 if s else s0
-        out = self.e.nyb_dbody_write(y, mb, s)
-        return torch.cat([seg[1:2], out]) if self.rank == 0 else out
+        head = bytes([info[0][2]]) if self.rank == 0 else b""   # the raw first byte
+        out = self.e.nyb_dbody_write(body, mb, s, head=head)
+        s_out = plans[self.rank][3] if s else plans[self.rank][2]
+        if right is not None and s_out == 1 and mb:
+            out[-1:].add_(right >> 4)   # (l & 7) << 4 + the next byte's high nybble (:753-795)
+        return out
 
     def decode_replica(self, seg, sizes, modify: bool):
         """Adaptive (or any) decode by replicas: every rank gathers the whole stream, decodes

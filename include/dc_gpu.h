@@ -168,6 +168,12 @@ int dc_huff_block_hist(dc_ctx *ctx, uint16_t *h_bh, uint64_t max_entries);
 int dc_huff_pack_async(dc_ctx *ctx, const uint8_t *d_in, uint64_t n, const dc_dtable *d_table,
                        uint64_t bit_base, uint32_t *d_words, uint64_t words_cap,
                        uint64_t *d_sync_base, uint16_t *d_sync_len, uint32_t sync_syms);
+/* ... with the stream's bit offset read by the kernels from device memory (*d_bit_base, a
+ * u64 written earlier on the stream, e.g. a shard's exclusive prefix of the ranks' payload
+ * bits): a sharded encode then needs no host read of the gathered bit counts. */
+int dc_huff_pack_async_dev(dc_ctx *ctx, const uint8_t *d_in, uint64_t n, const dc_dtable *d_table,
+                           const uint64_t *d_bit_base, uint32_t *d_words, uint64_t words_cap,
+                           uint64_t *d_sync_base, uint16_t *d_sync_len, uint32_t sync_syms);
 int dc_huff_pack_status(dc_ctx *ctx, const dc_dtable *d_table);
 /* Status word written by the table / plan kernels (host-synchronising read). */
 int dc_huff_table_status(dc_ctx *ctx, const dc_dtable *d_table, int32_t *max_bits);
@@ -175,6 +181,10 @@ int dc_huff_table_status(dc_ctx *ctx, const dc_dtable *d_table, int32_t *max_bit
 int dc_huff_decode(dc_ctx *ctx, const uint32_t *d_words, uint64_t bit_base, uint64_t words,
                    const uint64_t *d_sync_base, const uint16_t *d_sync_len, uint32_t sync_syms,
                    uint64_t n, const dc_dtable *d_table, uint8_t *d_out);
+/* ... with the bit offset in device memory (as dc_huff_pack_async_dev) */
+int dc_huff_decode_dev(dc_ctx *ctx, const uint32_t *d_words, const uint64_t *d_bit_base, uint64_t words,
+                       const uint64_t *d_sync_base, const uint16_t *d_sync_len, uint32_t sync_syms,
+                       uint64_t n, const dc_dtable *d_table, uint8_t *d_out);
 /* status of the last dc_huff_decode on this context (synchronising): 0 or DC_E_STREAM */
 int dc_huff_decode_status(dc_ctx *ctx);
 /* chunks of the last S = 64 dc_huff_decode on this context that took the exact redo (codes
@@ -274,6 +284,13 @@ int dc_small_decompress(dc_ctx *ctx, const uint8_t *d_in, uint64_t m, uint8_t *d
  * shards concatenate to the whole stream's body. d_out capacity >= nelem. */
 int dc_small_compress_body(dc_ctx *ctx, const uint8_t *d_in, uint64_t len, int left_halo, uint64_t nelem,
                            uint8_t *d_out, uint64_t *h_out_len);
+/* The same in two calls, so the caller can place the output once its size is known (a
+ * sharded encoder aligns its re-cut segment, dist.ShardedSmall): _plan returns the body
+ * length; _write, on the same input and arguments (DC_E_STATE otherwise), writes it. */
+int dc_small_compress_body_plan(dc_ctx *ctx, const uint8_t *d_in, uint64_t len, int left_halo, uint64_t nelem,
+                                uint64_t *h_len);
+int dc_small_compress_body_write(dc_ctx *ctx, const uint8_t *d_in, uint64_t len, int left_halo, uint64_t nelem,
+                                 uint8_t *d_out, uint64_t *h_len);
 /* decode of a body (every byte: >= 0x80 -> ' ' + byte - 0x80); d_out capacity >= 2*m */
 int dc_small_decompress_body(dc_ctx *ctx, const uint8_t *d_in, uint64_t m, uint8_t *d_out, uint64_t *h_out_len);
 

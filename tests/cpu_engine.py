@@ -62,6 +62,7 @@ class CpuEngine:
         return torch.zeros(max(n, 1), dtype=torch.uint8)
 
     def pack_async(self, x, tab, bit_base, words, sync, S):
+        bit_base = int(bit_base)   # an int, or a one-element tensor (device engine: read by the kernels)
         tab = self._tab(tab)
         xs = x.numpy()
         payload, bits, idx = orc.huff_pack(xs, tab["code"], tab["nb"], bit_base=bit_base, sync_syms=S)
@@ -74,6 +75,7 @@ class CpuEngine:
         sync[1][: len(lens)] = torch.from_numpy(lens.view(np.int16))
 
     def decode(self, words, bit_base, sync, S, n, tab, out):
+        bit_base = int(bit_base)
         tab = self._tab(tab)
         bits_all = np.unpackbits(words.numpy().view(np.uint8))
         stream = np.packbits(bits_all[bit_base & 31:])
@@ -82,7 +84,7 @@ class CpuEngine:
         out[:n] = torch.from_numpy(y)
 
     # ---- small front-end shard bodies (dist.ShardedSmall), restated with numpy ------------
-    def small_body(self, y, left_halo, nelem, head=b""):
+    def small_body(self, y, left_halo, nelem, head=b"", out=None):
         """small_compression.c:582-665 body of y[1..nelem] (dc_small_compress_body), after `head`."""
         a = y.numpy()
         i = np.arange(1, nelem + 1)
@@ -94,7 +96,17 @@ class CpuEngine:
         nxt_low[has] = low[i[has] + 1]
         start = sp[i] & nxt_low
         vals = np.where(start, 0x80 + a[np.minimum(i + 1, a.size - 1)].astype(np.int64), a[i]).astype(np.uint8)
-        return torch.from_numpy(np.concatenate([np.frombuffer(head, np.uint8), vals[~second]]))
+        res = torch.from_numpy(np.concatenate([np.frombuffer(head, np.uint8), vals[~second]]))
+        if out is None:
+            return res
+        out[: res.numel()] = res
+        return out[: res.numel()]
+
+    def small_body_plan(self, y, left_halo, nelem):
+        return self.small_body(y, left_halo, nelem).numel()
+
+    def small_body_write(self, y, left_halo, nelem, out, head=b""):
+        return self.small_body(y, left_halo, nelem, head=head, out=out)
 
     def small_decompress(self, seg):
         return torch.from_numpy(np.frombuffer(orc.small_decompress(seg.numpy().tobytes()), np.uint8).copy())
@@ -172,11 +184,11 @@ class CpuEngine:
         o1, s1 = self._walk(a, rk, 1, 0, False)
         return [len(o0), len(o1), s0, s1, rk[-1] if rk else 0xFF]
 
-    def nyb_body_write(self, y, modify, pend_rank, is_last):
+    def nyb_body_write(self, y, modify, pend_rank, is_last, head=b""):
         a, rk = self._plan
         assert a == bytes(y.numpy())
         out, _ = self._walk(a, rk, 1 if pend_rank >= 0 else 0, pend_rank, is_last)
-        return torch.from_numpy(np.frombuffer(out, np.uint8).copy())
+        return torch.from_numpy(np.frombuffer(bytes(head) + out, np.uint8).copy())
 
     def _dwalk(self, a, m, s):
         out = bytearray()
@@ -203,9 +215,9 @@ class CpuEngine:
         o1, s1 = self._dwalk(a, m, 1)
         return [len(o0), len(o1), s0, s1]
 
-    def nyb_dbody_write(self, y, m, s_in):
+    def nyb_dbody_write(self, y, m, s_in, head=b""):
         out, _ = self._dwalk(bytes(y.numpy()), m, s_in)
-        return torch.from_numpy(np.frombuffer(out, np.uint8).copy())
+        return torch.from_numpy(np.frombuffer(bytes(head) + out, np.uint8).copy())
 
     def nyb_decompress(self, comp, modify):
         return torch.from_numpy(np.frombuffer(orc.nybble_decompress(bytes(comp.numpy()), modify), np.uint8).copy())

@@ -191,9 +191,11 @@ def _nyb_input(kind, n):
     return rng.integers(ord("A"), ord("Z") + 1, size=n, dtype=np.uint8)   # all misses: LITERAL
 
 
-@pytest.mark.parametrize("world,kind,modify", [(2, "text", False), (3, "text", False), (4, "text", True),
-                                               (2, "text", True), (2, "upper", False), (3, "upper", True)])
-def test_sharded_nybble(world, kind, modify):
+@pytest.mark.parametrize("world,kind,modify,tiny", [(2, "text", False, False), (3, "text", False, False),
+                                                    (4, "text", True, False), (2, "text", True, False),
+                                                    (2, "upper", False, False), (3, "upper", True, False),
+                                                    (4, "text", False, True), (4, "text", True, True)])
+def test_sharded_nybble(world, kind, modify, tiny):
     """SURVEY §8(e) nybble rows (dist.ShardedNybble): 1-byte halos, carried run parity (and,
     adaptive, the composed move-to-front lists). The ranks' segments concatenate to the
     reference's single-stream compress_bytestring output; decoding gives the input back,
@@ -203,6 +205,8 @@ def test_sharded_nybble(world, kind, modify):
     x = _nyb_input(kind, total)
     rng = np.random.default_rng(world * 7 + modify)
     cuts = [0] + sorted(int(v) for v in rng.choice(np.arange(2, total - 1), world - 1, replace=False)) + [total]
+    if tiny:   # 1-byte shards (a rank whose only element is its halo-context element), one of them last
+        cuts = [0, 1500, 1501] + [total - 1][: world - 3] + [total]
     dcuts = [0.0] + sorted(float(v) for v in rng.uniform(0.05, 0.95, world - 1)) + [1.0]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

@@ -634,12 +634,33 @@ def test_nybble_chunked_container(torch_cuda, codec, modify):
     assert merge_chunked(per) == whole
 
 
-@pytest.mark.parametrize("world,n_ary,table_mode", [(2, 2, "replicate"), (3, 16, "replicate"), (3, 2, "broadcast")])
-def test_sharded_huffman_on_device(torch_cuda, world, n_ary, table_mode):
+def _thread_collectives(sh, tr, r, world, torch):
+    """ShardedHuffman collectives over thread ranks (all on one GPU)."""
+    def all_reduce(t):
+        tot = np.sum(np.array(tr.gather(r, t.cpu().tolist()), dtype=np.int64), axis=0)
+        t.copy_(torch.from_numpy(tot).to(t.device))
+
+    def all_gather_scalar(t):
+        v = tr.gather(r, [int(t.item())])
+        return torch.tensor([q[0] for q in v], dtype=t.dtype, device=t.device)
+
+    def broadcast_table(t):
+        v = tr.gather(r, t.cpu().numpy().tobytes())[world - 1]
+        t.copy_(torch.from_numpy(np.array(v, dtype=np.uint8)).to(t.device))
+    sh._all_reduce, sh._all_gather_scalar = all_reduce, all_gather_scalar
+    sh._reduce_to_src, sh._broadcast_table = all_reduce, broadcast_table   # the sum: read by the table rank only
+
+
+@pytest.mark.parametrize("world,n_ary,table_mode,prealloc", [(2, 2, "replicate", False), (3, 16, "replicate", False),
+                                                             (3, 2, "broadcast", False), (3, 2, "replicate", True),
+                                                             (4, 16, "broadcast", True)])
+def test_sharded_huffman_on_device(torch_cuda, world, n_ary, table_mode, prealloc):
     """dist.ShardedHuffman on the device engine (thread ranks, collectives by a barrier):
     each rank packs at its global bit offset; the OR-merged shards equal the single-GPU
     stream of the whole input bit for bit, and every rank decodes its own shard. In
-    broadcast mode the table bytes one rank's context built drive every other context."""
+    broadcast mode the table bytes one rank's context built drive every other context.
+    prealloc: words and sync index preallocated, so the rank's bit offset stays on the
+    device (dc_huff_pack_async_dev / dc_huff_decode_dev: no host read in the encode)."""
     import threading
 
     from data_compression_amd import synth
@@ -655,29 +676,22 @@ def test_sharded_huffman_on_device(torch_cuda, world, n_ary, table_mode):
     def run(r):
         try:
             torch.cuda.set_device(0)
-            sh = ShardedHuffman(Codec(0), table_mode=table_mode)
+            c = Codec(0)
+            sh = ShardedHuffman(c, table_mode=table_mode)
             sh.world, sh.rank = world, r
             sh.table_src = world - 1
-
-            def all_reduce(t):
-                tot = np.sum(np.array(tr.gather(r, t.cpu().tolist()), dtype=np.int64), axis=0)
-                t.copy_(torch.from_numpy(tot).to(t.device))
-
-            def all_gather_scalar(t):
-                v = tr.gather(r, [int(t.item())])
-                return torch.tensor([q[0] for q in v], dtype=t.dtype, device=t.device)
-            def reduce_to_src(t):   # the sum is only read by the table rank
-                all_reduce(t)
-
-            def broadcast_table(t):
-                v = tr.gather(r, t.cpu().numpy().tobytes())[world - 1]
-                t.copy_(torch.from_numpy(np.array(v, dtype=np.uint8)).to(t.device))
-            sh._all_reduce, sh._all_gather_scalar = all_reduce, all_gather_scalar
-            sh._reduce_to_src, sh._broadcast_table = reduce_to_src, broadcast_table
+            _thread_collectives(sh, tr, r, world, torch)
             lo = r * shard
             xs = torch.from_numpy(x[lo: x.size if r == world - 1 else lo + shard].copy()).cuda()
-            s = sh.encode(xs, n_ary=n_ary, sync_syms=S)
-            y = sh.decode(s)
+            if prealloc:
+                words = torch.empty(c.words_needed(31, 32 * xs.numel()) + 8, dtype=torch.int32, device="cuda")
+                s = sh.encode(xs, n_ary=n_ary, sync_syms=S, words=words, sync=c.alloc_sync(xs.numel(), S))
+                assert s.bits == -1 and isinstance(s.bit_base, torch.Tensor)
+                y = sh.decode(s)
+                sh.finalize(s)
+            else:
+                s = sh.encode(xs, n_ary=n_ary, sync_syms=S)
+                y = sh.decode(s)
             nw = (s.bit_base % 32 + s.bits + 31) // 32
             res[r] = (s.bit_base, s.bits, s.words[:nw].cpu().numpy().copy(), bool(torch.equal(y[: xs.numel()], xs)))
         except Exception as e:   # noqa: BLE001
@@ -701,6 +715,76 @@ def test_sharded_huffman_on_device(torch_cuda, world, n_ary, table_mode):
     assert enc["bits"] == total
     ref = enc["words"].cpu().numpy().view(np.uint32)[: merged.size]
     assert np.array_equal(merged, ref)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_small_on_device(torch_cuda, world):
+    """dist.ShardedSmall on the device engine (thread ranks): the halo elements settled on
+    the host, bodies sized then written in place (dc_small_compress_body_plan/_write) at
+    16-B aligned re-cut segments; the OR-merged Huffman shards equal the oracle's encoding
+    of the reference front-end output, and the decoded segments concatenate to the input."""
+    import threading
+
+    from data_compression_amd import synth
+    from data_compression_amd.device import Codec
+    from data_compression_amd.dist import ShardedSmall
+    torch = torch_cuda
+    S, n_ary = 64, 16
+    x = synth.log_like((1 << 20) * world + 777, seed=world)
+    cuts = [0]
+    for k in range(1, world):   # one cut inside a pair (' ' | letter), one just before a ' '
+        c = k * x.size // world
+        while not (x[c - 1] == ord(" ") and ord("a") <= x[c] <= ord("z")) if k % 2 else x[c] != ord(" "):
+            c += 1
+        cuts.append(c)
+    cuts.append(x.size)
+    tr = _ThreadRanks(world)
+    slots = [None] * world
+    res, errs = [None] * world, []
+
+    def run(r):
+        try:
+            torch.cuda.set_device(0)
+            sm = ShardedSmall(Codec(0))
+            sm.world = sm.h.world = world
+            sm.rank = sm.h.rank = r
+            sm.h.table_src = world - 1
+            _thread_collectives(sm.h, tr, r, world, torch)
+            sm._gather_i64 = lambda vals: tr.gather(r, vals)
+
+            def shift(send, recv):   # send to r + 1, receive from r - 1
+                slots[r] = send.clone() if send is not None else None
+                tr.bar.wait()
+                if recv is not None and recv.numel():
+                    recv.copy_(slots[r - 1])
+                tr.bar.wait()
+            sm._shift = shift
+            s = sm.encode(torch.from_numpy(x[cuts[r]: cuts[r + 1]].copy()).cuda(), n_ary=n_ary, sync_syms=S)
+            sm.h.finalize(s)
+            y = sm.decode(s)
+            nw = (s.bit_base % 32 + s.bits + 31) // 32
+            res[r] = (s.bit_base, s.bits, s.words[:nw].cpu().numpy().copy(), y.cpu().numpy().copy())
+        except Exception as e:   # noqa: BLE001
+            errs.append(repr(e))
+            tr.bar.abort()
+
+    ths = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(timeout=120)
+    assert not errs, errs
+    assert np.array_equal(np.concatenate([v[3] for v in res]), x)
+    fe = np.frombuffer(orc.small_compress(x.tobytes()), np.uint8)
+    L, el, ev, code, nb, mx = _oracle_encode(fe, n_ary)
+    payload, bits, _ = orc.huff_pack(fe, code, nb, sync_syms=S)
+    total = res[-1][0] + res[-1][1]
+    assert total == bits
+    merged = np.zeros((total + 31) // 32, np.uint32)
+    for base, nbits, w, _ in res:
+        w0 = base // 32
+        merged[w0: w0 + w.size] |= w.view(np.uint32)[: merged.size - w0]
+    assert np.array_equal(merged.view(np.uint8)[: len(payload)], payload)
 
 
 def test_histogram_running_counters_skewed(torch_cuda, codec):
