@@ -2706,7 +2706,8 @@ struct FsmAux {
     uint32_t is_last;     // M_NYB_ENC: the shard ends the stream (odd-tail byte, :1000-1009)
     uint32_t whole;       // M_NYB_ENC: whole stream (header 0xAF x[0], LITERAL fallback)
 };
-#define FSM_TILE 4096
+#define FSM_SUB 1                          /* 4096-element chunks per tile */
+#define FSM_TILE (4096 * FSM_SUB)
 
 struct Fsm {
     uint32_t c0, c1;   // bytes emitted when entering in state 0 / 1
@@ -2723,14 +2724,37 @@ static __device__ __forceinline__ Fsm fsm_then(const Fsm &a, const Fsm &b)
     return r;
 }
 
+// inclusive scan of compositions across a wave (lane order = element order): shuffles, no
+// barrier (the 8-round Hillis-Steele over the workgroup cost 16 barriers per 4096-element tile)
+static __device__ __forceinline__ Fsm fsm_wave_scan_incl(Fsm f, int lane)
+{
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        Fsm p;
+        p.c0 = (uint32_t)__shfl_up((int)f.c0, d, 64);
+        p.c1 = (uint32_t)__shfl_up((int)f.c1, d, 64);
+        const uint32_t ss = (uint32_t)__shfl_up((int)(f.s0 | (f.s1 << 1)), d, 64);
+        p.s0 = ss & 1u;
+        p.s1 = ss >> 1;
+        if (lane >= d) f = fsm_then(p, f);
+    }
+    return f;
+}
+static __device__ __forceinline__ uint4 fsm_pack(const Fsm &f) { return make_uint4(f.c0, f.c1, f.s0, f.s1); }
+static __device__ __forceinline__ Fsm fsm_unpack(const uint4 &v) { Fsm f; f.c0 = v.x; f.c1 = v.y; f.s0 = v.z; f.s1 = v.w; return f; }
+
 __constant__ uint8_t c_static_rank[256];   // " etaoins" -> 0..7, else 0xFF (initialize_dictionary)
 
 static __device__ __forceinline__ bool is_lower(uint32_t b) { return b >= 'a' && b <= 'z'; }
 
 // A lane's 16 elements read their bytes from one window of 20 bytes: window byte r = stream
 // byte g0 - 1 + r, g0 = the byte of the lane's first element (element j <-> byte j + FSM_OFF).
-// Six aligned dword loads (only granules holding a byte of [0, len): no access outside the
-// buffer) and five v_alignbyte replace 16-48 single-byte loads.
+// Lanes' windows start 16 bytes apart, so the misalignment m of the window start is the same
+// in every lane: each lane loads the one aligned 16-B granule its window starts in, takes the
+// next granule from the lane above (ds_bpermute; lane 63 loads its own), and five
+// v_alignbyte by m cut the 20 bytes (six dword loads per lane before: 6x the address work).
+// Granules wholly outside [in, in + len) are not read (zero); bytes outside it inside a read
+// granule are never used by the element rules.
 template <int M> struct FsmOff {
     static constexpr int v = (M == M_NYB_DEC || M == M_SMALL_DEC) ? 2 : (FsmMode<M>::body && !FsmMode<M>::small_enc) ? 0 : 1;
 };
@@ -2738,17 +2762,38 @@ struct FsmWin {
     uint32_t w[5];
     __device__ __forceinline__ uint32_t b(int r) const { return (w[r >> 2] >> (8 * (r & 3))) & 255u; }
 };
+static __device__ __forceinline__ uint4 fsm_granule(uintptr_t ad, uintptr_t lo, uintptr_t hi)
+{
+    return (ad + 16 > lo && ad < hi) ? *reinterpret_cast<const uint4 *>(ad) : make_uint4(0u, 0u, 0u, 0u);
+}
+static __device__ __forceinline__ uint4 fsm_shfl_down(const uint4 &v, int d)
+{
+    return make_uint4((uint32_t)__shfl_down((int)v.x, d, 64), (uint32_t)__shfl_down((int)v.y, d, 64),
+                      (uint32_t)__shfl_down((int)v.z, d, 64), (uint32_t)__shfl_down((int)v.w, d, 64));
+}
+// every lane of the wave must call this (shuffles), also lanes without elements
 static __device__ __forceinline__ FsmWin fsm_window(const uint8_t *__restrict__ in, uint64_t len, int64_t g0)
 {
     const uintptr_t lo = (uintptr_t)in, hi = (uintptr_t)(in + len);
     const uintptr_t s = (uintptr_t)(in + g0 - 1);
-    const uintptr_t a = s & ~(uintptr_t)3;
-    const uint32_t m = (uint32_t)(s & 3);
+    const uintptr_t a = s & ~(uintptr_t)15;
+    const uint32_t m = (uint32_t)(s & 3), dq = (uint32_t)((s >> 2) & 3);   // byte and dword shift (uniform)
+    const int lane = (int)(threadIdx.x & 63);
+    const uint4 v0 = fsm_granule(a, lo, hi);
+    uint4 v1 = fsm_shfl_down(v0, 1), v2 = make_uint4(0u, 0u, 0u, 0u);
+    if (lane == 63) v1 = fsm_granule(a + 16, lo, hi);
+    if (4 * dq + m > 14) {   // the window's 18 used bytes reach a third granule (uniform branch)
+        v2 = fsm_shfl_down(v0, 2);
+        if (lane >= 62) v2 = fsm_granule(a + 32, lo, hi);
+    }
+    const uint32_t d12[12] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w, v2.x, v2.y, v2.z, v2.w};
     uint32_t d[6];
 #pragma unroll
-    for (int q = 0; q < 6; ++q) {
-        const uintptr_t ad = a + 4 * q;
-        d[q] = (ad + 4 > lo && ad < hi) ? *reinterpret_cast<const uint32_t *>(ad) : 0u;
+    for (int q = 0; q < 6; ++q) {   // dwords dq + q (dq uniform: selects, no register indexing)
+        uint32_t v = d12[q];
+#pragma unroll
+        for (int k = 1; k < 4; ++k) v = dq == (uint32_t)k ? d12[q + k] : v;
+        d[q] = v;
     }
     FsmWin f;
 #pragma unroll
@@ -2813,35 +2858,36 @@ template <int M>
 __global__ __launch_bounds__(256) void k_fsm_tiles(const uint8_t *__restrict__ in, uint64_t len,
                                                    uint64_t nelem, uint4 *__restrict__ summ, FsmAux aux)
 {
-    __shared__ uint4 s_f[256];
+    __shared__ uint4 s_f[FSM_SUB][4];   // wave totals per chunk
     const int t = threadIdx.x;
-    const uint64_t j0 = (uint64_t)blockIdx.x * FSM_TILE + (uint64_t)t * 16;
-    Fsm f = fsm_id();
-    if (j0 < nelem) {
-        const FsmWin W = fsm_window(in, len, (int64_t)j0 + FsmOff<M>::v);
-        uint32_t rk[16];
-        fsm_ranks<M>(W, aux, j0, nelem, rk);
+    // chunk c of the tile: elements [c * 4096 + 16 t, +16) for lane t (coalesced per chunk);
+    // all chunks' windows are loaded before any is walked
+    FsmWin W[FSM_SUB];
 #pragma unroll
-        for (int k = 0; k < 16; ++k)
-            if (j0 + k < nelem) f = fsm_then(f, elem_fsm<M>(W, k, len, j0 + k, M == M_NYB_ENC ? rk[k] : 0u));
-    }
-    s_f[t] = make_uint4(f.c0, f.c1, f.s0, f.s1);
-    __syncthreads();
-    for (int stride = 128; stride > 0; stride >>= 1) {
-        const bool act = t < stride;
-        Fsm r = fsm_id();
-        if (act) {
-            const uint4 a = s_f[2 * t], b = s_f[2 * t + 1];
-            Fsm fa, fb;
-            fa.c0 = a.x; fa.c1 = a.y; fa.s0 = a.z; fa.s1 = a.w;
-            fb.c0 = b.x; fb.c1 = b.y; fb.s0 = b.z; fb.s1 = b.w;
-            r = fsm_then(fa, fb);
+    for (int c = 0; c < FSM_SUB; ++c)
+        W[c] = fsm_window(in, len, (int64_t)((uint64_t)blockIdx.x * FSM_TILE + (uint64_t)c * 4096 + (uint64_t)t * 16) +
+                                       FsmOff<M>::v);   // every lane (shuffles)
+#pragma unroll
+    for (int c = 0; c < FSM_SUB; ++c) {
+        const uint64_t j0 = (uint64_t)blockIdx.x * FSM_TILE + (uint64_t)c * 4096 + (uint64_t)t * 16;
+        Fsm f = fsm_id();
+        if (j0 < nelem) {
+            uint32_t rk[16];
+            fsm_ranks<M>(W[c], aux, j0, nelem, rk);
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                if (j0 + k < nelem) f = fsm_then(f, elem_fsm<M>(W[c], k, len, j0 + k, M == M_NYB_ENC ? rk[k] : 0u));
         }
-        __syncthreads();
-        if (act) s_f[t] = make_uint4(r.c0, r.c1, r.s0, r.s1);
-        __syncthreads();
+        const Fsm inc = fsm_wave_scan_incl(f, t & 63);
+        if ((t & 63) == 63) s_f[c][t >> 6] = fsm_pack(inc);
     }
-    if (t == 0) summ[blockIdx.x] = s_f[0];
+    __syncthreads();
+    if (t == 0) {
+        Fsm a = fsm_id();
+#pragma unroll
+        for (int q = 0; q < 4 * FSM_SUB; ++q) a = fsm_then(a, fsm_unpack(s_f[q >> 2][q & 3]));
+        summ[blockIdx.x] = fsm_pack(a);
+    }
 }
 
 // Scan of the tile summaries in two levels, all accesses coalesced: k_fsm_scan_up turns each
@@ -2960,9 +3006,8 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
     // the tile's output (<= 2 bytes per element) is staged in LDS, s_out[x] = out[o_al + x]
     // with o_al the 16-B granule of its first byte, then stored as whole uint4s (bytes only in
     // the two granules shared with the neighbouring tiles)
-    __shared__ uint4 s_f[256];
+    __shared__ uint4 s_f[FSM_SUB][4];   // wave totals per chunk
     __shared__ __attribute__((aligned(16))) uint8_t s_out[2 * FSM_TILE + 32];
-    __shared__ uint64_t s_end;
     const int t = threadIdx.x;
     const bool nyb_whole = M == M_NYB_ENC && aux.whole;
     const bool enc = FsmMode<M>::enc || nyb_whole;
@@ -2982,110 +3027,124 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
         else if (M == M_SMALL_ENC) { out[0] = 8; out[1] = in[0]; }
         else { out[0] = in[1]; }
     }
-    const uint64_t j0 = (uint64_t)blockIdx.x * FSM_TILE + (uint64_t)t * 16;
-    FsmWin W;
-    uint32_t rk[16];
-    Fsm f = fsm_id();
-    if (j0 < nelem) {
-        W = fsm_window(in, len, (int64_t)j0 + FsmOff<M>::v);
-        fsm_ranks<M>(W, aux, j0, nelem, rk);
+    FsmWin W_[FSM_SUB];
 #pragma unroll
-        for (int k = 0; k < 16; ++k)
-            if (j0 + k < nelem) f = fsm_then(f, elem_fsm<M>(W, k, len, j0 + k, M == M_NYB_ENC ? rk[k] : 0u));
-    }
-    // workgroup exclusive scan of compositions (Hillis-Steele on the 256 thread maps)
-    s_f[t] = make_uint4(f.c0, f.c1, f.s0, f.s1);
-    __syncthreads();
-    for (int d = 1; d < 256; d <<= 1) {
-        uint4 p = make_uint4(0, 0, 0, 1);
-        const bool has = t >= d;
-        if (has) p = s_f[t - d];
-        const uint4 me = s_f[t];
-        __syncthreads();
-        if (has) {
-            Fsm fa, fb;
-            fa.c0 = p.x; fa.c1 = p.y; fa.s0 = p.z; fa.s1 = p.w;
-            fb.c0 = me.x; fb.c1 = me.y; fb.s0 = me.z; fb.s1 = me.w;
-            const Fsm r = fsm_then(fa, fb);
-            s_f[t] = make_uint4(r.c0, r.c1, r.s0, r.s1);
+    for (int c = 0; c < FSM_SUB; ++c)
+        W_[c] = fsm_window(in, len, (int64_t)((uint64_t)blockIdx.x * FSM_TILE + (uint64_t)c * 4096 + (uint64_t)t * 16) +
+                                       FsmOff<M>::v);   // every lane (shuffles)
+    // per chunk: the lane's composition, scanned across the wave (shuffles); the wave totals of
+    // every chunk through LDS (one barrier)
+    const int lane = t & 63, wid = t >> 6;
+    Fsm ex[FSM_SUB];   // lanes before this one in the wave, per chunk
+#pragma unroll
+    for (int c = 0; c < FSM_SUB; ++c) {
+        const uint64_t j0 = (uint64_t)blockIdx.x * FSM_TILE + (uint64_t)c * 4096 + (uint64_t)t * 16;
+        Fsm f = fsm_id();
+        if (j0 < nelem) {
+            uint32_t rk[16];
+            fsm_ranks<M>(W_[c], aux, j0, nelem, rk);
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                if (j0 + k < nelem) f = fsm_then(f, elem_fsm<M>(W_[c], k, len, j0 + k, M == M_NYB_ENC ? rk[k] : 0u));
         }
-        __syncthreads();
+        const Fsm inc = fsm_wave_scan_incl(f, lane);
+        if (lane == 63) s_f[c][wid] = fsm_pack(inc);
+        const uint32_t c0 = (uint32_t)__shfl_up((int)inc.c0, 1, 64), c1 = (uint32_t)__shfl_up((int)inc.c1, 1, 64);
+        const uint32_t ss = (uint32_t)__shfl_up((int)(inc.s0 | (inc.s1 << 1)), 1, 64);
+        ex[c].c0 = c0; ex[c].c1 = c1; ex[c].s0 = ss & 1u; ex[c].s1 = ss >> 1;
+        if (lane == 0) ex[c] = fsm_id();
     }
+    __syncthreads();
     // entry = the group's entry, then the tile's local exclusive composition (k_fsm_scan_up)
     const uint64_t e = entry[blockIdx.x / FSM_GROUP];
     const uint4 lc = loc[blockIdx.x];
     const uint32_t s_g = (uint32_t)(e & 1);
     const uint64_t o_tile = (e >> 1) + (s_g ? lc.y : lc.x) + (headed ? (enc ? 2 : 1) : 0);   // first output byte
     const uint32_t s_tile = s_g ? lc.w : lc.z;
-    uint64_t o = o_tile;
-    uint32_t s = s_tile;
-    if (t > 0) {
-        const uint4 p = s_f[t - 1];
-        o += s ? p.y : p.x;
-        s = s ? p.w : p.z;
+    Fsm run = fsm_id();   // chunks before c, then waves before this one in chunk c
+    uint64_t o_c[FSM_SUB];
+    uint32_t st_c[FSM_SUB];
+#pragma unroll
+    for (int c = 0; c < FSM_SUB; ++c) {
+        Fsm pre = run;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const Fsm w = fsm_unpack(s_f[c][q]);
+            if (q < wid) pre = fsm_then(pre, w);
+            run = fsm_then(run, w);
+        }
+        const Fsm x = fsm_then(pre, ex[c]);
+        o_c[c] = o_tile + (s_tile ? x.c1 : x.c0);
+        st_c[c] = s_tile ? x.s1 : x.s0;
     }
-    if (t == 255) {   // the tile's end: inclusive composition from the entry state
-        const uint4 p = s_f[255];
-        s_end = o_tile + (s_tile ? p.y : p.x);
-    }
+    const uint64_t s_end = o_tile + (s_tile ? run.c1 : run.c0);   // the tile's end
     // granule of the tile's first byte, relative to out (negative when out is unaligned and
     // the tile starts in out's first granule)
     const int64_t o_al = (int64_t)((((uintptr_t)(out + o_tile)) & ~(uintptr_t)15) - (uintptr_t)out);
 #define so(o) s_out[(uint32_t)((int64_t)(o) - o_al)]   /* staged out[o] */
     const uint8_t *tbl = (const uint8_t *)" etaoins";
-    if (j0 < nelem) {
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const uint64_t j = j0 + k;
-            if (j >= nelem) break;
-            const uint32_t x = W.b(k + 1);
-            if (M == M_NYB_ENC) {
-                const uint64_t i = j + 1;
-                const uint32_t r = rk[k];
-                if (r != 0xFF) {
-                    if (s == 1) {
-                        const uint32_t rp = k ? rk[k - 1] : (j ? (aux.rk ? (uint32_t)aux.rk[j - 1]
-                                                                        : (uint32_t)c_static_rank[W.b(0)])
-                                                               : aux.pend_rank);
-                        so(o++) = (uint8_t)(((8u | rp) << 4) | (8u | r));
-                        s = 0;
+    for (int c = 0; c < FSM_SUB; ++c) {
+        const uint64_t j0 = (uint64_t)blockIdx.x * FSM_TILE + (uint64_t)c * 4096 + (uint64_t)t * 16;
+        const FsmWin &W = W_[c];
+        uint64_t o = o_c[c];
+        uint32_t s = st_c[c];
+        uint32_t rk[16];
+        if (j0 < nelem) fsm_ranks<M>(W, aux, j0, nelem, rk);
+        if (j0 < nelem) {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const uint64_t j = j0 + k;
+                if (j >= nelem) break;
+                const uint32_t x = W.b(k + 1);
+                if (M == M_NYB_ENC) {
+                    const uint64_t i = j + 1;
+                    const uint32_t r = rk[k];
+                    if (r != 0xFF) {
+                        if (s == 1) {
+                            const uint32_t rp = k ? rk[k - 1] : (j ? (aux.rk ? (uint32_t)aux.rk[j - 1]
+                                                                            : (uint32_t)c_static_rank[W.b(0)])
+                                                                   : aux.pend_rank);
+                            so(o++) = (uint8_t)(((8u | rp) << 4) | (8u | r));
+                            s = 0;
+                        } else {
+                            s = 1;
+                            if (aux.is_last && i == len - 1) out[o] = (uint8_t)x;   // odd tail (:1000-1009)
+                        }
                     } else {
-                        s = 1;
-                        if (aux.is_last && i == len - 1) out[o] = (uint8_t)x;   // odd tail (:1000-1009)
+                        if (s == 1) { so(o++) = (uint8_t)W.b(k); so(o++) = (uint8_t)x; }
+                        else so(o++) = (uint8_t)x;
+                        s = 0;
                     }
-                } else {
-                    if (s == 1) { so(o++) = (uint8_t)W.b(k); so(o++) = (uint8_t)x; }
-                    else so(o++) = (uint8_t)x;
-                    s = 0;
-                }
-            } else if (M == M_NYB_DEC || M == M_NYB_DBODY) {
-                const uint64_t kk = M == M_NYB_DBODY ? j : j + 2;
-                const uint32_t h = x >> 4, l = x & 15;
-                const uint32_t nxt = (kk + 1 < len) ? (W.b(k + 2) >> 4) : 0u;
-                if (s == 0) {
-                    if (h & 8) {
-                        so(o++) = tbl[h & 7];
+                } else if (M == M_NYB_DEC || M == M_NYB_DBODY) {
+                    const uint64_t kk = M == M_NYB_DBODY ? j : j + 2;
+                    const uint32_t h = x >> 4, l = x & 15;
+                    const uint32_t nxt = (kk + 1 < len) ? (W.b(k + 2) >> 4) : 0u;
+                    if (s == 0) {
+                        if (h & 8) {
+                            so(o++) = tbl[h & 7];
+                            if (l & 8) { so(o++) = tbl[l & 7]; s = 0; }
+                            else { so(o++) = (uint8_t)(((l & 7) << 4) + nxt); s = 1; }
+                        } else {
+                            so(o++) = (uint8_t)x;
+                            s = 0;
+                        }
+                    } else {
                         if (l & 8) { so(o++) = tbl[l & 7]; s = 0; }
                         else { so(o++) = (uint8_t)(((l & 7) << 4) + nxt); s = 1; }
-                    } else {
-                        so(o++) = (uint8_t)x;
-                        s = 0;
+                    }
+                } else if (FsmMode<M>::small_enc) {
+                    const uint64_t i = j + 1;
+                    const bool second = (M == M_SMALL_BODY1 || i >= 2) && W.b(k) == ' ' && is_lower(x);
+                    if (!second) {
+                        const uint32_t nx = W.b(k + 2);
+                        if (x == ' ' && i + 1 < len && is_lower(nx)) so(o++) = (uint8_t)(0x80 + nx);
+                        else so(o++) = (uint8_t)x;
                     }
                 } else {
-                    if (l & 8) { so(o++) = tbl[l & 7]; s = 0; }
-                    else { so(o++) = (uint8_t)(((l & 7) << 4) + nxt); s = 1; }
-                }
-            } else if (FsmMode<M>::small_enc) {
-                const uint64_t i = j + 1;
-                const bool second = (M == M_SMALL_BODY1 || i >= 2) && W.b(k) == ' ' && is_lower(x);
-                if (!second) {
-                    const uint32_t nx = W.b(k + 2);
-                    if (x == ' ' && i + 1 < len && is_lower(nx)) so(o++) = (uint8_t)(0x80 + nx);
+                    if (x >= 0x80) { so(o++) = ' '; so(o++) = (uint8_t)(x - 0x80); }
                     else so(o++) = (uint8_t)x;
                 }
-            } else {
-                if (x >= 0x80) { so(o++) = ' '; so(o++) = (uint8_t)(x - 0x80); }
-                else so(o++) = (uint8_t)x;
             }
         }
     }
@@ -3110,75 +3169,239 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
 }
 
 // ------------------------------------------------------------------------------------
-// Adaptive (modify=true) nybble codec: the context/move-to-front state depends on the
-// whole history (N4), so a single stream is walked by one lane; the 16x8
-// MTF lists live in LDS. Same algorithm as nybble_compression.c:643-1038.
+// Small front-end (small_compression.c:507-665) and its inverse, stateless: each element's
+// output (0 or 1 byte encoding, 1 or 2 decoding) depends only on its byte and the bytes
+// beside it, so a tile needs only output counts, not the transducer compositions above.
+// Geometry: tiles of SM_TILE bytes on the 16-B address grid of the element bytes (element j
+// = byte j + FsmOff of `in`); step s of a tile = 1024 bytes, wave w = its 256-byte quarter,
+// lane = one dword (4 elements). A wave's elements are contiguous, so a lane's neighbour
+// bytes come from the lanes beside it (ds_bpermute) and only lanes 0 and 63 read a byte of
+// the next wave's dwords; all 16 dword loads of a lane are issued before any is used.
+// The writer stages the tile's output in LDS: lane t's bytes land at consecutive positions
+// ~4 t apart, so its byte stores spread over the banks (the transducer writer's lanes, 16
+// elements apart, hit each bank 4 times per instruction).
 // ------------------------------------------------------------------------------------
-static __device__ __forceinline__ void mtf_touch(uint8_t *list, uint8_t v)
+#define SM_TILE 8192
+#define SM_STEPS (SM_TILE / 1024)
+
+template <int M> struct SmMode {
+    static constexpr bool dec = (M == M_SMALL_DEC || M == M_SMALL_DBODY);
+    static constexpr bool fast = (M == M_SMALL_ENC || M == M_SMALL_BODY0 || M == M_SMALL_BODY1 || dec);
+};
+
+// tile-relative bounds (uniform, 32-bit): tile byte u = A0 + tile * SM_TILE + u, u in [0, SM_TILE)
+struct SmTile {
+    int64_t base;          // tile byte 0 relative to `in` (may be negative in tile 0)
+    uint32_t lo, hi;       // element bytes: u in [lo, hi)
+    uint32_t two;          // u >= two <=> stream byte index >= 2 (a pair may end there)
+    uint32_t nxt;          // u < nxt <=> the byte after u is inside the stream
+};
+static __device__ __forceinline__ uint32_t sm_clamp(int64_t v) { return (uint32_t)(v < 0 ? 0 : v > SM_TILE ? SM_TILE : v); }
+static __device__ __forceinline__ SmTile sm_tile(const uint8_t *in, int off, uint64_t nelem, uint64_t len, uint64_t tile)
 {
-    uint8_t carry = v;
-    for (int p = 0; p < 8; ++p) {
-        const uint8_t old = list[p];
-        list[p] = carry;
-        carry = old;
-        if (carry == v) break;
+    const int64_t lead = (int64_t)(((uintptr_t)in + (uintptr_t)off) & 15u);   // element 0's offset in its granule
+    SmTile T;
+    T.base = (int64_t)off - lead + (int64_t)(tile * SM_TILE);
+    T.lo = sm_clamp((int64_t)off - T.base);
+    T.hi = sm_clamp((int64_t)off + (int64_t)nelem - T.base);
+    T.two = sm_clamp(2 - T.base);
+    T.nxt = sm_clamp((int64_t)len - 1 - T.base);
+    return T;
+}
+static uint64_t sm_ntiles(const uint8_t *in, int off, uint64_t nelem)
+{
+    const uint64_t lead = ((uintptr_t)in + (uintptr_t)off) & 15u;
+    return nelem ? (lead + nelem + SM_TILE - 1) / SM_TILE : 0;
+}
+
+// output count (and, when OUT, the bytes written at stage[pos..]) of the 4 elements in a
+// lane's dword d at tile byte u; p / q = the bytes before / after the dword
+#define SM_TRASH (2 * SM_TILE + 32)   /* stage bytes [SM_TRASH, +256): a sink per lane for unwritten bytes */
+template <int M, bool OUT>
+static __device__ __forceinline__ uint32_t sm_elems(uint32_t d, uint32_t p, uint32_t q, uint32_t u, const SmTile &T,
+                                                    uint8_t *stage, uint32_t pos)
+{
+    // branch-free: a byte that is not written goes to the lane's sink (an exec-masked store
+    // per byte cost a 64-bit mask pair each: SGPR spills, 211 VGPRs)
+    const uint32_t sink = SM_TRASH + 4u * (threadIdx.x & 63);
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t uk = u + (uint32_t)k;
+        const bool valid = uk >= T.lo && uk < T.hi;
+        const uint32_t cur = (d >> (8 * k)) & 255u;
+        if (SmMode<M>::dec) {
+            const bool two = cur >= 0x80;
+            if (OUT) {
+                stage[valid ? pos + cnt : sink] = (uint8_t)(two ? ' ' : cur);
+                stage[valid && two ? pos + cnt + 1 : sink] = (uint8_t)(cur - 0x80);
+            }
+            cnt += valid ? (two ? 2u : 1u) : 0u;
+        } else {
+            const uint32_t prv = k ? (d >> (8 * (k - 1))) & 255u : p;
+            const uint32_t nxt = k < 3 ? (d >> (8 * (k + 1))) & 255u : q;
+            const bool second = (M == M_SMALL_BODY1 || uk >= T.two) && prv == ' ' && is_lower(cur);
+            const bool keep = valid && !second;
+            if (OUT)
+                stage[keep ? pos + cnt : sink] = (uint8_t)((cur == ' ' && uk < T.nxt && is_lower(nxt)) ? 0x80 + nxt : cur);
+            cnt += keep ? 1u : 0u;
+        }
+    }
+    return cnt;
+}
+
+// the lane's 16 dwords (step st: tile byte st * 1024 + w * 256 + 4 lane), all loads issued
+// before any is used; the bytes at the waves' edges go through LDS (SmEdge), with one byte
+// before and after the tile read from memory
+template <int M>
+static __device__ __forceinline__ void sm_load(const uint8_t *__restrict__ in, uint64_t len, const SmTile &T, int w,
+                                               int lane, uint32_t (&dv)[SM_STEPS])
+{
+    const uint32_t ulo = T.lo ? T.lo - 1 : 0, uhi = T.hi + 1;   // bytes the elements read
+#pragma unroll
+    for (int st = 0; st < SM_STEPS; ++st) {
+        const uint32_t u = (uint32_t)(st * 1024 + w * 256 + lane * 4);
+        const int64_t o = T.base + (int64_t)u;   // relative to in
+        dv[st] = (u + 4 > ulo && u < uhi && o + 4 > 0 && o < (int64_t)len) ? *reinterpret_cast<const uint32_t *>(in + o) : 0u;
+    }
+}
+struct SmEdge {
+    uint8_t first[SM_STEPS][4], last[SM_STEPS][4];   // each wave's first / last byte per step
+    uint8_t before, after;                            // the bytes beside the tile
+};
+static __device__ __forceinline__ void sm_edges_put(SmEdge &E, const uint8_t *__restrict__ in, uint64_t len,
+                                                    const SmTile &T, int t, const uint32_t (&dv)[SM_STEPS])
+{
+    const int lane = t & 63, w = t >> 6;
+    if (lane == 0 || lane == 63) {
+#pragma unroll
+        for (int st = 0; st < SM_STEPS; ++st) {
+            if (lane == 0) E.first[st][w] = (uint8_t)dv[st];
+            else E.last[st][w] = (uint8_t)(dv[st] >> 24);
+        }
+    }
+    if (t == 0) E.before = (T.base - 1 >= 0 && T.base - 1 < (int64_t)len) ? in[T.base - 1] : 0;
+    if (t == 255) E.after = (T.base + SM_TILE >= 0 && T.base + SM_TILE < (int64_t)len) ? in[T.base + SM_TILE] : 0;
+}
+// bytes before / after the lane's dword at step st (after a barrier behind sm_edges_put):
+// x = before, y = after; branch-free (the wave-edge bytes are uniform broadcast reads)
+static __device__ __forceinline__ uint2 sm_nb(const SmEdge &E, uint32_t d, int st, int w, int lane)
+{
+    const uint32_t pu = (uint32_t)__shfl_up((int)d, 1, 64) >> 24;
+    const uint32_t qd = (uint32_t)__shfl_down((int)d, 1, 64) & 255u;
+    const uint32_t pe = w > 0 ? E.last[st][w - 1] : st > 0 ? E.last[st - 1][3] : E.before;
+    const uint32_t qe = w < 3 ? E.first[st][w + 1] : st + 1 < SM_STEPS ? E.first[st + 1][0] : E.after;
+    return make_uint2(lane == 0 ? pe : pu, lane == 63 ? qe : qd);
+}
+
+// One tile per workgroup. (A persistent grid with the next tile's loads issued ahead
+// measured 1.6-1.8x slower: 150-246 VGPRs, 2-3 waves per SIMD.)
+template <int M>
+__global__ __launch_bounds__(256) void k_small_tiles(const uint8_t *__restrict__ in, uint64_t len, uint64_t nelem,
+                                                     uint4 *__restrict__ summ)
+{
+    __shared__ uint32_t s_w[4];
+    __shared__ SmEdge E;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const SmTile T = sm_tile(in, FsmOff<M>::v, nelem, len, blockIdx.x);
+    uint32_t dv[SM_STEPS];
+    sm_load<M>(in, len, T, w, lane, dv);
+    if (!SmMode<M>::dec) {
+        sm_edges_put(E, in, len, T, t, dv);
+        __syncthreads();
+    }
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int st = 0; st < SM_STEPS; ++st) {
+        const uint2 nb = SmMode<M>::dec ? make_uint2(0u, 0u) : sm_nb(E, dv[st], st, w, lane);
+        cnt += sm_elems<M, false>(dv[st], nb.x, nb.y, (uint32_t)(st * 1024 + w * 256 + lane * 4), T, nullptr, 0);
+    }
+    const uint32_t tot = wave_scan_incl(cnt);
+    if (lane == 63) s_w[w] = tot;
+    __syncthreads();
+    if (t == 0) {
+        const uint32_t c = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+        summ[blockIdx.x] = make_uint4(c, c, 0u, 0u);   // a stateless composition
     }
 }
 
-__global__ void k_nyb_seq(const uint8_t *__restrict__ in, uint64_t len, int enc, int modify,
-                          uint8_t *__restrict__ out, uint64_t *__restrict__ meta)
+template <int M>
+__global__ __launch_bounds__(256) void k_small_write(const uint8_t *__restrict__ in, uint64_t len, uint64_t nelem,
+                                                     const uint64_t *__restrict__ entry, const uint4 *__restrict__ loc,
+                                                     const uint64_t *__restrict__ meta, uint8_t *__restrict__ out)
 {
-    __shared__ uint8_t lists[16][8];
-    if (threadIdx.x != 0) return;
-    const uint8_t init[8] = {' ', 'e', 't', 'a', 'o', 'i', 'n', 's'};
-    for (int c = 0; c < 16; ++c)
-        for (int r = 0; r < 8; ++r) lists[c][r] = init[r];
-    uint64_t o = 0;
-    if (enc) {
-        out[o++] = 0xAF;
-        out[o++] = in[0];
-        int half = 0;
-        for (uint64_t i = 1; i < len; ++i) {
-            const uint8_t xp = in[i - 1], x = in[i];
-            const int c = (xp >> 3) & 15;
-            int r = -1;
-            for (int q = 0; q < 8; ++q) if (lists[c][q] == x) { r = q; break; }
-            if (r < 0) {
-                if (!half) out[o++] = x;
-                else { out[o] = xp; out[o + 1] = x; o += 2; half = 0; }
+    __shared__ uint32_t s_w[SM_STEPS][4];
+    __shared__ SmEdge E;
+    __shared__ __attribute__((aligned(16))) uint8_t s_out[SM_TRASH + 256];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const bool enc = M == M_SMALL_ENC;
+    const uint64_t total = enc ? 2 + meta[0] : 1 + meta[0];
+    if (enc && total >= len) {   // LITERAL: ' ' + raw input (:655-662), one grid-stride pass
+        for (uint64_t i = (uint64_t)blockIdx.x * 256 + t; i < len; i += (uint64_t)gridDim.x * 256) out[1 + i] = in[i];
+        if (blockIdx.x == 0 && t == 0) out[0] = ' ';
+        return;
+    }
+    const bool headed = !FsmMode<M>::body;
+    if (blockIdx.x == 0 && t == 0 && headed) {
+        if (enc) { out[0] = 8; out[1] = in[0]; }
+        else out[0] = in[1];
+    }
+    const SmTile T = sm_tile(in, FsmOff<M>::v, nelem, len, blockIdx.x);
+    uint32_t dv[SM_STEPS];
+    sm_load<M>(in, len, T, w, lane, dv);
+    if (!SmMode<M>::dec) {
+        sm_edges_put(E, in, len, T, t, dv);
+        __syncthreads();
+    }
+    uint32_t ex[SM_STEPS];   // this lane's offset inside its wave's part of step st
+#pragma unroll
+    for (int st = 0; st < SM_STEPS; ++st) {
+        const uint2 nb = SmMode<M>::dec ? make_uint2(0u, 0u) : sm_nb(E, dv[st], st, w, lane);
+        const uint32_t c = sm_elems<M, false>(dv[st], nb.x, nb.y, (uint32_t)(st * 1024 + w * 256 + lane * 4), T, nullptr, 0);
+        const uint32_t inc = wave_scan_incl(c);
+        ex[st] = inc - c;
+        if (lane == 63) s_w[st][w] = inc;
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    __syncthreads();
+    const uint64_t e = entry[blockIdx.x / FSM_GROUP];
+    const uint64_t o_tile = (e >> 1) + loc[blockIdx.x].x + (headed ? (enc ? 2 : 1) : 0);   // first output byte
+    const int64_t o_al = (int64_t)((((uintptr_t)(out + o_tile)) & ~(uintptr_t)15) - (uintptr_t)out);
+    const uint32_t lead = (uint32_t)((int64_t)o_tile - o_al);   // stage offset of the tile's first byte
+    uint32_t run = 0;
+#pragma unroll
+    for (int st = 0; st < SM_STEPS; ++st) {
+        uint32_t pre = run;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t v = s_w[st][q];
+            pre += q < w ? v : 0u;
+            run += v;
+        }
+        // opaque: the write pass recomputes the counts' byte tests instead of keeping pass 1's
+        // 64 per-byte masks alive across the barrier (216 VGPRs, SGPR spills)
+        asm volatile("" : "+v"(dv[st]));
+        const uint2 nb = SmMode<M>::dec ? make_uint2(0u, 0u) : sm_nb(E, dv[st], st, w, lane);
+        (void)sm_elems<M, true>(dv[st], nb.x, nb.y, (uint32_t)(st * 1024 + w * 256 + lane * 4), T, s_out, lead + pre + ex[st]);
+        __builtin_amdgcn_sched_barrier(0);   // one step's stores at a time (registers)
+    }
+    __syncthreads();
+    // store [o_tile, o_tile + run): whole granules as uint4, the first and last bytewise
+    const int64_t beg = (int64_t)o_tile, end = beg + (int64_t)run;
+    if (end > beg) {
+        const int64_t ng = (end - o_al + 15) / 16;
+        for (int64_t q = t; q < ng; q += 256) {
+            const int64_t b0 = o_al + 16 * q;
+            if (b0 >= beg && b0 + 16 <= end) {
+                *reinterpret_cast<uint4 *>(out + b0) = *reinterpret_cast<const uint4 *>(s_out + 16 * q);
             } else {
-                const uint8_t nyb = (uint8_t)(8 | r);
-                if (!half) { out[o] = (uint8_t)(nyb << 4); half = 1; }
-                else { out[o] = (uint8_t)(out[o] | nyb); ++o; half = 0; }
+                for (int k = 0; k < 16; ++k) {
+                    const int64_t bq = b0 + k;
+                    if (bq >= beg && bq < end) out[bq] = s_out[16 * q + k];
+                }
             }
-            if (modify) mtf_touch(lists[c], x);
-        }
-        if (half) out[o++] = in[len - 1];
-        if (o >= len) {   // LITERAL fallback
-            out[0] = ' ';
-            for (uint64_t i = 0; i < len; ++i) out[1 + i] = in[i];
-            o = len + 1;
-        }
-    } else {
-        out[o++] = in[1];
-        uint64_t pos = 2;
-        int off = 0;
-        while (pos < len) {
-            const uint8_t b = in[pos];
-            int nyb, nxt;
-            if (off == 0) { nyb = b >> 4; nxt = b & 15; }
-            else { nyb = b & 15; nxt = (pos + 1 < len) ? (in[pos + 1] >> 4) : 0; }
-            const int c = (out[o - 1] >> 3) & 15;
-            int used;
-            if (nyb & 8) { out[o] = lists[c][nyb & 7]; used = 1; }
-            else { out[o] = (uint8_t)(((nyb & 7) << 4) + nxt); used = 2; }
-            if (modify) mtf_touch(lists[c], out[o]);
-            ++o;
-            off += used;
-            if (off >= 2) { ++pos; off -= 2; }
         }
     }
-    meta[0] = o;
 }
 
 // ------------------------------------------------------------------------------------
@@ -3336,6 +3559,116 @@ static __device__ __forceinline__ uint64_t mtf_init_word()
 {
     return 0x736E696F61746520ull;   // " etaoins", byte k = entry k
 }
+
+// Adaptive decode of one stream (decompress_bytestring with modify, :734-817): every byte
+// depends on the lists as every byte before it left them, so one wave walks the stream with
+// all state on the chip and nothing on the loop's dependency chain touching memory:
+//   * the 16 move-to-front lists as u64 words in VGPR lanes 0..15 (v_readlane /
+//     v_writelane by the uniform context index), touched with 64-bit scalar bit operations;
+//   * the input as two 256-B windows in one VGPR each (lane j = dword j), the next window's
+//     load issued 256 bytes before it is needed;
+//   * the output accumulated a dword at a time into a 256-B VGPR window (lane j = dword j)
+//     and stored whole, bytes outside [out, out + written) left untouched.
+// (The single-lane loop it replaces read in[pos] and out[o - 1] from global memory on every
+// byte: two dependent round trips per output byte.)
+// lane `lane` (uniform) of dst := val (uniform): a compare and a select (v_writelane_b32 needs
+// its lane index in M0 on gfx9 when the value is an SGPR)
+static __device__ __forceinline__ uint32_t writelane(uint32_t dst, uint32_t val, uint32_t lane)
+{
+    return (threadIdx.x & 63) == lane ? val : dst;
+}
+
+static __device__ __forceinline__ uint32_t adec_load(uintptr_t A, uintptr_t lo, uintptr_t hi, int lane)
+{
+    const uintptr_t ad = A + 4 * (uintptr_t)lane;
+    return (ad + 4 > lo && ad < hi) ? *reinterpret_cast<const uint32_t *>(ad) : 0u;
+}
+
+// store the output window (lane j = dword OA + 4j) restricted to bytes [lo, hi)
+static __device__ __forceinline__ void adec_flush(uint32_t w, uintptr_t OA, uintptr_t lo, uintptr_t hi, int lane)
+{
+    const uintptr_t ad = OA + 4 * (uintptr_t)lane;
+    if (ad >= lo && ad + 4 <= hi) {
+        *reinterpret_cast<uint32_t *>(ad) = w;
+    } else {
+        for (int k = 0; k < 4; ++k)
+            if (ad + k >= lo && ad + k < hi) *reinterpret_cast<uint8_t *>(ad + k) = (uint8_t)(w >> (8 * k));
+    }
+}
+
+__global__ __launch_bounds__(64) void k_nyb_adec(const uint8_t *__restrict__ in, uint64_t len,
+                                                 uint8_t *__restrict__ out, uint64_t *__restrict__ meta)
+{
+    const int lane = (int)threadIdx.x;
+    const uint64_t L0 = mtf_init_word();
+    uint32_t Llo = lane < 16 ? (uint32_t)L0 : 0u, Lhi = lane < 16 ? (uint32_t)(L0 >> 32) : 0u;
+    const uintptr_t ib = (uintptr_t)in, ie = ib + len, ob = (uintptr_t)out;
+    uintptr_t A = (ib + 2) & ~(uintptr_t)255;   // input window base (pos >= 2)
+    uint32_t win = adec_load(A, ib, ie, lane), winN = adec_load(A + 256, ib, ie, lane);
+    // output: out[0] = in[1]
+    const uint32_t first = (uint32_t)__builtin_amdgcn_readfirstlane((int)in[1]);
+    uintptr_t OA = ob & ~(uintptr_t)255;
+    uint32_t ow = 0;
+    uint64_t o = 0;
+    uint32_t acc = 0;   // output bytes of the current dword (bytes below ob + o's lane offset)
+    auto put = [&](uint32_t v) {
+        const uintptr_t a = ob + o;
+        if (a - OA >= 256) {   // window complete: store it, start the next
+            adec_flush(ow, OA, ob, a, lane);
+            OA += 256;
+            ow = 0;
+        }
+        const uint32_t sh = 8u * (uint32_t)(a & 3);
+        acc = (sh ? acc : 0u) | (v << sh);
+        ow = writelane(ow, (uint32_t)__builtin_amdgcn_readfirstlane((int)acc), (uint32_t)((a - OA) >> 2));
+        ++o;
+    };
+    put(first);
+    uint32_t pv = first;
+    uint64_t pos = 2;
+    uint32_t off = 0;
+    while (pos < len) {
+        const uintptr_t ap = ib + pos;
+        if (ap - A >= 256) {   // next input window; the one after it starts loading
+            A += 256;
+            win = winN;
+            winN = adec_load(A + 256, ib, ie, lane);
+        }
+        const uint32_t rel = (uint32_t)(ap - A);
+        const uint32_t b = ((uint32_t)__builtin_amdgcn_readlane((int)win, (int)(rel >> 2)) >> (8 * (ap & 3))) & 255u;
+        uint32_t nyb, nxt = b & 15u;
+        if (off == 0) {
+            nyb = b >> 4;
+        } else {
+            nyb = b & 15u;
+            nxt = 0;
+            if (pos + 1 < len) {
+                const uintptr_t an = ap + 1;
+                const uint32_t rn = (uint32_t)(an - A);
+                const uint32_t dw = rn < 256 ? (uint32_t)__builtin_amdgcn_readlane((int)win, (int)(rn >> 2))
+                                             : (uint32_t)__builtin_amdgcn_readlane((int)winN, (int)((rn - 256) >> 2));
+                nxt = ((dw >> (8 * (an & 3))) & 255u) >> 4;
+            }
+        }
+        const int c = (int)((pv >> 3) & 15u);
+        uint64_t L = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)Lhi, c) << 32) |
+                     (uint32_t)__builtin_amdgcn_readlane((int)Llo, c);
+        uint32_t v, used;
+        if (nyb & 8u) { v = (uint32_t)(L >> (8 * (nyb & 7u))) & 255u; used = 1; }
+        else { v = ((nyb & 7u) << 4) + nxt; used = 2; }
+        uint32_t cnt = 8;
+        (void)mtf_touch64(L, cnt, v);
+        Llo = writelane(Llo, (uint32_t)L, (uint32_t)c);
+        Lhi = writelane(Lhi, (uint32_t)(L >> 32), (uint32_t)c);
+        put(v);
+        pv = v;
+        off += used;
+        if (off >= 2) { ++pos; off -= 2; }
+    }
+    adec_flush(ow, OA, ob, ob + o, lane);
+    if (lane == 0) meta[0] = o;
+}
+
 
 __global__ __launch_bounds__(64) void k_nyb_chunk_enc(const uint8_t *__restrict__ in, uint64_t n, uint32_t K,
                                                       uint64_t nchunks, int modify, uint8_t *__restrict__ scr,
@@ -4091,7 +4424,7 @@ static int fsm_run(dc_ctx *c, const uint8_t *d_in, uint64_t len, uint64_t nelem,
                    const char *name, FsmAux aux = FsmAux{nullptr, 0, 0, 1, 1}, uint64_t *h_plan = nullptr,
                    bool write = true)
 {
-    const uint64_t ntiles = (nelem + FSM_TILE - 1) / FSM_TILE;
+    const uint64_t ntiles = SmMode<M>::fast ? sm_ntiles(d_in, FsmOff<M>::v, nelem) : (nelem + FSM_TILE - 1) / FSM_TILE;
     const uint64_t nt = ntiles ? ntiles : 1;
     const uint64_t ng = (nt + FSM_GROUP - 1) / FSM_GROUP;
     if (ensure((void **)&c->d_summ, &c->summ_cap, (nt + ng) * sizeof(uint4))) return DC_E_HIP;
@@ -4109,14 +4442,19 @@ static int fsm_run(dc_ctx *c, const uint8_t *d_in, uint64_t len, uint64_t nelem,
         HIPCHK(hipMemcpyAsync(c->d_summ, idn, sizeof(uint4), hipMemcpyHostToDevice, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
     } else {
-        LAUNCH(c, name, k_fsm_tiles<M>, ntiles, 256, d_in, len, nelem, c->d_summ, aux);
+        if constexpr (SmMode<M>::fast) LAUNCH(c, name, k_small_tiles<M>, ntiles, 256, d_in, len, nelem, c->d_summ);
+        else LAUNCH(c, name, k_fsm_tiles<M>, ntiles, 256, d_in, len, nelem, c->d_summ, aux);
         LAUNCH(c, "fsm_scan_up", k_fsm_scan_up, ng, FSM_GROUP, c->d_summ, ntiles, gsum);
         LAUNCH(c, "fsm_scan", k_fsm_scan, 1, 1024, (const uint4 *)gsum, ng, c->d_entry, c->d_meta, aux.s_init);
     }
     if (write) {
         const uint64_t wgrid = ntiles ? ntiles : 1;
-        LAUNCH(c, "fsm_write", k_fsm_write<M>, wgrid, 256, d_in, len, nelem, (const uint64_t *)c->d_entry,
-               (const uint4 *)c->d_summ, (const uint64_t *)c->d_meta, d_out, aux);
+        if constexpr (SmMode<M>::fast)
+            LAUNCH(c, "small_write", k_small_write<M>, wgrid, 256, d_in, len, nelem, (const uint64_t *)c->d_entry,
+                   (const uint4 *)c->d_summ, (const uint64_t *)c->d_meta, d_out);
+        else
+            LAUNCH(c, "fsm_write", k_fsm_write<M>, wgrid, 256, d_in, len, nelem, (const uint64_t *)c->d_entry,
+                   (const uint4 *)c->d_summ, (const uint64_t *)c->d_meta, d_out, aux);
     }
     HIPCHK(hipMemcpyAsync(c->h_pinned, c->d_meta, 6 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
@@ -4138,9 +4476,13 @@ static int fsm_write_planned(dc_ctx *c, const uint8_t *d_in, uint64_t len, uint6
                              uint64_t *h_len, FsmAux aux = FsmAux{nullptr, 0, 0, 1, 1})
 {
     if (c->fsm_in != d_in || c->fsm_len != len || c->fsm_nelem != nelem || c->fsm_mode != M) return DC_E_STATE;
-    const uint64_t ntiles = (nelem + FSM_TILE - 1) / FSM_TILE;
-    LAUNCH(c, "fsm_write", k_fsm_write<M>, ntiles ? ntiles : 1, 256, d_in, len, nelem, (const uint64_t *)c->d_entry,
-           (const uint4 *)c->d_summ, (const uint64_t *)c->d_meta, d_out, aux);
+    const uint64_t ntiles = SmMode<M>::fast ? sm_ntiles(d_in, FsmOff<M>::v, nelem) : (nelem + FSM_TILE - 1) / FSM_TILE;
+    if constexpr (SmMode<M>::fast)
+        LAUNCH(c, "small_write", k_small_write<M>, ntiles ? ntiles : 1, 256, d_in, len, nelem,
+               (const uint64_t *)c->d_entry, (const uint4 *)c->d_summ, (const uint64_t *)c->d_meta, d_out);
+    else
+        LAUNCH(c, "fsm_write", k_fsm_write<M>, ntiles ? ntiles : 1, 256, d_in, len, nelem, (const uint64_t *)c->d_entry,
+               (const uint4 *)c->d_summ, (const uint64_t *)c->d_meta, d_out, aux);
     HIPCHK(hipMemcpyAsync(c->h_pinned, c->d_meta, sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     c->fsm_in = nullptr;
@@ -4416,7 +4758,7 @@ int dc_nyb_decompress(dc_ctx *c, const uint8_t *d_in, uint64_t m, int modify, ui
     if (type == 0xAF) {
         if (m < 2) { *h_len = 0; return DC_OK; }
         if (!modify) return fsm_run<M_NYB_DEC>(c, d_in, m, m - 2, d_out, h_len, "nyb_dec_tiles");
-        LAUNCH(c, "nyb_seq_dec", k_nyb_seq, 1, 64, d_in, m, 0, 1, d_out, c->d_meta);
+        LAUNCH(c, "nyb_adec", k_nyb_adec, 1, 64, d_in, m, d_out, c->d_meta);
         HIPCHK(hipMemcpyAsync(c->h_pinned, c->d_meta, sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
         *h_len = c->h_pinned[0];

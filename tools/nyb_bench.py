@@ -1,60 +1,75 @@
-"""Nybble codec throughput on device (secondary path; not the bench.py headline).
-
-python tools/nyb_bench.py [--mib 1024] -> one JSON line: GB/s (input bytes / time) of the
-static transducer encode/decode, the parallel adaptive encode, and the chunked (DCNK)
-adaptive encode/decode, on english-like text resident in HBM (HIP events on the codec's
-stream = torch's current stream)."""
+"""Nybble codec throughput on the GPU beside the CPU oracle (one pinned host core), SURVEY
+§8 rows N1-N4 / BASELINE configs[0]: static and adaptive (modify) compress_bytestring /
+decompress_bytestring on a 4 KiB ASCII buffer (C1) and a 64 MiB english-like text.
+GPU times are HIP-event-free wall times of the device calls with inputs resident in HBM
+(each call ends in a host read of the output length, as the C ABI does).
+    python tools/nyb_bench.py [--big MiB] [--reps N]
+"""
 import argparse
 import json
 import os
 import sys
-
-import torch
+import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
 from data_compression_amd import synth  # noqa: E402
 from data_compression_amd.device import Codec  # noqa: E402
+from oracle import oracle as orc  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--big", type=int, default=64)
+ap.add_argument("--reps", type=int, default=5)
+a = ap.parse_args()
+c = Codec(0)
 
 
-def timed(fn, reps=3):
+def wall(fn, reps):
     fn()
     torch.cuda.synchronize()
-    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    a.record()
+    t = time.perf_counter()
     for _ in range(reps):
-        out = fn()
-    b.record()
+        fn()
     torch.cuda.synchronize()
-    return a.elapsed_time(b) / reps, out
+    return (time.perf_counter() - t) / reps
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--mib", type=int, default=1024)
-    ap.add_argument("--chunk", type=int, default=4096)
-    a = ap.parse_args()
-    n = a.mib << 20
-    base = torch.from_numpy(synth.english_like(64 << 20, seed=11)).cuda()
-    x = base.repeat((n + base.numel() - 1) // base.numel())[:n].contiguous()
-    c = Codec(0)
-    res = {"input": "english-like text (64 MiB generator tiled)", "bytes": n}
+def cpu_wall(fn, budget=10.0):
+    old = os.sched_getaffinity(0)
+    os.sched_setaffinity(0, {min(old)})
+    try:
+        t = time.perf_counter()
+        k = 0
+        while True:
+            fn()
+            k += 1
+            el = time.perf_counter() - t
+            if el > budget / 4 or k >= 1000:
+                return el / k
+    finally:
+        os.sched_setaffinity(0, old)
+
+
+rows = []
+for name, n in (("C1 4 KiB ascii", 4096), (f"{a.big} MiB english-like", a.big << 20)):
+    x = synth.english_like(n, seed=1)
+    xt = torch.from_numpy(x).cuda()
+    xb = x.tobytes()
     for modify in (False, True):
-        tag = "adaptive" if modify else "static"
-        ms, comp = timed(lambda: c.nyb_compress(x, modify))
-        res[f"{tag}_encode_GBps"] = round(n / ms / 1e6, 2)
-        res[f"{tag}_ratio"] = round(comp.numel() / n, 4)
-        if not modify:
-            ms, back = timed(lambda: c.nyb_decompress(comp, False))
-            assert torch.equal(back, x)
-            res["static_decode_GBps"] = round(n / ms / 1e6, 2)
-        ms, kc = timed(lambda: c.nyb_compress_chunked(x, modify, a.chunk))
-        res[f"{tag}_chunked_encode_GBps"] = round(n / ms / 1e6, 2)
-        ms, back = timed(lambda: c.nyb_decompress_chunked(kc))
-        assert torch.equal(back, x)
-        res[f"{tag}_chunked_decode_GBps"] = round(n / ms / 1e6, 2)
-        res[f"{tag}_chunked_ratio"] = round(kc.numel() / n, 4)
-    print(json.dumps(res))
-
-
-if __name__ == "__main__":
-    main()
+        comp = c.nyb_compress(xt, modify)
+        cb = comp.cpu().numpy().tobytes()
+        assert cb == orc.nybble_compress(xb, modify)
+        back = c.nyb_decompress(comp, modify)
+        assert np.array_equal(back.cpu().numpy(), x)
+        reps = a.reps if n > 1 << 20 else 50
+        te = wall(lambda: c.nyb_compress(xt, modify), reps)
+        td = wall(lambda: c.nyb_decompress(comp, modify), 1 if (modify and n > 1 << 20) else reps)
+        ce = cpu_wall(lambda: orc.nybble_compress(xb, modify))
+        cd = cpu_wall(lambda: orc.nybble_decompress(cb, modify))
+        rows.append({"input": name, "mode": "adaptive" if modify else "static", "bytes": n,
+                     "gpu_enc_MBps": round(n / te / 1e6, 1), "gpu_dec_MBps": round(n / td / 1e6, 1),
+                     "cpu_enc_MBps": round(n / ce / 1e6, 1), "cpu_dec_MBps": round(n / cd / 1e6, 1),
+                     "ratio": round(len(cb) / n, 4)})
+        print(json.dumps(rows[-1]), flush=True)
