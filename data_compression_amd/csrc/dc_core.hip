@@ -545,7 +545,12 @@ __global__ __launch_bounds__(256) void k_huff_table(const uint64_t *__restrict__
     __syncthreads();   // s_code, s_nb, s_maxbits
     T->code[t] = s_code[t];
     T->nbits[t] = s_nb[t];
+    // every coded byte 8 bits long (n = 16 on a flat byte distribution: a full depth-2 tree):
+    // pack and decode become byte maps (k_huff_pack / k_huff_decode8 fast paths)
+    const int fixed_ok = __syncthreads_and(s_nb[t] == 0u || s_nb[t] == 8u);
+    const int fixed_any = __syncthreads_or(s_nb[t] == 8u);
     if (t == 0) {
+        T->fixed8 = (fixed_ok && fixed_any) ? 1 : 0;
 #ifdef DC_DIAG
         g_tbldiag[4] = g_tbldiag[7] = __builtin_amdgcn_s_memtime();
 #endif
@@ -972,7 +977,48 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
     const bool vec_out = ((uintptr_t)out & 15) == 0;
     const uint64_t word_base = bit_base >> 5;
     const uint32_t slog = sync_syms ? (uint32_t)__builtin_ctz(sync_syms) : 0u;   // S is a power of two
+    // quarter mode (uniform): above 5.5 bits per symbol on average a fair share of 8-code
+    // halves exceed 64 bits, and a wave with one such lane ran both the half and the quarter
+    // path; such streams (e.g. C4's Zipf bytes, 6.25) code every half as two quarters
+    const bool qmode = 2 * block_off[nblocks] > 11 * n;
     __syncthreads();
+    if (T->fixed8 && vec_out && (bit_base & 127) == 0) {
+        // every code 8 bits: stream byte bit_base / 8 + i = code(in[i]) (bit_base % 128 == 0: the
+        // stream's first byte is out's first byte, 16-B aligned); the plan is 8 bits per byte
+        uint8_t *const ob = reinterpret_cast<uint8_t *>(out);
+        for (uint64_t b = bx; b < nblocks; b += gstride) {
+            const uint64_t blk_start = b * (uint64_t)DC_BLOCK_BYTES;
+            const uint64_t blk_end = (blk_start + DC_BLOCK_BYTES < n) ? blk_start + DC_BLOCK_BYTES : n;
+            if (blk_start + DC_BLOCK_BYTES <= n) {
+                uint4 v[PACK_PIECES];
+#pragma unroll
+                for (int k = 0; k < PACK_PIECES; ++k)
+                    v[k] = *reinterpret_cast<const uint4 *>(in + blk_start + (uint64_t)k * PACK_TILE + (uint64_t)t * 16);
+#pragma unroll
+                for (int k = 0; k < PACK_PIECES; ++k) {
+                    uint32_t w4[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const uint32_t x = w4[q];
+                        w4[q] = s_tab[x & 255u].x | (s_tab[(x >> 8) & 255u].x << 8) | (s_tab[(x >> 16) & 255u].x << 16) |
+                                (s_tab[x >> 24].x << 24);
+                    }
+                    *reinterpret_cast<uint4 *>(ob + blk_start + (uint64_t)k * PACK_TILE + (uint64_t)t * 16) =
+                        make_uint4(w4[0], w4[1], w4[2], w4[3]);
+                }
+            } else {
+                for (uint64_t i = blk_start + t; i < blk_end; i += 256) ob[i] = (uint8_t)s_tab[in[i]].x;
+            }
+            if (sync_len != nullptr) {   // chunks of S symbols: 8 S bits (the last: 8 x its symbols)
+                for (uint64_t c = (blk_start >> slog) + t; c < ((blk_end + sync_syms - 1) >> slog); c += 256) {
+                    const uint64_t s0 = c << slog;
+                    sync_len[c] = (uint16_t)(8u * (uint32_t)min((uint64_t)sync_syms, n - s0));
+                    if ((c & (DC_SYNC_GROUP - 1)) == 0) sync_base[c >> DC_SYNC_GROUP_LOG] = bit_base + 8 * s0;
+                }
+            }
+        }
+        return;
+    }
 
     for (uint64_t b = bx; b < nblocks; b += gstride) {
         const uint64_t blk_start = b * (uint64_t)DC_BLOCK_BYTES;
@@ -1065,7 +1111,7 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
                 for (int h = 0; h < 2; ++h) {
                     const uint32_t Th = h ? Tk[k] - Hk[k] : Hk[k];
                     const uint32_t pos = h ? rel + Hk[k] : rel;
-                    if (Th <= 64u) {
+                    if (!qmode && Th <= 64u) {
                         // (a packed 32-bit code|length table measured 4% slower: the
                         // extraction VALU costs more than the uint2 reads' bank conflicts)
                         uint64_t acc = 0;
@@ -1077,8 +1123,8 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
                         emit(acc, Th, pos);
                     } else {
                         // a half of more than 64 bits (skewed or long codes, e.g. C4's Zipf
-                        // bytes): two quarters of 4 codes, each <= 64 bits unless codes exceed
-                        // 16 bits, then code by code
+                        // bytes), or every half in quarter mode: two quarters of 4 codes, each
+                        // <= 64 bits unless codes exceed 16 bits, then code by code
                         uint32_t p = pos;
 #pragma unroll 1
                         for (int qq = 0; qq < 2; ++qq) {
@@ -1879,6 +1925,43 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode8(const uint32_t *__rest
     constexpr int NT = NW * 64;
     __shared__ Dec8Lds L;
     if (d_base) bit_base += *d_base;   // device-resident shard offset (dist: no host read)
+    if (T->fixed8 && (bit_base & 127) == 0 && ((uintptr_t)in & 15) == 0 && ((uintptr_t)out & 15) == 0 &&
+        (n + 3) / 4 <= nwords) {
+        // every code 8 bits: output symbol i = the symbol of stream byte bit_base / 8 + i (the
+        // words' first byte; bit_base % 128 == 0). No chunk is redone: the fix masks are zeroed.
+        uint16_t *const inv = reinterpret_cast<uint16_t *>(L.lut);   // byte -> symbol, 0x100 = no code
+        const int tt = threadIdx.x;
+        for (int i = tt; i < 256; i += NW * 64) inv[i] = 0x100;
+        __syncthreads();
+        for (int sy = tt; sy < 256; sy += NW * 64)
+            if (T->nbits[sy] == 8u) inv[T->code[sy] & 255u] = (uint16_t)sy;
+        if (blockIdx.x == 0 && tt == 0) queue[D8_FIX_CNT] = 0u;
+        __syncthreads();
+        const uint8_t *const ib = reinterpret_cast<const uint8_t *>(in);
+        const uint64_t nthr = (uint64_t)gridDim.x * NW * 64, me = (uint64_t)blockIdx.x * NW * 64 + tt;
+        uint32_t bad = 0;
+        for (uint64_t g = me; g < n / 16; g += nthr) {
+            const uint4 v = *reinterpret_cast<const uint4 *>(ib + 16 * g);
+            uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t x = w4[q];
+                const uint32_t a = inv[x & 255u], b2 = inv[(x >> 8) & 255u], c2 = inv[(x >> 16) & 255u], d2 = inv[x >> 24];
+                bad |= (a | b2 | c2 | d2) & 0x100u;
+                w4[q] = (a & 255u) | ((b2 & 255u) << 8) | ((c2 & 255u) << 16) | ((d2 & 255u) << 24);
+            }
+            *reinterpret_cast<uint4 *>(out + 16 * g) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+        }
+        for (uint64_t i = (n & ~15ull) + me; i < n; i += nthr) {
+            const uint32_t a = inv[ib[i]];
+            bad |= a & 0x100u;
+            out[i] = (uint8_t)a;
+        }
+        if (bad) atomicOr(err, 1);
+        const uint32_t ngr = (uint32_t)(((n + S - 1) / S + DC_SYNC_GROUP - 1) / DC_SYNC_GROUP);
+        for (uint64_t g = me; g < ngr; g += nthr) fix_mask[g] = 0ull;
+        return;
+    }
     const int t = threadIdx.x, lane = t & 63;
     const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
     // ---- table: the LSB-first 12-bit table (dc_dtable.dlut); codes longer than 12 bits

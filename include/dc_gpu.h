@@ -68,7 +68,9 @@ typedef struct dc_dtable {
      *       bits | sym << 8, 0: longer than 12 + dlut2_k bits or invalid (dlut2_k 0: none) */
     uint16_t dlut[1 << DC_LUT_BITS];
     uint16_t dlut2[DC_LUT2_CAP];
-    int32_t dlut2_k, dec_ready, pad_[4];   /* dec_ready: lut/dlut/dlut2/dlut14 are current */
+    int32_t dlut2_k, dec_ready;   /* dec_ready: lut/dlut/dlut2/dlut14 are current */
+    int32_t fixed8;               /* every byte's code is 8 bits (or absent): pack and decode are byte maps */
+    int32_t pad_[3];
     /* dlut14: next 14 bits -> bits | sym << 8 for codes of <= 14 bits; bits 0: longer, sym =
      * the escape id of its 12-bit prefix (as dlut); 16-B aligned for vector copies */
     uint16_t dlut14[1 << DC_LUT14_BITS];

@@ -196,6 +196,36 @@ def test_pack_at_bit_offset(torch_cuda, codec, bit_base):
     assert np.array_equal(out.cpu().numpy(), x)
 
 
+@pytest.mark.parametrize("bit_base", [0, 128 * 3, 8, 32])
+def test_fixed8_byte_map_paths(torch_cuda, codec, bit_base):
+    """n = 16 on flat bytes: every code is 8 bits (dc_dtable.fixed8), so pack and decode run
+    as byte maps when the stream starts on a 128-bit boundary (bit_base 0, 384), and the
+    general kernels otherwise (8, 32); both bit-exact vs the oracle, ragged ends included."""
+    torch = torch_cuda
+    rng = np.random.default_rng(bit_base + 7)
+    for n in (1 << 20, (1 << 20) + 12_345, 100_003):
+        # C3's alphabet (bytes 1..255, flat): 255 symbols + 1 dummy fill a depth-2 16-ary tree
+        x = rng.permutation(np.resize(np.arange(1, 256, dtype=np.uint8), n))
+        L, el, ev, code, nb, mx = _oracle_encode(x, 16)
+        assert set(np.unique(nb[:256])) <= {0, 8}
+        S = 64
+        payload, bits, idx = orc.huff_pack(x, code, nb, bit_base=bit_base, sync_syms=S)
+        xt = torch.from_numpy(x).cuda()
+        enc = codec.encode(xt, n_ary=16, sync_syms=S, bit_base=bit_base)
+        assert enc["bits"] == bits == 8 * n
+        got = enc["words"].cpu().numpy().view(np.uint8)
+        off = (bit_base >> 3) - ((bit_base >> 5) << 2)
+        assert np.array_equal(got[off: off + len(payload)], payload), (n, bit_base)
+        base, lens = orc.sync_compact(idx, bit_base, bits)
+        assert np.array_equal(enc["sync"][0].cpu().numpy().astype(np.uint64), base), (n, bit_base)
+        assert np.array_equal(enc["sync"][1].cpu().numpy().view(np.uint16), lens), (n, bit_base)
+        out = torch.empty(n, dtype=torch.uint8, device="cuda")
+        codec.decode_into(enc, out)
+        assert codec.decode_status() == 0 and np.array_equal(out.cpu().numpy(), x), (n, bit_base)
+        if bit_base % 128 == 0:   # the byte map redoes nothing (the general decoder redoes the ragged tail)
+            assert codec.decode_redo_count() == 0
+
+
 @pytest.mark.parametrize("case", ["unaligned-out", "long-halves"])
 def test_pack_store_paths(torch_cuda, codec, case):
     """k_huff_pack fast path: word stores when the output is not 16-B aligned, and the
