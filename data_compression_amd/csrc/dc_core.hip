@@ -3300,37 +3300,75 @@ static uint64_t sm_ntiles(const uint8_t *in, int off, uint64_t nelem)
 // output count (and, when OUT, the bytes written at stage[pos..]) of the 4 elements in a
 // lane's dword d at tile byte u; p / q = the bytes before / after the dword
 #define SM_TRASH (2 * SM_TILE + 32)   /* stage bytes [SM_TRASH, +256): a sink per lane for unwritten bytes */
-template <int M, bool OUT>
-static __device__ __forceinline__ uint32_t sm_elems(uint32_t d, uint32_t p, uint32_t q, uint32_t u, const SmTile &T,
-                                                    uint8_t *stage, uint32_t pos)
+
+// SWAR byte tests on a dword (bit 7 of each byte = the test; the kernels are VALU-issue
+// bound, and one 32-bit op here tests 4 bytes: 31 VALU per byte per element rule before)
+static __device__ __forceinline__ uint32_t swar_eq(uint32_t x, uint32_t c4)   // byte == c
 {
-    // branch-free: a byte that is not written goes to the lane's sink (an exec-masked store
-    // per byte cost a 64-bit mask pair each: SGPR spills, 211 VGPRs)
+    const uint32_t v = x ^ c4;
+    return ~(((v & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | v) & 0x80808080u;
+}
+static __device__ __forceinline__ uint32_t swar_lower(uint32_t x)   // 'a' <= byte <= 'z'
+{
+    const uint32_t t = x & 0x7F7F7F7Fu;
+    return (t + 0x1F1F1F1Fu) & ~(t + 0x05050505u) & ~x & 0x80808080u;
+}
+// bytes k of the dword at tile byte u with u + k >= lim / < lim
+static __device__ __forceinline__ uint32_t swar_ge(uint32_t u, uint32_t lim)
+{
+    const uint32_t a = lim > u ? min(lim - u, 4u) : 0u;   // leading bytes below lim
+    return a >= 4u ? 0u : 0x80808080u << (8u * a);
+}
+static __device__ __forceinline__ uint32_t swar_lt(uint32_t u, uint32_t lim)
+{
+    const uint32_t b = lim > u ? min(lim - u, 4u) : 0u;   // bytes below lim
+    return b == 0u ? 0u : 0x80808080u >> (8u * (4u - b));
+}
+
+// The 4 elements of a lane's dword d at tile byte u (p / q = the bytes before / after it):
+// encode: *val = the output byte of each position, *keep = the positions that emit one;
+// decode: *keep = the valid positions (a byte >= 0x80 emits two). Returns the output count.
+template <int M, bool INTERIOR>
+static __device__ __forceinline__ uint32_t sm_swar(uint32_t d, uint32_t p, uint32_t q, uint32_t u, const SmTile &T,
+                                                   uint32_t &val, uint32_t &keep)
+{
+    const uint32_t valid = INTERIOR ? 0x80808080u : (swar_ge(u, T.lo) & swar_lt(u, T.hi));
+    if (SmMode<M>::dec) {
+        keep = valid;
+        val = d;
+        return (uint32_t)__popc(valid) + (uint32_t)__popc(valid & d & 0x80808080u);
+    }
+    const uint32_t prev = (d << 8) | p, next = (d >> 8) | (q << 24);
+    uint32_t second = swar_eq(prev, 0x20202020u) & swar_lower(d);
+    if (!INTERIOR && M != M_SMALL_BODY1) second &= swar_ge(u, T.two);   // stream bytes 0-1 never pair
+    uint32_t start = swar_eq(d, 0x20202020u) & swar_lower(next);
+    if (!INTERIOR) start &= swar_lt(u, T.nxt);   // the next byte must be inside the stream
+    const uint32_t m8 = (start - (start >> 7)) | start;   // 0x80 -> 0xFF per byte
+    val = (d & ~m8) | ((next | 0x80808080u) & m8);       // ' ' + letter -> 0x80 + letter
+    keep = valid & ~second;
+    return (uint32_t)__popc(keep);
+}
+
+// the output bytes of one dword, branch-free (bytes not written go to the lane's sink)
+template <int M>
+static __device__ __forceinline__ void sm_store(uint32_t val, uint32_t keep, uint8_t *stage, uint32_t pos)
+{
     const uint32_t sink = SM_TRASH + 4u * (threadIdx.x & 63);
-    uint32_t cnt = 0;
+    uint32_t c = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        const uint32_t uk = u + (uint32_t)k;
-        const bool valid = uk >= T.lo && uk < T.hi;
-        const uint32_t cur = (d >> (8 * k)) & 255u;
+        const uint32_t on = (keep >> (8 * k + 7)) & 1u;
+        const uint32_t v = (val >> (8 * k)) & 255u;
         if (SmMode<M>::dec) {
-            const bool two = cur >= 0x80;
-            if (OUT) {
-                stage[valid ? pos + cnt : sink] = (uint8_t)(two ? ' ' : cur);
-                stage[valid && two ? pos + cnt + 1 : sink] = (uint8_t)(cur - 0x80);
-            }
-            cnt += valid ? (two ? 2u : 1u) : 0u;
+            const uint32_t two = v >> 7;
+            stage[on ? pos + c : sink] = (uint8_t)(two ? 0x20u : v);
+            stage[(on & two) ? pos + c + 1 : sink] = (uint8_t)(v & 0x7Fu);
+            c += on + (on & two);
         } else {
-            const uint32_t prv = k ? (d >> (8 * (k - 1))) & 255u : p;
-            const uint32_t nxt = k < 3 ? (d >> (8 * (k + 1))) & 255u : q;
-            const bool second = (M == M_SMALL_BODY1 || uk >= T.two) && prv == ' ' && is_lower(cur);
-            const bool keep = valid && !second;
-            if (OUT)
-                stage[keep ? pos + cnt : sink] = (uint8_t)((cur == ' ' && uk < T.nxt && is_lower(nxt)) ? 0x80 + nxt : cur);
-            cnt += keep ? 1u : 0u;
+            stage[on ? pos + c : sink] = (uint8_t)v;
+            c += on;
         }
     }
-    return cnt;
 }
 
 // the lane's 16 dwords (step st: tile byte st * 1024 + w * 256 + 4 lane), all loads issued
@@ -3394,10 +3432,14 @@ __global__ __launch_bounds__(256) void k_small_tiles(const uint8_t *__restrict__
         __syncthreads();
     }
     uint32_t cnt = 0;
+    const bool interior = T.lo == 0 && T.hi == SM_TILE && T.two == 0 && T.nxt == SM_TILE;
 #pragma unroll
     for (int st = 0; st < SM_STEPS; ++st) {
         const uint2 nb = SmMode<M>::dec ? make_uint2(0u, 0u) : sm_nb(E, dv[st], st, w, lane);
-        cnt += sm_elems<M, false>(dv[st], nb.x, nb.y, (uint32_t)(st * 1024 + w * 256 + lane * 4), T, nullptr, 0);
+        const uint32_t u = (uint32_t)(st * 1024 + w * 256 + lane * 4);
+        uint32_t val, keep;
+        cnt += interior ? sm_swar<M, true>(dv[st], nb.x, nb.y, u, T, val, keep)
+                        : sm_swar<M, false>(dv[st], nb.x, nb.y, u, T, val, keep);
     }
     const uint32_t tot = wave_scan_incl(cnt);
     if (lane == 63) s_w[w] = tot;
@@ -3436,15 +3478,20 @@ __global__ __launch_bounds__(256) void k_small_write(const uint8_t *__restrict__
         sm_edges_put(E, in, len, T, t, dv);
         __syncthreads();
     }
-    uint32_t ex[SM_STEPS];   // this lane's offset inside its wave's part of step st
+    uint32_t ex[SM_STEPS], kp[SM_STEPS];   // lane offset in its wave's part of step st; kept bytes
+    const bool interior = T.lo == 0 && T.hi == SM_TILE && T.two == 0 && T.nxt == SM_TILE;
 #pragma unroll
     for (int st = 0; st < SM_STEPS; ++st) {
         const uint2 nb = SmMode<M>::dec ? make_uint2(0u, 0u) : sm_nb(E, dv[st], st, w, lane);
-        const uint32_t c = sm_elems<M, false>(dv[st], nb.x, nb.y, (uint32_t)(st * 1024 + w * 256 + lane * 4), T, nullptr, 0);
+        const uint32_t u = (uint32_t)(st * 1024 + w * 256 + lane * 4);
+        uint32_t val, keep;
+        const uint32_t c = interior ? sm_swar<M, true>(dv[st], nb.x, nb.y, u, T, val, keep)
+                                    : sm_swar<M, false>(dv[st], nb.x, nb.y, u, T, val, keep);
+        dv[st] = val;   // encode: the output bytes (decode: the input bytes)
+        kp[st] = keep;
         const uint32_t inc = wave_scan_incl(c);
         ex[st] = inc - c;
         if (lane == 63) s_w[st][w] = inc;
-        __builtin_amdgcn_sched_barrier(0);
     }
     __syncthreads();
     const uint64_t e = entry[blockIdx.x / FSM_GROUP];
@@ -3461,12 +3508,7 @@ __global__ __launch_bounds__(256) void k_small_write(const uint8_t *__restrict__
             pre += q < w ? v : 0u;
             run += v;
         }
-        // opaque: the write pass recomputes the counts' byte tests instead of keeping pass 1's
-        // 64 per-byte masks alive across the barrier (216 VGPRs, SGPR spills)
-        asm volatile("" : "+v"(dv[st]));
-        const uint2 nb = SmMode<M>::dec ? make_uint2(0u, 0u) : sm_nb(E, dv[st], st, w, lane);
-        (void)sm_elems<M, true>(dv[st], nb.x, nb.y, (uint32_t)(st * 1024 + w * 256 + lane * 4), T, s_out, lead + pre + ex[st]);
-        __builtin_amdgcn_sched_barrier(0);   // one step's stores at a time (registers)
+        sm_store<M>(dv[st], kp[st], s_out, lead + pre + ex[st]);
     }
     __syncthreads();
     // store [o_tile, o_tile + run): whole granules as uint4, the first and last bytewise
