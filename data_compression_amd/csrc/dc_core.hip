@@ -942,6 +942,13 @@ __global__ void k_zero_bounds(const uint64_t *__restrict__ off, uint64_t nblocks
 // Only the two words a block shares with its neighbour blocks are OR-ed into HBM with
 // global atomics. The stream is MSB-first: staged words are byte-swapped on store.
 // ------------------------------------------------------------------------------------
+// A workgroup barrier that orders LDS only (the pack's barriers order its LDS stage). (A
+// prefetch of the next block by LDS-DMA, issued after the stage atomics, measured 10% slower.)
+static __device__ __forceinline__ void lds_barrier()
+{
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 #define PACK_TILE 4096
 #define PACK_STAGE (PACK_TILE + 64)
 #define PACK_BLK_WORDS 9216     /* 36 KiB: a full block of <= 9 bits/symbol is staged whole  */
@@ -1069,7 +1076,7 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
 #pragma unroll
                 for (int k = 0; k < PACK_PIECES; ++k) s_tot[k][wid] = Ik[k];
             }
-            __syncthreads();
+            lds_barrier();
             const uint64_t org = (blk_first_word - sh) << 5;   // absolute bit of stage bit 0
             const uint32_t cm = sync_syms >> 4;                 // lanes per sync chunk
             uint64_t run = blk_abs;   // absolute bit where piece k starts
@@ -1152,7 +1159,7 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
                 }
                 __builtin_amdgcn_sched_barrier(0);   // keep the pieces' lookups from being hoisted
             }
-            __syncthreads();
+            lds_barrier();
             // stage word sh = the block's first word, shared with the previous block; the last
             // word is shared with the next one when the block ends inside it: those two are
             // OR-ed into HBM by one lane each, the rest are plain stores (uint4 where whole)
@@ -1174,7 +1181,7 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
             }
             if (t == 0) atomicOr(&dst[sh], bswap32(s_stage[sh]));
             if (t == 64 && last_plain < nwa && nw_blk > 1) atomicOr(&dst[nwa - 1], bswap32(s_stage[nwa - 1]));
-            __syncthreads();
+            lds_barrier();
             continue;
         }
         __syncthreads();
