@@ -1035,8 +1035,9 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
         uint64_t tile_abs = blk_abs;
         if (t == 0) s_stage[0] = 0u;
         // the whole 32 KiB block: 8 independent 16-B loads per lane in flight at once (loading
-        // the next block ahead in registers measured 8% slower: 147 VGPRs, 3 waves/SIMD)
-        uint4 blkv[DC_BLOCK_BYTES / PACK_TILE];
+        // the next block ahead measured slower every way tried: in extra registers -8%
+        // (147 VGPRs), into these registers once pass B is done -4%, into the caches -10%)
+        uint4 blkv[PACK_PIECES];
         const bool full = (blk_start + DC_BLOCK_BYTES <= n);
         if (full) {
 #pragma unroll
