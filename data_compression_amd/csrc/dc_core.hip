@@ -566,7 +566,7 @@ __global__ __launch_bounds__(256) void k_huff_table(const uint64_t *__restrict__
 }
 
 // ------------------------------------------------------------------------------------
-// Decoder tables of a code table (dc_gpu.h: lut, dlut, dlut2, dlut14), built by one
+// Decoder tables of a code table (dc_gpu.h: lut, dlut, dlut2, dlut14, dlut15), built by one
 // 256-thread workgroup from the canonical arrays k_huff_table wrote. Not on the encoder's
 // critical path: k_huff_pack runs it in an extra workgroup beside the pack (its LDS is the
 // pack stage), and dc_huff_decode launches k_dec_tables first, which returns at once when the
@@ -688,14 +688,14 @@ static __device__ void dec_tables_build(dc_dtable *__restrict__ T, DecBuildLds &
         }
     }
     __syncthreads();   // dlut2 complete
-    // dlut14, two entries per u32 store (coalesced): entry x = dlut entry x & 4095 (from
-    // s_lut1, as d1 above), an escape there resolved on the next 2 bits by dlut2 when that
-    // code fits 14 bits
-    {
-        const bool l2_14 = l2ok && K >= DC_LUT14_BITS - DC_LUT_BITS;
-        uint32_t *const d14 = reinterpret_cast<uint32_t *>(T->dlut14);
+    // dlut14 and dlut15, two entries per u32 store (coalesced): entry x = dlut entry x & 4095
+    // (from s_lut1, as d1 above), an escape there resolved on the next 2 (3) bits by dlut2
+    // when that code fits 14 (15) bits
+    auto wide = [&](uint16_t *dst, uint32_t bits) {
+        const bool l2w = l2ok && K >= bits - DC_LUT_BITS;
+        uint32_t *const dw = reinterpret_cast<uint32_t *>(dst);
 #pragma unroll 8
-        for (uint32_t p = t; p < (1u << DC_LUT14_BITS) / 2; p += 256) {
+        for (uint32_t p = t; p < (1u << bits) / 2; p += 256) {
             uint32_t pr = 0;
 #pragma unroll
             for (uint32_t q = 0; q < 2; ++q) {
@@ -704,14 +704,16 @@ static __device__ void dec_tables_build(dc_dtable *__restrict__ T, DecBuildLds &
                 uint32_t e = (a >> 8) | ((a & 255u) << 8);
                 if (!a) {
                     const uint32_t esc = s_esc[i];
-                    const uint32_t e2 = l2_14 ? T->dlut2[(esc << K) | h] : 0u;
-                    e = (e2 && (e2 & 255u) <= DC_LUT14_BITS) ? e2 : ((esc & 255u) << 8);
+                    const uint32_t e2 = l2w ? T->dlut2[(esc << K) | h] : 0u;
+                    e = (e2 && (e2 & 255u) <= bits) ? e2 : ((esc & 255u) << 8);
                 }
                 pr |= e << (16 * q);
             }
-            d14[p] = pr;
+            dw[p] = pr;
         }
-    }
+    };
+    wide(T->dlut14, DC_LUT14_BITS);
+    wide(T->dlut15, DC_LUT15_BITS);
     if (t == 0) T->dlut2_k = l2ok ? (int32_t)K : 0;
     __syncthreads();
     if (t == 0) {   // every table store of the workgroup before the flag (agent scope)
@@ -1555,15 +1557,16 @@ __global__ __launch_bounds__(DEC_WAVES * 64) void k_huff_decode(const uint32_t *
 //    makes the wave redo its two chunks exactly (d8_chunk_hbm).
 // Partial groups and groups whose span exceeds the stage also go through d8_chunk_hbm.
 // ------------------------------------------------------------------------------------
-#define D8_CHAINS 24           /* chains (groups being decoded) per CU: waves x chains/wave */
-#define D8_LUT_BITS 14         /* first-level table of the fast decoder (32 KiB of LDS)      */
+#define D8_CHAINS 22           /* chains (groups being decoded) per CU: waves x chains/wave */
+#define D8_LUT_BITS 15         /* first-level table of the fast decoder (64 KiB of LDS)      */
+#define D8F_LUT_BITS 14        /* first level of the exact redo (32 KiB of LDS)             */
 #define D8_STAGE_WORDS 1088    /* per chain: 4352 B = 4096 symbols at <= 8.4 bits/symbol   */
 #define D8_L2_CAP 7168         /* second-level entries (u16)                               */
 #define D8_K_MAX 8
 #define D8_MAX_WAVES 16
 
 struct Dec8Lds {
-    __attribute__((aligned(16))) uint16_t lut[1 << D8_LUT_BITS];   // LSB-first 14-bit window -> len | sym << 8; len 0: a longer code
+    __attribute__((aligned(16))) uint16_t lut[1 << D8_LUT_BITS];   // LSB-first 15-bit window -> len | sym << 8; len 0: a longer code
     uint32_t exhausted;               // scheduler: bit h = slice h is empty
     __attribute__((aligned(16))) uint32_t stage[D8_CHAINS][D8_STAGE_WORDS];
     uint32_t tail_pad[64];            // a corrupt stream's windows may run past the last stage
@@ -1976,11 +1979,11 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode8(const uint32_t *__rest
     // read length 0
     // D8_LUT_BITS first level from the 12-bit one and its second level: 2.9% of C2 chunks hold a
     // code of > 14 bits (to the exact redo), 6.6% one of > 12
-    // the 14-bit first level (dc_dtable.dlut14, built by dec_tables_build): 2.5% of C2 chunks
-    // hold a code of > 14 bits (to the exact redo)
-    static_assert(D8_LUT_BITS == DC_LUT14_BITS, "table width");
+    // the 15-bit first level (dc_dtable.dlut15, built by dec_tables_build): 1.2% of C2 chunks
+    // hold a code of > 15 bits (to the exact redo; 2.5% with the 14-bit table of r1)
+    static_assert(D8_LUT_BITS == DC_LUT15_BITS, "table width");
     for (int i = t; i < (1 << D8_LUT_BITS) / 8; i += NT)
-        reinterpret_cast<uint4 *>(L.lut)[i] = reinterpret_cast<const uint4 *>(T->dlut14)[i];
+        reinterpret_cast<uint4 *>(L.lut)[i] = reinterpret_cast<const uint4 *>(T->dlut15)[i];
 #ifdef DC_DIAG_SYNTH_LUT   // timing ablation only: every window is a 4-bit code (garbage output)
     for (int i = t; i < (1 << D8_LUT_BITS); i += NT) L.lut[i] = (uint16_t)(4u | ((i & 255u) << 8));
 #endif
@@ -2341,9 +2344,10 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode9(const uint32_t *__rest
 #ifndef D8F_ROW
 #define D8F_ROW 24   /* words of a lane's staged span (longer chunks re-stage it further on) */
 #endif
-static_assert(offsetof(dc_dtable, dlut14) % 16 == 0 && offsetof(dc_dtable, dlut2) % 8 == 0, "table copies");
+static_assert(offsetof(dc_dtable, dlut14) % 16 == 0 && offsetof(dc_dtable, dlut15) % 16 == 0 && offsetof(dc_dtable, dlut2) % 8 == 0,
+              "table copies");
 struct FixLds {
-    __attribute__((aligned(16))) uint16_t lut[1 << D8_LUT_BITS];   // the fast decoder's 14-bit first level
+    __attribute__((aligned(16))) uint16_t lut[1 << D8F_LUT_BITS];   // the fast decoder's 14-bit first level
     uint16_t lut2[DC_LUT2_CAP];
     uint64_t lim[33];
     uint32_t first[DC_MAX_DIGITS + 1], count[DC_MAX_DIGITS + 1], start[DC_MAX_DIGITS + 1];
@@ -2453,11 +2457,11 @@ __global__ __launch_bounds__(D8F_WAVES * 64) void k_huff_decode8_fix(const uint3
         // (the positions' dependent loads issued before the copy held its stores back: 29k of a
         // wave's 121k cycles, r2 diag)
         constexpr int NT = D8F_WAVES * 64;
-        static_assert((1 << D8_LUT_BITS) / 8 <= 2 * NT && DC_LUT2_CAP / 4 <= 2 * NT && DC_MAX_SYMS <= NT &&
+        static_assert((1 << D8F_LUT_BITS) / 8 <= 2 * NT && DC_LUT2_CAP / 4 <= 2 * NT && DC_MAX_SYMS <= NT &&
                       DC_MAX_DIGITS + 1 <= NT, "one copy pass");
         const uint4 *l1 = reinterpret_cast<const uint4 *>(T->dlut14);
         const uint2 *l2 = reinterpret_cast<const uint2 *>(T->dlut2);   // dlut2 is 8-B aligned
-        constexpr int N1 = (1 << D8_LUT_BITS) / 8, N2 = DC_LUT2_CAP / 4;
+        constexpr int N1 = (1 << D8F_LUT_BITS) / 8, N2 = DC_LUT2_CAP / 4;
         const uint4 a0 = l1[t], a1 = t + NT < N1 ? l1[t + NT] : make_uint4(0u, 0u, 0u, 0u);
         const uint2 b0 = t < N2 ? l2[t] : make_uint2(0u, 0u), b1 = t + NT < N2 ? l2[t + NT] : make_uint2(0u, 0u);
         const uint16_t sy = t < DC_MAX_SYMS ? T->syms[t] : (uint16_t)0;
@@ -2564,7 +2568,7 @@ __global__ __launch_bounds__(D8F_WAVES * 64) void k_huff_decode8_fix(const uint3
             for (int k = 0; k < 4; ++k) {
                 const uint32_t a = c >> 5;
                 const uint32_t lo = __builtin_amdgcn_alignbit(row[a + 1], row[a], c);
-                uint32_t e = F.lut[lo & ((1u << D8_LUT_BITS) - 1)];
+                uint32_t e = F.lut[lo & ((1u << D8F_LUT_BITS) - 1)];
                 if (__builtin_amdgcn_ballot_w64((e & 255u) == 0u)) {   // the second level, only when a lane needs it
                     const uint32_t i2 = min(((e >> 8) << K2) | ((lo >> DC_LUT_BITS) & kmask), (uint32_t)DC_LUT2_CAP - 1);
                     const uint32_t e2 = F.lut2[(e & 255u) ? 0u : i2];
@@ -4443,8 +4447,8 @@ static int decode_impl(dc_ctx *c, const uint32_t *d_words, uint64_t bit_base, co
             LAUNCH(c, "huff_decode", k_huff_decode9<12>, groups < 256 * 12 ? (groups + 11) / 12 : 256, 12 * 64,
                    d_words, bit_base, d_base, d_sync_base, d_sync_len, n, words, d_table, d_out, c->d_err + 1, c->d_queue,
                    spct, (uint64_t *)c->d_fix, (uint64_t *)c->d_fixpos, (uint8_t *)c->d_scr);
-        } else {   // one code per lookup, 12 waves x 2 chains
-            D8_LAUNCH(12, 2);
+        } else {   // one code per lookup, 11 waves x 2 chains (the 15-bit table takes 64 KiB of LDS)
+            D8_LAUNCH(11, 2);
         }
 #undef D8_LAUNCH
         c->last_groups = groups;

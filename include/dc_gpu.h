@@ -41,7 +41,8 @@ enum {
 #define DC_MAX_SYMS 1024        /* max_symbol_value + 1 supported by the table kernel */
 #define DC_MAX_DIGITS 128       /* longest code length (in base-n digits) handled */
 #define DC_LUT2_CAP 7168        /* second-level decode entries (escape prefixes x 2^k) */
-#define DC_LUT14_BITS 14        /* the fast decoder's first level: 2^14 entries */
+#define DC_LUT14_BITS 14        /* the exact redo's first level: 2^14 entries */
+#define DC_LUT15_BITS 15        /* the fast decoder's first level: 2^15 entries */
 #define DC_SYNC_MAX 1024        /* largest sync granularity (u16 chunk bit lengths) */
 
 typedef struct dc_ctx dc_ctx;
@@ -68,12 +69,14 @@ typedef struct dc_dtable {
      *       bits | sym << 8, 0: longer than 12 + dlut2_k bits or invalid (dlut2_k 0: none) */
     uint16_t dlut[1 << DC_LUT_BITS];
     uint16_t dlut2[DC_LUT2_CAP];
-    int32_t dlut2_k, dec_ready;   /* dec_ready: lut/dlut/dlut2/dlut14 are current */
+    int32_t dlut2_k, dec_ready;   /* dec_ready: lut/dlut/dlut2/dlut14/dlut15 are current */
     int32_t fixed8;               /* every byte's code is 8 bits (or absent): pack and decode are byte maps */
     int32_t pad_[3];
     /* dlut14: next 14 bits -> bits | sym << 8 for codes of <= 14 bits; bits 0: longer, sym =
      * the escape id of its 12-bit prefix (as dlut); 16-B aligned for vector copies */
     uint16_t dlut14[1 << DC_LUT14_BITS];
+    /* dlut15: the same on the next 15 bits (the fast decoder's table) */
+    uint16_t dlut15[1 << DC_LUT15_BITS];
 } dc_dtable;
 
 /* Node list of the n-ary Huffman tree (generate_huffman_tree's in-out list[],
