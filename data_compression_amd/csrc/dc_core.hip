@@ -691,7 +691,9 @@ static __device__ void dec_tables_build(dc_dtable *__restrict__ T, DecBuildLds &
     // dlut14 and dlut15, two entries per u32 store (coalesced): entry x = dlut entry x & 4095
     // (from s_lut1, as d1 above), an escape there resolved on the next 2 (3) bits by dlut2
     // when that code fits 14 (15) bits
-    auto wide = [&](uint16_t *dst, uint32_t bits) {
+    // zesc: an entry of no code in the table is 0 (the fast decoder tests min(entry) == 0)
+    // instead of carrying the escape id
+    auto wide = [&](uint16_t *dst, uint32_t bits, bool zesc) {
         const bool l2w = l2ok && K >= bits - DC_LUT_BITS;
         uint32_t *const dw = reinterpret_cast<uint32_t *>(dst);
 #pragma unroll 8
@@ -705,15 +707,15 @@ static __device__ void dec_tables_build(dc_dtable *__restrict__ T, DecBuildLds &
                 if (!a) {
                     const uint32_t esc = s_esc[i];
                     const uint32_t e2 = l2w ? T->dlut2[(esc << K) | h] : 0u;
-                    e = (e2 && (e2 & 255u) <= bits) ? e2 : ((esc & 255u) << 8);
+                    e = (e2 && (e2 & 255u) <= bits) ? e2 : zesc ? 0u : ((esc & 255u) << 8);
                 }
                 pr |= e << (16 * q);
             }
             dw[p] = pr;
         }
     };
-    wide(T->dlut14, DC_LUT14_BITS);
-    wide(T->dlut15, DC_LUT15_BITS);
+    wide(T->dlut14, DC_LUT14_BITS, false);
+    wide(T->dlut15, DC_LUT15_BITS, true);
     if (t == 0) T->dlut2_k = l2ok ? (int32_t)K : 0;
     __syncthreads();
     if (t == 0) {   // every table store of the workgroup before the flag (agent scope)
@@ -965,8 +967,12 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
                                                    const int *__restrict__ err, int build_dec)
 {
     __shared__ uint2 s_tab[256];
-    __shared__ uint8_t s_nb8[256];   // bit lengths alone: pass A reads 1 byte, not 8
-    __shared__ __attribute__((aligned(16))) uint32_t s_stage[PACK_BLK_WORDS];
+#ifdef DC_PACK_NB8   // A/B only: 1-byte lengths (each read masked, the byte extracted apart)
+    __shared__ uint8_t s_nb8[256];
+#else   // bit lengths alone, one dword per byte value: the address is one SDWA shift of the byte
+    __shared__ uint32_t s_nb8[256];
+#endif
+    __shared__ __attribute__((aligned(16))) uint32_t s_stage[PACK_BLK_WORDS + 4];   // +4: emit's no-op ORs past the end
     __shared__ uint32_t s_scan[4];
     __shared__ uint32_t s_tot[PACK_PIECES][4];
     static_assert(sizeof(DecBuildLds) <= sizeof(s_stage), "decoder-table builder uses the stage");
@@ -982,7 +988,7 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
     // output buffer smaller than the planned stream -> write nothing
     if (err[0] != 0 || ((bit_base & 31) + block_off[nblocks] + 31) / 32 > words_cap) return;
     s_tab[t] = make_uint2(T->code[t], T->nbits[t]);
-    s_nb8[t] = (uint8_t)T->nbits[t];
+    s_nb8[t] = T->nbits[t];
     const bool vec_out = ((uintptr_t)out & 15) == 0;
     const uint64_t word_base = bit_base >> 5;
     const uint32_t slog = sync_syms ? (uint32_t)__builtin_ctz(sync_syms) : 0u;   // S is a power of two
@@ -1110,12 +1116,17 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
                 asm volatile("" : "+v"(w4[0]), "+v"(w4[1]), "+v"(w4[2]), "+v"(w4[3]));
                 const uint32_t rel = (uint32_t)(As - org);
                 // OR a right-justified run of nb <= 64 bits into the stage at bit pos (<= 3 words)
+                // Branch-free: the run left-justified in 64 bits has zeros below it, so the
+                // words it does not reach receive 0 (a no-op OR; some lane of a wave needs each
+                // of the 3 ORs anyway, so skipping them per lane saved no LDS cycle and cost
+                // compares and exec-mask branches). nb == 0 only for an all-zero acc (absent
+                // symbols have code 0), where the unmasked shift by 64 & 63 = 0 is harmless.
                 auto emit = [&](uint64_t acc, uint32_t nb, uint32_t pos) {
-                    const uint64_t al = nb ? acc << (64u - nb) : 0ull;
+                    const uint64_t al = acc << ((64u - nb) & 63u);
                     const uint32_t hi = (uint32_t)(al >> 32), lo = (uint32_t)al, r = pos & 31u, wi = pos >> 5;
                     atomicOr(&s_stage[wi], hi >> r);
-                    if (r + nb > 32u) atomicOr(&s_stage[wi + 1], __builtin_amdgcn_alignbit(hi, lo, r));
-                    if (r + nb > 64u) atomicOr(&s_stage[wi + 2], __builtin_amdgcn_alignbit(lo, 0u, r));
+                    atomicOr(&s_stage[wi + 1], __builtin_amdgcn_alignbit(hi, lo, r));
+                    atomicOr(&s_stage[wi + 2], __builtin_amdgcn_alignbit(lo, 0u, r));
                 };
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
@@ -1653,34 +1664,47 @@ template <int NC>
 static __device__ __forceinline__ void d8_batch(const uint32_t *const *st, uint32_t *c, uint32_t *o,
                                                 const uint16_t *__restrict__ lut, uint32_t *mn)
 {
+    // 4 VALU + 1 LDS read per symbol: the window starts one bit early (c is biased by 31
+    // and the words are read from the stage row's base - 1 word: the bit below the chunk's is
+    // a don't-care), so (win >> off) & (2^16 - 2) is the entry's byte address (no index
+    // scaling); the whole
+    // entry (len | sym << 8) is added to off, whose low 6 bits (all v_lshrrev_b64 reads) are
+    // then the bits consumed (the sym bits start at bit 8; the lengths of a batch sum to
+    // < 64, so they never carry into bit 8); an entry of no code is 0 (dlut15 escapes are
+    // zeroed), so min over the entries finds it
     uint64_t win[NC];
     uint32_t off[NC];
 #pragma unroll
     for (int j = 0; j < NC; ++j) {
         const uint32_t a = c[j] >> 5;
-        const uint32_t w0 = st[j][a], w1 = st[j][a + 1], w2 = st[j][a + 2];
+        const uint32_t *const sm1 = st[j] - 1;
+        const uint32_t w0 = sm1[a], w1 = sm1[a + 1], w2 = sm1[a + 2];
         win[j] = ((uint64_t)__builtin_amdgcn_alignbit(w2, w1, c[j]) << 32) | __builtin_amdgcn_alignbit(w1, w0, c[j]);
         off[j] = 0;
     }
+    const char *const lb = reinterpret_cast<const char *>(lut);
     // output byte k <- entry byte 1 (v_perm: S0 = entry bytes 4-7, S1 = output bytes 0-3)
     constexpr uint32_t SEL[4] = {0x0c0c0c05u, 0x0c0c0500u, 0x0c050100u, 0x05020100u};
+    uint32_t e[NC][4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
 #pragma unroll
         for (int j = 0; j < NC; ++j) {
-            const uint32_t x = (uint32_t)(win[j] >> off[j]);
+            const uint32_t x = (uint32_t)(win[j] >> (off[j] & 63u));
 #ifdef DC_DIAG_LUTMASK   // timing ablation only: lookups confined to the first entries
-            const uint32_t e = lut[x & DC_DIAG_LUTMASK];
+            e[j][k] = *reinterpret_cast<const uint16_t *>(lb + (x & (2u * DC_DIAG_LUTMASK)));
 #else
-            const uint32_t e = lut[x & ((1u << D8_LUT_BITS) - 1)];
+            e[j][k] = *reinterpret_cast<const uint16_t *>(lb + (x & ((2u << D8_LUT_BITS) - 2u)));
 #endif
-            mn[j] = min(mn[j], e & 255u);
-            o[j] = __builtin_amdgcn_perm(e, k ? o[j] : 0u, SEL[k]);
-            off[j] += e & 255u;
+            o[j] = __builtin_amdgcn_perm(e[j][k], k ? o[j] : 0u, SEL[k]);
+            off[j] += e[j][k];
         }
     }
 #pragma unroll
-    for (int j = 0; j < NC; ++j) c[j] += off[j];
+    for (int j = 0; j < NC; ++j) {
+        mn[j] = min(mn[j], min(min(e[j][0], e[j][1]), min(e[j][2], e[j][3])));
+        c[j] += off[j] & 255u;
+    }
 }
 
 // The 16 batches of a 64-symbol chunk (4 pieces of 16 B per lane), unrolled by template
@@ -2063,7 +2087,7 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode8(const uint32_t *__rest
         for (int j = 0; j < NC; ++j) {
             // the group's 4 KiB of output (d8_out); a tuple that is not fast (its chunks are
             // all rewritten by the redo) stores into the chain's trash rows instead
-            c[j] = cur.fast ? cur.lead[j] + cur.off[j] : 0u;
+            c[j] = (cur.fast ? cur.lead[j] + cur.off[j] : 0u) + 31u;   // d8_batch's bias
             dst[j] = cur.fast ? reinterpret_cast<uint4 *>(out + (uint64_t)(cur.g0 + j) * DC_SYNC_GROUP * S)
                               : trash + j * 256;
         }
@@ -2072,7 +2096,14 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode8(const uint32_t *__rest
         uint32_t o[NC][16], mn[NC];
 #pragma unroll
         for (int j = 0; j < NC; ++j) mn[j] = cur.fast ? 255u : 0u;
+#ifdef DC_DIAG_NODECODE   // timing ablation only: no lookups (the skeleton: spans, stage, output stores)
+#pragma unroll
+        for (int j = 0; j < NC; ++j)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) o[j][q] = c[j] + q;
+#else
         D8Pieces<NC, 0>::run(st, c, o, L.lut, mn);
+#endif
         d8_out<NC>(stw, o, dst, lane);
 #ifdef DC_DIAG
         D8_STAMP(s2);

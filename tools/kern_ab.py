@@ -23,6 +23,7 @@ ap.add_argument("--option", default="hist_prefetch")
 ap.add_argument("--values", default="1,2")
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--iters", type=int, default=10)
+ap.add_argument("--no-check", action="store_true", help="ablation builds with garbage output")
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
 x = synth.device_text(a.cfg, a.size, seed=0xC2, device=dev)
@@ -59,7 +60,7 @@ for r in range(a.rounds):
             res[v].setdefault(name, []).append(ms)
         if a.stage == "hist":
             assert torch.equal(c.hist(x), ref_hist), v
-        if a.stage in ("decode", "step"):
+        if a.stage in ("decode", "step") and not a.no_check:
             assert c.decode_status() == 0 and torch.equal(out, x), v
 for v in vals:
     print(f"{a.option}={v}: " + ", ".join(f"{k} {np.median(m):.4f}" for k, m in res[v].items()), flush=True)
