@@ -2831,6 +2831,7 @@ struct FsmAux {
     uint32_t s_init;      // entry state of element 0
     uint32_t is_last;     // M_NYB_ENC: the shard ends the stream (odd-tail byte, :1000-1009)
     uint32_t whole;       // M_NYB_ENC: whole stream (header 0xAF x[0], LITERAL fallback)
+    uint32_t tokens;      // M_NYB_DEC: a hit writes 0x80 | rank, not its static byte (k_nyb_resolve)
 };
 #define FSM_SUB 1                          /* 4096-element chunks per tile */
 #define FSM_TILE (4096 * FSM_SUB)
@@ -3208,7 +3209,7 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
     // the tile starts in out's first granule)
     const int64_t o_al = (int64_t)((((uintptr_t)(out + o_tile)) & ~(uintptr_t)15) - (uintptr_t)out);
 #define so(o) s_out[(uint32_t)((int64_t)(o) - o_al)]   /* staged out[o] */
-    const uint8_t *tbl = (const uint8_t *)" etaoins";
+    const uint8_t *tbl = (const uint8_t *)(aux.tokens ? "\x80\x81\x82\x83\x84\x85\x86\x87" : " etaoins");
 #pragma unroll
     for (int c = 0; c < FSM_SUB; ++c) {
         const uint64_t j0 = (uint64_t)blockIdx.x * FSM_TILE + (uint64_t)c * 4096 + (uint64_t)t * 16;
@@ -3764,6 +3765,103 @@ static __device__ __forceinline__ void adec_flush(uint32_t w, uintptr_t OA, uint
     }
 }
 
+// Adaptive decode, second form (the product path): two passes.
+//  1. The token structure of a nybble stream does not depend on the lists: a nybble with its
+//     high bit set is a hit (rank = its low 3 bits), any other starts a 2-nybble literal. So
+//     the static decoder's transducer kernels (k_fsm_*<M_NYB_DEC>, parallel) write one token
+//     byte per output byte straight into the output buffer: the literal itself (always < 0x80)
+//     or 0x80 | rank (FsmAux.tokens), after out[0] = in[1].
+//  2. k_nyb_resolve, one wave, replaces every token in place by its byte. The sequential loop
+//     holds no parsing: per byte, the list of the context of the byte before is read from VGPR
+//     lane c (v_readlane), touched with 64-bit scalar operations (a hit's rank is its position,
+//     a literal's position is found by a SWAR zero-byte test), and written back (v_writelane).
+//     Tokens arrive by scalar loads one 64-byte block ahead; the 64 bytes of a block are
+//     assembled in SGPRs at static positions (the loop is unrolled over the block) and leave
+//     as 16 dwords of one VGPR.
+typedef __attribute__((address_space(4))) const uint32_t c_u32;   // scalar (s_load) reads
+
+// one token -> its byte, with the list touch. The list of context c lives in VGPR lane c
+// (Llo, Hhi); all else is wave-uniform (SGPRs). Move to front (update_context :665-687) of
+// the entry at p (a hit: its rank; a literal: its position, or 7 when absent, so the last
+// entry drops): bytes [0, p] of the new list come from L << 8 (byte 0 then is 0, | v), the
+// rest from L.
+static __device__ __forceinline__ uint32_t adec_step(uint32_t t, uint32_t &Llo, uint32_t &Lhi, uint32_t &ctx,
+                                                     int lane)
+{
+    const uint64_t L = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)Lhi, (int)ctx) << 32) |
+                       (uint32_t)__builtin_amdgcn_readlane((int)Llo, (int)ctx);
+    uint32_t v, p;
+    if (t & 0x80u) {
+        p = t & 7u;
+        v = (uint32_t)(L >> (8u * p)) & 255u;
+    } else {
+        v = t;
+        const uint64_t ones = 0x0101010101010101ull;
+        const uint64_t x = L ^ (ones * v);
+        const uint64_t z = (x - ones) & ~x & (ones << 7);   // the lowest flagged byte is the first match
+        p = z ? (uint32_t)__builtin_ctzll(z) >> 3 : 7u;
+    }
+    const uint64_t keep = 0xFFFFFFFFFFFFFF00ull << (8u * p);   // bytes above p
+    const uint64_t N = (L ^ ((L ^ (L << 8)) & ~keep)) | (uint64_t)v;
+    const bool mine = lane == (int)ctx;
+    Llo = mine ? (uint32_t)N : Llo;
+    Lhi = mine ? (uint32_t)(N >> 32) : Lhi;
+    ctx = (v >> 3) & 15u;
+    return v;
+}
+
+// lane j (an immediate) of dst := val (an SGPR)
+#define ADEC_PUT(dst, val, j) asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(dst) : "s"(val), "i"(j))
+
+// out[0] is the first byte, out[1..n) the tokens of pass 1; all replaced in place
+__global__ __launch_bounds__(64) void k_nyb_resolve(uint8_t *__restrict__ out, uint64_t n)
+{
+    const int lane = (int)threadIdx.x;
+    const uint64_t L0 = mtf_init_word();
+    uint32_t Llo = lane < 16 ? (uint32_t)L0 : 0u, Lhi = lane < 16 ? (uint32_t)(L0 >> 32) : 0u;
+    uint32_t ctx = ((uint32_t)__builtin_amdgcn_readfirstlane((int)out[0]) >> 3) & 15u;
+    // whole 64-byte blocks at 64-B aligned addresses: tokens by scalar loads a block ahead,
+    // bytes assembled at static positions; the bytes before the first and after the last such
+    // block one at a time (a block of tokens in one VGPR, lane = byte)
+    const uint64_t k0 = min((uint64_t)((64 - (((uintptr_t)out + 1) & 63)) & 63) + 1, n);
+    const uint64_t nblk = (n - k0) / 64, k1 = k0 + 64 * nblk;
+    auto edge = [&](uint64_t ka, uint64_t kb) {   // positions [ka, kb), kb - ka < 64
+        if (ka >= kb) return;
+        const uint64_t m = kb - ka;
+        const uint32_t tv = (uint64_t)lane < m ? out[ka + lane] : 0u;
+        uint32_t ov = 0;
+        for (uint32_t i = 0; i < (uint32_t)m; ++i) {
+            const uint32_t v = adec_step((uint32_t)__builtin_amdgcn_readlane((int)tv, (int)i), Llo, Lhi, ctx, lane);
+            ov = lane == (int)i ? v : ov;
+        }
+        if ((uint64_t)lane < m) out[ka + lane] = (uint8_t)ov;
+    };
+    edge(1, k0);
+    if (nblk) {
+        uint32_t T[16], Tn[16];
+        c_u32 *src = (c_u32 *)(out + k0);
+#pragma unroll
+        for (int j = 0; j < 16; ++j) T[j] = src[j];
+        for (uint64_t b = 0; b < nblk; ++b) {
+            c_u32 *nx = (c_u32 *)(out + k0 + 64 * (b + 1 < nblk ? b + 1 : b));
+#pragma unroll
+            for (int j = 0; j < 16; ++j) Tn[j] = nx[j];   // the next block's tokens, in flight
+            uint32_t dw = 0;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                uint32_t w = 0;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) w |= adec_step((T[j] >> (8 * q)) & 255u, Llo, Lhi, ctx, lane) << (8 * q);
+                ADEC_PUT(dw, w, j);
+            }
+            if (lane < 16) reinterpret_cast<uint32_t *>(out + k0 + 64 * b)[lane] = dw;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) T[j] = Tn[j];
+        }
+    }
+    edge(k1, n);
+}
+
 __global__ __launch_bounds__(64) void k_nyb_adec(const uint8_t *__restrict__ in, uint64_t len,
                                                  uint8_t *__restrict__ out, uint64_t *__restrict__ meta)
 {
@@ -4007,6 +4105,7 @@ struct dc_ctx {
     uint32_t opt_decode_general;  // 1: always the general decoder (k_huff_decode)
     uint32_t opt_hist_pf;         // histogram: blocks of loads in flight ahead (1..2, 0 = default 1)
     uint32_t opt_decode_variant;  // fast decoder: 0 one code per lookup (k_huff_decode8), 1 up to 3 (k_huff_decode9)
+    uint32_t opt_adec_v1;         // adaptive nybble decode: 1 = the one-pass k_nyb_adec (A/B)
     // timing
     int timing;
     int nev;
@@ -4158,6 +4257,10 @@ int dc_ctx_set_option(dc_ctx *c, int option, int64_t value)
     case DC_OPT_DECODE_VARIANT:
         if (value < 0 || value > 1) return DC_E_ARG;
         c->opt_decode_variant = (uint32_t)value;
+        return DC_OK;
+    case DC_OPT_NYB_ADEC_V1:
+        if (value != 0 && value != 1) return DC_E_ARG;
+        c->opt_adec_v1 = (uint32_t)value;
         return DC_OK;
     case DC_OPT_HIST_PREFETCH:
         if (value < 0 || value > 2) return DC_E_ARG;
@@ -4926,10 +5029,18 @@ int dc_nyb_decompress(dc_ctx *c, const uint8_t *d_in, uint64_t m, int modify, ui
     if (type == 0xAF) {
         if (m < 2) { *h_len = 0; return DC_OK; }
         if (!modify) return fsm_run<M_NYB_DEC>(c, d_in, m, m - 2, d_out, h_len, "nyb_dec_tiles");
-        LAUNCH(c, "nyb_adec", k_nyb_adec, 1, 64, d_in, m, d_out, c->d_meta);
-        HIPCHK(hipMemcpyAsync(c->h_pinned, c->d_meta, sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+        if (c->opt_adec_v1) {   // A/B only: the one-pass single-wave decoder
+            LAUNCH(c, "nyb_adec", k_nyb_adec, 1, 64, d_in, m, d_out, c->d_meta);
+            HIPCHK(hipMemcpyAsync(c->h_pinned, c->d_meta, sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipStreamSynchronize(c->stream));
+            *h_len = c->h_pinned[0];
+            return DC_OK;
+        }
+        // tokens by the static transducer (parallel), then one wave resolves them in place
+        r = fsm_run<M_NYB_DEC>(c, d_in, m, m - 2, d_out, h_len, "nyb_tok_tiles", FsmAux{nullptr, 0, 0, 1, 1, 1});
+        if (r) return r;
+        if (*h_len > 1) LAUNCH(c, "nyb_resolve", k_nyb_resolve, 1, 64, d_out, *h_len);
         HIPCHK(hipStreamSynchronize(c->stream));
-        *h_len = c->h_pinned[0];
         return DC_OK;
     }
     bool handled = false;

@@ -76,7 +76,7 @@ class Codec:
         check("dc_ctx_set_timing", self.L.dc_ctx_set_timing(self.ctx, int(enable)))
 
     OPTIONS = {"hist_grid": 1, "pack_grid": 2, "decode_static_pct": 3, "decode_general": 4, "hist_prefetch": 5,
-               "decode_variant": 6}
+               "decode_variant": 6, "nyb_adec_v1": 7}
 
     def set_option(self, name, value: int):
         """dc_ctx_set_option (dc_gpu.h DC_OPT_*): tuning knobs of this context."""
@@ -257,9 +257,13 @@ class Codec:
                                                         C.byref(n)))
         return out[: n.value]
 
-    def nyb_decompress(self, comp, modify: bool):
-        """decompress_bytestring (nybble_compression.c:734-817) of device bytes comp."""
-        out = self._t(max(2 * comp.numel(), 1))
+    def nyb_decompress(self, comp, modify: bool, out=None):
+        """decompress_bytestring (nybble_compression.c:734-817) of device bytes comp (into
+        `out`, any alignment, when given: at least 2 * comp.numel() bytes)."""
+        if out is None:
+            out = self._t(max(2 * comp.numel(), 1))
+        elif out.numel() < 2 * comp.numel():
+            raise ValueError("out holds fewer than 2 * comp.numel() bytes")
         n = C.c_uint64(0)
         check("dc_nyb_decompress", self.L.dc_nyb_decompress(self.ctx, _ptr(comp), comp.numel(), int(modify),
                                                             _ptr(out), C.byref(n)))

@@ -564,6 +564,33 @@ def test_nybble_encode_parallel_vs_oracle(torch_cuda, codec, modify):
                 assert np.array_equal(back.cpu().numpy(), x), (kind, x.size)
 
 
+@pytest.mark.parametrize("v1", [False, True])
+def test_nybble_adaptive_decode_edges(torch_cuda, codec, v1):
+    """Adaptive decode (tokens by the static transducer, then k_nyb_resolve in place; v1 = the
+    one-pass k_nyb_adec): every output size 1..200 and block-boundary sizes, output buffers
+    at every offset mod 64 (the resolve kernel's guarded first and last blocks), against the
+    reference restatement."""
+    torch = torch_cuda
+    from data_compression_amd import synth
+    codec.set_option("nyb_adec_v1", int(v1))
+    try:
+        rng = np.random.default_rng(17)
+        sizes = list(range(1, 201)) + [255, 256, 257, 4095, 4096, 4097, 65536 + 63, 200_001]
+        for n in sizes:
+            x = synth.english_like(n, seed=n) if n % 3 else rng.integers(1, 128, size=n, dtype=np.uint8)
+            ref = orc.nybble_compress(x.tobytes(), True)
+            comp = torch.from_numpy(np.frombuffer(ref, np.uint8).copy()).cuda()
+            want = orc.nybble_decompress(ref, True)
+            off = (n * 7) % 64
+            big = torch.full((2 * len(ref) + off + 64,), 0xEE, dtype=torch.uint8, device="cuda")
+            got = codec.nyb_decompress(comp, True, out=big[off: off + 2 * len(ref)])
+            assert got.cpu().numpy().tobytes() == want, (n, off)
+            tail = big[off + len(want):].cpu().numpy()
+            assert (big[:off].cpu().numpy() == 0xEE).all() and (tail[: 2 * len(ref) - len(want)] == 0xEE).all(), n
+    finally:
+        codec.set_option("nyb_adec_v1", 0)
+
+
 class _ThreadRanks:
     """world ranks as threads over one GPU (one Codec each), all_gather by a barrier: runs
     dist.ShardedNybble's orchestration unchanged on the device engine."""
