@@ -778,10 +778,11 @@ __global__ __launch_bounds__(256) void k_block_bits(const uint16_t *__restrict__
 
 // single-workgroup exclusive scan; off[b] relative, off[nblocks] = total
 __global__ __launch_bounds__(1024) void k_block_scan(uint64_t *__restrict__ bits_off, uint64_t nblocks,
-                                                     uint64_t *__restrict__ d_total)
+                                                     uint64_t *__restrict__ d_total, int *__restrict__ err_next)
 {
     __shared__ uint64_t s[1024];
     const int t = threadIdx.x;
+    if (t < 4) err_next[t] = 0;   // the next plan's error slot
     const uint64_t per = (nblocks + 1023) / 1024;
     const uint64_t b0 = (uint64_t)t * per;
     const uint64_t b1 = (b0 + per < nblocks) ? b0 + per : nblocks;
@@ -881,11 +882,12 @@ __global__ __launch_bounds__(256) void k_block_local(const uint16_t *__restrict_
 __global__ __launch_bounds__(256) void k_block_final_wide(const uint32_t *__restrict__ local,
                                                           const uint32_t *__restrict__ wgtot, uint64_t nblocks,
                                                           uint32_t nwg, uint64_t *__restrict__ off,
-                                                          uint64_t *__restrict__ d_total)
+                                                          uint64_t *__restrict__ d_total, int *__restrict__ err_next)
 {
     __shared__ uint64_t s_w[4];
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const uint32_t g = blockIdx.x;
+    if (g == 0 && t < 4) err_next[t] = 0;   // the next plan's error slot
     const bool last = g + 1 == nwg;
     const uint32_t lim = last ? nwg : g;   // the last workgroup sums everything (the total)
     uint64_t before = 0, all = 0;
@@ -1451,10 +1453,16 @@ __global__ __launch_bounds__(DEC_WAVES * 64) void k_huff_decode(const uint32_t *
                                                      const uint64_t *__restrict__ sync_base,
                                                      const uint16_t *__restrict__ sync_len, uint32_t S,
                                                      uint64_t n, const dc_dtable *__restrict__ T,
-                                                     uint8_t *__restrict__ out, int *__restrict__ err)
+                                                     uint8_t *__restrict__ out, int *__restrict__ err,
+                                                     int *__restrict__ err_next)
 {
     __shared__ DecLds L;
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    if (blockIdx.x == 0 && t < 4) err_next[t] = 0;   // the next decode's error slot
+    if (!__hip_atomic_load(&T->dec_ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {   // tables rebuilt since
+        if (threadIdx.x == 0) atomicOr(err, 1);
+        return;
+    }
     if (d_base) bit_base += *d_base;   // device-resident shard offset (dist: no host read)
     {
         const uint4 *src = reinterpret_cast<const uint4 *>(T->lut);
@@ -1959,6 +1967,10 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode8(const uint32_t *__rest
     constexpr uint32_t S = 64;
     constexpr int NT = NW * 64;
     __shared__ Dec8Lds L;
+    if (!__hip_atomic_load(&T->dec_ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {   // tables rebuilt since
+        if (threadIdx.x == 0) atomicOr(err, 1);
+        return;
+    }
     if (d_base) bit_base += *d_base;   // device-resident shard offset (dist: no host read)
     if (T->fixed8 && (bit_base & 127) == 0 && ((uintptr_t)in & 15) == 0 && ((uintptr_t)out & 15) == 0 &&
         (n + 3) / 4 <= nwords) {
@@ -2211,6 +2223,10 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode9(const uint32_t *__rest
     constexpr int NT = NW * 64;
     constexpr uint32_t MB = (1u << DC_MULTI_BITS) - 1;
     __shared__ Dec9Lds<NW> L;
+    if (!__hip_atomic_load(&T->dec_ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {   // tables rebuilt since
+        if (threadIdx.x == 0) atomicOr(err, 1);
+        return;
+    }
     if (d_base) bit_base += *d_base;   // device-resident shard offset (dist: no host read)
     const int t = threadIdx.x, lane = t & 63;
     const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -2419,10 +2435,11 @@ static __device__ __noinline__ uint32_t d8_long_lds(uint32_t lo, uint32_t hi, co
 // to the fixup's waves instead left them 1 or 2 windows of ~100 chunks each: 2.3x max/mean.)
 __global__ __launch_bounds__(1024) void k_huff_fix_list(const uint64_t *__restrict__ fix_mask, uint32_t ngroups,
                                                         uint32_t nchunks, uint32_t *__restrict__ list,
-                                                        uint32_t *__restrict__ cnt)
+                                                        uint32_t *__restrict__ cnt, int *__restrict__ err_next)
 {
     __shared__ uint32_t s_w[16];
     __shared__ uint32_t s_base;
+    if (blockIdx.x == 0 && threadIdx.x < 4) err_next[threadIdx.x] = 0;   // the next decode's error slot
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t g = blockIdx.x * 1024 + threadIdx.x;
     uint64_t m = g < ngroups ? fix_mask[g] : 0ull;
@@ -4079,7 +4096,12 @@ struct dc_ctx {
     uint16_t *d_bh;         size_t bh_cap;        // block histograms (u16 x 256 per block)
     uint64_t *d_off;        size_t off_cap;       // nblocks + 1
     uint32_t *d_plan;       size_t plan_cap;      // plan: per-block local offsets + workgroup totals
-    int *d_err;                                   // [0] plan, [1] decode
+    int *d_err;                                   // [8] text parse
+    // error flags of plan/pack and of decode in rotating slots (32 x 4 ints each): every call
+    // takes the next slot, which a kernel of the call before cleared (no memset launch)
+    int *d_errp, *d_errd;
+    uint32_t gen_p, gen_d;
+    const dc_dtable *dec_fresh;                   // decoder tables current: this context's last pack built them
     uint32_t *d_queue;                            // decode tuple scheduler heads (D8Sched)
     uint32_t *d_fix;        size_t fix_cap;       // decode redo: a u64 chunk mask per group
     uint32_t *d_fixlist;    size_t fixlist_cap;   // decode redo: flagged chunk indices, compacted
@@ -4176,11 +4198,14 @@ static int ctx_create(dc_ctx **out, int device, void *stream, bool own)
         c->own_stream = true;
     }
     if (hipMalloc((void **)&c->d_err, 16 * sizeof(int)) != hipSuccess ||
+        hipMalloc((void **)&c->d_errp, 2 * 128 * sizeof(int)) != hipSuccess ||
+        hipMemset(c->d_errp, 0, 2 * 128 * sizeof(int)) != hipSuccess ||
         hipMalloc((void **)&c->d_meta, 16 * sizeof(uint64_t)) != hipSuccess ||
         hipHostMalloc((void **)&c->h_pinned, 16 * sizeof(uint64_t), 0) != hipSuccess) {
         free(c);
         return DC_E_HIP;
     }
+    c->d_errd = c->d_errp + 128;
     if (hipMalloc((void **)&c->d_queue, D8_QWORDS * sizeof(uint32_t)) != hipSuccess ||
         hipMemset(c->d_queue, 0, D8_QWORDS * sizeof(uint32_t)) != hipSuccess) {
         free(c);
@@ -4215,6 +4240,7 @@ void dc_ctx_destroy(dc_ctx *c)
     if (c->d_off) (void)hipFree(c->d_off);
     if (c->d_plan) (void)hipFree(c->d_plan);
     if (c->d_err) (void)hipFree(c->d_err);
+    if (c->d_errp) (void)hipFree(c->d_errp);
     if (c->d_queue) (void)hipFree(c->d_queue);
     if (c->d_fix) (void)hipFree(c->d_fix);
     if (c->d_fixlist) (void)hipFree(c->d_fixlist);
@@ -4356,6 +4382,7 @@ static int table_common(dc_ctx *c, const uint64_t *d_freq, int is_hist, const in
                         int nary, dc_dtable *d_table)
 {
     if (!c || !d_table || M < 0 || M >= DC_MAX_SYMS || nary < 2 || nary > 256) return DC_E_ARG;
+    c->dec_fresh = nullptr;
     LAUNCH(c, "huff_table", k_huff_table, 1, 256, d_freq, is_hist, d_len, M, nary, d_table, (dc_tree *)nullptr);
     return DC_OK;
 }
@@ -4363,6 +4390,7 @@ static int table_common(dc_ctx *c, const uint64_t *d_freq, int is_hist, const in
 int dc_huff_tree(dc_ctx *c, const uint64_t *d_freq, int M, int nary, dc_dtable *d_table, dc_tree *d_tree)
 {
     if (!c || !d_freq || !d_table || !d_tree || M < 0 || M >= DC_MAX_SYMS || nary < 2 || nary > 256) return DC_E_ARG;
+    c->dec_fresh = nullptr;
     LAUNCH(c, "huff_tree", k_huff_table, 1, 256, d_freq, 0, (const int32_t *)nullptr, M, nary, d_table, d_tree);
     return DC_OK;
 }
@@ -4401,14 +4429,20 @@ int dc_huff_table_status(dc_ctx *c, const dc_dtable *d_table, int32_t *max_bits)
     return v[1];
 }
 
+static int *plan_err(dc_ctx *c) { return c->d_errp + 4 * (c->gen_p & 31u); }
+static int *plan_err_next(dc_ctx *c) { return c->d_errp + 4 * ((c->gen_p + 1) & 31u); }
+static int *dec_err(dc_ctx *c) { return c->d_errd + 4 * (c->gen_d & 31u); }
+static int *dec_err_next(dc_ctx *c) { return c->d_errd + 4 * ((c->gen_d + 1) & 31u); }
+
 int dc_huff_plan(dc_ctx *c, const dc_dtable *d_table, uint64_t *d_total_bits)
 {
     if (!c || !d_table || !d_total_bits) return DC_E_ARG;
     if (!c->hist_in && c->hist_n) return DC_E_STATE;
     const uint64_t nb = nblocks_of(c->hist_n);
     if (ensure((void **)&c->d_off, &c->off_cap, (nb + 1) * sizeof(uint64_t))) return DC_E_HIP;
-    HIPCHK(hipMemsetAsync(c->d_err, 0, 16 * sizeof(int), c->stream));
+    ++c->gen_p;   // this plan's error slot (cleared by the plan before; the next one is cleared below)
     if (nb == 0) {
+        HIPCHK(hipMemsetAsync(plan_err_next(c), 0, 4 * sizeof(int), c->stream));
         HIPCHK(hipMemsetAsync(c->d_off, 0, sizeof(uint64_t), c->stream));
         HIPCHK(hipMemsetAsync(d_total_bits, 0, sizeof(uint64_t), c->stream));
         c->plan_ok = true;
@@ -4418,13 +4452,13 @@ int dc_huff_plan(dc_ctx *c, const dc_dtable *d_table, uint64_t *d_total_bits)
     if (nwg <= PLAN_MAX_WG) {
         if (ensure((void **)&c->d_plan, &c->plan_cap, (nb + nwg + 64) * sizeof(uint32_t))) return DC_E_HIP;
         uint32_t *loc = c->d_plan, *tot = c->d_plan + nb + 32;
-        LAUNCH(c, "block_bits", k_block_local, nwg, 256, (const uint16_t *)c->d_bh, nb, d_table, loc, tot, c->d_err);
+        LAUNCH(c, "block_bits", k_block_local, nwg, 256, (const uint16_t *)c->d_bh, nb, d_table, loc, tot, plan_err(c));
         LAUNCH(c, "block_scan", k_block_final_wide, nwg, 256, (const uint32_t *)loc, (const uint32_t *)tot, nb,
-               (uint32_t)nwg, c->d_off, d_total_bits);
+               (uint32_t)nwg, c->d_off, d_total_bits, plan_err_next(c));
     } else {
         LAUNCH(c, "block_bits", k_block_bits, (nb + 3) / 4, 256, (const uint16_t *)c->d_bh, nb, d_table, c->d_off,
-               c->d_err);
-        LAUNCH(c, "block_scan", k_block_scan, 1, 1024, c->d_off, nb, d_total_bits);
+               plan_err(c));
+        LAUNCH(c, "block_scan", k_block_scan, 1, 1024, c->d_off, nb, d_total_bits, plan_err_next(c));
     }
     c->plan_ok = true;
     return DC_OK;
@@ -4474,14 +4508,15 @@ static int pack_impl(dc_ctx *c, const uint8_t *d_in, uint64_t n, const dc_dtable
     const uint64_t nb = nblocks_of(n);
     if (nb == 0) return DC_OK;
     LAUNCH(c, "zero_bounds", k_zero_bounds, (nb + 1 + 255) / 256, 256, (const uint64_t *)c->d_off, nb, bit_base,
-           d_base, d_words, words_cap, c->d_err);
+           d_base, d_words, words_cap, plan_err(c));
     // two blocks per workgroup (grid-stride): on 1 GiB C2, 16384 workgroups ran pack in
     // 0.452 ms against 0.481 at 4096, 0.469 at 32768, 0.504 at 1024 (r1 v15 A/B)
     const uint64_t gmax = c->opt_pack_grid ? c->opt_pack_grid : (nb + 1) / 2;
     const uint64_t grid = nb < gmax ? nb : gmax;
     // + workgroup 0: the decoder tables (k_huff_table leaves them to the pack's idle CU time)
     LAUNCH(c, "huff_pack", k_huff_pack, grid + 1, 256, d_in, n, d_table, (const uint64_t *)c->d_off, bit_base, d_base, d_words,
-           d_sync_base, d_sync_len, sync_syms, nb, words_cap, (const int *)c->d_err, 1);
+           d_sync_base, d_sync_len, sync_syms, nb, words_cap, (const int *)plan_err(c), 1);
+    c->dec_fresh = d_table;   // workgroup 0 built the decoder tables
     return DC_OK;
 }
 
@@ -4503,7 +4538,7 @@ int dc_huff_pack_async_dev(dc_ctx *c, const uint8_t *d_in, uint64_t n, const dc_
 int dc_huff_pack_status(dc_ctx *c, const dc_dtable *d_table)
 {
     int v[3] = {0, 0, 0};
-    HIPCHK(hipMemcpyAsync(v, c->d_err, 3 * sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(v, plan_err(c), 3 * sizeof(int), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     if (v[0]) {
         const int st = dc_huff_table_status(c, d_table, nullptr);
@@ -4522,7 +4557,7 @@ int dc_huff_pack(dc_ctx *c, const uint8_t *d_in, uint64_t n, const dc_dtable *d_
     if (d_sync_len && !sync_ok(sync_syms)) return DC_E_ARG;
     // plan errors (a byte without a code) are checked here: host read of one int
     int err = 0;
-    HIPCHK(hipMemcpyAsync(c->h_pinned, c->d_err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(c->h_pinned, plan_err(c), sizeof(int), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipMemcpyAsync(c->h_pinned + 1, c->d_off + nblocks_of(n), sizeof(uint64_t), hipMemcpyDeviceToHost,
                           c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
@@ -4562,8 +4597,11 @@ static int decode_impl(dc_ctx *c, const uint32_t *d_words, uint64_t bit_base, co
     if (n == 0) return DC_OK;
     if (words < 4) return DC_E_ARG;
     const uint64_t groups = dc_huff_sync_groups(n, S);
-    // decoder tables unless the pack built them (returns at once then); clears the error flag
-    LAUNCH(c, "dec_tables", k_dec_tables, 1, 256, const_cast<dc_dtable *>(d_table), c->d_err + 1);
+    ++c->gen_d;   // this decode's error slot (cleared by the decode before; it clears the next one)
+    int *const derr = dec_err(c), *const derr_next = dec_err_next(c);
+    // the decoder tables, unless this context's last pack built them for this table (no launch
+    // then; a table rebuilt elsewhere since reads dec_ready 0 in the decoder: a stream error)
+    if (c->dec_fresh != d_table) LAUNCH(c, "dec_tables", k_dec_tables, 1, 256, const_cast<dc_dtable *>(d_table), derr);
     if (S == 64 && n < (1ull << 37) && words < (1ull << 31) && !c->opt_decode_general) {
         // 12 waves x 2 chains, one workgroup per CU: the stage and the 14-bit table fill the
         // LDS (the 8 x 4 split measured 0.89 vs 0.70 ms on 1 GiB C2: spills)
@@ -4575,11 +4613,11 @@ static int decode_impl(dc_ctx *c, const uint32_t *d_words, uint64_t bit_base, co
         if (ensure((void **)&c->d_scr, &c->scr_cap, (size_t)D8_SCRATCH_WAVES * D8_WSCR)) return DC_E_HIP;
 #define D8_LAUNCH(NW_, NC_)                                                                                   \
         LAUNCH(c, "huff_decode", (k_huff_decode8<NW_, NC_>), (tuples + NW_ - 1) / NW_ < 256 ? (tuples + NW_ - 1) / NW_ : 256, \
-               NW_ * 64, d_words, bit_base, d_base, d_sync_base, d_sync_len, n, words, d_table, d_out, c->d_err + 1,       \
+               NW_ * 64, d_words, bit_base, d_base, d_sync_base, d_sync_len, n, words, d_table, d_out, derr,       \
                c->d_queue, spct, (uint64_t *)c->d_fix, (uint64_t *)c->d_fixpos, (uint8_t *)c->d_scr)
         if (c->opt_decode_variant == 1) {   // multi-symbol lookups, one group per wave
             LAUNCH(c, "huff_decode", k_huff_decode9<12>, groups < 256 * 12 ? (groups + 11) / 12 : 256, 12 * 64,
-                   d_words, bit_base, d_base, d_sync_base, d_sync_len, n, words, d_table, d_out, c->d_err + 1, c->d_queue,
+                   d_words, bit_base, d_base, d_sync_base, d_sync_len, n, words, d_table, d_out, derr, c->d_queue,
                    spct, (uint64_t *)c->d_fix, (uint64_t *)c->d_fixpos, (uint8_t *)c->d_scr);
         } else {   // one code per lookup, 11 waves x 2 chains (the 15-bit table takes 64 KiB of LDS)
             D8_LAUNCH(11, 2);
@@ -4589,15 +4627,15 @@ static int decode_impl(dc_ctx *c, const uint32_t *d_words, uint64_t bit_base, co
         if (ensure((void **)&c->d_fixlist, &c->fixlist_cap, (groups * 64 + 64) * sizeof(uint32_t))) return DC_E_HIP;
         const uint64_t nchunks = (n + 63) / 64;
         LAUNCH(c, "huff_fix_list", k_huff_fix_list, (groups + 1023) / 1024, 1024, (const uint64_t *)c->d_fix,
-               (uint32_t)groups, (uint32_t)nchunks, c->d_fixlist, c->d_queue + D8_FIX_CNT);
+               (uint32_t)groups, (uint32_t)nchunks, c->d_fixlist, c->d_queue + D8_FIX_CNT, derr_next);
         LAUNCH(c, "huff_decode_fix", k_huff_decode8_fix, 256, D8F_WAVES * 64, d_words, n, words, d_table, d_out,
-               c->d_err + 1, (const uint32_t *)c->d_fixlist, (const uint64_t *)c->d_fixpos, c->d_queue);
+               derr, (const uint32_t *)c->d_fixlist, (const uint64_t *)c->d_fixpos, c->d_queue);
         return DC_OK;
     }
     const uint64_t wgs = (groups + DEC_WAVES - 1) / DEC_WAVES;
     const uint64_t grid = wgs < 256 ? wgs : 256;   // persistent: one 16-wave workgroup per CU
     LAUNCH(c, "huff_decode", k_huff_decode, grid, DEC_WAVES * 64, d_words, bit_base, d_base, d_sync_base, d_sync_len, S, n, d_table,
-           d_out, c->d_err + 1);
+           d_out, derr, derr_next);
     return DC_OK;
 }
 
@@ -4635,7 +4673,7 @@ int dc_huff_decode_redo_count(dc_ctx *c, uint64_t *count)
 int dc_huff_decode_status(dc_ctx *c)
 {
     int v = 0;
-    HIPCHK(hipMemcpyAsync(&v, c->d_err + 1, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(&v, dec_err(c), sizeof(int), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return v ? DC_E_STREAM : DC_OK;
 }

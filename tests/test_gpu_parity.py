@@ -449,6 +449,33 @@ def test_decode_corrupt_stream_reports(torch_cuda, codec):
     torch.cuda.synchronize()
 
 
+def test_decode_error_slots_and_stale_tables(torch_cuda, codec):
+    """Error flags live in per-call rotating slots (no clearing launch): an error stays with
+    its own call. A decode right after this context's pack skips the decoder-table launch; a
+    table rebuilt since by another context reads dec_ready 0 in the decoder: reported as a
+    stream error, never silent garbage. Every later call is clean again."""
+    torch = torch_cuda
+    from data_compression_amd import synth
+    from data_compression_amd.device import Codec
+    other = Codec(0)
+    x = synth.enwik_like(300_000, seed=31)
+    xt = torch.from_numpy(x).cuda()
+    out = torch.empty_like(xt)
+    for _ in range(40):   # > 32 slots: the rotation wraps
+        enc = codec.encode(xt, n_ary=2, sync_syms=64)
+        codec.decode_into(enc, out)
+        assert codec.decode_status() == 0 and torch.equal(out, xt)
+    enc = codec.encode(xt, n_ary=2, sync_syms=64)
+    other.table(other.hist(torch.from_numpy(synth.uniform_bytes(4096, seed=3)).cuda()), 2, out=enc["table"])
+    codec.decode_into(enc, out)
+    assert codec.decode_status() != 0   # stale decoder tables: reported
+    enc = codec.encode(xt, n_ary=2, sync_syms=64)
+    codec.decode_into(enc, out)
+    assert codec.decode_status() == 0 and torch.equal(out, xt)
+    codec.decode_into(enc, out)   # twice without a pack between
+    assert codec.decode_status() == 0 and torch.equal(out, xt)
+
+
 TEXT_CASES = [("base64url", 2), ("base16", 2), ("digits", 2), ("digits", 3), ("digits", 9), ("digits", 16),
               ("z85", 3), ("z85", 9), ("trits5", 3)]
 

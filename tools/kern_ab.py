@@ -6,6 +6,7 @@ stages: hist (k_hist_blocks), encode (hist+table+plan+pack), decode, step (encod
 import argparse
 import os
 import sys
+import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np  # noqa: E402
@@ -51,6 +52,12 @@ for r in range(a.rounds):
         c.set_option(a.option, v)
         run()
         torch.cuda.synchronize()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(a.iters):
+            run()
+        torch.cuda.synchronize()
+        res[v].setdefault("wall", []).append((time.perf_counter() - t0) / a.iters * 1e3)
         c.timing(True)
         for _ in range(a.iters):
             run()
