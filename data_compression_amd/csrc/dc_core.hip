@@ -960,7 +960,7 @@ static __device__ __forceinline__ void lds_barrier()
 #define PACK_BLK_WORDS 9216     /* 36 KiB: a full block of <= 9 bits/symbol is staged whole  */
 #define PACK_PIECES (DC_BLOCK_BYTES / PACK_TILE)
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_huff_pack(const uint8_t *__restrict__ in, uint64_t n,
+__global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ in, uint64_t n,
                                                    const dc_dtable *__restrict__ T,
                                                    const uint64_t *__restrict__ block_off, uint64_t bit_base,
                                                    const uint64_t *__restrict__ d_base, uint32_t *__restrict__ out, uint64_t *__restrict__ sync_base,
@@ -969,11 +969,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
                                                    const int *__restrict__ err, int build_dec)
 {
     __shared__ uint2 s_tab[256];
-#ifdef DC_PACK_NB8   // A/B only: 1-byte lengths (each read masked, the byte extracted apart)
+    // bit lengths alone (pass A reads 1 byte, not 8): 64 dwords, so at most 2 distinct dwords
+    // per bank. (As dwords, one SDWA shift per byte instead of an extract and a mask, pass A
+    // had 256 dwords, 8 per bank: the bank conflicts cost more than the VALU saved, C4 pack +2%;
+    // one lookup per byte with the codes held in registers through the scan, in two groups
+    // of 4 pieces to fit 128 VGPRs, measured equal on C2 and +3% on C4.)
     __shared__ uint8_t s_nb8[256];
-#else   // bit lengths alone, one dword per byte value: the address is one SDWA shift of the byte
-    __shared__ uint32_t s_nb8[256];
-#endif
     __shared__ __attribute__((aligned(16))) uint32_t s_stage[PACK_BLK_WORDS + 4];   // +4: emit's no-op ORs past the end
     __shared__ uint32_t s_scan[4];
     __shared__ uint32_t s_tot[PACK_PIECES][4];
@@ -990,7 +991,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     // output buffer smaller than the planned stream -> write nothing
     if (err[0] != 0 || ((bit_base & 31) + block_off[nblocks] + 31) / 32 > words_cap) return;
     s_tab[t] = make_uint2(T->code[t], T->nbits[t]);
-    s_nb8[t] = T->nbits[t];
+    s_nb8[t] = (uint8_t)T->nbits[t];
     const bool vec_out = ((uintptr_t)out & 15) == 0;
     const uint64_t word_base = bit_base >> 5;
     const uint32_t slog = sync_syms ? (uint32_t)__builtin_ctz(sync_syms) : 0u;   // S is a power of two
@@ -1068,66 +1069,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
             const uint32_t nwa = sh + nw_blk;
             for (uint32_t i = 4u * t; i < nwa; i += 1024u)
                 *reinterpret_cast<uint4 *>(&s_stage[i]) = make_uint4(0u, 0u, 0u, 0u);
-            // in two groups of 4 pieces (lookups -> scan -> barrier -> stage ORs each): the
-            // group's gathered codes stay in registers through its scan without the other
-            // group's (all 8 pieces at once took 181 VGPRs: 2 waves per SIMD)
-            constexpr int GP = PACK_PIECES / 2;
+            uint32_t Tk[PACK_PIECES], Hk[PACK_PIECES], Ik[PACK_PIECES];
+#pragma unroll
+            for (int k = 0; k < PACK_PIECES; ++k) {
+                const uint32_t w4[4] = {blkv[k].x, blkv[k].y, blkv[k].z, blkv[k].w};
+                uint32_t s0 = 0, s1 = 0;
+#pragma unroll
+                for (int i = 0; i < 8; ++i) s0 += s_nb8[(w4[i >> 2] >> (8 * (i & 3))) & 255u];
+#pragma unroll
+                for (int i = 8; i < 16; ++i) s1 += s_nb8[(w4[i >> 2] >> (8 * (i & 3))) & 255u];
+                Hk[k] = s0;
+                Tk[k] = s0 + s1;
+                __builtin_amdgcn_sched_barrier(0);
+            }
+#pragma unroll
+            for (int k = 0; k < PACK_PIECES; ++k) Ik[k] = wave_scan_incl(Tk[k]);
+            if (lane == 63) {
+#pragma unroll
+                for (int k = 0; k < PACK_PIECES; ++k) s_tot[k][wid] = Ik[k];
+            }
+            lds_barrier();
             const uint64_t org = (blk_first_word - sh) << 5;   // absolute bit of stage bit 0
             const uint32_t cm = sync_syms >> 4;                 // lanes per sync chunk
             uint64_t run = blk_abs;   // absolute bit where piece k starts
 #pragma unroll
-            for (int g = 0; g < 2; ++g) {
-            uint32_t Tk[GP], Hk[GP], Ik[GP];
-#ifndef DC_PACK_TWOPASS
-            // one lookup per byte (half mode): the 8 codes of each half are gathered here, with
-            // their bit count, and kept in registers through the scan (a separate length pass
-            // cost a second LDS read per byte: pass A was ~40% of the kernel's LDS cycles)
-            uint64_t hacc[GP][2];
-#endif
-#pragma unroll
-            for (int kk = 0; kk < GP; ++kk) {
-                const int k = g * GP + kk;
-                const uint32_t w4[4] = {blkv[k].x, blkv[k].y, blkv[k].z, blkv[k].w};
-                uint32_t s0 = 0, s1 = 0;
-#ifndef DC_PACK_TWOPASS
-                if (!qmode) {
-                    uint64_t a0 = 0, a1 = 0;
-#pragma unroll
-                    for (int i = 0; i < 8; ++i) {
-                        const uint2 e = s_tab[(w4[i >> 2] >> (8 * (i & 3))) & 255u];
-                        a0 = (a0 << e.y) | e.x;
-                        s0 += e.y;
-                    }
-#pragma unroll
-                    for (int i = 8; i < 16; ++i) {
-                        const uint2 e = s_tab[(w4[i >> 2] >> (8 * (i & 3))) & 255u];
-                        a1 = (a1 << e.y) | e.x;
-                        s1 += e.y;
-                    }
-                    hacc[kk][0] = a0;
-                    hacc[kk][1] = a1;
-                } else
-#endif
-                {
-#pragma unroll
-                    for (int i = 0; i < 8; ++i) s0 += s_nb8[(w4[i >> 2] >> (8 * (i & 3))) & 255u];
-#pragma unroll
-                    for (int i = 8; i < 16; ++i) s1 += s_nb8[(w4[i >> 2] >> (8 * (i & 3))) & 255u];
-                }
-                Hk[kk] = s0;
-                Tk[kk] = s0 + s1;
-                __builtin_amdgcn_sched_barrier(0);
-            }
-#pragma unroll
-            for (int kk = 0; kk < GP; ++kk) Ik[kk] = wave_scan_incl(Tk[kk]);
-            if (lane == 63) {
-#pragma unroll
-                for (int kk = 0; kk < GP; ++kk) s_tot[g * GP + kk][wid] = Ik[kk];
-            }
-            lds_barrier();
-#pragma unroll
-            for (int kk = 0; kk < GP; ++kk) {
-                const int k = g * GP + kk;
+            for (int k = 0; k < PACK_PIECES; ++k) {
                 uint32_t wo = 0, kt = 0;
 #pragma unroll
                 for (int w = 0; w < 4; ++w) {
@@ -1135,15 +1101,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
                     wo += (w < wid) ? v : 0u;
                     kt += v;
                 }
-                const uint64_t As = run + wo + (Ik[kk] - Tk[kk]);
+                const uint64_t As = run + wo + (Ik[k] - Tk[k]);
                 run += kt;
                 const uint64_t p = blk_start + (uint64_t)k * PACK_TILE + (uint64_t)t * 16;
                 if (sync_len != nullptr) {
                     // chunk bits = inclusive scan at the chunk's last lane - exclusive at its first
-                    const uint32_t last = (cm == 4) ? (uint32_t)__builtin_amdgcn_update_dpp(0, (int)Ik[kk], 0xff, 0xf, 0xf, false)
-                                                    : (uint32_t)__shfl((int)Ik[kk], lane | (int)(cm - 1), 64);
+                    const uint32_t last = (cm == 4) ? (uint32_t)__builtin_amdgcn_update_dpp(0, (int)Ik[k], 0xff, 0xf, 0xf, false)
+                                                    : (uint32_t)__shfl((int)Ik[k], lane | (int)(cm - 1), 64);
                     if ((p & (uint64_t)(sync_syms - 1)) == 0) {
-                        sync_len[p >> slog] = (uint16_t)(last - (Ik[kk] - Tk[kk]));
+                        sync_len[p >> slog] = (uint16_t)(last - (Ik[k] - Tk[k]));
                         if ((p & ((uint64_t)sync_syms * DC_SYNC_GROUP - 1)) == 0)
                             sync_base[p >> (slog + DC_SYNC_GROUP_LOG)] = As;
                     }
@@ -1167,12 +1133,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
                 };
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
-                    const uint32_t Th = h ? Tk[kk] - Hk[kk] : Hk[kk];
-                    const uint32_t pos = h ? rel + Hk[kk] : rel;
+                    const uint32_t Th = h ? Tk[k] - Hk[k] : Hk[k];
+                    const uint32_t pos = h ? rel + Hk[k] : rel;
                     if (!qmode && Th <= 64u) {
-#ifndef DC_PACK_TWOPASS
-                        emit(hacc[kk][h], Th, pos);
-#else
                         // (a packed 32-bit code|length table measured 4% slower: the
                         // extraction VALU costs more than the uint2 reads' bank conflicts)
                         uint64_t acc = 0;
@@ -1182,7 +1145,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
                             acc = (acc << e.y) | e.x;
                         }
                         emit(acc, Th, pos);
-#endif
                     } else {
                         // a half of more than 64 bits (skewed or long codes, e.g. C4's Zipf
                         // bytes), or every half in quarter mode: two quarters of 4 codes, each
@@ -1213,7 +1175,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
                     }
                 }
                 __builtin_amdgcn_sched_barrier(0);   // keep the pieces' lookups from being hoisted
-            }
             }
             lds_barrier();
             // stage word sh = the block's first word, shared with the previous block; the last
