@@ -196,6 +196,40 @@ def test_pack_at_bit_offset(torch_cuda, codec, bit_base):
     assert np.array_equal(out.cpu().numpy(), x)
 
 
+@pytest.mark.parametrize("bit_base", [0, 5, 31, 32, 1000, 128 * 3])
+@pytest.mark.parametrize("kind", ["text", "flat16", "tail"])
+def test_pack_into_dirty_words(torch_cuda, codec, bit_base, kind):
+    """No zeroing launch precedes the pack: blocks that share a word clear and set only their
+    own bits (the first block also the bits before bit_base, the last the pad). Into a words
+    buffer full of ones, every word the stream touches must match the oracle's bit for bit,
+    zero bits before bit_base and after the last code included; words outside stay ones."""
+    torch = torch_cuda
+    from data_compression_amd import synth
+    if kind == "text":
+        x, n_ary = synth.enwik_like(200_003, seed=51), 2          # fast path, ragged last block
+    elif kind == "flat16":
+        x, n_ary = synth.uniform_bytes((3 << 15) + 13, seed=52), 16   # 8-bit codes: byte map at bit_base % 128 == 0
+    else:
+        x, n_ary = synth.enwik_like((2 << 15) + 1, seed=53), 2        # a 1-byte last block (slow path)
+    L, el, ev, code, nb, mx = _oracle_encode(x, n_ary)
+    payload, bits, _ = orc.huff_pack(x, code, nb, bit_base=bit_base)
+    xt = torch.from_numpy(x).cuda()
+    hist = codec.hist(xt)
+    tab = codec.table(hist, n_ary)
+    total = codec.plan(tab)
+    assert int(total.item()) == bits
+    nw = codec.words_needed(bit_base, bits)
+    words = torch.full((nw,), -1, dtype=torch.int32, device="cuda")
+    codec.pack(xt, tab, bit_base, words, None, 0)
+    got = words.cpu().numpy().view(np.uint8)
+    off = (bit_base >> 3) - ((bit_base >> 5) << 2)
+    end = ((bit_base & 31) + bits + 31) // 32 * 4   # bytes of the words the stream touches
+    want = np.zeros(end, np.uint8)
+    want[off: off + len(payload)] = payload
+    assert np.array_equal(got[:end], want), (kind, bit_base)
+    assert (got[end:] == 0xFF).all(), (kind, bit_base)
+
+
 @pytest.mark.parametrize("bit_base", [0, 128 * 3, 8, 32])
 def test_fixed8_byte_map_paths(torch_cuda, codec, bit_base):
     """n = 16 on flat bytes: every code is 8 bits (dc_dtable.fixed8), so pack and decode run
