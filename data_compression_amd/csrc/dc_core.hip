@@ -1186,7 +1186,13 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
                 const uint32_t nq = last_plain >> 2;   // uint4 q covers stage words [4q, 4q+4)
                 for (uint32_t q = 1 + t; q < nq; q += 256) {
                     const uint4 v = *reinterpret_cast<const uint4 *>(&s_stage[4 * q]);
-                    *reinterpret_cast<uint4 *>(dst + 4 * q) = make_uint4(bswap32(v.x), bswap32(v.y), bswap32(v.z), bswap32(v.w));
+                    // streaming (nt) stores: same-box A/B on 1 GiB C2, pack 0.420 -> 0.382 ms
+                    // (the decode after it reads the payload no slower)
+                    uint4 *const d4 = reinterpret_cast<uint4 *>(dst + 4 * q);
+                    __builtin_nontemporal_store(bswap32(v.x), &d4->x);
+                    __builtin_nontemporal_store(bswap32(v.y), &d4->y);
+                    __builtin_nontemporal_store(bswap32(v.z), &d4->z);
+                    __builtin_nontemporal_store(bswap32(v.w), &d4->w);
                 }
                 // head: words sh+1..3 of uint4 0; tail: words of the last, partial uint4
                 const uint32_t hend = last_plain < 4u ? last_plain : 4u;
@@ -1767,7 +1773,14 @@ static __device__ __forceinline__ void d8_out(uint32_t *const *stw, const uint32
 #ifdef DC_DIAG_NOSTORE
             asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
 #else
-            dst[j][s * 64 + lane] = v;
+            // streaming (nt) stores: the decoded output is not read again here, and written
+            // back at once it leaves no dirty lines for the next kernels' reads to evict
+            // (1 GiB C2 step, same-box A/B: the next histogram 0.244 -> 0.208 ms, the decode
+            // itself 0.432 -> 0.420, the redo 0.046 -> 0.038)
+            __builtin_nontemporal_store(v.x, &dst[j][s * 64 + lane].x);
+            __builtin_nontemporal_store(v.y, &dst[j][s * 64 + lane].y);
+            __builtin_nontemporal_store(v.z, &dst[j][s * 64 + lane].z);
+            __builtin_nontemporal_store(v.w, &dst[j][s * 64 + lane].w);
 #endif
         }
     }
@@ -1998,7 +2011,11 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode8(const uint32_t *__rest
                 bad |= (a | b2 | c2 | d2) & 0x100u;
                 w4[q] = (a & 255u) | ((b2 & 255u) << 8) | ((c2 & 255u) << 16) | ((d2 & 255u) << 24);
             }
-            *reinterpret_cast<uint4 *>(out + 16 * g) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+            uint4 *const o4 = reinterpret_cast<uint4 *>(out + 16 * g);   // streaming stores, as d8_out
+            __builtin_nontemporal_store(w4[0], &o4->x);
+            __builtin_nontemporal_store(w4[1], &o4->y);
+            __builtin_nontemporal_store(w4[2], &o4->z);
+            __builtin_nontemporal_store(w4[3], &o4->w);
         }
         for (uint64_t i = (n & ~15ull) + me; i < n; i += nthr) {
             const uint32_t a = inv[ib[i]];
