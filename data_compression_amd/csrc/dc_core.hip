@@ -33,6 +33,13 @@ static __device__ __forceinline__ uint4 ld_nt(const uint4 *p)
 // is read by a later kernel only after far more than the caches hold: nt loads and stores for
 // them (same-box A/B on the 1 GiB C2 step against plain ones: histogram 0.207 -> 0.188 ms,
 // pack 0.379 -> 0.364, decode 0.422 -> 0.418 from the loads; the stores: see d8_out, k_huff_pack)
+static __device__ __forceinline__ void st_nt(uint4 *p, const uint4 &v)
+{
+    __builtin_nontemporal_store(v.x, &p->x);
+    __builtin_nontemporal_store(v.y, &p->y);
+    __builtin_nontemporal_store(v.z, &p->z);
+    __builtin_nontemporal_store(v.w, &p->w);
+}
 #define LD_HIST(p) ld_nt(p)
 #define LD_PACK(p) ld_nt(p)
 #define LD_DEC(p) ld_nt(p)
@@ -1024,7 +1031,7 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
                 uint4 v[PACK_PIECES];
 #pragma unroll
                 for (int k = 0; k < PACK_PIECES; ++k)
-                    v[k] = *reinterpret_cast<const uint4 *>(in + blk_start + (uint64_t)k * PACK_TILE + (uint64_t)t * 16);
+                    v[k] = LD_PACK(reinterpret_cast<const uint4 *>(in + blk_start + (uint64_t)k * PACK_TILE + (uint64_t)t * 16));
 #pragma unroll
                 for (int k = 0; k < PACK_PIECES; ++k) {
                     uint32_t w4[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
@@ -1034,8 +1041,8 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
                         w4[q] = s_tab[x & 255u].x | (s_tab[(x >> 8) & 255u].x << 8) | (s_tab[(x >> 16) & 255u].x << 16) |
                                 (s_tab[x >> 24].x << 24);
                     }
-                    *reinterpret_cast<uint4 *>(ob + blk_start + (uint64_t)k * PACK_TILE + (uint64_t)t * 16) =
-                        make_uint4(w4[0], w4[1], w4[2], w4[3]);
+                    st_nt(reinterpret_cast<uint4 *>(ob + blk_start + (uint64_t)k * PACK_TILE + (uint64_t)t * 16),
+                          make_uint4(w4[0], w4[1], w4[2], w4[3]));
                 }
             } else {
                 for (uint64_t i = blk_start + t; i < blk_end; i += 256) ob[i] = (uint8_t)s_tab[in[i]].x;
@@ -2015,7 +2022,7 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode8(const uint32_t *__rest
         const uint64_t nthr = (uint64_t)gridDim.x * NW * 64, me = (uint64_t)blockIdx.x * NW * 64 + tt;
         uint32_t bad = 0;
         for (uint64_t g = me; g < n / 16; g += nthr) {
-            const uint4 v = *reinterpret_cast<const uint4 *>(ib + 16 * g);
+            const uint4 v = LD_DEC(reinterpret_cast<const uint4 *>(ib + 16 * g));
             uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -2939,7 +2946,7 @@ struct FsmWin {
 };
 static __device__ __forceinline__ uint4 fsm_granule(uintptr_t ad, uintptr_t lo, uintptr_t hi)
 {
-    return (ad + 16 > lo && ad < hi) ? *reinterpret_cast<const uint4 *>(ad) : make_uint4(0u, 0u, 0u, 0u);
+    return (ad + 16 > lo && ad < hi) ? ld_nt(reinterpret_cast<const uint4 *>(ad)) : make_uint4(0u, 0u, 0u, 0u);
 }
 static __device__ __forceinline__ uint4 fsm_shfl_down(const uint4 &v, int d)
 {
@@ -3332,7 +3339,7 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
         for (int64_t g = t; g < ng; g += 256) {
             const int64_t b0 = o_al + 16 * g;
             if (b0 >= beg && b0 + 16 <= end) {
-                *reinterpret_cast<uint4 *>(out + b0) = *reinterpret_cast<const uint4 *>(s_out + 16 * g);
+                st_nt(reinterpret_cast<uint4 *>(out + b0), *reinterpret_cast<const uint4 *>(s_out + 16 * g));
             } else {
                 for (int q = 0; q < 16; ++q) {
                     const int64_t bq = b0 + q;
@@ -3475,7 +3482,8 @@ static __device__ __forceinline__ void sm_load(const uint8_t *__restrict__ in, u
     for (int st = 0; st < SM_STEPS; ++st) {
         const uint32_t u = (uint32_t)(st * 1024 + w * 256 + lane * 4);
         const int64_t o = T.base + (int64_t)u;   // relative to in
-        dv[st] = (u + 4 > ulo && u < uhi && o + 4 > 0 && o < (int64_t)len) ? *reinterpret_cast<const uint32_t *>(in + o) : 0u;
+        dv[st] = (u + 4 > ulo && u < uhi && o + 4 > 0 && o < (int64_t)len)
+                     ? __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(in + o)) : 0u;
     }
 }
 struct SmEdge {
@@ -3610,7 +3618,7 @@ __global__ __launch_bounds__(256) void k_small_write(const uint8_t *__restrict__
         for (int64_t q = t; q < ng; q += 256) {
             const int64_t b0 = o_al + 16 * q;
             if (b0 >= beg && b0 + 16 <= end) {
-                *reinterpret_cast<uint4 *>(out + b0) = *reinterpret_cast<const uint4 *>(s_out + 16 * q);
+                st_nt(reinterpret_cast<uint4 *>(out + b0), *reinterpret_cast<const uint4 *>(s_out + 16 * q));
             } else {
                 for (int k = 0; k < 16; ++k) {
                     const int64_t bq = b0 + k;
