@@ -174,6 +174,8 @@ def main():
         ngroups, nchunks = c.sync_sizes(nh, S)
     sync_bytes = ngroups * 8 + nchunks * 2
     alg = {"hist_blocks": nh, "huff_pack": nh + payload + sync_bytes, "huff_decode": payload + sync_bytes + nh}
+    if a.frontend:   # SURVEY §8(d), as for nybble: the front-end moves N + its output each way
+        alg.update({"small_write": n + nh, "small_body_tiles": n, "small_dec_tiles": nh})
     kernels = {}
     for name, v in per.items():
         m = float(np.mean(v))
@@ -189,7 +191,7 @@ def main():
 
     # whole-pipeline rooflines (SURVEY §8(d) bytes over the whole encode / whole decode time:
     # extra passes such as the histogram's read of the input count against them)
-    enc_alg = nh + payload + sync_bytes
+    enc_alg = n + payload + sync_bytes   # the pipeline's input (C5: before the front-end) + its output
     enc_frac = enc_alg / (enc_ms * 1e-3) / HBM_PEAK
     dec_frac = enc_alg / (dec_ms * 1e-3) / HBM_PEAK
     value = world * n / (ms_step * 1e-3) / 1e9
