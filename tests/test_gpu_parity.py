@@ -510,6 +510,26 @@ def test_decode_error_slots_and_stale_tables(torch_cuda, codec):
     assert codec.decode_status() == 0 and torch.equal(out, xt)
 
 
+@pytest.mark.parametrize("variant", [0, 1])
+def test_decode_variants(torch_cuda, codec, variant):
+    """The fast decoder's variants (0: one code per 15-bit lookup; 1: up to 3 per 13-bit
+    lookup) on text, Zipf and flat bytes at n = 2, 3, 16, ragged sizes: exact round trips."""
+    torch = torch_cuda
+    from data_compression_amd import synth
+    codec.set_option("decode_variant", variant)
+    try:
+        for x, n_ary in ((synth.enwik_like(3 << 20, seed=61), 2), (synth.zipf_bytes((2 << 20) + 5, seed=62), 2),
+                         (synth.english_like(1_000_003, seed=63), 3), (synth.enwik_like(777_777, seed=64), 16),
+                         (synth.uniform_bytes(300_001, seed=65, lo=0, hi=255), 2)):
+            xt = torch.from_numpy(x).cuda()
+            enc = codec.encode(xt, n_ary=n_ary, sync_syms=64)
+            out = torch.empty_like(xt)
+            codec.decode_into(enc, out)
+            assert codec.decode_status() == 0 and torch.equal(out, xt), (variant, n_ary, x.size)
+    finally:
+        codec.set_option("decode_variant", 0)
+
+
 TEXT_CASES = [("base64url", 2), ("base16", 2), ("digits", 2), ("digits", 3), ("digits", 9), ("digits", 16),
               ("z85", 3), ("z85", 9), ("trits5", 3)]
 
