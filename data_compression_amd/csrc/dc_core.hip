@@ -82,10 +82,17 @@ static __device__ __forceinline__ uint32_t wg_scan_excl_u32(uint32_t v, uint32_t
 template <int PF>   // full blocks whose loads are in flight ahead of the one being counted
 __global__ __launch_bounds__(256) void k_hist_blocks(const uint8_t *__restrict__ in, uint64_t n,
                                                      uint64_t nblocks, uint16_t *__restrict__ bh,
-                                                     uint64_t *__restrict__ hist)
+                                                     uint64_t *__restrict__ hist, uint32_t *__restrict__ hflag,
+                                                     uint32_t gen)
 {
     __shared__ __attribute__((aligned(16))) uint32_t cnt[256 * 64];
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    if (blockIdx.x == 0) {   // hist[] zeroed here, not by a memset launch; *hflag = gen says so
+        hist[t] = 0ull;
+        __threadfence();
+        __syncthreads();
+        if (t == 0) __hip_atomic_store(hflag, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
     const uint32_t inc = 1u << (8 * wv);
     const uint32_t lane4 = 4u * (uint32_t)lane;
     char *const cbase = reinterpret_cast<char *>(cnt);
@@ -168,8 +175,12 @@ __global__ __launch_bounds__(256) void k_hist_blocks(const uint8_t *__restrict__
         total += acc;
         __syncthreads();
     }
-    // this workgroup's bin totals straight into hist[] (zeroed by the launcher): 512 u64
-    // atomics per bin at the end, no reduce launch (A/B r1 v14: step 1.379 -> 1.368 ms)
+    // this workgroup's bin totals straight into hist[] (zeroed by workgroup 0 at its start,
+    // long before any workgroup gets here; all 512 are resident): 512 u64 atomics per bin at
+    // the end, no reduce launch (A/B r1 v14: step 1.379 -> 1.368 ms)
+    if (t == 0)
+        while (__hip_atomic_load(hflag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != gen) __builtin_amdgcn_s_sleep(2);
+    __syncthreads();
     if (total) atomicAdd(reinterpret_cast<unsigned long long *>(&hist[t]), total);
 }
 
@@ -4164,7 +4175,8 @@ struct dc_ctx {
     uint32_t opt_pack_grid;       // pack workgroups (0: default, two blocks per workgroup)
     uint32_t opt_d8_static;       // decoder: static share of the tuples, percent (0..100)
     uint32_t opt_decode_general;  // 1: always the general decoder (k_huff_decode)
-    uint32_t opt_hist_pf;         // histogram: blocks of loads in flight ahead (1..2, 0 = default 1)
+    uint32_t opt_hist_pf;         // histogram: blocks of loads in flight ahead (1..2, 0 = default 2)
+    uint32_t *d_hflag, gen_h;     // histogram zeroed by its workgroup 0 (flag = this call's generation)
     uint32_t opt_decode_variant;  // fast decoder: 0 one code per lookup (k_huff_decode8), 1 up to 3 (k_huff_decode9)
     uint32_t opt_adec_v1;         // adaptive nybble decode: 1 = the one-pass k_nyb_adec (A/B)
     // timing
@@ -4245,6 +4257,10 @@ static int ctx_create(dc_ctx **out, int device, void *stream, bool own)
         return DC_E_HIP;
     }
     c->d_errd = c->d_errp + 128;
+    if (hipMalloc((void **)&c->d_hflag, 64) != hipSuccess || hipMemset(c->d_hflag, 0, 64) != hipSuccess) {
+        free(c);
+        return DC_E_HIP;
+    }
     if (hipMalloc((void **)&c->d_queue, D8_QWORDS * sizeof(uint32_t)) != hipSuccess ||
         hipMemset(c->d_queue, 0, D8_QWORDS * sizeof(uint32_t)) != hipSuccess) {
         free(c);
@@ -4280,6 +4296,7 @@ void dc_ctx_destroy(dc_ctx *c)
     if (c->d_plan) (void)hipFree(c->d_plan);
     if (c->d_err) (void)hipFree(c->d_err);
     if (c->d_errp) (void)hipFree(c->d_errp);
+    if (c->d_hflag) (void)hipFree(c->d_hflag);
     if (c->d_queue) (void)hipFree(c->d_queue);
     if (c->d_fix) (void)hipFree(c->d_fix);
     if (c->d_fixlist) (void)hipFree(c->d_fixlist);
@@ -4409,11 +4426,12 @@ int dc_huff_hist(dc_ctx *c, const uint8_t *d_in, uint64_t n, uint64_t *d_hist)
     }
     const uint64_t hmax = c->opt_hist_grid ? c->opt_hist_grid : 512u;
     const uint64_t grid = nb < hmax ? nb : hmax;   // 512: 2 resident per CU (64 KiB LDS each)
-    HIPCHK(hipMemsetAsync(d_hist, 0, 256 * sizeof(uint64_t), c->stream));
-    // one block of loads in flight ahead: 0.1995 ms on 1 GiB C2 (5.4 TB/s) against 0.2022 with
-    // two (230 VGPRs) and 0.292 with three (1 wave per SIMD) (r2 A/B, tools/kern_ab.py)
-    if (c->opt_hist_pf == 2) LAUNCH(c, "hist_blocks", k_hist_blocks<2>, grid, 256, d_in, n, nb, c->d_bh, d_hist);
-    else LAUNCH(c, "hist_blocks", k_hist_blocks<1>, grid, 256, d_in, n, nb, c->d_bh, d_hist);
+    // two blocks of loads in flight ahead (with nt loads; same-box A/B in the 1 GiB C2 step:
+    // 0.176 ms against 0.179 with one; before the nt loads one was best, 0.1995 vs 0.2022 ms)
+    if (++c->gen_h == 0) c->gen_h = 1;
+    if (c->opt_hist_pf == 1)
+        LAUNCH(c, "hist_blocks", k_hist_blocks<1>, grid, 256, d_in, n, nb, c->d_bh, d_hist, c->d_hflag, c->gen_h);
+    else LAUNCH(c, "hist_blocks", k_hist_blocks<2>, grid, 256, d_in, n, nb, c->d_bh, d_hist, c->d_hflag, c->gen_h);
     return DC_OK;
 }
 

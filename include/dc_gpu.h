@@ -114,7 +114,7 @@ enum {
     DC_OPT_PACK_GRID = 2,         /* pack workgroups, 0 = default (two blocks each)        */
     DC_OPT_DECODE_STATIC_PCT = 3, /* fast decoder: statically dealt share of work, 0..100  */
     DC_OPT_DECODE_GENERAL = 4,    /* 1: decode with the general (any-S) decoder            */
-    DC_OPT_HIST_PREFETCH = 5,     /* histogram: 32 KiB blocks in flight ahead, 1..2, 0 = 1 */
+    DC_OPT_HIST_PREFETCH = 5,     /* histogram: 32 KiB blocks in flight ahead, 1..2, 0 = 2 */
     DC_OPT_DECODE_VARIANT = 6,    /* fast decoder: 0 one code per lookup (k_huff_decode8),
                                      1 up to 3 codes per lookup (k_huff_decode9) */
     DC_OPT_NYB_ADEC_V1 = 7        /* adaptive nybble decode: 0 tokens + k_nyb_resolve,

@@ -3,6 +3,6 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 for r in 1 2; do
-  echo "tree:"; timeout -k 10 200 python -u tools/kern_ab.py --stage ${3:-step} --values 1 --cfg ${2:-C2} --rounds 3 || exit 1
-  echo "abl$1:"; DC_CORE_LIB=$PWD/tools/_abl$1/libdc_core.so timeout -k 10 200 python -u tools/kern_ab.py --stage ${3:-step} --values 1 --cfg ${2:-C2} --rounds 3 || exit 1
+  echo "tree:"; timeout -k 10 200 python -u tools/kern_ab.py --stage ${3:-step} --option decode_static_pct --values 60 --cfg ${2:-C2} --rounds 3 || exit 1
+  echo "abl$1:"; DC_CORE_LIB=$PWD/tools/_abl$1/libdc_core.so timeout -k 10 200 python -u tools/kern_ab.py --stage ${3:-step} --option decode_static_pct --values 60 --cfg ${2:-C2} --rounds 3 || exit 1
 done
