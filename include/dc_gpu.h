@@ -184,7 +184,11 @@ int dc_huff_pack_async_dev(dc_ctx *ctx, const uint8_t *d_in, uint64_t n, const d
 int dc_huff_pack_status(dc_ctx *ctx, const dc_dtable *d_table);
 /* Status word written by the table / plan kernels (host-synchronising read). */
 int dc_huff_table_status(dc_ctx *ctx, const dc_dtable *d_table, int32_t *max_bits);
-/* (5) decode n symbols. d_words/bit_base and the sync index as written by pack. */
+/* (5) decode n symbols. d_words/bit_base and the sync index as written by pack. The
+ * decoder tables (dc_dtable dlut*) are rebuilt first unless this context's last pack built
+ * them for d_table; a table rewritten since by other means (another context, a copy) and
+ * not packed or rebuilt through this context is reported by dc_huff_decode_status as
+ * DC_E_STREAM (the decoder checks dec_ready), never decoded with stale tables. */
 int dc_huff_decode(dc_ctx *ctx, const uint32_t *d_words, uint64_t bit_base, uint64_t words,
                    const uint64_t *d_sync_base, const uint16_t *d_sync_len, uint32_t sync_syms,
                    uint64_t n, const dc_dtable *d_table, uint8_t *d_out);
@@ -195,7 +199,7 @@ int dc_huff_decode_dev(dc_ctx *ctx, const uint32_t *d_words, const uint64_t *d_b
 /* status of the last dc_huff_decode on this context (synchronising): 0 or DC_E_STREAM */
 int dc_huff_decode_status(dc_ctx *ctx);
 /* chunks of the last S = 64 dc_huff_decode on this context that took the exact redo (codes
- * longer than the 12-bit table, partial or over-long groups); synchronising, diagnostic */
+ * longer than the 15-bit table, partial or over-long groups); synchronising, diagnostic */
 int dc_huff_decode_redo_count(dc_ctx *ctx, uint64_t *count);
 /* base64url text (6 bits per char, MSB-first) of bits [bit_base, bit_base+bits) */
 int dc_huff_base64url(dc_ctx *ctx, const uint32_t *d_words, uint64_t bit_base, uint64_t bits,
