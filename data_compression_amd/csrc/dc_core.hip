@@ -3385,22 +3385,26 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
 // Small front-end (small_compression.c:507-665) and its inverse, stateless: each element's
 // output (0 or 1 byte encoding, 1 or 2 decoding) depends only on its byte and the bytes
 // beside it, so a tile needs only output counts, not the transducer compositions above.
-// Geometry: tiles of SM_TILE bytes on the 16-B address grid of the element bytes (element j
+// Geometry: tiles of SM_TILE bytes (per mode, SmMode::tile) on the 16-B address grid of the element bytes (element j
 // = byte j + FsmOff of `in`); step s of a tile = 1024 bytes, wave w = its 256-byte quarter,
 // lane = one dword (4 elements). A wave's elements are contiguous, so a lane's neighbour
 // bytes come from the lanes beside it (ds_bpermute) and only lanes 0 and 63 read a byte of
-// the next wave's dwords; all 16 dword loads of a lane are issued before any is used.
+// the next wave's dwords; all SM_STEPS dword loads of a lane are issued before any is used.
 // The writer stages the tile's output in LDS: lane t's bytes land at consecutive positions
 // ~4 t apart, so its byte stores spread over the banks (the transducer writer's lanes, 16
 // elements apart, hit each bank 4 times per instruction).
 // ------------------------------------------------------------------------------------
-#define SM_TILE 8192
-#define SM_STEPS (SM_TILE / 1024)
-
 template <int M> struct SmMode {
     static constexpr bool dec = (M == M_SMALL_DEC || M == M_SMALL_DBODY);
     static constexpr bool fast = (M == M_SMALL_ENC || M == M_SMALL_BODY0 || M == M_SMALL_BODY1 || dec);
+    // tile bytes: 16 KiB for the encoders (the count kernel: 0.238 -> 0.200 ms per GiB of C5
+    // text against 8 KiB; the writer equal), 8 KiB for decode (its writer stages up to 2 bytes
+    // per element: 33 KiB of LDS at 16 KiB, 4 workgroups per CU, 0.554 against 0.53 ms)
+    static constexpr uint32_t tile = dec ? 8192u : 16384u;
+    static constexpr int steps = (int)(tile / 1024);
 };
+#define SM_TILE (SmMode<M>::tile)   /* inside template <int M> code only */
+#define SM_STEPS (SmMode<M>::steps)
 
 // tile-relative bounds (uniform, 32-bit): tile byte u = A0 + tile * SM_TILE + u, u in [0, SM_TILE)
 struct SmTile {
@@ -3409,19 +3413,19 @@ struct SmTile {
     uint32_t two;          // u >= two <=> stream byte index >= 2 (a pair may end there)
     uint32_t nxt;          // u < nxt <=> the byte after u is inside the stream
 };
-static __device__ __forceinline__ uint32_t sm_clamp(int64_t v) { return (uint32_t)(v < 0 ? 0 : v > SM_TILE ? SM_TILE : v); }
-static __device__ __forceinline__ SmTile sm_tile(const uint8_t *in, int off, uint64_t nelem, uint64_t len, uint64_t tile)
+template <int M> static __device__ __forceinline__ uint32_t sm_clamp(int64_t v) { return (uint32_t)(v < 0 ? 0 : v > SM_TILE ? SM_TILE : v); }
+template <int M> static __device__ __forceinline__ SmTile sm_tile(const uint8_t *in, int off, uint64_t nelem, uint64_t len, uint64_t tile)
 {
     const int64_t lead = (int64_t)(((uintptr_t)in + (uintptr_t)off) & 15u);   // element 0's offset in its granule
     SmTile T;
     T.base = (int64_t)off - lead + (int64_t)(tile * SM_TILE);
-    T.lo = sm_clamp((int64_t)off - T.base);
-    T.hi = sm_clamp((int64_t)off + (int64_t)nelem - T.base);
-    T.two = sm_clamp(2 - T.base);
-    T.nxt = sm_clamp((int64_t)len - 1 - T.base);
+    T.lo = sm_clamp<M>((int64_t)off - T.base);
+    T.hi = sm_clamp<M>((int64_t)off + (int64_t)nelem - T.base);
+    T.two = sm_clamp<M>(2 - T.base);
+    T.nxt = sm_clamp<M>((int64_t)len - 1 - T.base);
     return T;
 }
-static uint64_t sm_ntiles(const uint8_t *in, int off, uint64_t nelem)
+template <int M> static uint64_t sm_ntiles(const uint8_t *in, int off, uint64_t nelem)
 {
     const uint64_t lead = ((uintptr_t)in + (uintptr_t)off) & 15u;
     return nelem ? (lead + nelem + SM_TILE - 1) / SM_TILE : 0;
@@ -3429,7 +3433,9 @@ static uint64_t sm_ntiles(const uint8_t *in, int off, uint64_t nelem)
 
 // output count (and, when OUT, the bytes written at stage[pos..]) of the 4 elements in a
 // lane's dword d at tile byte u; p / q = the bytes before / after the dword
-#define SM_TRASH (2 * SM_TILE + 32)   /* stage bytes [SM_TRASH, +256): a sink per lane for unwritten bytes */
+// stage bytes [sm_trash<M>, +256): a sink per lane for unwritten bytes (decode writes up to 2
+// bytes per element, encode at most 1)
+template <int M> constexpr uint32_t sm_trash() { return (SmMode<M>::dec ? 2 * SM_TILE : SM_TILE) + 32; }
 
 // SWAR byte tests on a dword (bit 7 of each byte = the test; the kernels are VALU-issue
 // bound, and one 32-bit op here tests 4 bytes: 31 VALU per byte per element rule before)
@@ -3483,7 +3489,7 @@ static __device__ __forceinline__ uint32_t sm_swar(uint32_t d, uint32_t p, uint3
 template <int M>
 static __device__ __forceinline__ void sm_store(uint32_t val, uint32_t keep, uint8_t *stage, uint32_t pos)
 {
-    const uint32_t sink = SM_TRASH + 4u * (threadIdx.x & 63);
+    const uint32_t sink = sm_trash<M>() + 4u * (threadIdx.x & 63);
     uint32_t c = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -3517,11 +3523,12 @@ static __device__ __forceinline__ void sm_load(const uint8_t *__restrict__ in, u
                      ? __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(in + o)) : 0u;
     }
 }
-struct SmEdge {
+template <int M> struct SmEdge {
     uint8_t first[SM_STEPS][4], last[SM_STEPS][4];   // each wave's first / last byte per step
     uint8_t before, after;                            // the bytes beside the tile
 };
-static __device__ __forceinline__ void sm_edges_put(SmEdge &E, const uint8_t *__restrict__ in, uint64_t len,
+template <int M>
+static __device__ __forceinline__ void sm_edges_put(SmEdge<M> &E, const uint8_t *__restrict__ in, uint64_t len,
                                                     const SmTile &T, int t, const uint32_t (&dv)[SM_STEPS])
 {
     const int lane = t & 63, w = t >> 6;
@@ -3537,7 +3544,8 @@ static __device__ __forceinline__ void sm_edges_put(SmEdge &E, const uint8_t *__
 }
 // bytes before / after the lane's dword at step st (after a barrier behind sm_edges_put):
 // x = before, y = after; branch-free (the wave-edge bytes are uniform broadcast reads)
-static __device__ __forceinline__ uint2 sm_nb(const SmEdge &E, uint32_t d, int st, int w, int lane)
+template <int M>
+static __device__ __forceinline__ uint2 sm_nb(const SmEdge<M> &E, uint32_t d, int st, int w, int lane)
 {
     const uint32_t pu = (uint32_t)__shfl_up((int)d, 1, 64) >> 24;
     const uint32_t qd = (uint32_t)__shfl_down((int)d, 1, 64) & 255u;
@@ -3553,20 +3561,20 @@ __global__ __launch_bounds__(256) void k_small_tiles(const uint8_t *__restrict__
                                                      uint4 *__restrict__ summ)
 {
     __shared__ uint32_t s_w[4];
-    __shared__ SmEdge E;
+    __shared__ SmEdge<M> E;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    const SmTile T = sm_tile(in, FsmOff<M>::v, nelem, len, blockIdx.x);
+    const SmTile T = sm_tile<M>(in, FsmOff<M>::v, nelem, len, blockIdx.x);
     uint32_t dv[SM_STEPS];
     sm_load<M>(in, len, T, w, lane, dv);
     if (!SmMode<M>::dec) {
-        sm_edges_put(E, in, len, T, t, dv);
+        sm_edges_put<M>(E, in, len, T, t, dv);
         __syncthreads();
     }
     uint32_t cnt = 0;
     const bool interior = T.lo == 0 && T.hi == SM_TILE && T.two == 0 && T.nxt == SM_TILE;
 #pragma unroll
     for (int st = 0; st < SM_STEPS; ++st) {
-        const uint2 nb = SmMode<M>::dec ? make_uint2(0u, 0u) : sm_nb(E, dv[st], st, w, lane);
+        const uint2 nb = SmMode<M>::dec ? make_uint2(0u, 0u) : sm_nb<M>(E, dv[st], st, w, lane);
         const uint32_t u = (uint32_t)(st * 1024 + w * 256 + lane * 4);
         uint32_t val, keep;
         cnt += interior ? sm_swar<M, true>(dv[st], nb.x, nb.y, u, T, val, keep)
@@ -3587,8 +3595,8 @@ __global__ __launch_bounds__(256) void k_small_write(const uint8_t *__restrict__
                                                      const uint64_t *__restrict__ meta, uint8_t *__restrict__ out)
 {
     __shared__ uint32_t s_w[SM_STEPS][4];
-    __shared__ SmEdge E;
-    __shared__ __attribute__((aligned(16))) uint8_t s_out[SM_TRASH + 256];
+    __shared__ SmEdge<M> E;
+    __shared__ __attribute__((aligned(16))) uint8_t s_out[sm_trash<M>() + 256];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const bool enc = M == M_SMALL_ENC;
     const uint64_t total = enc ? 2 + meta[0] : 1 + meta[0];
@@ -3602,18 +3610,18 @@ __global__ __launch_bounds__(256) void k_small_write(const uint8_t *__restrict__
         if (enc) { out[0] = 8; out[1] = in[0]; }
         else out[0] = in[1];
     }
-    const SmTile T = sm_tile(in, FsmOff<M>::v, nelem, len, blockIdx.x);
+    const SmTile T = sm_tile<M>(in, FsmOff<M>::v, nelem, len, blockIdx.x);
     uint32_t dv[SM_STEPS];
     sm_load<M>(in, len, T, w, lane, dv);
     if (!SmMode<M>::dec) {
-        sm_edges_put(E, in, len, T, t, dv);
+        sm_edges_put<M>(E, in, len, T, t, dv);
         __syncthreads();
     }
     uint32_t ex[SM_STEPS], kp[SM_STEPS];   // lane offset in its wave's part of step st; kept bytes
     const bool interior = T.lo == 0 && T.hi == SM_TILE && T.two == 0 && T.nxt == SM_TILE;
 #pragma unroll
     for (int st = 0; st < SM_STEPS; ++st) {
-        const uint2 nb = SmMode<M>::dec ? make_uint2(0u, 0u) : sm_nb(E, dv[st], st, w, lane);
+        const uint2 nb = SmMode<M>::dec ? make_uint2(0u, 0u) : sm_nb<M>(E, dv[st], st, w, lane);
         const uint32_t u = (uint32_t)(st * 1024 + w * 256 + lane * 4);
         uint32_t val, keep;
         const uint32_t c = interior ? sm_swar<M, true>(dv[st], nb.x, nb.y, u, T, val, keep)
@@ -4810,7 +4818,7 @@ static int fsm_run(dc_ctx *c, const uint8_t *d_in, uint64_t len, uint64_t nelem,
                    const char *name, FsmAux aux = FsmAux{nullptr, 0, 0, 1, 1}, uint64_t *h_plan = nullptr,
                    bool write = true)
 {
-    const uint64_t ntiles = SmMode<M>::fast ? sm_ntiles(d_in, FsmOff<M>::v, nelem) : (nelem + FSM_TILE - 1) / FSM_TILE;
+    const uint64_t ntiles = SmMode<M>::fast ? sm_ntiles<M>(d_in, FsmOff<M>::v, nelem) : (nelem + FSM_TILE - 1) / FSM_TILE;
     const uint64_t nt = ntiles ? ntiles : 1;
     const uint64_t ng = (nt + FSM_GROUP - 1) / FSM_GROUP;
     if (ensure((void **)&c->d_summ, &c->summ_cap, (nt + ng) * sizeof(uint4))) return DC_E_HIP;
@@ -4836,7 +4844,7 @@ static int fsm_run(dc_ctx *c, const uint8_t *d_in, uint64_t len, uint64_t nelem,
     if (write) {
         const uint64_t wgrid = ntiles ? ntiles : 1;
         if constexpr (SmMode<M>::fast)
-            LAUNCH(c, "small_write", k_small_write<M>, wgrid, 256, d_in, len, nelem, (const uint64_t *)c->d_entry,
+            LAUNCH(c, SmMode<M>::dec ? "small_dec_write" : "small_write", k_small_write<M>, wgrid, 256, d_in, len, nelem, (const uint64_t *)c->d_entry,
                    (const uint4 *)c->d_summ, (const uint64_t *)c->d_meta, d_out);
         else
             LAUNCH(c, "fsm_write", k_fsm_write<M>, wgrid, 256, d_in, len, nelem, (const uint64_t *)c->d_entry,
@@ -4862,9 +4870,9 @@ static int fsm_write_planned(dc_ctx *c, const uint8_t *d_in, uint64_t len, uint6
                              uint64_t *h_len, FsmAux aux = FsmAux{nullptr, 0, 0, 1, 1})
 {
     if (c->fsm_in != d_in || c->fsm_len != len || c->fsm_nelem != nelem || c->fsm_mode != M) return DC_E_STATE;
-    const uint64_t ntiles = SmMode<M>::fast ? sm_ntiles(d_in, FsmOff<M>::v, nelem) : (nelem + FSM_TILE - 1) / FSM_TILE;
+    const uint64_t ntiles = SmMode<M>::fast ? sm_ntiles<M>(d_in, FsmOff<M>::v, nelem) : (nelem + FSM_TILE - 1) / FSM_TILE;
     if constexpr (SmMode<M>::fast)
-        LAUNCH(c, "small_write", k_small_write<M>, ntiles ? ntiles : 1, 256, d_in, len, nelem,
+        LAUNCH(c, SmMode<M>::dec ? "small_dec_write" : "small_write", k_small_write<M>, ntiles ? ntiles : 1, 256, d_in, len, nelem,
                (const uint64_t *)c->d_entry, (const uint4 *)c->d_summ, (const uint64_t *)c->d_meta, d_out);
     else
         LAUNCH(c, "fsm_write", k_fsm_write<M>, ntiles ? ntiles : 1, 256, d_in, len, nelem, (const uint64_t *)c->d_entry,
