@@ -3390,9 +3390,7 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
 // lane = one dword (4 elements). A wave's elements are contiguous, so a lane's neighbour
 // bytes come from the lanes beside it (ds_bpermute) and only lanes 0 and 63 read a byte of
 // the next wave's dwords; all SM_STEPS dword loads of a lane are issued before any is used.
-// The writer stages the tile's output in LDS: lane t's bytes land at consecutive positions
-// ~4 t apart, so its byte stores spread over the banks (the transducer writer's lanes, 16
-// elements apart, hit each bank 4 times per instruction).
+// The writer (k_small_write) uses its own lane-contiguous geometry over the same tiles.
 // ------------------------------------------------------------------------------------
 template <int M> struct SmMode {
     static constexpr bool dec = (M == M_SMALL_DEC || M == M_SMALL_DBODY);
@@ -3402,6 +3400,9 @@ template <int M> struct SmMode {
     // per element: 33 KiB of LDS at 16 KiB, 4 workgroups per CU, 0.554 against 0.53 ms)
     static constexpr uint32_t tile = dec ? 8192u : 16384u;
     static constexpr int steps = (int)(tile / 1024);
+    // the writer's threads: 64 bytes per lane encoding, 32 decoding (measured against 32 / 64:
+    // encode 0.53 vs 0.59 ms, decode 0.45 vs 0.45)
+    static constexpr int wthreads = (int)(dec ? tile / 32 : tile / 64);
 };
 #define SM_TILE (SmMode<M>::tile)   /* inside template <int M> code only */
 #define SM_STEPS (SmMode<M>::steps)
@@ -3430,12 +3431,6 @@ template <int M> static uint64_t sm_ntiles(const uint8_t *in, int off, uint64_t 
     const uint64_t lead = ((uintptr_t)in + (uintptr_t)off) & 15u;
     return nelem ? (lead + nelem + SM_TILE - 1) / SM_TILE : 0;
 }
-
-// output count (and, when OUT, the bytes written at stage[pos..]) of the 4 elements in a
-// lane's dword d at tile byte u; p / q = the bytes before / after the dword
-// stage bytes [sm_trash<M>, +256): a sink per lane for unwritten bytes (decode writes up to 2
-// bytes per element, encode at most 1)
-template <int M> constexpr uint32_t sm_trash() { return (SmMode<M>::dec ? 2 * SM_TILE : SM_TILE) + 32; }
 
 // SWAR byte tests on a dword (bit 7 of each byte = the test; the kernels are VALU-issue
 // bound, and one 32-bit op here tests 4 bytes: 31 VALU per byte per element rule before)
@@ -3485,28 +3480,6 @@ static __device__ __forceinline__ uint32_t sm_swar(uint32_t d, uint32_t p, uint3
     return (uint32_t)__popc(keep);
 }
 
-// the output bytes of one dword, branch-free (bytes not written go to the lane's sink)
-template <int M>
-static __device__ __forceinline__ void sm_store(uint32_t val, uint32_t keep, uint8_t *stage, uint32_t pos)
-{
-    const uint32_t sink = sm_trash<M>() + 4u * (threadIdx.x & 63);
-    uint32_t c = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const uint32_t on = (keep >> (8 * k + 7)) & 1u;
-        const uint32_t v = (val >> (8 * k)) & 255u;
-        if (SmMode<M>::dec) {
-            const uint32_t two = v >> 7;
-            stage[on ? pos + c : sink] = (uint8_t)(two ? 0x20u : v);
-            stage[(on & two) ? pos + c + 1 : sink] = (uint8_t)(v & 0x7Fu);
-            c += on + (on & two);
-        } else {
-            stage[on ? pos + c : sink] = (uint8_t)v;
-            c += on;
-        }
-    }
-}
-
 // the lane's 16 dwords (step st: tile byte st * 1024 + w * 256 + 4 lane), all loads issued
 // before any is used; the bytes at the waves' edges go through LDS (SmEdge), with one byte
 // before and after the tile read from memory
@@ -3547,8 +3520,10 @@ static __device__ __forceinline__ void sm_edges_put(SmEdge<M> &E, const uint8_t 
 template <int M>
 static __device__ __forceinline__ uint2 sm_nb(const SmEdge<M> &E, uint32_t d, int st, int w, int lane)
 {
-    const uint32_t pu = (uint32_t)__shfl_up((int)d, 1, 64) >> 24;
-    const uint32_t qd = (uint32_t)__shfl_down((int)d, 1, 64) & 255u;
+    // the neighbour lanes' dwords by DPP wave shifts (VALU; the bpermutes they replace were a
+    // fifth of the writer's LDS instructions)
+    const uint32_t pu = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)d, 0x138, 0xf, 0xf, false) >> 24;   // wave_shr:1
+    const uint32_t qd = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)d, 0x130, 0xf, 0xf, false) & 255u;  // wave_shl:1
     const uint32_t pe = w > 0 ? E.last[st][w - 1] : st > 0 ? E.last[st - 1][3] : E.before;
     const uint32_t qe = w < 3 ? E.first[st][w + 1] : st + 1 < SM_STEPS ? E.first[st + 1][0] : E.after;
     return make_uint2(lane == 0 ? pe : pu, lane == 63 ? qe : qd);
@@ -3589,19 +3564,30 @@ __global__ __launch_bounds__(256) void k_small_tiles(const uint8_t *__restrict__
     }
 }
 
+// The writer: lane-contiguous geometry (unlike the count kernel's, whose tile totals are the
+// same): wave w owns bytes [w * WB, +WB) of the tile and lane l its LB contiguous bytes, so
+// a lane's output is one contiguous run. The lane packs its kept bytes into a 64-bit accumulator and ORs whole dwords into the zeroed LDS stage (ds_or_b32: the
+// dwords it shares with its neighbours' runs merge without ordering). One dword store per 4
+// output bytes instead of one byte store per element (per GiB of C5 text: decode 0.51 -> 0.45
+// ms; encode equal, 0.53).
 template <int M>
-__global__ __launch_bounds__(256) void k_small_write(const uint8_t *__restrict__ in, uint64_t len, uint64_t nelem,
+__global__ __launch_bounds__(SmMode<M>::wthreads) void k_small_write(const uint8_t *__restrict__ in, uint64_t len, uint64_t nelem,
                                                      const uint64_t *__restrict__ entry, const uint4 *__restrict__ loc,
                                                      const uint64_t *__restrict__ meta, uint8_t *__restrict__ out)
 {
-    __shared__ uint32_t s_w[SM_STEPS][4];
-    __shared__ SmEdge<M> E;
-    __shared__ __attribute__((aligned(16))) uint8_t s_out[sm_trash<M>() + 256];
+    constexpr bool dec = SmMode<M>::dec;
+    constexpr uint32_t NT = SmMode<M>::wthreads, NW = NT / 64;
+    constexpr uint32_t TILE = SM_TILE, WB = TILE / NW, LB = TILE / NT, LD = LB / 4;
+    constexpr uint32_t SW = ((dec ? 2 * TILE : TILE) + 32) / 4;   // stage dwords: output + lead + flush slack
+    static_assert(LB % 16 == 0 && SW % 4 == 0, "uint4 geometry");
+    __shared__ uint32_t s_w[NW];
+    __shared__ uint8_t s_first[NW], s_last[NW], s_before, s_after;
+    __shared__ __attribute__((aligned(16))) uint32_t s_out[SW];
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const bool enc = M == M_SMALL_ENC;
     const uint64_t total = enc ? 2 + meta[0] : 1 + meta[0];
     if (enc && total >= len) {   // LITERAL: ' ' + raw input (:655-662), one grid-stride pass
-        for (uint64_t i = (uint64_t)blockIdx.x * 256 + t; i < len; i += (uint64_t)gridDim.x * 256) out[1 + i] = in[i];
+        for (uint64_t i = (uint64_t)blockIdx.x * NT + t; i < len; i += (uint64_t)gridDim.x * NT) out[1 + i] = in[i];
         if (blockIdx.x == 0 && t == 0) out[0] = ' ';
         return;
     }
@@ -3611,57 +3597,104 @@ __global__ __launch_bounds__(256) void k_small_write(const uint8_t *__restrict__
         else out[0] = in[1];
     }
     const SmTile T = sm_tile<M>(in, FsmOff<M>::v, nelem, len, blockIdx.x);
-    uint32_t dv[SM_STEPS];
-    sm_load<M>(in, len, T, w, lane, dv);
-    if (!SmMode<M>::dec) {
-        sm_edges_put<M>(E, in, len, T, t, dv);
-        __syncthreads();
-    }
-    uint32_t ex[SM_STEPS], kp[SM_STEPS];   // lane offset in its wave's part of step st; kept bytes
-    const bool interior = T.lo == 0 && T.hi == SM_TILE && T.two == 0 && T.nxt == SM_TILE;
+    const uint32_t u0 = (uint32_t)w * WB + (uint32_t)lane * LB;   // the lane's first tile byte
+    uint32_t d[LD];
+    {
+        const uint32_t ulo = T.lo ? T.lo - 1 : 0, uhi = T.hi + 1;   // bytes the elements read
 #pragma unroll
-    for (int st = 0; st < SM_STEPS; ++st) {
-        const uint2 nb = SmMode<M>::dec ? make_uint2(0u, 0u) : sm_nb<M>(E, dv[st], st, w, lane);
-        const uint32_t u = (uint32_t)(st * 1024 + w * 256 + lane * 4);
-        uint32_t val, keep;
-        const uint32_t c = interior ? sm_swar<M, true>(dv[st], nb.x, nb.y, u, T, val, keep)
-                                    : sm_swar<M, false>(dv[st], nb.x, nb.y, u, T, val, keep);
-        dv[st] = val;   // encode: the output bytes (decode: the input bytes)
-        kp[st] = keep;
-        const uint32_t inc = wave_scan_incl(c);
-        ex[st] = inc - c;
-        if (lane == 63) s_w[st][w] = inc;
+        for (uint32_t k = 0; k < LD / 4; ++k) {
+            const uint32_t u = u0 + 16 * k;
+            const int64_t o = T.base + (int64_t)u;   // relative to in; in + T.base is 16-B aligned
+            const uint4 v = (u + 16 > ulo && u < uhi && o + 16 > 0 && o < (int64_t)len)
+                                ? ld_nt(reinterpret_cast<const uint4 *>(in + o)) : make_uint4(0u, 0u, 0u, 0u);
+            d[4 * k] = v.x; d[4 * k + 1] = v.y; d[4 * k + 2] = v.z; d[4 * k + 3] = v.w;
+        }
     }
+#pragma unroll
+    for (uint32_t k = 0; k < SW / 4 / NT + 1; ++k)   // zero the stage (ordered before the ORs by the barrier below)
+        if (t + NT * k < SW / 4) reinterpret_cast<uint4 *>(s_out)[t + NT * k] = make_uint4(0u, 0u, 0u, 0u);
+    uint32_t p = 0, q = 0;   // the bytes before / after the lane's run
+    if (!dec) {
+        if (lane == 0) s_first[w] = (uint8_t)d[0];
+        if (lane == 63) s_last[w] = (uint8_t)(d[LD - 1] >> 24);
+        if (t == 0) s_before = (T.base - 1 >= 0 && T.base - 1 < (int64_t)len) ? in[T.base - 1] : 0;
+        if (t == (int)NT - 1) s_after = (T.base + TILE >= 0 && T.base + TILE < (int64_t)len) ? in[T.base + TILE] : 0;
+        __syncthreads();
+        const uint32_t pu = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)d[LD - 1], 0x138, 0xf, 0xf, false) >> 24;   // wave_shr:1
+        const uint32_t qd = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)d[0], 0x130, 0xf, 0xf, false) & 255u;       // wave_shl:1
+        p = lane == 0 ? (w > 0 ? s_last[w - 1] : s_before) : pu;
+        q = lane == 63 ? (w + 1 < (int)NW ? s_first[w + 1] : s_after) : qd;
+    }
+    const bool interior = T.lo == 0 && T.hi == TILE && T.two == 0 && T.nxt == TILE;
+    auto swar = [&](uint32_t k, uint32_t &val, uint32_t &keep) -> uint32_t {
+        const uint32_t pk = k > 0 ? d[k - 1] >> 24 : p, qk = k + 1 < LD ? d[k + 1] & 255u : q;
+        const uint32_t u = u0 + 4 * k;
+        return interior ? sm_swar<M, true>(d[k], pk, qk, u, T, val, keep) : sm_swar<M, false>(d[k], pk, qk, u, T, val, keep);
+    };
+    uint32_t cnt = 0, vals[LD], keeps[LD];
+#pragma unroll
+    for (uint32_t k = 0; k < LD; ++k) cnt += swar(k, vals[k], keeps[k]);
+    const uint32_t incl = wave_scan_incl(cnt);
+    if (lane == 63) s_w[w] = incl;
     __syncthreads();
+    uint32_t pre = 0, run = 0;
+#pragma unroll
+    for (int x = 0; x < (int)NW; ++x) {
+        const uint32_t v = s_w[x];
+        pre += x < w ? v : 0u;
+        run += v;
+    }
     const uint64_t e = entry[blockIdx.x / FSM_GROUP];
     const uint64_t o_tile = (e >> 1) + loc[blockIdx.x].x + (headed ? (enc ? 2 : 1) : 0);   // first output byte
     const int64_t o_al = (int64_t)((((uintptr_t)(out + o_tile)) & ~(uintptr_t)15) - (uintptr_t)out);
     const uint32_t lead = (uint32_t)((int64_t)o_tile - o_al);   // stage offset of the tile's first byte
-    uint32_t run = 0;
+    {   // the lane's run: from stage byte P, packed 4 bytes to a dword
+        const uint32_t P = lead + pre + incl - cnt;
+        uint32_t di = P >> 2, nb = 8u * (P & 3u);
+        uint64_t acc = 0;
+        auto flush = [&]() {
+            if (nb >= 32u) {
+                atomicOr(&s_out[di], (uint32_t)acc);
+                acc >>= 32;
+                nb -= 32u;
+                ++di;
+            }
+        };
 #pragma unroll
-    for (int st = 0; st < SM_STEPS; ++st) {
-        uint32_t pre = run;
+        for (uint32_t k = 0; k < LD; ++k) {
+            const uint32_t val = vals[k], keep = keeps[k];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const uint32_t v = s_w[st][q];
-            pre += q < w ? v : 0u;
-            run += v;
+            for (int b = 0; b < 4; ++b) {
+                const uint32_t on = (keep >> (8 * b + 7)) & 1u, v = (val >> (8 * b)) & 255u;
+                if (dec) {   // >= 0x80: ' ' then the letter
+                    const uint32_t two = v >> 7;
+                    const uint32_t piece = two ? (0x20u | ((v & 0x7Fu) << 8)) : v;
+                    acc |= (uint64_t)(on ? piece : 0u) << nb;
+                    nb += on ? (two ? 16u : 8u) : 0u;
+                    if (b & 1) flush();   // <= 32 bits per 2 elements
+                } else {
+                    acc |= (uint64_t)(on ? v : 0u) << nb;
+                    nb += on ? 8u : 0u;
+                }
+            }
+            if (!dec) flush();   // <= 32 bits per dword
         }
-        sm_store<M>(dv[st], kp[st], s_out, lead + pre + ex[st]);
+        if (nb) atomicOr(&s_out[di], (uint32_t)acc);
     }
     __syncthreads();
     // store [o_tile, o_tile + run): whole granules as uint4, the first and last bytewise
+    const uint8_t *stage = reinterpret_cast<const uint8_t *>(s_out);
     const int64_t beg = (int64_t)o_tile, end = beg + (int64_t)run;
     if (end > beg) {
         const int64_t ng = (end - o_al + 15) / 16;
-        for (int64_t q = t; q < ng; q += 256) {
-            const int64_t b0 = o_al + 16 * q;
+        for (int64_t g = t; g < ng; g += NT) {
+            const int64_t b0 = o_al + 16 * g;
             if (b0 >= beg && b0 + 16 <= end) {
-                st_nt(reinterpret_cast<uint4 *>(out + b0), *reinterpret_cast<const uint4 *>(s_out + 16 * q));
+                st_nt(reinterpret_cast<uint4 *>(out + b0), *reinterpret_cast<const uint4 *>(stage + 16 * g));
             } else {
                 for (int k = 0; k < 16; ++k) {
                     const int64_t bq = b0 + k;
-                    if (bq >= beg && bq < end) out[bq] = s_out[16 * q + k];
+                    if (bq >= beg && bq < end) out[bq] = stage[16 * g + k];
                 }
             }
         }
@@ -4844,7 +4877,7 @@ static int fsm_run(dc_ctx *c, const uint8_t *d_in, uint64_t len, uint64_t nelem,
     if (write) {
         const uint64_t wgrid = ntiles ? ntiles : 1;
         if constexpr (SmMode<M>::fast)
-            LAUNCH(c, SmMode<M>::dec ? "small_dec_write" : "small_write", k_small_write<M>, wgrid, 256, d_in, len, nelem, (const uint64_t *)c->d_entry,
+            LAUNCH(c, SmMode<M>::dec ? "small_dec_write" : "small_write", k_small_write<M>, wgrid, SmMode<M>::wthreads, d_in, len, nelem, (const uint64_t *)c->d_entry,
                    (const uint4 *)c->d_summ, (const uint64_t *)c->d_meta, d_out);
         else
             LAUNCH(c, "fsm_write", k_fsm_write<M>, wgrid, 256, d_in, len, nelem, (const uint64_t *)c->d_entry,
@@ -4872,7 +4905,7 @@ static int fsm_write_planned(dc_ctx *c, const uint8_t *d_in, uint64_t len, uint6
     if (c->fsm_in != d_in || c->fsm_len != len || c->fsm_nelem != nelem || c->fsm_mode != M) return DC_E_STATE;
     const uint64_t ntiles = SmMode<M>::fast ? sm_ntiles<M>(d_in, FsmOff<M>::v, nelem) : (nelem + FSM_TILE - 1) / FSM_TILE;
     if constexpr (SmMode<M>::fast)
-        LAUNCH(c, SmMode<M>::dec ? "small_dec_write" : "small_write", k_small_write<M>, ntiles ? ntiles : 1, 256, d_in, len, nelem,
+        LAUNCH(c, SmMode<M>::dec ? "small_dec_write" : "small_write", k_small_write<M>, ntiles ? ntiles : 1, SmMode<M>::wthreads, d_in, len, nelem,
                (const uint64_t *)c->d_entry, (const uint4 *)c->d_summ, (const uint64_t *)c->d_meta, d_out);
     else
         LAUNCH(c, "fsm_write", k_fsm_write<M>, ntiles ? ntiles : 1, 256, d_in, len, nelem, (const uint64_t *)c->d_entry,
