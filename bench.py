@@ -51,7 +51,7 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--table-mode", default="replicate", choices=["replicate", "broadcast"],
                     help="multi-GPU code table: built on every rank, or on rank 0 and broadcast")
-    ap.add_argument("--profile-steps", type=int, default=5)
+    ap.add_argument("--profile-steps", type=int, default=20)
     return ap.parse_args()
 
 
@@ -150,7 +150,8 @@ def main():
         ok = bool(okt.item())
 
     # ---- encode / decode split and per-kernel HIP-event durations ------------------------
-    def timed(fn, k):
+    def timed(fn, k):   # host-timed calls, one untimed call first (the stage switch)
+        fn()
         torch.cuda.synchronize()
         t = time.perf_counter()
         for _ in range(k):
