@@ -57,13 +57,21 @@ def parse():
 
 def main():
     a = parse()
+    if os.environ.get("DC_BENCH_TRACE_AFTER"):   # diagnosis of a stuck rank: Python stacks, then exit
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ["DC_BENCH_TRACE_AFTER"]), exit=True)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # ranks beyond the visible GPUs share them (a rehearsal of the multi-rank path on a
+    # smaller box; one rank per GPU otherwise)
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        # RCCL; DC_BENCH_BACKEND=gloo rehearses the multi-rank path with ranks sharing a GPU
+        # (RCCL refuses two ranks on one device)
+        backend = os.environ.get("DC_BENCH_BACKEND", "nccl")
+        dist.init_process_group(backend, **({"device_id": dev} if backend == "nccl" else {}))
 
     from data_compression_amd import synth
     from data_compression_amd.device import Codec
