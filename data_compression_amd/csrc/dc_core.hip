@@ -82,17 +82,12 @@ static __device__ __forceinline__ uint32_t wg_scan_excl_u32(uint32_t v, uint32_t
 template <int PF>   // full blocks whose loads are in flight ahead of the one being counted
 __global__ __launch_bounds__(256) void k_hist_blocks(const uint8_t *__restrict__ in, uint64_t n,
                                                      uint64_t nblocks, uint16_t *__restrict__ bh,
-                                                     uint64_t *__restrict__ hist, uint32_t *__restrict__ hflag,
-                                                     uint32_t gen)
+                                                     uint64_t *__restrict__ hist, uint64_t *__restrict__ hacc,
+                                                     uint32_t *__restrict__ hdone)
 {
     __shared__ __attribute__((aligned(16))) uint32_t cnt[256 * 64];
+    __shared__ uint32_t s_last;
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-    if (blockIdx.x == 0) {   // hist[] zeroed here, not by a memset launch; *hflag = gen says so
-        hist[t] = 0ull;
-        __threadfence();
-        __syncthreads();
-        if (t == 0) __hip_atomic_store(hflag, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    }
     const uint32_t inc = 1u << (8 * wv);
     const uint32_t lane4 = 4u * (uint32_t)lane;
     char *const cbase = reinterpret_cast<char *>(cnt);
@@ -175,13 +170,20 @@ __global__ __launch_bounds__(256) void k_hist_blocks(const uint8_t *__restrict__
         total += acc;
         __syncthreads();
     }
-    // this workgroup's bin totals straight into hist[] (zeroed by workgroup 0 at its start,
-    // long before any workgroup gets here; all 512 are resident): 512 u64 atomics per bin at
-    // the end, no reduce launch (A/B r1 v14: step 1.379 -> 1.368 ms)
-    if (t == 0)
-        while (__hip_atomic_load(hflag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != gen) __builtin_amdgcn_s_sleep(2);
+    // this workgroup's bin totals into the context's accumulator (zero at every launch), and
+    // the last workgroup out moves it to hist[] and zeroes it for the next launch: no memset
+    // or reduce launch, and no workgroup waits on another (a workgroup-0 reset that the
+    // others waited for assumed all of the grid resident, which ranks sharing a GPU broke)
+    if (total) atomicAdd(reinterpret_cast<unsigned long long *>(&hacc[t]), total);
+    __threadfence();
     __syncthreads();
-    if (total) atomicAdd(reinterpret_cast<unsigned long long *>(&hist[t]), total);
+    if (t == 0) s_last = atomicAdd(hdone, 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (s_last) {
+        __threadfence();
+        hist[t] = atomicExch(reinterpret_cast<unsigned long long *>(&hacc[t]), 0ull);
+        if (t == 0) atomicExch(hdone, 0u);
+    }
 }
 
 // ------------------------------------------------------------------------------------
@@ -4237,7 +4239,7 @@ struct dc_ctx {
     uint32_t opt_d8_static;       // decoder: static share of the tuples, percent (0..100)
     uint32_t opt_decode_general;  // 1: always the general decoder (k_huff_decode)
     uint32_t opt_hist_pf;         // histogram: blocks of loads in flight ahead (1..2, 0 = default 2)
-    uint32_t *d_hflag, gen_h;     // histogram zeroed by its workgroup 0 (flag = this call's generation)
+    uint32_t *d_hflag;            // histogram accumulator (256 u64) + done counter, zero between launches
     uint32_t opt_decode_variant;  // fast decoder: 0 one code per lookup (k_huff_decode8), 1 up to 3 (k_huff_decode9)
     uint32_t opt_adec_v1;         // adaptive nybble decode: 1 = the one-pass k_nyb_adec (A/B)
     // timing
@@ -4318,7 +4320,7 @@ static int ctx_create(dc_ctx **out, int device, void *stream, bool own)
         return DC_E_HIP;
     }
     c->d_errd = c->d_errp + 128;
-    if (hipMalloc((void **)&c->d_hflag, 64) != hipSuccess || hipMemset(c->d_hflag, 0, 64) != hipSuccess) {
+    if (hipMalloc((void **)&c->d_hflag, 4096) != hipSuccess || hipMemset(c->d_hflag, 0, 4096) != hipSuccess) {
         free(c);
         return DC_E_HIP;
     }
@@ -4489,10 +4491,11 @@ int dc_huff_hist(dc_ctx *c, const uint8_t *d_in, uint64_t n, uint64_t *d_hist)
     const uint64_t grid = nb < hmax ? nb : hmax;   // 512: 2 resident per CU (64 KiB LDS each)
     // two blocks of loads in flight ahead (with nt loads; same-box A/B in the 1 GiB C2 step:
     // 0.176 ms against 0.179 with one; before the nt loads one was best, 0.1995 vs 0.2022 ms)
-    if (++c->gen_h == 0) c->gen_h = 1;
+    uint64_t *const hacc = reinterpret_cast<uint64_t *>(c->d_hflag);
+    uint32_t *const hdone = c->d_hflag + 512;
     if (c->opt_hist_pf == 1)
-        LAUNCH(c, "hist_blocks", k_hist_blocks<1>, grid, 256, d_in, n, nb, c->d_bh, d_hist, c->d_hflag, c->gen_h);
-    else LAUNCH(c, "hist_blocks", k_hist_blocks<2>, grid, 256, d_in, n, nb, c->d_bh, d_hist, c->d_hflag, c->gen_h);
+        LAUNCH(c, "hist_blocks", k_hist_blocks<1>, grid, 256, d_in, n, nb, c->d_bh, d_hist, hacc, hdone);
+    else LAUNCH(c, "hist_blocks", k_hist_blocks<2>, grid, 256, d_in, n, nb, c->d_bh, d_hist, hacc, hdone);
     return DC_OK;
 }
 
