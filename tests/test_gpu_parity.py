@@ -935,3 +935,24 @@ def test_histogram_running_counters_skewed(torch_cuda, codec):
         x[::4099] = torch.arange(256, device="cuda", dtype=torch.int64).repeat(n // 4099 // 256 + 1)[: x[::4099].numel()].to(torch.uint8)
         h = codec.hist(x)
         assert torch.equal(h, torch.bincount(x.to(torch.int64), minlength=256)), (n, fill)
+
+
+@pytest.mark.gpu
+def test_histogram_grids_and_repeats(torch_cuda):
+    """The bins go through a per-context accumulator that the last workgroup out empties:
+    any grid (1 workgroup, a few, more than the input's blocks), launches back to back on
+    one context, a sub-block input in between, two contexts interleaved."""
+    torch = torch_cuda
+    from data_compression_amd.device import Codec
+    from data_compression_amd import synth
+    a, b = Codec(0), Codec(0)
+    xs = [torch.from_numpy(synth.enwik_like((5 << 20) + 77, seed=s)).cuda() for s in (1, 2)]
+    ref = [torch.bincount(x.to(torch.int64), minlength=256) for x in xs]
+    tiny = xs[1][:100]   # under one block
+    for grid in (1, 3, 64, 0):   # 0: the default grid
+        a.set_option("hist_grid", grid)
+        for k in range(3):
+            assert torch.equal(a.hist(xs[k & 1]), ref[k & 1]), (grid, k)
+            assert torch.equal(b.hist(xs[(k + 1) & 1]), ref[(k + 1) & 1]), (grid, k)
+        assert torch.equal(a.hist(tiny), torch.bincount(tiny.to(torch.int64), minlength=256)), grid
+        assert torch.equal(a.hist(xs[0]), ref[0]), grid
