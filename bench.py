@@ -39,8 +39,8 @@ METRIC = "GB/s encode+decode on 1 GiB byte stream at 1/2/4/8 MI355X; % HBM roofl
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=50)   # ~1 ms each: amortises the bracketing syncs
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--cfg", default="C2")
     ap.add_argument("--frontend", action="store_true",
                     help="C5 pipeline: small_compression.c front-end, then n-ary Huffman (dist.ShardedSmall)")
