@@ -174,14 +174,26 @@ __global__ __launch_bounds__(256) void k_hist_blocks(const uint8_t *__restrict__
     // the last workgroup out moves it to hist[] and zeroes it for the next launch: no memset
     // or reduce launch, and no workgroup waits on another (a workgroup-0 reset that the
     // others waited for assumed all of the grid resident, which ranks sharing a GPU broke)
-    // (Device-scope atomics are performed past the XCDs' L2s; the workgroup waits for its
-    // own to be acknowledged before it counts itself done. Same-box A/B on 1 GiB: 0.224 ms
-    // against 0.218-0.221 for the workgroup-0 reset, 0.228-0.237 with a __threadfence here,
-    // which also writes back the XCD's L2.)
+    // The hand-off is the agent-scope release/acquire pair (cdna_hip_programming.md §6
+    // Guideline 16, counter form): every thread's accumulator atomic drained, a barrier, ONE
+    // release fence by thread 0 before the ticket, and in the last workgroup ONE acquire
+    // fence before it reads the accumulator. (r2 used the drain alone: it relied on the
+    // device-scope atomics being performed past the XCDs' L2s, which the memory model does
+    // not promise; a __threadfence in every thread cost 2-5% of the kernel.)
     if (total) atomicAdd(reinterpret_cast<unsigned long long *>(&hacc[t]), total);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (t == 0) s_last = atomicAdd(hdone, 1u) == gridDim.x - 1;
+    if (t == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // keep: the fence's own wait may be dropped
+        const bool last = __hip_atomic_fetch_add(hdone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                          gridDim.x - 1;
+        if (last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        s_last = last;
+    }
     __syncthreads();
     if (s_last) {
         hist[t] = atomicExch(reinterpret_cast<unsigned long long *>(&hacc[t]), 0ull);
@@ -1778,6 +1790,103 @@ static __device__ __forceinline__ void d8_batch(const uint32_t *const *st, uint3
     }
 }
 
+// Register window of a chain (DC_D8_QWIN, the default): 2 stage qwords q0:q1 in VGPRs and
+// the window's bit position qb in them (0..63). A batch's 64-bit window is a funnel shift of
+// q0:q1 (no stage read on the chain); the qword after q1 is read at the batch start, while
+// the 4 lookups run, and when the batch's codes carry qb past 64 it moves in (q0 <- q1 <- it)
+// by selects. One ds_read_b64 per batch where the r2 batch read 3 words at random banks
+// (0.75 LDS reads per symbol, ~5.2 LDS cycles per symbol with their ~3.5-way conflicts:
+// about 40% of the kernel's LDS cycles, profiles/r2k_pmc.txt). (An exec-masked read only
+// where a lane needs it measured worse in code: the compiler waited for it inside the branch
+// and the 16 unrolled branches cost 168 VGPRs with spills.)
+#ifndef DC_D8_QWIN
+#define DC_D8_QWIN 1
+#endif
+template <int NC>
+struct D8Win {
+    uint64_t q0[NC], q1[NC];
+    uint32_t qb[NC], qp[NC];   // bit position in q0:q1, index of the qword after q1
+};
+
+// chain start at stage bit P (a row of 64-bit words, 8-B aligned): the window starts one bit
+// early (d8_batch's bias), i.e. at P' - 64 with P' = P + 63: q0 = qword P'/64 - 1, which for
+// P < 1 is the 8 bytes before the row (LDS in bounds: the previous row's tail, or the
+// scheduler word and padding before the first row; a don't-care bit)
+template <int NC>
+static __device__ __forceinline__ void d8_win_init(D8Win<NC> &w, const uint64_t *const *st, const uint32_t *P)
+{
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+        const uint32_t p = P[j] + 63u, a = p >> 6;
+        w.q0[j] = st[j][(int)a - 1];
+        w.q1[j] = st[j][a];
+        w.qb[j] = p & 63u;
+        w.qp[j] = a + 1;
+    }
+}
+
+template <int NC>
+static __device__ __forceinline__ void d8_batch_q(const uint64_t *const *st, D8Win<NC> &w, uint32_t *o,
+                                                  const uint16_t *__restrict__ lut, uint32_t *mn)
+{
+    uint64_t win[NC], nx[NC];
+    uint32_t off[NC];
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+        nx[j] = st[j][w.qp[j]];   // in flight during the lookups
+        const uint32_t W0 = (uint32_t)w.q0[j], W1 = (uint32_t)(w.q0[j] >> 32);
+        const uint32_t W2 = (uint32_t)w.q1[j], W3 = (uint32_t)(w.q1[j] >> 32);
+        const bool k = w.qb[j] >= 32u;
+        const uint32_t A = k ? W1 : W0, B = k ? W2 : W1, Cw = k ? W3 : W2;
+        win[j] = ((uint64_t)__builtin_amdgcn_alignbit(Cw, B, w.qb[j]) << 32) | __builtin_amdgcn_alignbit(B, A, w.qb[j]);
+        off[j] = 0;
+    }
+    const char *const lb = reinterpret_cast<const char *>(lut);
+    constexpr uint32_t SEL[4] = {0x0c0c0c05u, 0x0c0c0500u, 0x0c050100u, 0x05020100u};
+    uint32_t e[NC][4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+#pragma unroll
+        for (int j = 0; j < NC; ++j) {
+            const uint32_t x = (uint32_t)(win[j] >> (off[j] & 63u));
+            e[j][k] = *reinterpret_cast<const uint16_t *>(lb + (x & ((2u << D8_LUT_BITS) - 2u)));
+            o[j] = __builtin_amdgcn_perm(e[j][k], k ? o[j] : 0u, SEL[k]);
+            off[j] += e[j][k];
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+        mn[j] = min(mn[j], min(min(e[j][0], e[j][1]), min(e[j][2], e[j][3])));
+        // a batch takes <= 60 bits (4 codes of <= 15), so qb < 124: one qword at most
+        const uint32_t qb = w.qb[j] + (off[j] & 255u);
+        const bool r = qb >= 64u;
+        w.q0[j] = r ? w.q1[j] : w.q0[j];
+        w.q1[j] = r ? nx[j] : w.q1[j];
+        w.qp[j] += r ? 1u : 0u;
+        w.qb[j] = qb & 63u;
+    }
+}
+
+template <int NC, int Q>
+struct D8PiecesQ {
+    static __device__ __forceinline__ void run(const uint64_t *const *st, D8Win<NC> &w, uint32_t (*o)[16],
+                                               const uint16_t *__restrict__ lut, uint32_t *mn)
+    {
+        uint32_t b[NC];
+        d8_batch_q<NC>(st, w, b, lut, mn);
+#pragma unroll
+        for (int j = 0; j < NC; ++j) o[j][Q] = b[j];
+        D8PiecesQ<NC, Q + 1>::run(st, w, o, lut, mn);
+    }
+};
+template <int NC>
+struct D8PiecesQ<NC, 16> {
+    static __device__ __forceinline__ void run(const uint64_t *const *, D8Win<NC> &, uint32_t (*)[16],
+                                               const uint16_t *__restrict__, uint32_t *)
+    {
+    }
+};
+
 // The 16 batches of a 64-symbol chunk (4 pieces of 16 B per lane), unrolled by template
 // recursion; the pieces stay in registers until the chunk is done.
 template <int NC, int Q>
@@ -2021,6 +2130,28 @@ static __device__ __forceinline__ void d8_stage(const D8Geo<NC> &cur, const uint
     }
 }
 
+// A fast decoder that finds its tables stale (dec_ready 0: the table was rewritten since
+// they were built) reports a stream error and decodes nothing. The launches after it must
+// then find nothing to redo: workgroup 0 zeroes the redo counter, every workgroup zeroes its
+// grid-stride share of the groups' redo masks, and every wave still counts itself out of the
+// scheduler (the last one out resets the dequeue heads), so the next decode on this context
+// starts clean even when only some workgroups took this exit.
+static __device__ void d8_stale_exit(int *__restrict__ err, uint32_t *__restrict__ queue,
+                                     uint64_t *__restrict__ fix_mask, uint64_t n, int nw)
+{
+    const int t = threadIdx.x;
+    if (t == 0) atomicOr(err, 1);
+    if (blockIdx.x == 0 && t == 0) queue[D8_FIX_CNT] = 0u;
+    const uint64_t ngroups = ((n + 63) / 64 + DC_SYNC_GROUP - 1) / DC_SYNC_GROUP;
+    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + t; g < ngroups; g += (uint64_t)gridDim.x * blockDim.x)
+        fix_mask[g] = 0ull;
+    if ((t & 63) == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        if (atomicAdd(queue + 8 * D8_QSTRIDE, 1u) == gridDim.x * (uint32_t)nw - 1)
+            for (int h = 0; h <= 8; ++h) atomicExch(queue + h * D8_QSTRIDE, 0u);
+    }
+}
+
 // NW waves per workgroup (one workgroup per CU), NC chains per wave: wave w of workgroup b
 // decodes the NC consecutive groups of "tuple" b*NW + w (+ grid stride), lane = chunk.
 template <int NW, int NC>
@@ -2038,7 +2169,8 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode8(const uint32_t *__rest
     constexpr int NT = NW * 64;
     __shared__ Dec8Lds L;
     if (!__hip_atomic_load(&T->dec_ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {   // tables rebuilt since
-        if (threadIdx.x == 0) atomicOr(err, 1);
+        // reported as a stream error; the redo launches that follow must find nothing to do
+        d8_stale_exit(err, queue, fix_mask, n, NW);
         return;
     }
     if (d_base) bit_base += *d_base;   // device-resident shard offset (dist: no host read)
@@ -2110,6 +2242,10 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode8(const uint32_t *__rest
     uint32_t *stw[NC];
 #pragma unroll
     for (int j = 0; j < NC; ++j) { stw[j] = L.stage[wv * NC + j]; st[j] = stw[j]; }
+    const uint64_t *st64[NC];
+#pragma unroll
+    for (int j = 0; j < NC; ++j) st64[j] = reinterpret_cast<const uint64_t *>(stw[j]);
+    (void)st64;
     const uint32_t stride = gridDim.x * NW;
     // Software pipeline (per wave, one tuple of NC groups per iteration): while tuple i
     // decodes, the spans of tuple i+1 are in flight into registers and the sync index of
@@ -2187,6 +2323,15 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode8(const uint32_t *__rest
         for (int j = 0; j < NC; ++j)
 #pragma unroll
             for (int q = 0; q < 16; ++q) o[j][q] = c[j] + q;
+#elif DC_D8_QWIN
+        {
+            uint32_t P[NC];
+#pragma unroll
+            for (int j = 0; j < NC; ++j) P[j] = c[j] - 31u;   // the chunk's stage bit
+            D8Win<NC> wq;
+            d8_win_init<NC>(wq, st64, P);
+            D8PiecesQ<NC, 0>::run(st64, wq, o, L.lut, mn);
+        }
 #else
         D8Pieces<NC, 0>::run(st, c, o, L.lut, mn);
 #endif
@@ -2298,7 +2443,7 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode9(const uint32_t *__rest
     constexpr uint32_t MB = (1u << DC_MULTI_BITS) - 1;
     __shared__ Dec9Lds<NW> L;
     if (!__hip_atomic_load(&T->dec_ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {   // tables rebuilt since
-        if (threadIdx.x == 0) atomicOr(err, 1);
+        d8_stale_exit(err, queue, fix_mask, n, NW);
         return;
     }
     if (d_base) bit_base += *d_base;   // device-resident shard offset (dist: no host read)
@@ -2655,7 +2800,9 @@ __global__ __launch_bounds__(D8F_WAVES * 64) void k_huff_decode8_fix(const uint3
         const uint32_t chc = chunk_of(ra + 2 * wstride);
         const uint64_t posc = fix_pos[chc != ~0u ? chc : 0u];
         // decode round A
-        const bool valid = cha != ~0u;
+        // (a listed chunk is < nchunks by construction; the clamp keeps a corrupt list from
+        // writing past the output)
+        const bool valid = cha != ~0u && (uint64_t)cha * S < n;
         const uint64_t s0 = (uint64_t)(valid ? cha : 0u) * S;
         const uint32_t cntc = valid ? (uint32_t)((n - s0 < S) ? n - s0 : S) : 0u;
         uint32_t c = (uint32_t)(posa - (a0 << 5));

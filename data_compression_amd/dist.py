@@ -130,12 +130,18 @@ class ShardedHuffman:
 
     def finalize(self, s: ShardStream):
         """Host values of the bit offset and payload bit count (one host read) if encode()
-        left them on the device."""
+        left them on the device, and the pack's outcome: with the offset on the device, a
+        preallocated `words` too small for bit_base % 32 + bits (size it with
+        words_needed(31, bits)) makes the kernels write nothing, which is raised here
+        rather than gathered as an empty stream."""
         if s.totals is not None:
             tv = s.totals.cpu().tolist()
             s.bit_base, s.bits, s.totals = int(sum(tv[: self.rank])), int(tv[self.rank]), None
         elif s.bits < 0:
             s.bits = int(self.e.plan_total())
+        st = self.e.pack_status(s.table)
+        if st != 0:
+            raise RuntimeError(f"rank {self.rank}: pack failed with status {st} (dc_huff_pack_status)")
         return s
 
     def decode(self, s: ShardStream, out=None):

@@ -511,6 +511,39 @@ def test_decode_error_slots_and_stale_tables(torch_cuda, codec):
 
 
 @pytest.mark.parametrize("variant", [0, 1])
+def test_decode_stale_tables_after_larger_decode(torch_cuda, variant):
+    """a decode that finds its tables stale must leave the redo stage
+    nothing to do. A large decode with many redo chunks first (its redo counter and masks
+    stay behind), then a much smaller stream whose table was rebuilt by another context:
+    reported, and nothing written past the smaller output (guard bytes intact); the next
+    decodes on the context are exact again."""
+    torch = torch_cuda
+    from data_compression_amd import synth
+    from data_compression_amd.device import Codec
+    c = Codec(0)
+    other = Codec(0)
+    c.set_option("decode_variant", variant)
+    big = torch.from_numpy(_chain_stream(20, 5)).cuda()   # codes past the 15-bit table: many redo chunks
+    enc = c.encode(big, n_ary=2, sync_syms=64)
+    out = torch.empty_like(big)
+    c.decode_into(enc, out)
+    assert c.decode_status() == 0 and torch.equal(out, big)
+    assert variant == 1 or c.decode_redo_count() > 0
+    small = torch.from_numpy(synth.enwik_like(70_001, seed=33)).cuda()
+    enc_s = c.encode(small, n_ary=2, sync_syms=64)
+    other.table(other.hist(torch.from_numpy(synth.uniform_bytes(4096, seed=4)).cuda()), 2, out=enc_s["table"])
+    guard = torch.full((small.numel() + 4096,), 0xA5, dtype=torch.uint8, device=small.device)
+    c.decode_into(enc_s, guard[: small.numel()])
+    assert c.decode_status() != 0
+    assert bool((guard[small.numel():] == 0xA5).all()), "stale-table decode wrote past its output"
+    for x in (small, big):
+        e = c.encode(x, n_ary=2, sync_syms=64)
+        o = torch.empty_like(x)
+        c.decode_into(e, o)
+        assert c.decode_status() == 0 and torch.equal(o, x)
+
+
+@pytest.mark.parametrize("variant", [0, 1])
 def test_decode_variants(torch_cuda, codec, variant):
     """The fast decoder's variants (0: one code per 15-bit lookup; 1: up to 3 per 13-bit
     lookup) on text, Zipf and flat bytes at n = 2, 3, 16, ragged sizes: exact round trips."""
