@@ -49,19 +49,28 @@ def parse():
     ap.add_argument("--sync", type=int, default=0, help="sync-index granularity (0 = default)")
     ap.add_argument("--cpu-sample", type=int, default=256 << 20)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--table-mode", default="replicate", choices=["replicate", "broadcast"],
-                    help="multi-GPU code table: built on every rank, or on rank 0 and broadcast")
+    ap.add_argument("--table-mode", default=None, choices=["replicate", "broadcast"],
+                    help="multi-GPU code table: built on rank 0 and broadcast over RCCL (the default at "
+                         "N > 1, north_star's 'RCCL broadcast of the shared code table'), or built on every rank")
+    ap.add_argument("--gather-reps", type=int, default=5,
+                    help="N > 1: timed gathers of the whole stream to rank 0 after the timed region")
     ap.add_argument("--profile-steps", type=int, default=20)
+    ap.add_argument("--codec", default="huffman", choices=["huffman", "nybble"],
+                    help="nybble: nybble_compression.c's codec on 1 GiB of English-like text (--mode)")
+    ap.add_argument("--mode", default="static", choices=["static", "adaptive"],
+                    help="nybble: static (compress_bytestring modify=false: encode + decode per step) or adaptive "
+                         "(nybble_compress: encode per step; the sequential decode timed on a sample)")
     return ap.parse_args()
 
 
 def main():
     a = parse()
-    if os.environ.get("DC_BENCH_TRACE_AFTER"):   # diagnosis of a stuck rank: Python stacks, then exit
-        import faulthandler
-        faulthandler.dump_traceback_later(float(os.environ["DC_BENCH_TRACE_AFTER"]), exit=True)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    if a.table_mode is None:
+        a.table_mode = "broadcast" if world > 1 else "replicate"
+    _trace_setup(rank)
+    _phase(rank, "start")
     # ranks beyond the visible GPUs share them (a rehearsal of the multi-rank path on a
     # smaller box; one rank per GPU otherwise)
     local = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
@@ -76,9 +85,13 @@ def main():
     from data_compression_amd import synth
     from data_compression_amd.device import Codec
 
+    if a.codec == "nybble":
+        return main_nybble(a, dev, rank, world)
     n = a.size
-    x = synth.device_text(a.cfg, n, seed=0xC2 + 7919 * rank, device=dev)
+    _phase(rank, "device up")
+    x = synth.device_text(a.cfg, n, seed=input_seed(a.cfg, rank), device=dev)
     torch.cuda.synchronize()
+    _phase(rank, "input generated")
     c = Codec(local)   # launches on torch's current stream
     # sync granularity: chosen once from this stream's planned payload (outside the timed
     # region), as the encoder would for a stream of these statistics (dc_huff_choose_sync)
@@ -122,9 +135,11 @@ def main():
         encode()
         decode()
 
+    _phase(rank, "buffers ready")
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
+    _phase(rank, "warmup done")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -140,6 +155,7 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
     ms_step = el / a.steps * 1e3
+    _phase(rank, "timed steps done")
 
     # ---- correctness of the measured configuration (outside the timed region) ----------
     st = c.pack_status(state["s"].table if a.frontend else tab)
@@ -156,6 +172,37 @@ def main():
         okt = torch.tensor([1 if ok else 0], device=dev)
         dist.all_reduce(okt, op=dist.ReduceOp.MIN)
         ok = bool(okt.item())
+
+    # ---- N > 1: the gather of the whole stream to rank 0 (end-to-end GB/s
+    # beside the codec-only value), timed separately, outside the codec's timed region --------
+    gather = None
+    if world > 1 and not a.frontend and a.gather_reps > 0:
+        s_enc = state["s"]
+        sh.gather(s_enc)   # untimed first call: host finalize, buffer allocation
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        tg = time.perf_counter()
+        for _ in range(a.gather_reps):
+            g = sh.gather(s_enc)
+        torch.cuda.synchronize()
+        dist.barrier()
+        gel = time.perf_counter() - tg
+        gt = torch.tensor([gel], dtype=torch.float64, device=dev)
+        dist.all_reduce(gt, op=dist.ReduceOp.MAX)
+        gather_ms = float(gt.item()) / a.gather_reps * 1e3
+        # the merged stream holds every rank's payload bits (after finalize, s_enc.bits is this rank's)
+        allbits = torch.tensor([s_enc.bits], dtype=torch.int64, device=dev)
+        dist.all_reduce(allbits)
+        ok_g = g is not None and int(g[1]) == int(allbits.item()) if rank == 0 else g is None
+        okg = torch.tensor([1 if ok_g else 0], device=dev)
+        dist.all_reduce(okg, op=dist.ReduceOp.MIN)
+        gather = {"gather_ms": round(gather_ms, 4), "reps": a.gather_reps,
+                  "e2e_GBps": round(world * n / ((ms_step + gather_ms) * 1e-3) / 1e9, 2),
+                  "bytes_to_rank0": None, "ok": bool(okg.item())}
+        if rank == 0 and g is not None:
+            gather["bytes_to_rank0"] = int(g[0].numel() * 4 + g[2].numel() * 8 + g[3].numel() * 2)
+        _phase(rank, "gather timed")
 
     # ---- encode / decode split and per-kernel HIP-event durations ------------------------
     def timed(fn, k):   # host-timed calls, one untimed call first (the stage switch)
@@ -237,12 +284,211 @@ def main():
         "kernels": kernels,
         "roundtrip_ok": ok,
     }
+    if world > 1:
+        res["table_mode"] = a.table_mode
+        if gather is not None:
+            res["gather"] = gather
     if rank == 0 and world == 1 and not a.no_cpu:
         res["cpu_baseline"] = cpu_baseline(x, a)
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+NYB_METRIC = "GB/s nybble encode+decode on 1 GiB byte stream per MI355X; % HBM roofline"
+
+
+def main_nybble(a, dev, rank, world):
+    """nybble_compression.c's codec as a bench line: 1 GiB of the C1
+    English-like text generator per GPU, device-resident. A step = the whole codec call(s),
+    each ending in its host read of the output length (the reference API returns the length):
+      static   compress_bytestring(modify=false) + decompress_bytestring of its output
+      adaptive nybble_compress (modify=true); its decode is sequential by definition (each
+               byte's list depends on every byte before it), timed once on a 16 MiB sample
+    N > 1: every rank codes its own 1 GiB stream (independent objects, no collective)."""
+    from data_compression_amd import synth
+    from data_compression_amd.device import Codec
+    n = a.size
+    modify = a.mode == "adaptive"
+    x = synth.device_text("C1", n, seed=0xC1 + 7919 * rank, device=dev)
+    torch.cuda.synchronize()
+    c = Codec(dev.index or 0)
+    comp_buf = torch.empty(n + 2, dtype=torch.uint8, device=dev)
+    out = torch.empty(2 * n + 16, dtype=torch.uint8, device=dev)
+    st = {}
+
+    def encode():
+        st["comp"] = c.nyb_compress(x, modify, out=comp_buf)
+
+    def decode():
+        st["y"] = c.nyb_decompress(st["comp"], modify, out=out)
+
+    def step():
+        encode()
+        if not modify:
+            decode()
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+    ms_step = el / a.steps * 1e3
+    m = st["comp"].numel()
+
+    def timed(fn, k):
+        fn()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(k):
+            fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t) / k * 1e3
+
+    enc_ms = timed(encode, a.profile_steps)
+    if modify:   # the sequential whole-stream decode, on a sample; the round trip of that sample
+        xs = x[: 16 << 20]
+        cs = c.nyb_compress(xs, True)
+        ys = c.nyb_decompress(cs, True)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        ys = c.nyb_decompress(cs, True)
+        torch.cuda.synchronize()
+        dec_sample_ms = (time.perf_counter() - t) * 1e3
+        ok = bool(torch.equal(ys, xs))
+        dec_ms = None
+    else:
+        dec_ms = timed(decode, a.profile_steps)
+        ok = bool(torch.equal(st["y"], x))
+    c.timing(True)
+    for _ in range(a.profile_steps):
+        step()
+    kt = c.timings()
+    c.timing(False)
+    per = {}
+    for name, ms in kt:
+        per.setdefault(name, []).append(ms)
+    # SURVEY §8(d), nybble: N + N_comp each way; the plan (tiles) passes read one side
+    alg = {"nyb_enc_tiles": n, "nyb_enca_tiles": n, "nyb_enc_write": n + m, "nyb_dec_tiles": m,
+           "nyb_dec_write": m + n, "mtf_tiles": n, "mtf_ranks": 2 * n}
+    kernels = {}
+    for name, v in per.items():
+        mm = float(np.mean(v))
+        e = {"ms": round(mm, 4), "launches_per_step": len(v) // a.profile_steps}
+        if name in alg:
+            e["GBps"] = round(alg[name] / (mm * 1e-3) / 1e9, 1)
+        kernels[name] = e
+    dom = max(per, key=lambda k: float(np.sum(per[k])))
+    dom_ms = float(np.mean(per[dom]))
+    dom_bytes = alg.get(dom, n)
+    achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
+    wl = f"C1-nyb-{a.mode}"
+    traffic, traffic_src = pmc_traffic("k_" + dom, argparse.Namespace(cfg=wl, nary=0), n)
+    kern_sum = sum(float(np.sum(v)) for v in per.values()) / a.profile_steps
+    enc_frac = (n + m) / (enc_ms * 1e-3) / HBM_PEAK
+    res = {
+        "metric": NYB_METRIC if not modify else NYB_METRIC.replace("encode+decode", "encode"),
+        "value": round(world * n / (ms_step * 1e-3) / 1e9, 2),
+        "unit": "GB/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "u8", "data": "synthetic",
+        "config": {"workload": f"nybble {'adaptive (nybble_compress)' if modify else 'static (compress_bytestring)'}"
+                               f" on {n >> 20} MiB of C1 English-like text per GPU"
+                               + ("; encode per step (decode: sequential, decode_sample)" if modify else
+                                  "; encode + decode per step"),
+                   "codec": "nybble", "mode": a.mode, "bytes_per_gpu": n,
+                   "parallelism": f"replica{world}" if world > 1 else "single"},
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK / 1e9,
+                     "unit": "GB/s", "frac": round(achieved * 1e9 / HBM_PEAK, 4), "traffic": traffic,
+                     "traffic_source": traffic_src, "alg_bytes_per_launch": dom_bytes, "mean_ms": round(dom_ms, 4),
+                     "encode_frac": round(enc_frac, 4), "encode_ms": round(enc_ms, 4),
+                     "kernel_sum_ms_per_step": round(kern_sum, 4), "pipeline_alg_bytes": n + m},
+        "encode_GBps": round(n / (enc_ms * 1e-3) / 1e9, 2),
+        "ratio": round(m / n, 4),
+        "kernels": kernels,
+        "roundtrip_ok": ok,
+    }
+    if dec_ms is not None:
+        res["roofline"].update({"decode_frac": round((m + n) / (dec_ms * 1e-3) / HBM_PEAK, 4),
+                                "decode_ms": round(dec_ms, 4)})
+        res["decode_GBps"] = round(n / (dec_ms * 1e-3) / 1e9, 2)
+    else:
+        res["decode_sample"] = {"bytes": 16 << 20, "ms": round(dec_sample_ms, 2),
+                                "MBps": round((16 << 20) / (dec_sample_ms * 1e-3) / 1e6, 1),
+                                "path": "tokens (parallel transducer) + k_nyb_resolve (one wave)"}
+    if rank == 0 and world == 1 and not a.no_cpu:
+        res["cpu_baseline"] = cpu_baseline_nybble(x, a, modify)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline_nybble(x, a, modify):
+    """The oracle's nybble codec (oracle/dc_oracle.c, nybble_compression.c restated) on one
+    pinned host core: a bounded sample of the same stream, encode + decode."""
+    from oracle import oracle as orc
+    m = min(a.cpu_sample, x.numel()) if not modify else min(a.cpu_sample, 64 << 20, x.numel())
+    s = x[:m].cpu().numpy().tobytes()
+    old = os.sched_getaffinity(0)
+    core = min(old)
+    os.sched_setaffinity(0, {core})
+    try:
+        t0 = time.perf_counter()
+        comp = orc.nybble_compress(s, modify)
+        t1 = time.perf_counter()
+        back = orc.nybble_decompress(comp, modify)
+        t2 = time.perf_counter()
+    finally:
+        os.sched_setaffinity(0, old)
+    assert back == s
+    r = _cpu_report(m, t0, t1, t2, core, f"nybble {'adaptive' if modify else 'static'}, ")
+    r["encode_GBps"] = round(m / (t1 - t0) / 1e9, 4)
+    r["decode_GBps"] = round(m / (t2 - t1) / 1e9, 4)
+    return r
+
+
+def input_seed(cfg, rank):
+    """Seed of rank r's synthetic shard (C4 is seeded 0xC4 + rank; the other
+    configs keep the r2 seeds, 0xC2 + 7919 r, which the committed profiles were measured on)."""
+    return 0xC4 + rank if cfg == "C4" else 0xC2 + 7919 * rank
+
+
+_T0 = time.perf_counter()
+
+
+def _phase(rank, what):
+    """DC_BENCH_PHASES=1: a timestamped progress line per rank on stderr (multi-rank
+    rehearsals: where each rank is when one stalls)."""
+    if os.environ.get("DC_BENCH_PHASES"):
+        sys.stderr.write(f"[rank {rank}] {time.perf_counter() - _T0:8.2f} s  {what}\n")
+        sys.stderr.flush()
+
+
+def _trace_setup(rank):
+    """DC_BENCH_TRACE_AFTER=T: every rank writes its Python stacks every T seconds to
+    gpurun_out/trace_rank<r>.log and keeps running (none exits first, so a stall leaves
+    the stacks of all ranks, not just of the one whose timer fired)."""
+    t = os.environ.get("DC_BENCH_TRACE_AFTER")
+    if not t:
+        return
+    import faulthandler
+    os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
+    f = open(os.path.join(REPO, "gpurun_out", f"trace_rank{rank}.log"), "w")
+    _trace_setup.f = f   # keep the file open for the process's lifetime
+    faulthandler.dump_traceback_later(float(t), repeat=True, file=f, exit=False)
 
 
 def _pos_checksum(t, off):

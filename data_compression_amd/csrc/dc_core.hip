@@ -79,14 +79,33 @@ static __device__ __forceinline__ uint32_t wg_scan_excl_u32(uint32_t v, uint32_t
 // so an 8-bit counter cannot overflow. Reduction reads and clears with a rotated column
 // index so it is conflict free as well.
 // ------------------------------------------------------------------------------------
+struct TblLds;
+static __device__ void huff_table_body(TblLds &S, const uint64_t *__restrict__ freq, int freq_is_hist256,
+                                       const int32_t *__restrict__ lens_in, int M, int nary,
+                                       dc_dtable *__restrict__ T, dc_tree *__restrict__ tree,
+                                       const uint64_t *plan_hist, uint64_t *__restrict__ d_total,
+                                       int *__restrict__ perr, int *__restrict__ perr_next);
+
+// The table build of a fused launch (HistFuse.T set): the last workgroup out, which holds the
+// final histogram, builds the code table and the encode plan total right away (no table
+// launch, no plan launch: dc_huff_encode_plan)
+struct HistFuse {
+    dc_dtable *T;          // nullptr: histogram only
+    int M, nary;
+    uint64_t *d_total;     // payload bits of this input under the new code
+    int *perr, *perr_next; // plan error slot of this call, and the next one (cleared)
+};
+
 template <int PF>   // full blocks whose loads are in flight ahead of the one being counted
 __global__ __launch_bounds__(256) void k_hist_blocks(const uint8_t *__restrict__ in, uint64_t n,
                                                      uint64_t nblocks, uint16_t *__restrict__ bh,
                                                      uint64_t *__restrict__ hist, uint64_t *__restrict__ hacc,
-                                                     uint32_t *__restrict__ hdone)
+                                                     uint32_t *__restrict__ hdone, uint64_t *__restrict__ hloc,
+                                                     HistFuse fuse)
 {
     __shared__ __attribute__((aligned(16))) uint32_t cnt[256 * 64];
     __shared__ uint32_t s_last;
+    __shared__ uint64_t s_h[256];
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const uint32_t inc = 1u << (8 * wv);
     const uint32_t lane4 = 4u * (uint32_t)lane;
@@ -196,8 +215,16 @@ __global__ __launch_bounds__(256) void k_hist_blocks(const uint8_t *__restrict__
     }
     __syncthreads();
     if (s_last) {
-        hist[t] = atomicExch(reinterpret_cast<unsigned long long *>(&hacc[t]), 0ull);
+        const uint64_t hv = atomicExch(reinterpret_cast<unsigned long long *>(&hacc[t]), 0ull);
+        hist[t] = hv;
+        hloc[t] = hv;   // this context's own histogram (hist[] may be all-reduced in place later)
         if (t == 0) atomicExch(hdone, 0u);
+        if (fuse.T) {   // the counters are free now: their LDS holds the table build
+            s_h[t] = hv;
+            __syncthreads();
+            huff_table_body(*reinterpret_cast<TblLds *>(cnt), s_h, 1, nullptr, fuse.M, fuse.nary, fuse.T, nullptr,
+                            s_h, fuse.d_total, fuse.perr, fuse.perr_next);
+        }
     }
 }
 
@@ -241,22 +268,45 @@ extern "C" int dc_diag_tbl_read(void *h)
 #define TBL_SORT_MAX 2048
 #define TBL_NODES 4096
 
-__global__ __launch_bounds__(256) void k_huff_table(const uint64_t *__restrict__ freq, int freq_is_hist256,
-                                                    const int32_t *__restrict__ lens_in, int M, int nary,
-                                                    dc_dtable *__restrict__ T, dc_tree *__restrict__ tree)
+struct TblLds {   // k_huff_table's LDS (also carved from k_hist_blocks' counters by its last workgroup)
+    __attribute__((aligned(16))) uint64_t key[TBL_SORT_MAX];
+    uint64_t q2[TBL_SORT_MAX];
+    int16_t parent[TBL_NODES];
+    int32_t len[DC_MAX_SYMS];
+    __attribute__((aligned(16))) uint32_t cnt[DC_MAX_DIGITS + 2];   // also the merge's 64-key window
+    uint32_t startv[DC_MAX_DIGITS + 2];
+    uint32_t starti[DC_MAX_DIGITS + 2];
+    uint32_t code[256];
+    uint32_t nb[256];
+    int k, mn, mx, maxbits, bad;
+    uint32_t rbase[DC_MAX_DIGITS + 1];
+    uint32_t wcnt[4][DC_MAX_DIGITS + 1];
+    uint64_t red[4];
+};
+static_assert(sizeof(TblLds) <= 256 * 64 * sizeof(uint32_t), "k_hist_blocks' last workgroup builds the table in its counters' LDS");
+
+// The table of k_huff_table, by one 256-thread workgroup on the LDS S. With d_total set it
+// also writes the encode plan of plan_hist (the histogram of the bytes to be packed): the
+// payload bits sum_s plan_hist[s] * nbits[s] (the reference's formula, n_ary_huffman.c:2485)
+// and the plan error flag (a byte present without a code), and clears the next plan's slot.
+static __device__ void huff_table_body(TblLds &S, const uint64_t *__restrict__ freq, int freq_is_hist256,
+                                       const int32_t *__restrict__ lens_in, int M, int nary,
+                                       dc_dtable *__restrict__ T, dc_tree *__restrict__ tree,
+                                       const uint64_t *plan_hist, uint64_t *__restrict__ d_total,
+                                       int *__restrict__ perr, int *__restrict__ perr_next)
 {
-    __shared__ __attribute__((aligned(16))) uint64_t s_key[TBL_SORT_MAX];
-    __shared__ uint64_t s_q2[TBL_SORT_MAX];
-    __shared__ int16_t s_parent[TBL_NODES];
-    __shared__ int32_t s_len[DC_MAX_SYMS];
-    __shared__ __attribute__((aligned(16))) uint32_t s_cnt[DC_MAX_DIGITS + 2];   // also the merge's 64-key window
-    __shared__ uint32_t s_startv[DC_MAX_DIGITS + 2];
-    __shared__ uint32_t s_starti[DC_MAX_DIGITS + 2];
-    __shared__ uint32_t s_code[256];
-    __shared__ uint32_t s_nb[256];
-    __shared__ int s_k, s_min, s_max, s_maxbits, s_bad;
-    __shared__ uint32_t s_rbase[DC_MAX_DIGITS + 1];
-    __shared__ uint32_t s_wcnt[4][DC_MAX_DIGITS + 1];
+    uint64_t *const s_key = S.key;
+    uint64_t *const s_q2 = S.q2;
+    int16_t *const s_parent = S.parent;
+    int32_t *const s_len = S.len;
+    uint32_t *const s_cnt = S.cnt;
+    uint32_t *const s_startv = S.startv;
+    uint32_t *const s_starti = S.starti;
+    uint32_t *const s_code = S.code;
+    uint32_t *const s_nb = S.nb;
+    int &s_k = S.k, &s_min = S.mn, &s_max = S.mx, &s_maxbits = S.maxbits, &s_bad = S.bad;
+    uint32_t *const s_rbase = S.rbase;
+    uint32_t (*const s_wcnt)[DC_MAX_DIGITS + 1] = S.wcnt;
 
     const int t = threadIdx.x;
     const int leaves = M + 1;
@@ -631,6 +681,55 @@ __global__ __launch_bounds__(256) void k_huff_table(const uint64_t *__restrict__
         T->dec_ready = 0;   // the decoder tables follow (k_huff_pack's builder, or k_dec_tables)
         T->status = s_bad ? DC_E_ARG : (s_maxbits > 32 ? DC_E_CODE_TOO_LONG : DC_OK);
     }
+    if (d_total) {   // the plan: payload bits of plan_hist under this code, missing codes
+        const uint64_t h = plan_hist[t];
+        const uint32_t nb = s_nb[t];
+        uint64_t v = h * nb;
+        const bool miss = h != 0 && nb == 0;
+#pragma unroll
+        for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, 64);
+        const bool anymiss = __syncthreads_or(miss);
+        if ((t & 63) == 0) S.red[t >> 6] = v;
+        __syncthreads();
+        if (t == 0) {
+            *d_total = S.red[0] + S.red[1] + S.red[2] + S.red[3];
+            perr[0] = anymiss ? 1 : 0;
+        }
+        if (t < 4) perr_next[t] = 0;   // the next plan's error slot
+    }
+}
+
+__global__ __launch_bounds__(256) void k_huff_table(const uint64_t *__restrict__ freq, int freq_is_hist256,
+                                                    const int32_t *__restrict__ lens_in, int M, int nary,
+                                                    dc_dtable *__restrict__ T, dc_tree *__restrict__ tree,
+                                                    const uint64_t *__restrict__ plan_hist, uint64_t *__restrict__ d_total,
+                                                    int *__restrict__ perr, int *__restrict__ perr_next)
+{
+    __shared__ TblLds S;
+    huff_table_body(S, freq, freq_is_hist256, lens_in, M, nary, T, tree, plan_hist, d_total, perr, perr_next);
+}
+
+// dc_huff_plan: the encode plan of this context's last histogram under a table built elsewhere
+// (the multi-rank paths: the table comes from the all-reduced or broadcast histogram)
+__global__ __launch_bounds__(256) void k_plan_total(const uint64_t *__restrict__ plan_hist, const dc_dtable *__restrict__ T,
+                                                    uint64_t *__restrict__ d_total, int *__restrict__ perr,
+                                                    int *__restrict__ perr_next)
+{
+    __shared__ uint64_t red[4];
+    const int t = threadIdx.x;
+    const uint64_t h = plan_hist[t];
+    const uint32_t nb = T->nbits[t];
+    uint64_t v = h * nb;
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, 64);
+    const bool anymiss = __syncthreads_or(h != 0 && nb == 0);
+    if ((t & 63) == 0) red[t >> 6] = v;
+    __syncthreads();
+    if (t == 0) {
+        *d_total = red[0] + red[1] + red[2] + red[3];
+        perr[0] = anymiss ? 1 : 0;
+    }
+    if (t < 4) perr_next[t] = 0;
 }
 
 // ------------------------------------------------------------------------------------
@@ -988,25 +1087,6 @@ __global__ __launch_bounds__(256) void k_block_final_wide(const uint32_t *__rest
     }
 }
 
-// zero every word that two blocks share (the words holding a block start) before
-// k_huff_pack OR-merges into them
-__global__ void k_zero_bounds(const uint64_t *__restrict__ off, uint64_t nblocks, uint64_t bit_base,
-                              const uint64_t *__restrict__ d_base,
-                              uint32_t *__restrict__ words, uint64_t words_cap, int *__restrict__ err)
-{
-    const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (d_base) bit_base += *d_base;   // device-resident shard offset (dist: no host read)
-    if (b > nblocks || err[0] != 0) return;
-    if (((bit_base & 31) + off[nblocks] + 31) / 32 > words_cap) {
-        if (b == 0) err[2] = 1;
-        return;
-    }
-    const uint64_t abs = bit_base + off[b];
-    if (b == nblocks && (abs & 31) == 0) return;
-    words[(abs >> 5) - (bit_base >> 5)] = 0u;
-}
-
-
 // ------------------------------------------------------------------------------------
 // (H7) pack. One workgroup per 32 KiB block (grid-stride), 8 tiles of 4 KiB; a lane
 // codes 16 bytes (one 16-B load). Per tile: LDS table lookups -> workgroup scan of bit
@@ -1028,13 +1108,117 @@ static __device__ __forceinline__ void lds_barrier()
 #define PACK_BLK_WORDS 9216     /* 36 KiB: a full block of <= 9 bits/symbol is staged whole  */
 #define PACK_PIECES (DC_BLOCK_BYTES / PACK_TILE)
 
+// Block offsets inside the pack (no plan launches): decoupled look-back over the blocks. A
+// block's bit count comes from its histogram row (bh . nbits, the reference's own payload
+// formula, n_ary_huffman.c:2485) before its bytes have even arrived, so it is published at
+// once; wave 0 then reads up to 64 predecessors' flags per step until it meets an inclusive
+// prefix. Flag = value (46 bits) | epoch (16) | state (2: 1 aggregate, 2 inclusive prefix),
+// one 64-bit agent-scope atomic (no separate payload to order); the epoch (a per-context
+// launch count) tells this launch's flags from older ones, so the flags are never cleared
+// (dc_ctx resets them when the epoch wraps). Blocks wait only on blocks of lower index,
+// which were dispatched earlier (a workgroup's second block waits on blocks whose
+// workgroups are resident or done), so the waits end.
+#define LB_VALUE_BITS 46
+#define LB_FLAG(epoch, state, value) ((uint64_t)(value) | ((uint64_t)(epoch) << LB_VALUE_BITS) | ((uint64_t)(state) << 62))
+static __device__ __noinline__ uint64_t pack_lookback(uint64_t *__restrict__ flags, uint64_t p, uint64_t agg,
+                                                      uint32_t epoch, int lane)
+{
+    // flags per claimed PAIR of blocks; one step reads 256 predecessors (4 per lane, in flight
+    // together): at ~55 claims per us and ~2 us per agent-scope round trip, a 64-flag window
+    // covered 1.2 us of claims, less than the time its own round trip took, so look-backs
+    // rarely met an inclusive prefix and chained (1 GiB C2 pack 0.60 ms, against 0.376 with
+    // the plan launches)
+    constexpr uint64_t VMASK = (1ull << LB_VALUE_BITS) - 1;
+    constexpr int W = 4;
+    if (lane == 0)
+        __hip_atomic_store(&flags[p], LB_FLAG(epoch, p == 0 ? 2u : 1u, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint64_t excl = 0;
+    int64_t base = (int64_t)p - 1;   // the nearest predecessor not yet summed
+    while (base >= 0) {
+        uint64_t v[W];
+#pragma unroll
+        for (int j = 0; j < W; ++j) {
+            const int64_t i = base - 64 * j - lane;
+            v[j] = i >= 0 ? __hip_atomic_load(&flags[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                          : LB_FLAG(epoch, 2u, 0u);
+        }
+        bool done = false, wait = false;
+#pragma unroll
+        for (int j = 0; j < W; ++j) {
+            if (done || wait) break;
+            const uint32_t st = ((uint32_t)(v[j] >> LB_VALUE_BITS) & 0xFFFFu) == epoch ? (uint32_t)(v[j] >> 62) : 0u;
+            const uint64_t inc = __ballot(st == 2u), none = __ballot(st == 0u);
+            const int fi = inc ? __builtin_ctzll(inc) : 64, fn = none ? __builtin_ctzll(none) : 64;
+            const int upto = fn < fi ? fn : (fi < 64 ? fi + 1 : 64);   // lanes whose values count
+            uint64_t x = lane < upto ? (v[j] & VMASK) : 0ull;
+#pragma unroll
+            for (int d = 32; d > 0; d >>= 1) x += __shfl_xor(x, d, 64);
+            excl += x;
+            base -= upto;
+            done = fi < 64 && fi < fn;   // met an inclusive prefix
+            wait = !done && fn < 64;     // a predecessor has not published yet: re-read from it
+        }
+        if (done) break;
+        if (wait) __builtin_amdgcn_s_sleep(1);
+    }
+    if (lane == 0 && p > 0)
+        __hip_atomic_store(&flags[p], LB_FLAG(epoch, 2u, excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return excl;
+}
+
+// The offsets of a claimed pair of blocks (wave 0; out of line so that its registers are not
+// added to the block loop's): both blocks' bit counts from their histogram rows, the pair's
+// aggregate published at once (the next pairs' look-backs never wait on a whole block), its
+// offset by the look-back; lane 0 writes the blocks' offsets and bit counts to LDS
+static __device__ __noinline__ void pack_pair_offset(const uint16_t *__restrict__ bh, const uint8_t *nb8, uint64_t pair,
+                                                     uint64_t nblocks, uint64_t *__restrict__ flags, uint32_t epoch,
+                                                     int lane, uint64_t *excl2, uint64_t *bits2)
+{
+    const uint64_t b = 2 * pair;
+    const bool two = b + 1 < nblocks;
+    uint32_t agg[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const uint64_t bq = (q && two) ? b + 1 : b;
+        const uint2 h = *reinterpret_cast<const uint2 *>(bh + bq * 256 + lane * 4);
+        const uint32_t a = (h.x & 0xFFFFu) * nb8[4 * lane] + (h.x >> 16) * nb8[4 * lane + 1] +
+                           (h.y & 0xFFFFu) * nb8[4 * lane + 2] + (h.y >> 16) * nb8[4 * lane + 3];
+        agg[q] = (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_incl(a), 63);   // <= 2^20 per block
+    }
+    if (!two) agg[1] = 0;
+    const uint64_t ex = pack_lookback(flags, pair, (uint64_t)agg[0] + agg[1], epoch, lane);
+    if (lane == 0) {
+        excl2[0] = ex;
+        excl2[1] = ex + agg[0];
+        bits2[0] = agg[0];
+        bits2[1] = agg[1];
+    }
+}
+
+// A word two blocks share (the block boundary falls inside it): each side ORs its bits into
+// the boundary's slot with its side mark (1: the earlier block's tail, 2: the later block's
+// head); the side that arrives second finds the other's mark, writes the merged word and
+// clears the slot for the next launch. No zeroing launch and no OR into HBM.
+static __device__ __forceinline__ void pack_exchange(uint64_t *slot, uint32_t bits, uint32_t side, uint32_t *dst)
+{
+    const unsigned long long old =
+        atomicOr(reinterpret_cast<unsigned long long *>(slot), ((unsigned long long)side << 32) | bits);
+    if ((uint32_t)(old >> 32) & (3u ^ side)) {
+        *dst = bswap32(bits | (uint32_t)old);
+        atomicExch(reinterpret_cast<unsigned long long *>(slot), 0ull);
+    }
+}
+
 __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ in, uint64_t n,
                                                    const dc_dtable *__restrict__ T,
-                                                   const uint64_t *__restrict__ block_off, uint64_t bit_base,
+                                                   const uint16_t *__restrict__ bh, const uint64_t *__restrict__ d_total,
+                                                   uint64_t bit_base,
                                                    const uint64_t *__restrict__ d_base, uint32_t *__restrict__ out, uint64_t *__restrict__ sync_base,
                                                    uint16_t *__restrict__ sync_len, uint32_t sync_syms,
                                                    uint64_t nblocks, uint64_t words_cap,
-                                                   const int *__restrict__ err, int build_dec)
+                                                   int *__restrict__ err, int build_dec,
+                                                   uint64_t *__restrict__ lb_flags, uint32_t epoch,
+                                                   uint64_t *__restrict__ xslot, uint32_t *__restrict__ claim)
 {
     __shared__ uint2 s_tab[256];
     // bit lengths alone (pass A reads 1 byte, not 8): 64 dwords, so at most 2 distinct dwords
@@ -1046,8 +1230,12 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
     __shared__ __attribute__((aligned(16))) uint32_t s_stage[PACK_BLK_WORDS + 4];   // +4: emit's no-op ORs past the end
     __shared__ uint32_t s_scan[4];
     __shared__ uint32_t s_tot[PACK_PIECES][4];
+    __shared__ uint64_t s_excl2[2], s_bits2[2];   // the claimed blocks' offsets (look-back) and bit counts
+    __shared__ uint32_t s_pair;           // the claimed pair of blocks
     static_assert(sizeof(DecBuildLds) <= sizeof(s_stage), "decoder-table builder uses the stage");
     const int t = threadIdx.x;
+    // the claim counter of the next launch (they alternate by epoch; this one started at 0)
+    if (blockIdx.x == 0 && t == 0) claim[(epoch + 1) & 1] = 0u;
     if (build_dec && blockIdx.x == 0) {   // workgroup 0: the decoder tables, beside the pack
         if (T->status == DC_OK)
             dec_tables_build(const_cast<dc_dtable *>(T), *reinterpret_cast<DecBuildLds *>(s_stage));
@@ -1057,7 +1245,12 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
     if (d_base) bit_base += *d_base;   // device-resident shard offset (dist: no host read)
     // device-side guards (no host round trip): a byte without a code (plan error) or an
     // output buffer smaller than the planned stream -> write nothing
-    if (err[0] != 0 || ((bit_base & 31) + block_off[nblocks] + 31) / 32 > words_cap) return;
+    const uint64_t total = *d_total;
+    if (err[0] != 0) return;
+    if (((bit_base & 31) + total + 31) / 32 > words_cap) {
+        if (t == 0) err[2] = 1;   // (pack status: DC_E_CAPACITY)
+        return;
+    }
     s_tab[t] = make_uint2(T->code[t], T->nbits[t]);
     s_nb8[t] = (uint8_t)T->nbits[t];
     const bool vec_out = ((uintptr_t)out & 15) == 0;
@@ -1066,7 +1259,10 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
     // quarter mode (uniform): above 5.5 bits per symbol on average a fair share of 8-code
     // halves exceed 64 bits, and a wave with one such lane ran both the half and the quarter
     // path; such streams (e.g. C4's Zipf bytes, 6.25) code every half as two quarters
-    const bool qmode = 2 * block_off[nblocks] > 11 * n;
+    const bool qmode = 2 * total > 11 * n;
+    // the stage is all zero at every block start (each block zeroes what it used)
+    for (uint32_t i = 4u * t; i < PACK_BLK_WORDS + 4; i += 1024u)
+        *reinterpret_cast<uint4 *>(&s_stage[i]) = make_uint4(0u, 0u, 0u, 0u);
     __syncthreads();
     if (T->fixed8 && vec_out && (bit_base & 127) == 0) {
         // every code 8 bits: stream byte bit_base / 8 + i = code(in[i]) (bit_base % 128 == 0: the
@@ -1095,6 +1291,9 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
             } else {
                 for (uint64_t i = blk_start + t; i < blk_end; i += 256) ob[i] = (uint8_t)s_tab[in[i]].x;
             }
+            // the stream's last word: its bytes past the stream are zero (the pad), whatever
+            // the buffer held
+            if (blk_end == n && t < 4 && ((n + 3) & ~3ull) > n + (uint64_t)t) ob[n + t] = 0;
             if (sync_len != nullptr) {   // chunks of S symbols: 8 S bits (the last: 8 x its symbols)
                 for (uint64_t c = (blk_start >> slog) + t; c < ((blk_end + sync_syms - 1) >> slog); c += 256) {
                     const uint64_t s0 = c << slog;
@@ -1106,27 +1305,43 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
         return;
     }
 
-    for (uint64_t b = bx; b < nblocks; b += gstride) {
+    // Blocks are claimed in pairs of consecutive blocks from a counter, not dealt by
+    // workgroup index: the look-back makes a block wait for every block before it, so the
+    // order blocks are taken in must be the order they are waited on. (Grid-stride dealing,
+    // wg w taking blocks w and w + G, deadlocked: the second blocks of the first resident
+    // workgroups waited on first blocks of workgroups that could not be dispatched.) Pairs
+    // keep the counter at ~55 claims/us on 1 GiB, below a word's ~88/us.
+    for (;;) {
+    if (t == 0) s_pair = atomicAdd(&claim[epoch & 1], 1u);
+    __syncthreads();
+    const uint64_t pair = s_pair;
+    if (2 * pair >= nblocks) break;
+    for (uint64_t b = 2 * pair; b < nblocks && b < 2 * pair + 2; ++b) {
         const uint64_t blk_start = b * (uint64_t)DC_BLOCK_BYTES;
         const uint64_t blk_end = (blk_start + DC_BLOCK_BYTES < n) ? blk_start + DC_BLOCK_BYTES : n;
-        const uint64_t blk_abs = bit_base + block_off[b];
-        const uint64_t blk_first_word = blk_abs >> 5;
-        uint64_t tile_abs = blk_abs;
-        if (t == 0) s_stage[0] = 0u;
-        // the whole 32 KiB block: 8 independent 16-B loads per lane in flight at once (loading
-        // the next block ahead measured slower every way tried: in extra registers -8%
-        // (147 VGPRs), into these registers once pass B is done -4%, into the caches -10%)
         uint4 blkv[PACK_PIECES];
         const bool full = (blk_start + DC_BLOCK_BYTES <= n);
         if (full) {
+            // the whole 32 KiB block: 8 independent 16-B loads per lane in flight at once
+            // (loading the next block ahead measured slower every way tried: in extra
+            // registers -8% (147 VGPRs), into these registers once pass B is done -4%, into
+            // the caches -10%)
 #pragma unroll
             for (int k = 0; k < (int)(DC_BLOCK_BYTES / PACK_TILE); ++k)
                 blkv[k] = LD_PACK(reinterpret_cast<const uint4 *>(in + blk_start + (uint64_t)k * PACK_TILE + (uint64_t)t * 16));
         }
-        const uint32_t nw_blk = (uint32_t)(((blk_abs & 31) + (block_off[b + 1] - block_off[b]) + 31) >> 5);
+        if (t < 64 && b == 2 * pair)   // wave 0, while the block's bytes are in flight
+            pack_pair_offset(bh, s_nb8, pair, nblocks, lb_flags, epoch, t, s_excl2, s_bits2);
+        lds_barrier();   // s_excl2, s_bits2
+        const uint64_t s_excl = s_excl2[b & 1], s_bits = s_bits2[b & 1];
+        const uint64_t blk_abs = bit_base + s_excl;
+        const uint64_t blk_first_word = blk_abs >> 5;
+        uint64_t tile_abs = blk_abs;
+        const uint32_t nw_blk = (uint32_t)(((blk_abs & 31) + s_bits + 31) >> 5);
         // stage origin: the block's first word rounded down to a 16-B boundary of `out`, so
         // the store phase moves whole uint4s (sh = stage index of the block's first word)
         const uint32_t sh = vec_out ? (uint32_t)((blk_first_word - word_base) & 3) : 0u;
+        const bool head_shared = b > 0 && (blk_abs & 31) != 0;   // the first word holds the previous block's tail
         if (full && nw_blk + sh <= PACK_BLK_WORDS) {
             // ---- fast path: the whole block at once, 3 barriers ----
             // lane t of wave w codes piece k = bytes [k*4096 + t*16, +16) of the block, as
@@ -1135,8 +1350,6 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
             // bits takes the per-code flush loop instead (exact, rare on text).
             const int lane = t & 63, wid = t >> 6;
             const uint32_t nwa = sh + nw_blk;
-            for (uint32_t i = 4u * t; i < nwa; i += 1024u)
-                *reinterpret_cast<uint4 *>(&s_stage[i]) = make_uint4(0u, 0u, 0u, 0u);
             uint32_t Tk[PACK_PIECES], Hk[PACK_PIECES], Ik[PACK_PIECES];
 #pragma unroll
             for (int k = 0; k < PACK_PIECES; ++k) {
@@ -1250,10 +1463,14 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
             // OR-ed into HBM by one lane each, the rest are plain stores (uint4 where whole)
             const uint32_t last_plain = ((run & 31) != 0) ? nwa - 1 : nwa;   // plain: [sh+1, last_plain)
             uint32_t *dst = out + (blk_first_word - word_base) - sh;
+            // every stage word read below is zeroed by the thread that read it (the stage is
+            // zero at the next block's start; words < sh and past nwa were never written)
             if (vec_out) {
                 const uint32_t nq = last_plain >> 2;   // uint4 q covers stage words [4q, 4q+4)
                 for (uint32_t q = 1 + t; q < nq; q += 256) {
-                    const uint4 v = *reinterpret_cast<const uint4 *>(&s_stage[4 * q]);
+                    uint4 *const sq = reinterpret_cast<uint4 *>(&s_stage[4 * q]);
+                    const uint4 v = *sq;
+                    *sq = make_uint4(0u, 0u, 0u, 0u);
                     // streaming (nt) stores: same-box A/B on 1 GiB C2, pack 0.420 -> 0.382 ms
                     // (the decode after it reads the payload no slower)
                     uint4 *const d4 = reinterpret_cast<uint4 *>(dst + 4 * q);
@@ -1264,18 +1481,31 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
                 }
                 // head: words sh+1..3 of uint4 0; tail: words of the last, partial uint4
                 const uint32_t hend = last_plain < 4u ? last_plain : 4u;
-                if (t < 4 && (uint32_t)t > sh && (uint32_t)t < hend) dst[t] = bswap32(s_stage[t]);
+                if (t < 4 && (uint32_t)t > sh && (uint32_t)t < hend) { dst[t] = bswap32(s_stage[t]); s_stage[t] = 0u; }
                 const uint32_t tb = nq > 0 ? 4 * nq : 4u;
-                if (t >= 8 && t < 12 && tb + (t - 8) < last_plain) dst[tb + (t - 8)] = bswap32(s_stage[tb + (t - 8)]);
+                if (t >= 8 && t < 12 && tb + (t - 8) < last_plain) {
+                    dst[tb + (t - 8)] = bswap32(s_stage[tb + (t - 8)]);
+                    s_stage[tb + (t - 8)] = 0u;
+                }
             } else {
-                for (uint32_t i = t + 1; i < last_plain; i += 256) dst[i] = bswap32(s_stage[i]);
+                for (uint32_t i = t + 1; i < last_plain; i += 256) { dst[i] = bswap32(s_stage[i]); s_stage[i] = 0u; }
             }
-            if (t == 0) atomicOr(&dst[sh], bswap32(s_stage[sh]));
-            if (t == 64 && last_plain < nwa && nw_blk > 1) atomicOr(&dst[nwa - 1], bswap32(s_stage[nwa - 1]));
+            // the first word: shared with the previous block when the block starts inside it;
+            // the last: shared with the next block when the block ends inside it (the
+            // stream's first and last words are this block's alone)
+            if (t == 0) {
+                if (head_shared) pack_exchange(&xslot[b], s_stage[sh], 2u, &dst[sh]);
+                else dst[sh] = bswap32(s_stage[sh]);
+                s_stage[sh] = 0u;
+            }
+            if (t == 64 && last_plain < nwa && nw_blk > 1) {
+                if (b + 1 < nblocks) pack_exchange(&xslot[b + 1], s_stage[nwa - 1], 1u, &dst[nwa - 1]);
+                else dst[nwa - 1] = bswap32(s_stage[nwa - 1]);
+                s_stage[nwa - 1] = 0u;
+            }
             lds_barrier();
             continue;
         }
-        __syncthreads();
 #pragma unroll
         for (int k = 0; k < (int)(DC_BLOCK_BYTES / PACK_TILE); ++k) {
             const uint64_t tile = blk_start + (uint64_t)k * PACK_TILE;
@@ -1345,18 +1575,28 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
             const uint64_t tile_end_abs = tile_abs + tile_bits;
             const uint32_t nfull = (uint32_t)((tile_end_abs >> 5) - TB);
             for (uint32_t i = t; i < nfull; i += 256) {
-                const uint32_t v = bswap32(s_stage[i]);
                 const uint64_t gw = TB + i;
-                if (gw == blk_first_word) atomicOr(&out[gw - word_base], v);
-                else out[gw - word_base] = v;
+                if (gw == blk_first_word && head_shared) pack_exchange(&xslot[b], s_stage[i], 2u, &out[gw - word_base]);
+                else out[gw - word_base] = bswap32(s_stage[i]);
             }
             __syncthreads();
             if (t == 0) s_stage[0] = (tile_end_abs & 31) ? s_stage[nfull] : 0u;
             tile_abs = tile_end_abs;
             __syncthreads();
         }
-        if (t == 0 && (tile_abs & 31)) atomicOr(&out[(tile_abs >> 5) - word_base], bswap32(s_stage[0]));
+        if (t == 0 && (tile_abs & 31)) {   // the block's partial last word
+            const uint64_t gw = tile_abs >> 5;
+            uint32_t *const d = &out[gw - word_base];
+            if (gw == blk_first_word && head_shared) pack_exchange(&xslot[b], s_stage[0], 2u, d);   // (a block inside one word: the stream's last)
+            else if (b + 1 < nblocks) pack_exchange(&xslot[b + 1], s_stage[0], 1u, d);
+            else *d = bswap32(s_stage[0]);
+        }
         __syncthreads();
+        // the tile loop leaves its stage dirty: zero it for the next block (rare path)
+        for (uint32_t i = 4u * t; i < PACK_BLK_WORDS + 4; i += 1024u)
+            *reinterpret_cast<uint4 *>(&s_stage[i]) = make_uint4(0u, 0u, 0u, 0u);
+        __syncthreads();
+    }
     }
 }
 
@@ -3062,6 +3302,9 @@ template <int M> struct FsmMode {
     static constexpr bool small_enc = M == M_SMALL_ENC || M == M_SMALL_BODY0 || M == M_SMALL_BODY1;
     static constexpr bool body = M == M_SMALL_BODY0 || M == M_SMALL_BODY1 || M == M_SMALL_DBODY || M == M_NYB_DBODY;
     static constexpr bool enc = M == M_SMALL_ENC;   // header + LITERAL fallback (nybble: FsmAux.whole)
+    // the write pass's name in the HIP-event timings (nybble encode and decode told apart)
+    static constexpr const char *wname = M == M_NYB_ENC ? "nyb_enc_write" : M == M_NYB_DEC ? "nyb_dec_write"
+                                       : M == M_NYB_DBODY ? "nyb_dbody_write" : "fsm_write";
 };
 struct FsmAux {
     const uint8_t *rk;    // M_NYB_ENC: rank per element (0..7, 0xFF = miss); null = static dictionary
@@ -4142,6 +4385,79 @@ __global__ __launch_bounds__(64) void k_nyb_resolve(uint8_t *__restrict__ out, u
     edge(k1, n);
 }
 
+// Third form of pass 2 (the product path since r3): the 16 lists stay in SGPRs. They are one
+// wave-uniform vector of 16 u64; the uniform context index selects one by s_movrels_b64 and
+// the touched list goes back by s_movreld_b64 (M0-relative SGPR addressing), so a byte is
+// ~25 scalar instructions with no VALU on its dependency chain. (k_nyb_resolve read the list
+// from VGPR lane c by two v_readlanes and wrote it back by two per-lane selects: ~190 cycles
+// per byte, 12.4 MB/s.) Tokens by scalar loads a 64-B block ahead; the block's 64 bytes are
+// gathered into one VGPR (v_writelane, immediate lane) and leave as 16 dwords.
+typedef uint64_t u64x16 __attribute__((ext_vector_type(16)));
+
+static __device__ __forceinline__ uint32_t adec_step_s(uint32_t t, u64x16 &lists, uint32_t &ctx)
+{
+    const uint64_t L = lists[ctx];
+    const uint64_t ones = 0x0101010101010101ull;
+    const uint32_t ph = t & 7u;
+    const uint32_t vh = (uint32_t)(L >> (8u * ph)) & 255u;       // a hit: the byte at its rank
+    const uint64_t x = L ^ (ones * (uint64_t)t);
+    const uint64_t z = (x - ones) & ~x & (ones << 7);              // a literal: its first match
+    const uint32_t pl = z ? (uint32_t)__builtin_ctzll(z) >> 3 : 7u;   // (absent: the last drops)
+    const bool hit = (t & 0x80u) != 0;
+    const uint32_t v = hit ? vh : t, p = hit ? ph : pl;
+    const uint64_t keep = 0xFFFFFFFFFFFFFF00ull << (8u * p);      // bytes above p stay
+    lists[ctx] = (L ^ ((L ^ (L << 8)) & ~keep)) | (uint64_t)v;    // move to front (:665-687)
+    ctx = (v >> 3) & 15u;
+    return v;
+}
+
+// out[0] is the first byte, out[1..n) the tokens of pass 1; all replaced in place
+__global__ __launch_bounds__(64) void k_nyb_resolve_s(uint8_t *__restrict__ out, uint64_t n)
+{
+    const int lane = (int)threadIdx.x;
+    u64x16 lists;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) lists[c] = mtf_init_word();
+    uint32_t ctx = ((uint32_t)__builtin_amdgcn_readfirstlane((int)out[0]) >> 3) & 15u;
+    const uint64_t k0 = min((uint64_t)((64 - (((uintptr_t)out + 1) & 63)) & 63) + 1, n);
+    const uint64_t nblk = (n - k0) / 64, k1 = k0 + 64 * nblk;
+    auto edge = [&](uint64_t ka, uint64_t kb) {   // positions [ka, kb), kb - ka < 64
+        if (ka >= kb) return;
+        const uint64_t m = kb - ka;
+        const uint32_t tv = (uint64_t)lane < m ? out[ka + lane] : 0u;
+        uint32_t ov = 0;
+        for (uint32_t i = 0; i < (uint32_t)m; ++i) {
+            const uint32_t v = adec_step_s((uint32_t)__builtin_amdgcn_readlane((int)tv, (int)i), lists, ctx);
+            ov = lane == (int)i ? v : ov;
+        }
+        if ((uint64_t)lane < m) out[ka + lane] = (uint8_t)ov;
+    };
+    edge(1, k0);
+    if (nblk) {
+        uint32_t T[16], Tn[16];
+        c_u32 *src = (c_u32 *)(out + k0);
+#pragma unroll
+        for (int j = 0; j < 16; ++j) T[j] = src[j];
+        for (uint64_t b = 0; b < nblk; ++b) {
+            c_u32 *nx = (c_u32 *)(out + k0 + 64 * (b + 1 < nblk ? b + 1 : b));
+#pragma unroll
+            for (int j = 0; j < 16; ++j) Tn[j] = nx[j];   // the next block's tokens, in flight
+            uint32_t dw = 0;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                uint32_t w = 0;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) w |= adec_step_s((T[j] >> (8 * q)) & 255u, lists, ctx) << (8 * q);
+                ADEC_PUT(dw, w, j);
+            }
+            if (lane < 16) reinterpret_cast<uint32_t *>(out + k0 + 64 * b)[lane] = dw;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) T[j] = Tn[j];
+        }
+    }
+    edge(k1, n);
+}
+
 __global__ __launch_bounds__(64) void k_nyb_adec(const uint8_t *__restrict__ in, uint64_t len,
                                                  uint8_t *__restrict__ out, uint64_t *__restrict__ meta)
 {
@@ -4370,6 +4686,13 @@ struct dc_ctx {
     uint32_t *d_fixlist;    size_t fixlist_cap;   // decode redo: flagged chunk indices, compacted
     uint32_t *d_fixpos;     size_t fixpos_cap;    // decode redo: bit offset of a flagged chunk
     uint64_t last_groups;                         // groups of the last S = 64 decode (redo mask length)
+    uint64_t *d_hloc;                             // this context's last histogram (256 u64; hist[] may be all-reduced)
+    uint64_t *d_lbf;        size_t lbf_cap;       // pack: look-back flag per block (k_huff_pack)
+    uint64_t *d_xslot;      size_t xslot_cap;     // pack: boundary-word exchange slot per block boundary
+    uint32_t pack_epoch;                          // pack launches since the flags were last cleared (1..65535)
+    uint32_t *d_claim;                            // pack: block-pair claim counters (2, alternating by epoch)
+    const dc_dtable *plan_table;                  // the table and device total of the last plan
+    uint64_t *plan_total;
     void *d_scr;            size_t scr_cap;       // per-wave garbage sinks of the decoders
     uint64_t *d_meta;                             // small device scalars
     uint4 *d_summ;          size_t summ_cap;
@@ -4470,7 +4793,11 @@ static int ctx_create(dc_ctx **out, int device, void *stream, bool own)
         return DC_E_HIP;
     }
     c->d_errd = c->d_errp + 128;
-    if (hipMalloc((void **)&c->d_hflag, 4096) != hipSuccess || hipMemset(c->d_hflag, 0, 4096) != hipSuccess) {
+    if (hipMalloc((void **)&c->d_hflag, 4096) != hipSuccess || hipMemset(c->d_hflag, 0, 4096) != hipSuccess ||
+        hipMalloc((void **)&c->d_hloc, 256 * sizeof(uint64_t)) != hipSuccess ||
+        hipMemset(c->d_hloc, 0, 256 * sizeof(uint64_t)) != hipSuccess ||
+        hipMalloc((void **)&c->d_claim, 2 * sizeof(uint32_t)) != hipSuccess ||
+        hipMemset(c->d_claim, 0, 2 * sizeof(uint32_t)) != hipSuccess) {
         free(c);
         return DC_E_HIP;
     }
@@ -4510,6 +4837,10 @@ void dc_ctx_destroy(dc_ctx *c)
     if (c->d_err) (void)hipFree(c->d_err);
     if (c->d_errp) (void)hipFree(c->d_errp);
     if (c->d_hflag) (void)hipFree(c->d_hflag);
+    if (c->d_hloc) (void)hipFree(c->d_hloc);
+    if (c->d_claim) (void)hipFree(c->d_claim);
+    if (c->d_lbf) (void)hipFree(c->d_lbf);
+    if (c->d_xslot) (void)hipFree(c->d_xslot);
     if (c->d_queue) (void)hipFree(c->d_queue);
     if (c->d_fix) (void)hipFree(c->d_fix);
     if (c->d_fixlist) (void)hipFree(c->d_fixlist);
@@ -4554,7 +4885,7 @@ int dc_ctx_set_option(dc_ctx *c, int option, int64_t value)
         c->opt_decode_variant = (uint32_t)value;
         return DC_OK;
     case DC_OPT_NYB_ADEC_V1:
-        if (value != 0 && value != 1) return DC_E_ARG;
+        if (value < 0 || value > 2) return DC_E_ARG;
         c->opt_adec_v1 = (uint32_t)value;
         return DC_OK;
     case DC_OPT_HIST_PREFETCH:
@@ -4624,7 +4955,7 @@ int dc_memset(dc_ctx *c, void *d, int v, size_t bytes)
 // ---- Huffman -----------------------------------------------------------------------
 static uint64_t nblocks_of(uint64_t n) { return (n + DC_BLOCK_BYTES - 1) / DC_BLOCK_BYTES; }
 
-int dc_huff_hist(dc_ctx *c, const uint8_t *d_in, uint64_t n, uint64_t *d_hist)
+static int hist_impl(dc_ctx *c, const uint8_t *d_in, uint64_t n, uint64_t *d_hist, HistFuse fuse)
 {
     if (!c || !d_hist || (n && !d_in)) return DC_E_ARG;
     if (((uintptr_t)d_in) & 15) return DC_E_ARG;
@@ -4635,6 +4966,10 @@ int dc_huff_hist(dc_ctx *c, const uint8_t *d_in, uint64_t n, uint64_t *d_hist)
     c->plan_ok = false;
     if (nb == 0) {
         HIPCHK(hipMemsetAsync(d_hist, 0, 256 * sizeof(uint64_t), c->stream));
+        HIPCHK(hipMemsetAsync(c->d_hloc, 0, 256 * sizeof(uint64_t), c->stream));
+        if (fuse.T) LAUNCH(c, "huff_table", k_huff_table, 1, 256, (const uint64_t *)c->d_hloc, 1, (const int32_t *)nullptr,
+                           fuse.M, fuse.nary, fuse.T, (dc_tree *)nullptr, (const uint64_t *)c->d_hloc, fuse.d_total,
+                           fuse.perr, fuse.perr_next);
         return DC_OK;
     }
     const uint64_t hmax = c->opt_hist_grid ? c->opt_hist_grid : 512u;
@@ -4644,9 +4979,14 @@ int dc_huff_hist(dc_ctx *c, const uint8_t *d_in, uint64_t n, uint64_t *d_hist)
     uint64_t *const hacc = reinterpret_cast<uint64_t *>(c->d_hflag);
     uint32_t *const hdone = c->d_hflag + 512;
     if (c->opt_hist_pf == 1)
-        LAUNCH(c, "hist_blocks", k_hist_blocks<1>, grid, 256, d_in, n, nb, c->d_bh, d_hist, hacc, hdone);
-    else LAUNCH(c, "hist_blocks", k_hist_blocks<2>, grid, 256, d_in, n, nb, c->d_bh, d_hist, hacc, hdone);
+        LAUNCH(c, "hist_blocks", k_hist_blocks<1>, grid, 256, d_in, n, nb, c->d_bh, d_hist, hacc, hdone, c->d_hloc, fuse);
+    else LAUNCH(c, "hist_blocks", k_hist_blocks<2>, grid, 256, d_in, n, nb, c->d_bh, d_hist, hacc, hdone, c->d_hloc, fuse);
     return DC_OK;
+}
+
+int dc_huff_hist(dc_ctx *c, const uint8_t *d_in, uint64_t n, uint64_t *d_hist)
+{
+    return hist_impl(c, d_in, n, d_hist, HistFuse{nullptr, 0, 0, nullptr, nullptr, nullptr});
 }
 
 static int table_common(dc_ctx *c, const uint64_t *d_freq, int is_hist, const int32_t *d_len, int M,
@@ -4654,7 +4994,8 @@ static int table_common(dc_ctx *c, const uint64_t *d_freq, int is_hist, const in
 {
     if (!c || !d_table || M < 0 || M >= DC_MAX_SYMS || nary < 2 || nary > 256) return DC_E_ARG;
     c->dec_fresh = nullptr;
-    LAUNCH(c, "huff_table", k_huff_table, 1, 256, d_freq, is_hist, d_len, M, nary, d_table, (dc_tree *)nullptr);
+    LAUNCH(c, "huff_table", k_huff_table, 1, 256, d_freq, is_hist, d_len, M, nary, d_table, (dc_tree *)nullptr,
+           (const uint64_t *)nullptr, (uint64_t *)nullptr, (int *)nullptr, (int *)nullptr);
     return DC_OK;
 }
 
@@ -4662,7 +5003,8 @@ int dc_huff_tree(dc_ctx *c, const uint64_t *d_freq, int M, int nary, dc_dtable *
 {
     if (!c || !d_freq || !d_table || !d_tree || M < 0 || M >= DC_MAX_SYMS || nary < 2 || nary > 256) return DC_E_ARG;
     c->dec_fresh = nullptr;
-    LAUNCH(c, "huff_tree", k_huff_table, 1, 256, d_freq, 0, (const int32_t *)nullptr, M, nary, d_table, d_tree);
+    LAUNCH(c, "huff_tree", k_huff_table, 1, 256, d_freq, 0, (const int32_t *)nullptr, M, nary, d_table, d_tree,
+           (const uint64_t *)nullptr, (uint64_t *)nullptr, (int *)nullptr, (int *)nullptr);
     return DC_OK;
 }
 
@@ -4709,38 +5051,59 @@ int dc_huff_plan(dc_ctx *c, const dc_dtable *d_table, uint64_t *d_total_bits)
 {
     if (!c || !d_table || !d_total_bits) return DC_E_ARG;
     if (!c->hist_in && c->hist_n) return DC_E_STATE;
-    const uint64_t nb = nblocks_of(c->hist_n);
-    if (ensure((void **)&c->d_off, &c->off_cap, (nb + 1) * sizeof(uint64_t))) return DC_E_HIP;
     ++c->gen_p;   // this plan's error slot (cleared by the plan before; the next one is cleared below)
-    if (nb == 0) {
-        HIPCHK(hipMemsetAsync(plan_err_next(c), 0, 4 * sizeof(int), c->stream));
-        HIPCHK(hipMemsetAsync(c->d_off, 0, sizeof(uint64_t), c->stream));
-        HIPCHK(hipMemsetAsync(d_total_bits, 0, sizeof(uint64_t), c->stream));
-        c->plan_ok = true;
-        return DC_OK;
-    }
-    const uint64_t nwg = (nb + PLAN_WG_BLOCKS - 1) / PLAN_WG_BLOCKS;
-    if (nwg <= PLAN_MAX_WG) {
-        if (ensure((void **)&c->d_plan, &c->plan_cap, (nb + nwg + 64) * sizeof(uint32_t))) return DC_E_HIP;
-        uint32_t *loc = c->d_plan, *tot = c->d_plan + nb + 32;
-        LAUNCH(c, "block_bits", k_block_local, nwg, 256, (const uint16_t *)c->d_bh, nb, d_table, loc, tot, plan_err(c));
-        LAUNCH(c, "block_scan", k_block_final_wide, nwg, 256, (const uint32_t *)loc, (const uint32_t *)tot, nb,
-               (uint32_t)nwg, c->d_off, d_total_bits, plan_err_next(c));
-    } else {
-        LAUNCH(c, "block_bits", k_block_bits, (nb + 3) / 4, 256, (const uint16_t *)c->d_bh, nb, d_table, c->d_off,
-               plan_err(c));
-        LAUNCH(c, "block_scan", k_block_scan, 1, 1024, c->d_off, nb, d_total_bits, plan_err_next(c));
-    }
+    // the payload bits of this context's last histogram under d_table (and the missing-code
+    // flag): one 256-thread launch; the blocks' offsets are the pack's own look-back
+    LAUNCH(c, "plan_total", k_plan_total, 1, 256, (const uint64_t *)c->d_hloc, d_table, d_total_bits, plan_err(c),
+           plan_err_next(c));
+    c->plan_table = d_table;
+    c->plan_total = d_total_bits;
+    c->plan_ok = true;
+    return DC_OK;
+}
+
+int dc_huff_encode_plan(dc_ctx *c, const uint8_t *d_in, uint64_t n, int M, int nary, uint64_t *d_hist,
+                        dc_dtable *d_table, uint64_t *d_total_bits)
+{
+    if (!c || !d_table || !d_total_bits || M < 0 || M >= DC_MAX_SYMS || nary < 2 || nary > 256) return DC_E_ARG;
+    ++c->gen_p;
+    c->dec_fresh = nullptr;
+    const int r = hist_impl(c, d_in, n, d_hist,
+                            HistFuse{d_table, M, nary, d_total_bits, plan_err(c), plan_err_next(c)});
+    if (r != DC_OK) { --c->gen_p; return r; }
+    c->plan_table = d_table;
+    c->plan_total = d_total_bits;
     c->plan_ok = true;
     return DC_OK;
 }
 
 int dc_huff_plan_offsets(dc_ctx *c, uint64_t *h_off, uint64_t max_entries, uint64_t *h_n)
 {
-    if (!c || !c->plan_ok) return DC_E_STATE;
-    const uint64_t nb = nblocks_of(c->hist_n) + 1;
-    const uint64_t k = nb < max_entries ? nb : max_entries;
-    if (h_n) *h_n = nb;
+    // inspection only: the per-block exclusive bit offsets (the pack computes them itself, by
+    // its look-back), recomputed here by the two plan kernels
+    if (!c || !c->plan_ok || !c->plan_table) return DC_E_STATE;
+    const uint64_t nb = nblocks_of(c->hist_n);
+    if (h_n) *h_n = nb + 1;
+    const uint64_t k = nb + 1 < max_entries ? nb + 1 : max_entries;
+    if (ensure((void **)&c->d_off, &c->off_cap, (nb + 1) * sizeof(uint64_t))) return DC_E_HIP;
+    if (nb == 0) {
+        HIPCHK(hipMemsetAsync(c->d_off, 0, sizeof(uint64_t), c->stream));
+    } else {
+        const uint64_t nwg = (nb + PLAN_WG_BLOCKS - 1) / PLAN_WG_BLOCKS;
+        int *const scratch_err = c->d_err + 12;   // not a plan slot: the flags of the real plan stay
+        if (nwg <= PLAN_MAX_WG) {
+            if (ensure((void **)&c->d_plan, &c->plan_cap, (nb + nwg + 64) * sizeof(uint32_t))) return DC_E_HIP;
+            uint32_t *loc = c->d_plan, *tot = c->d_plan + nb + 32;
+            LAUNCH(c, "block_bits", k_block_local, nwg, 256, (const uint16_t *)c->d_bh, nb, c->plan_table, loc, tot,
+                   scratch_err);
+            LAUNCH(c, "block_scan", k_block_final_wide, nwg, 256, (const uint32_t *)loc, (const uint32_t *)tot, nb,
+                   (uint32_t)nwg, c->d_off, c->d_meta + 15, scratch_err);
+        } else {
+            LAUNCH(c, "block_bits", k_block_bits, (nb + 3) / 4, 256, (const uint16_t *)c->d_bh, nb, c->plan_table,
+                   c->d_off, scratch_err);
+            LAUNCH(c, "block_scan", k_block_scan, 1, 1024, c->d_off, nb, c->d_meta + 15, scratch_err);
+        }
+    }
     if (k) {
         HIPCHK(hipMemcpyAsync(h_off, c->d_off, k * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
@@ -4768,25 +5131,52 @@ static bool sync_ok(uint32_t S) { return S >= 16 && S <= DC_SYNC_MAX && (S & (S 
 uint64_t dc_huff_sync_chunks(uint64_t n, uint32_t S) { return S ? (n + S - 1) / S : 0; }
 uint64_t dc_huff_sync_groups(uint64_t n, uint32_t S) { return (dc_huff_sync_chunks(n, S) + DC_SYNC_GROUP - 1) / DC_SYNC_GROUP; }
 
+// zeroed on (re)allocation: the look-back flags of epoch 0 are never current, and the
+// exchange slots are empty between launches
+static int ensure_zeroed(dc_ctx *c, void **p, size_t *cap, size_t bytes, bool *fresh)
+{
+    const size_t before = *cap;
+    void *const old = *p;
+    if (ensure(p, cap, bytes)) return DC_E_HIP;
+    *fresh = (*p != old || *cap != before);
+    if (*fresh) HIPCHK(hipMemsetAsync(*p, 0, *cap, c->stream));
+    return DC_OK;
+}
+
 static int pack_impl(dc_ctx *c, const uint8_t *d_in, uint64_t n, const dc_dtable *d_table, uint64_t bit_base,
                      const uint64_t *d_base, uint32_t *d_words, uint64_t words_cap, uint64_t *d_sync_base,
                      uint16_t *d_sync_len, uint32_t sync_syms)
 {
     if (!c || !d_table || !d_words) return DC_E_ARG;
-    if (d_in != c->hist_in || n != c->hist_n || !c->plan_ok) return DC_E_STATE;
+    if (d_in != c->hist_in || n != c->hist_n || !c->plan_ok || !c->plan_total) return DC_E_STATE;
     if ((d_sync_base != nullptr) != (d_sync_len != nullptr)) return DC_E_ARG;
     if (d_sync_len && !sync_ok(sync_syms)) return DC_E_ARG;
     const uint64_t nb = nblocks_of(n);
     if (nb == 0) return DC_OK;
-    LAUNCH(c, "zero_bounds", k_zero_bounds, (nb + 1 + 255) / 256, 256, (const uint64_t *)c->d_off, nb, bit_base,
-           d_base, d_words, words_cap, plan_err(c));
-    // two blocks per workgroup (grid-stride): on 1 GiB C2, 16384 workgroups ran pack in
-    // 0.452 ms against 0.481 at 4096, 0.469 at 32768, 0.504 at 1024 (r1 v15 A/B)
-    const uint64_t gmax = c->opt_pack_grid ? c->opt_pack_grid : (nb + 1) / 2;
-    const uint64_t grid = nb < gmax ? nb : gmax;
+    bool fresh = false, fresh2 = false;
+    if (ensure_zeroed(c, (void **)&c->d_lbf, &c->lbf_cap, ((nb + 1) / 2) * sizeof(uint64_t), &fresh) ||
+        ensure_zeroed(c, (void **)&c->d_xslot, &c->xslot_cap, (nb + 1) * sizeof(uint64_t), &fresh2))
+        return DC_E_HIP;
+    if (fresh) {   // epochs restart: so do the claim counters
+        c->pack_epoch = 0;
+        HIPCHK(hipMemsetAsync(c->d_claim, 0, 2 * sizeof(uint32_t), c->stream));
+    }
+    if (++c->pack_epoch > 0xFFFFu) {   // the 16-bit epoch wraps: every flag is cleared once
+        HIPCHK(hipMemsetAsync(c->d_lbf, 0, c->lbf_cap, c->stream));
+        HIPCHK(hipMemsetAsync(c->d_claim, 0, 2 * sizeof(uint32_t), c->stream));
+        c->pack_epoch = 1;
+    }
+    // workgroups enough to keep every CU busy (4 resident per CU), but never more than pairs:
+    // each one claims pairs of blocks until none is left
+    // (r1, static dealing: 16384 workgroups ran 1 GiB C2 in 0.452 ms against 0.481 at 4096,
+    // 0.469 at 32768, 0.504 at 1024)
+    const uint64_t pairs = (nb + 1) / 2;
+    const uint64_t gmax = c->opt_pack_grid ? c->opt_pack_grid : pairs;
+    const uint64_t grid = pairs < gmax ? pairs : gmax;
     // + workgroup 0: the decoder tables (k_huff_table leaves them to the pack's idle CU time)
-    LAUNCH(c, "huff_pack", k_huff_pack, grid + 1, 256, d_in, n, d_table, (const uint64_t *)c->d_off, bit_base, d_base, d_words,
-           d_sync_base, d_sync_len, sync_syms, nb, words_cap, (const int *)plan_err(c), 1);
+    LAUNCH(c, "huff_pack", k_huff_pack, grid + 1, 256, d_in, n, d_table, (const uint16_t *)c->d_bh,
+           (const uint64_t *)c->plan_total, bit_base, d_base, d_words, d_sync_base, d_sync_len, sync_syms, nb, words_cap,
+           plan_err(c), 1, c->d_lbf, c->pack_epoch, c->d_xslot, c->d_claim);
     c->dec_fresh = d_table;   // workgroup 0 built the decoder tables
     return DC_OK;
 }
@@ -4823,14 +5213,13 @@ int dc_huff_pack(dc_ctx *c, const uint8_t *d_in, uint64_t n, const dc_dtable *d_
                  uint32_t sync_syms)
 {
     if (!c || !d_table || !d_words) return DC_E_ARG;
-    if (d_in != c->hist_in || n != c->hist_n || !c->plan_ok) return DC_E_STATE;
+    if (d_in != c->hist_in || n != c->hist_n || !c->plan_ok || !c->plan_total) return DC_E_STATE;
     if ((d_sync_base != nullptr) != (d_sync_len != nullptr)) return DC_E_ARG;
     if (d_sync_len && !sync_ok(sync_syms)) return DC_E_ARG;
     // plan errors (a byte without a code) are checked here: host read of one int
     int err = 0;
     HIPCHK(hipMemcpyAsync(c->h_pinned, plan_err(c), sizeof(int), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipMemcpyAsync(c->h_pinned + 1, c->d_off + nblocks_of(n), sizeof(uint64_t), hipMemcpyDeviceToHost,
-                          c->stream));
+    HIPCHK(hipMemcpyAsync(c->h_pinned + 1, c->plan_total, sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     err = *(int *)c->h_pinned;
     if (err) {
@@ -5033,7 +5422,7 @@ static int fsm_run(dc_ctx *c, const uint8_t *d_in, uint64_t len, uint64_t nelem,
             LAUNCH(c, SmMode<M>::dec ? "small_dec_write" : "small_write", k_small_write<M>, wgrid, SmMode<M>::wthreads, d_in, len, nelem, (const uint64_t *)c->d_entry,
                    (const uint4 *)c->d_summ, (const uint64_t *)c->d_meta, d_out);
         else
-            LAUNCH(c, "fsm_write", k_fsm_write<M>, wgrid, 256, d_in, len, nelem, (const uint64_t *)c->d_entry,
+            LAUNCH(c, FsmMode<M>::wname, k_fsm_write<M>, wgrid, 256, d_in, len, nelem, (const uint64_t *)c->d_entry,
                    (const uint4 *)c->d_summ, (const uint64_t *)c->d_meta, d_out, aux);
     }
     HIPCHK(hipMemcpyAsync(c->h_pinned, c->d_meta, 6 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
@@ -5061,7 +5450,7 @@ static int fsm_write_planned(dc_ctx *c, const uint8_t *d_in, uint64_t len, uint6
         LAUNCH(c, SmMode<M>::dec ? "small_dec_write" : "small_write", k_small_write<M>, ntiles ? ntiles : 1, SmMode<M>::wthreads, d_in, len, nelem,
                (const uint64_t *)c->d_entry, (const uint4 *)c->d_summ, (const uint64_t *)c->d_meta, d_out);
     else
-        LAUNCH(c, "fsm_write", k_fsm_write<M>, ntiles ? ntiles : 1, 256, d_in, len, nelem, (const uint64_t *)c->d_entry,
+        LAUNCH(c, FsmMode<M>::wname, k_fsm_write<M>, ntiles ? ntiles : 1, 256, d_in, len, nelem, (const uint64_t *)c->d_entry,
                (const uint4 *)c->d_summ, (const uint64_t *)c->d_meta, d_out, aux);
     HIPCHK(hipMemcpyAsync(c->h_pinned, c->d_meta, sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
@@ -5338,7 +5727,7 @@ int dc_nyb_decompress(dc_ctx *c, const uint8_t *d_in, uint64_t m, int modify, ui
     if (type == 0xAF) {
         if (m < 2) { *h_len = 0; return DC_OK; }
         if (!modify) return fsm_run<M_NYB_DEC>(c, d_in, m, m - 2, d_out, h_len, "nyb_dec_tiles");
-        if (c->opt_adec_v1) {   // A/B only: the one-pass single-wave decoder
+        if (c->opt_adec_v1 == 1) {   // A/B only: the one-pass single-wave decoder
             LAUNCH(c, "nyb_adec", k_nyb_adec, 1, 64, d_in, m, d_out, c->d_meta);
             HIPCHK(hipMemcpyAsync(c->h_pinned, c->d_meta, sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
             HIPCHK(hipStreamSynchronize(c->stream));
@@ -5348,7 +5737,10 @@ int dc_nyb_decompress(dc_ctx *c, const uint8_t *d_in, uint64_t m, int modify, ui
         // tokens by the static transducer (parallel), then one wave resolves them in place
         r = fsm_run<M_NYB_DEC>(c, d_in, m, m - 2, d_out, h_len, "nyb_tok_tiles", FsmAux{nullptr, 0, 0, 1, 1, 1});
         if (r) return r;
-        if (*h_len > 1) LAUNCH(c, "nyb_resolve", k_nyb_resolve, 1, 64, d_out, *h_len);
+        if (*h_len > 1) {
+            if (c->opt_adec_v1 == 2) LAUNCH(c, "nyb_resolve", k_nyb_resolve, 1, 64, d_out, *h_len);   // A/B: r2's
+            else LAUNCH(c, "nyb_resolve", k_nyb_resolve_s, 1, 64, d_out, *h_len);
+        }
         HIPCHK(hipStreamSynchronize(c->stream));
         return DC_OK;
     }

@@ -131,6 +131,22 @@ class Codec:
         self._last_total = total
         return total
 
+    @property
+    def fused_plan(self) -> bool:
+        """Whether the library has dc_huff_encode_plan (hist + table + plan in one launch)."""
+        return hasattr(self.L, "dc_huff_encode_plan")
+
+    def encode_plan(self, x, n_ary: int, max_symbol_value: int = 258, hist=None, table=None, total=None):
+        """hist -> table -> plan in one launch (dc_huff_encode_plan): the histogram kernel's
+        last workgroup builds the table and the payload bit count. Returns (hist, table, total)."""
+        hist = hist if hist is not None else self._t(256, torch.int64)
+        table = table if table is not None else self._t(self.table_bytes)
+        total = total if total is not None else self._t(1, torch.int64)
+        check("dc_huff_encode_plan", self.L.dc_huff_encode_plan(self.ctx, _ptr(x), x.numel(), max_symbol_value, n_ary,
+                                                                _ptr(hist), _ptr(table), _ptr(total)))
+        self._last_total = total
+        return hist, table, total
+
     def plan_total(self) -> int:
         return int(self._last_total.item())
 
@@ -249,9 +265,13 @@ class Codec:
         return out[: n.value]
 
     # ---- nybble codec, whole streams and shard bodies (dist.ShardedNybble) -----
-    def nyb_compress(self, x, modify: bool):
-        """compress_bytestring (nybble_compression.c:887-1038) of device bytes x."""
-        out = self._t(x.numel() + 2)
+    def nyb_compress(self, x, modify: bool, out=None):
+        """compress_bytestring (nybble_compression.c:887-1038) of device bytes x (into `out`
+        when given: at least x.numel() + 2 bytes)."""
+        if out is None:
+            out = self._t(x.numel() + 2)
+        elif out.numel() < x.numel() + 2 or out.dtype != torch.uint8 or not out.is_contiguous():
+            raise ValueError("nyb_compress output: contiguous uint8 of >= n + 2 bytes")
         n = C.c_uint64(0)
         check("dc_nyb_compress", self.L.dc_nyb_compress(self.ctx, _ptr(x), x.numel(), int(modify), _ptr(out),
                                                         C.byref(n)))
@@ -372,9 +392,12 @@ class Codec:
     def encode(self, x, n_ary: int = 2, sync_syms: int | None = None, bit_base: int = 0):
         """hist -> table -> plan -> pack on one device. Returns dict of device tensors."""
         n = x.numel()
-        hist = self.hist(x)
-        tab = self.table(hist, n_ary)
-        total = self.plan(tab)
+        if hasattr(self.L, "dc_huff_encode_plan"):
+            hist, tab, total = self.encode_plan(x, n_ary)
+        else:   # an older diagnostic library (tools/, DC_CORE_LIB): the three launches
+            hist = self.hist(x)
+            tab = self.table(hist, n_ary)
+            total = self.plan(tab)
         bits = int(total.item())
         S = sync_syms or self.choose_sync(n, bits)
         words = self._t(self.words_needed(bit_base, bits), torch.int32)

@@ -86,6 +86,9 @@ class ShardedHuffman:
     def plan(self, x, n_ary: int, hist=None, table=None, total=None):
         """Steps 1-3: global table and this rank's payload bit count (device tensors), and
         the gathered per-rank bit counts (device tensor; None at world size 1)."""
+        if self.world == 1 and getattr(self.e, "fused_plan", False):   # no exchange: one fused launch
+            hist, tab, total = self.e.encode_plan(x, n_ary, hist=hist, table=table, total=total)
+            return tab, total, None
         hist = self.e.hist(x, out=hist) if hist is not None else self.e.hist(x)
         if self.table_mode == "broadcast" and self.world > 1:
             self._reduce_to_src(hist)

@@ -117,8 +117,9 @@ enum {
     DC_OPT_HIST_PREFETCH = 5,     /* histogram: 32 KiB blocks in flight ahead, 1..2, 0 = 2 */
     DC_OPT_DECODE_VARIANT = 6,    /* fast decoder: 0 one code per lookup (k_huff_decode8),
                                      1 up to 3 codes per lookup (k_huff_decode9) */
-    DC_OPT_NYB_ADEC_V1 = 7        /* adaptive nybble decode: 0 tokens + k_nyb_resolve,
-                                     1 the one-pass single-wave k_nyb_adec (A/B) */
+    DC_OPT_NYB_ADEC_V1 = 7        /* adaptive nybble decode: 0 tokens + the SGPR-list resolve
+                                     (k_nyb_resolve_s), 1 the one-pass single-wave k_nyb_adec,
+                                     2 tokens + r2's VGPR-list resolve (A/B) */
 };
 int dc_ctx_set_option(dc_ctx *ctx, int option, int64_t value);
 const char *dc_version(void);
@@ -150,9 +151,16 @@ int dc_huff_tree(dc_ctx *ctx, const uint64_t *d_freq, int max_symbol_value, int 
 /* (2e) summarize_tree_with_lengths' walk for any node list: d_depth[i] (i < leaves) = parent
  *      hops from node i to the root (-1: the walk exceeds the list, a cycle) */
 int dc_tree_depths(dc_ctx *ctx, const int32_t *d_parent, int list_length, int leaves, int32_t *d_depth);
-/* (3) per-block bit counts + exclusive scan for the input of the last dc_huff_hist;
- *     writes the payload bit count to *d_total_bits (device u64). */
+/* (3) the encode plan of the input of the last dc_huff_hist under d_table: its payload bit
+ *     count into *d_total_bits (device u64) and the missing-code flag (dc_huff_pack_status).
+ *     The per-block offsets are the pack's own (a decoupled look-back inside k_huff_pack). */
 int dc_huff_plan(dc_ctx *ctx, const dc_dtable *d_table, uint64_t *d_total_bits);
+/* (1+2+3 fused) histogram, table and plan of d_in[0..n) in ONE launch: the histogram's last
+ *     workgroup builds the table (as dc_huff_table) and the plan total (as dc_huff_plan) from
+ *     the histogram it holds. The single-stream encoder's path (a sharded encode must reduce
+ *     the histograms between the two, so it calls them separately). */
+int dc_huff_encode_plan(dc_ctx *ctx, const uint8_t *d_in, uint64_t n, int max_symbol_value, int n_ary,
+                        uint64_t *d_hist, dc_dtable *d_table, uint64_t *d_total_bits);
 /* (4) pack at global bit offset bit_base into d_words (word 0 = stream word bit_base/32,
  *     MSB-first bytes; 16-B aligned). Capacity: dc_huff_words_needed().
  *     Sync index (DESIGN.md "Sync index v1"), both arrays NULL for none: chunks of
@@ -165,8 +173,9 @@ int dc_huff_pack(dc_ctx *ctx, const uint8_t *d_in, uint64_t n, const dc_dtable *
 uint64_t dc_huff_sync_chunks(uint64_t n, uint32_t sync_syms);
 uint64_t dc_huff_sync_groups(uint64_t n, uint32_t sync_syms);
 uint64_t dc_huff_words_needed(uint64_t bit_base, uint64_t total_bits);
-/* inspection (synchronising): the plan's exclusive per-block bit offsets (nblocks+1
- * entries, last = total) and the per-block u16 histograms of the last dc_huff_hist */
+/* inspection (synchronising): the exclusive per-block bit offsets of the last plan (nblocks+1
+ * entries, last = total; recomputed on demand) and the per-block u16 histograms of the last
+ * dc_huff_hist */
 int dc_huff_plan_offsets(dc_ctx *ctx, uint64_t *h_off, uint64_t max_entries, uint64_t *h_n);
 int dc_huff_block_hist(dc_ctx *ctx, uint16_t *h_bh, uint64_t max_entries);
 /* (4') the same without any host round trip (graph/timing friendly): a byte without a

@@ -6,8 +6,8 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 TAG=${1:-r3}; K=${2:-decode}; ABL=${3:-}; STAGE=${4:-decode}
 mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -q -k "$K" --timeout 200 --timeout-method thread > gpurun_out/${TAG}_tests.log 2>&1
-rc=$?; tail -3 gpurun_out/${TAG}_tests.log
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -v -k "$K" --timeout 100 --timeout-method thread > gpurun_out/${TAG}_tests.log 2>&1
+rc=$?; grep -cE "PASSED" gpurun_out/${TAG}_tests.log; tail -2 gpurun_out/${TAG}_tests.log
 if [ $rc -ne 0 ]; then grep -E "^(FAILED|ERROR)|Error|assert" gpurun_out/${TAG}_tests.log | head -20; exit $rc; fi
 for r in 1 2; do
   echo "base:"; timeout -k 10 200 python -u tools/kern_ab.py --stage $STAGE --option decode_static_pct --values 60 --cfg C2 --rounds 3 || exit 1
