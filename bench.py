@@ -244,6 +244,8 @@ def main():
     dom_bytes = alg.get(dom, n)
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
     traffic, traffic_src = pmc_traffic("k_" + dom, a, n)
+    rp_ms, rp_src = rocprof_mean("k_" + dom, a, n)
+    copy_gbps = copy_probe(c, x, a.profile_steps)
 
     # whole-pipeline rooflines (SURVEY §8(d) bytes over the whole encode / whole decode time:
     # extra passes such as the histogram's read of the input count against them)
@@ -275,7 +277,12 @@ def main():
                      "unit": "GB/s", "frac": round(achieved * 1e9 / HBM_PEAK, 4), "traffic": traffic,
                      "traffic_source": traffic_src,
                      "alg_bytes_per_launch": dom_bytes, "mean_ms": round(dom_ms, 4),
+                     "frac_rocprof": round(dom_bytes / (rp_ms * 1e-3) / HBM_PEAK, 4) if rp_ms else None,
+                     "rocprof_mean_ms": round(rp_ms, 4) if rp_ms else None, "rocprof_source": rp_src,
+                     "copy_probe_GBps": round(copy_gbps, 1), "frac_vs_copy": round(achieved / copy_gbps, 4),
                      "encode_frac": round(enc_frac, 4), "decode_frac": round(dec_frac, 4),
+                     "encode_frac_vs_copy": round(enc_frac * HBM_PEAK / 1e9 / copy_gbps, 4),
+                     "decode_frac_vs_copy": round(dec_frac * HBM_PEAK / 1e9 / copy_gbps, 4),
                      "encode_ms": round(enc_ms, 4), "decode_ms": round(dec_ms, 4),
                      "pipeline_alg_bytes": enc_alg},
         "encode_GBps": round(n / (enc_ms * 1e-3) / 1e9, 2),
@@ -541,6 +548,40 @@ def pmc_traffic(kernel, a, n):
         if k:
             return k["traffic_bytes"], os.path.relpath(f, REPO)
     return None, None
+
+
+def rocprof_mean(kernel, a, n):
+    """Mean launch duration (ms) of `kernel` from the newest committed rocprofv3 --stats summary
+    of this bench command (profiles/*_rocprof.json, tools/rocprof_report.py), when its workload
+    matches: the roofline fraction by rocprof beside the HIP-event one."""
+    import glob
+    for f in reversed(sorted(glob.glob(os.path.join(REPO, "profiles", "*_rocprof.json")))):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        w = d.get("workload", {})
+        if (w.get("cfg"), w.get("size"), w.get("n_ary")) != (a.cfg, n, a.nary):
+            continue
+        k = d.get("kernels", {}).get(kernel)
+        if k:
+            return k["mean_ms"], os.path.relpath(f, REPO)
+    return None, None
+
+
+def copy_probe(c, x, reps):
+    """The chip's achievable HBM rate on this box, the reference for the fractions: a
+    hand-written float4 copy of the input (dc_copy_probe: 16-B nt loads and stores), read +
+    write bytes over its mean HIP-event time on the codec's stream."""
+    y = torch.empty_like(x)
+    c.copy_probe(x, y)
+    c.timing(True)
+    for _ in range(reps):
+        c.copy_probe(x, y)
+    ms = float(np.mean([m for name, m in c.timings() if name == "copy_probe"]))
+    c.timing(False)
+    del y
+    return 2 * x.numel() / (ms * 1e-3) / 1e9
 
 
 def cpu_baseline(x, a):

@@ -1046,10 +1046,15 @@ __global__ __launch_bounds__(256) void k_block_local(const uint16_t *__restrict_
 // (2), one workgroup per PLAN_WG_BLOCKS blocks: its base = the sum of the workgroup totals
 // before it (every workgroup re-reads the <= PLAN_MAX_WG totals: 2 KiB on 1 GiB), then its
 // blocks' absolute offsets; the last workgroup writes the stream total
+// With `words` set it also zeroes every word two blocks share (the word holding a block's
+// first bit, and the stream's partial last word), which k_huff_pack OR-merges into: words
+// whose index is past words_cap are left alone (the pack reports the capacity error).
 __global__ __launch_bounds__(256) void k_block_final_wide(const uint32_t *__restrict__ local,
                                                           const uint32_t *__restrict__ wgtot, uint64_t nblocks,
                                                           uint32_t nwg, uint64_t *__restrict__ off,
-                                                          uint64_t *__restrict__ d_total, int *__restrict__ err_next)
+                                                          uint64_t *__restrict__ d_total, int *__restrict__ err_next,
+                                                          uint64_t bit_base, const uint64_t *__restrict__ d_base,
+                                                          uint32_t *__restrict__ words, uint64_t words_cap)
 {
     __shared__ uint64_t s_w[4];
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -1081,9 +1086,19 @@ __global__ __launch_bounds__(256) void k_block_final_wide(const uint32_t *__rest
             *d_total = tot;
         }
     }
+    if (d_base) bit_base += *d_base;   // device-resident shard offset (dist: no host read)
     if (t < PLAN_WG_BLOCKS) {
         const uint64_t b = (uint64_t)g * PLAN_WG_BLOCKS + t;
-        if (b < nblocks) off[b] = base + local[b];
+        if (b < nblocks) {
+            const uint64_t o = base + local[b];
+            off[b] = o;
+            const uint64_t wi = ((bit_base + o) >> 5) - (bit_base >> 5);
+            if (words && wi < words_cap) words[wi] = 0u;
+        }
+    } else if (t == PLAN_WG_BLOCKS && last && words) {   // the stream's partial last word
+        const uint64_t abs = bit_base + s_w[0] + s_w[1] + s_w[2] + s_w[3];
+        const uint64_t wi = (abs >> 5) - (bit_base >> 5);
+        if ((abs & 31) != 0 && wi < words_cap) words[wi] = 0u;
     }
 }
 
@@ -1108,117 +1123,31 @@ static __device__ __forceinline__ void lds_barrier()
 #define PACK_BLK_WORDS 9216     /* 36 KiB: a full block of <= 9 bits/symbol is staged whole  */
 #define PACK_PIECES (DC_BLOCK_BYTES / PACK_TILE)
 
-// Block offsets inside the pack (no plan launches): decoupled look-back over the blocks. A
-// block's bit count comes from its histogram row (bh . nbits, the reference's own payload
-// formula, n_ary_huffman.c:2485) before its bytes have even arrived, so it is published at
-// once; wave 0 then reads up to 64 predecessors' flags per step until it meets an inclusive
-// prefix. Flag = value (46 bits) | epoch (16) | state (2: 1 aggregate, 2 inclusive prefix),
-// one 64-bit agent-scope atomic (no separate payload to order); the epoch (a per-context
-// launch count) tells this launch's flags from older ones, so the flags are never cleared
-// (dc_ctx resets them when the epoch wraps). Blocks wait only on blocks of lower index,
-// which were dispatched earlier (a workgroup's second block waits on blocks whose
-// workgroups are resident or done), so the waits end.
-#define LB_VALUE_BITS 46
-#define LB_FLAG(epoch, state, value) ((uint64_t)(value) | ((uint64_t)(epoch) << LB_VALUE_BITS) | ((uint64_t)(state) << 62))
-static __device__ __noinline__ uint64_t pack_lookback(uint64_t *__restrict__ flags, uint64_t p, uint64_t agg,
-                                                      uint32_t epoch, int lane)
+// zero every word two blocks share (plan fallback above PLAN_MAX_WG workgroups of blocks,
+// where k_block_final_wide does not run)
+__global__ void k_zero_bounds(const uint64_t *__restrict__ off, uint64_t nblocks, uint64_t bit_base,
+                              const uint64_t *__restrict__ d_base, uint32_t *__restrict__ words, uint64_t words_cap)
 {
-    // flags per claimed PAIR of blocks; one step reads 256 predecessors (4 per lane, in flight
-    // together): at ~55 claims per us and ~2 us per agent-scope round trip, a 64-flag window
-    // covered 1.2 us of claims, less than the time its own round trip took, so look-backs
-    // rarely met an inclusive prefix and chained (1 GiB C2 pack 0.60 ms, against 0.376 with
-    // the plan launches)
-    constexpr uint64_t VMASK = (1ull << LB_VALUE_BITS) - 1;
-    constexpr int W = 4;
-    if (lane == 0)
-        __hip_atomic_store(&flags[p], LB_FLAG(epoch, p == 0 ? 2u : 1u, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    uint64_t excl = 0;
-    int64_t base = (int64_t)p - 1;   // the nearest predecessor not yet summed
-    while (base >= 0) {
-        uint64_t v[W];
-#pragma unroll
-        for (int j = 0; j < W; ++j) {
-            const int64_t i = base - 64 * j - lane;
-            v[j] = i >= 0 ? __hip_atomic_load(&flags[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                          : LB_FLAG(epoch, 2u, 0u);
-        }
-        bool done = false, wait = false;
-#pragma unroll
-        for (int j = 0; j < W; ++j) {
-            if (done || wait) break;
-            const uint32_t st = ((uint32_t)(v[j] >> LB_VALUE_BITS) & 0xFFFFu) == epoch ? (uint32_t)(v[j] >> 62) : 0u;
-            const uint64_t inc = __ballot(st == 2u), none = __ballot(st == 0u);
-            const int fi = inc ? __builtin_ctzll(inc) : 64, fn = none ? __builtin_ctzll(none) : 64;
-            const int upto = fn < fi ? fn : (fi < 64 ? fi + 1 : 64);   // lanes whose values count
-            uint64_t x = lane < upto ? (v[j] & VMASK) : 0ull;
-#pragma unroll
-            for (int d = 32; d > 0; d >>= 1) x += __shfl_xor(x, d, 64);
-            excl += x;
-            base -= upto;
-            done = fi < 64 && fi < fn;   // met an inclusive prefix
-            wait = !done && fn < 64;     // a predecessor has not published yet: re-read from it
-        }
-        if (done) break;
-        if (wait) __builtin_amdgcn_s_sleep(1);
-    }
-    if (lane == 0 && p > 0)
-        __hip_atomic_store(&flags[p], LB_FLAG(epoch, 2u, excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return excl;
+    const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (d_base) bit_base += *d_base;
+    if (b > nblocks) return;
+    const uint64_t abs = bit_base + off[b], wi = (abs >> 5) - (bit_base >> 5);
+    if ((b < nblocks || (abs & 31) != 0) && wi < words_cap) words[wi] = 0u;
 }
 
-// The offsets of a claimed pair of blocks (wave 0; out of line so that its registers are not
-// added to the block loop's): both blocks' bit counts from their histogram rows, the pair's
-// aggregate published at once (the next pairs' look-backs never wait on a whole block), its
-// offset by the look-back; lane 0 writes the blocks' offsets and bit counts to LDS
-static __device__ __noinline__ void pack_pair_offset(const uint16_t *__restrict__ bh, const uint8_t *nb8, uint64_t pair,
-                                                     uint64_t nblocks, uint64_t *__restrict__ flags, uint32_t epoch,
-                                                     int lane, uint64_t *excl2, uint64_t *bits2)
-{
-    const uint64_t b = 2 * pair;
-    const bool two = b + 1 < nblocks;
-    uint32_t agg[2];
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        const uint64_t bq = (q && two) ? b + 1 : b;
-        const uint2 h = *reinterpret_cast<const uint2 *>(bh + bq * 256 + lane * 4);
-        const uint32_t a = (h.x & 0xFFFFu) * nb8[4 * lane] + (h.x >> 16) * nb8[4 * lane + 1] +
-                           (h.y & 0xFFFFu) * nb8[4 * lane + 2] + (h.y >> 16) * nb8[4 * lane + 3];
-        agg[q] = (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_incl(a), 63);   // <= 2^20 per block
-    }
-    if (!two) agg[1] = 0;
-    const uint64_t ex = pack_lookback(flags, pair, (uint64_t)agg[0] + agg[1], epoch, lane);
-    if (lane == 0) {
-        excl2[0] = ex;
-        excl2[1] = ex + agg[0];
-        bits2[0] = agg[0];
-        bits2[1] = agg[1];
-    }
-}
-
-// A word two blocks share (the block boundary falls inside it): each side ORs its bits into
-// the boundary's slot with its side mark (1: the earlier block's tail, 2: the later block's
-// head); the side that arrives second finds the other's mark, writes the merged word and
-// clears the slot for the next launch. No zeroing launch and no OR into HBM.
-static __device__ __forceinline__ void pack_exchange(uint64_t *slot, uint32_t bits, uint32_t side, uint32_t *dst)
-{
-    const unsigned long long old =
-        atomicOr(reinterpret_cast<unsigned long long *>(slot), ((unsigned long long)side << 32) | bits);
-    if ((uint32_t)(old >> 32) & (3u ^ side)) {
-        *dst = bswap32(bits | (uint32_t)old);
-        atomicExch(reinterpret_cast<unsigned long long *>(slot), 0ull);
-    }
-}
-
+// The pack's block offsets come from the two plan kernels (k_block_local, k_block_final_wide,
+// which also zeroes the words two blocks share). (r3 measured the alternatives in one launch:
+// a decoupled look-back over pairs of blocks claimed from a counter, 0.60-0.70 ms on 1 GiB C2,
+// and over ranges of 4-16 blocks per workgroup, 0.45-0.50 ms, against 0.373 for this pack after
+// the plan launches: a look-back costs ~2 us per agent-scope round trip, and ranges of blocks
+// long enough to hide it leave the last dispatch round unbalanced.)
 __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ in, uint64_t n,
                                                    const dc_dtable *__restrict__ T,
-                                                   const uint16_t *__restrict__ bh, const uint64_t *__restrict__ d_total,
-                                                   uint64_t bit_base,
+                                                   const uint64_t *__restrict__ block_off, uint64_t bit_base,
                                                    const uint64_t *__restrict__ d_base, uint32_t *__restrict__ out, uint64_t *__restrict__ sync_base,
                                                    uint16_t *__restrict__ sync_len, uint32_t sync_syms,
                                                    uint64_t nblocks, uint64_t words_cap,
-                                                   int *__restrict__ err, int build_dec,
-                                                   uint64_t *__restrict__ lb_flags, uint32_t epoch,
-                                                   uint64_t *__restrict__ xslot, uint32_t *__restrict__ claim)
+                                                   int *__restrict__ err, int build_dec)
 {
     __shared__ uint2 s_tab[256];
     // bit lengths alone (pass A reads 1 byte, not 8): 64 dwords, so at most 2 distinct dwords
@@ -1230,12 +1159,8 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
     __shared__ __attribute__((aligned(16))) uint32_t s_stage[PACK_BLK_WORDS + 4];   // +4: emit's no-op ORs past the end
     __shared__ uint32_t s_scan[4];
     __shared__ uint32_t s_tot[PACK_PIECES][4];
-    __shared__ uint64_t s_excl2[2], s_bits2[2];   // the claimed blocks' offsets (look-back) and bit counts
-    __shared__ uint32_t s_pair;           // the claimed pair of blocks
     static_assert(sizeof(DecBuildLds) <= sizeof(s_stage), "decoder-table builder uses the stage");
     const int t = threadIdx.x;
-    // the claim counter of the next launch (they alternate by epoch; this one started at 0)
-    if (blockIdx.x == 0 && t == 0) claim[(epoch + 1) & 1] = 0u;
     if (build_dec && blockIdx.x == 0) {   // workgroup 0: the decoder tables, beside the pack
         if (T->status == DC_OK)
             dec_tables_build(const_cast<dc_dtable *>(T), *reinterpret_cast<DecBuildLds *>(s_stage));
@@ -1245,7 +1170,7 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
     if (d_base) bit_base += *d_base;   // device-resident shard offset (dist: no host read)
     // device-side guards (no host round trip): a byte without a code (plan error) or an
     // output buffer smaller than the planned stream -> write nothing
-    const uint64_t total = *d_total;
+    const uint64_t total = block_off[nblocks];
     if (err[0] != 0) return;
     if (((bit_base & 31) + total + 31) / 32 > words_cap) {
         if (t == 0) err[2] = 1;   // (pack status: DC_E_CAPACITY)
@@ -1305,18 +1230,9 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
         return;
     }
 
-    // Blocks are claimed in pairs of consecutive blocks from a counter, not dealt by
-    // workgroup index: the look-back makes a block wait for every block before it, so the
-    // order blocks are taken in must be the order they are waited on. (Grid-stride dealing,
-    // wg w taking blocks w and w + G, deadlocked: the second blocks of the first resident
-    // workgroups waited on first blocks of workgroups that could not be dispatched.) Pairs
-    // keep the counter at ~55 claims/us on 1 GiB, below a word's ~88/us.
-    for (;;) {
-    if (t == 0) s_pair = atomicAdd(&claim[epoch & 1], 1u);
-    __syncthreads();
-    const uint64_t pair = s_pair;
-    if (2 * pair >= nblocks) break;
-    for (uint64_t b = 2 * pair; b < nblocks && b < 2 * pair + 2; ++b) {
+    // two blocks per workgroup, grid-stride (r1, 1 GiB C2: 16384 workgroups 0.452 ms against
+    // 0.481 at 4096, 0.469 at 32768, 0.504 at 1024)
+    for (uint64_t b = bx; b < nblocks; b += gstride) {
         const uint64_t blk_start = b * (uint64_t)DC_BLOCK_BYTES;
         const uint64_t blk_end = (blk_start + DC_BLOCK_BYTES < n) ? blk_start + DC_BLOCK_BYTES : n;
         uint4 blkv[PACK_PIECES];
@@ -1330,10 +1246,7 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
             for (int k = 0; k < (int)(DC_BLOCK_BYTES / PACK_TILE); ++k)
                 blkv[k] = LD_PACK(reinterpret_cast<const uint4 *>(in + blk_start + (uint64_t)k * PACK_TILE + (uint64_t)t * 16));
         }
-        if (t < 64 && b == 2 * pair)   // wave 0, while the block's bytes are in flight
-            pack_pair_offset(bh, s_nb8, pair, nblocks, lb_flags, epoch, t, s_excl2, s_bits2);
-        lds_barrier();   // s_excl2, s_bits2
-        const uint64_t s_excl = s_excl2[b & 1], s_bits = s_bits2[b & 1];
+        const uint64_t s_excl = block_off[b], s_bits = block_off[b + 1] - s_excl;
         const uint64_t blk_abs = bit_base + s_excl;
         const uint64_t blk_first_word = blk_abs >> 5;
         uint64_t tile_abs = blk_abs;
@@ -1341,7 +1254,6 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
         // stage origin: the block's first word rounded down to a 16-B boundary of `out`, so
         // the store phase moves whole uint4s (sh = stage index of the block's first word)
         const uint32_t sh = vec_out ? (uint32_t)((blk_first_word - word_base) & 3) : 0u;
-        const bool head_shared = b > 0 && (blk_abs & 31) != 0;   // the first word holds the previous block's tail
         if (full && nw_blk + sh <= PACK_BLK_WORDS) {
             // ---- fast path: the whole block at once, 3 barriers ----
             // lane t of wave w codes piece k = bytes [k*4096 + t*16, +16) of the block, as
@@ -1490,17 +1402,15 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
             } else {
                 for (uint32_t i = t + 1; i < last_plain; i += 256) { dst[i] = bswap32(s_stage[i]); s_stage[i] = 0u; }
             }
-            // the first word: shared with the previous block when the block starts inside it;
-            // the last: shared with the next block when the block ends inside it (the
-            // stream's first and last words are this block's alone)
+            // the first word (shared with the previous block when the block starts inside it)
+            // and the last (shared with the next one when the block ends inside it) are
+            // OR-ed into HBM, where k_block_final_wide zeroed them (no-return atomics)
             if (t == 0) {
-                if (head_shared) pack_exchange(&xslot[b], s_stage[sh], 2u, &dst[sh]);
-                else dst[sh] = bswap32(s_stage[sh]);
+                atomicOr(&dst[sh], bswap32(s_stage[sh]));
                 s_stage[sh] = 0u;
             }
             if (t == 64 && last_plain < nwa && nw_blk > 1) {
-                if (b + 1 < nblocks) pack_exchange(&xslot[b + 1], s_stage[nwa - 1], 1u, &dst[nwa - 1]);
-                else dst[nwa - 1] = bswap32(s_stage[nwa - 1]);
+                atomicOr(&dst[nwa - 1], bswap32(s_stage[nwa - 1]));
                 s_stage[nwa - 1] = 0u;
             }
             lds_barrier();
@@ -1576,7 +1486,7 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
             const uint32_t nfull = (uint32_t)((tile_end_abs >> 5) - TB);
             for (uint32_t i = t; i < nfull; i += 256) {
                 const uint64_t gw = TB + i;
-                if (gw == blk_first_word && head_shared) pack_exchange(&xslot[b], s_stage[i], 2u, &out[gw - word_base]);
+                if (gw == blk_first_word) atomicOr(&out[gw - word_base], bswap32(s_stage[i]));
                 else out[gw - word_base] = bswap32(s_stage[i]);
             }
             __syncthreads();
@@ -1584,19 +1494,12 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
             tile_abs = tile_end_abs;
             __syncthreads();
         }
-        if (t == 0 && (tile_abs & 31)) {   // the block's partial last word
-            const uint64_t gw = tile_abs >> 5;
-            uint32_t *const d = &out[gw - word_base];
-            if (gw == blk_first_word && head_shared) pack_exchange(&xslot[b], s_stage[0], 2u, d);   // (a block inside one word: the stream's last)
-            else if (b + 1 < nblocks) pack_exchange(&xslot[b + 1], s_stage[0], 1u, d);
-            else *d = bswap32(s_stage[0]);
-        }
+        if (t == 0 && (tile_abs & 31)) atomicOr(&out[(tile_abs >> 5) - word_base], bswap32(s_stage[0]));   // partial last word
         __syncthreads();
         // the tile loop leaves its stage dirty: zero it for the next block (rare path)
         for (uint32_t i = 4u * t; i < PACK_BLK_WORDS + 4; i += 1024u)
             *reinterpret_cast<uint4 *>(&s_stage[i]) = make_uint4(0u, 0u, 0u, 0u);
         __syncthreads();
-    }
     }
 }
 
@@ -2708,7 +2611,6 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode9(const uint32_t *__rest
     const uint32_t ntuples = ngroups;   // one group per tuple
     const uint64_t word_base = bit_base >> 5;
     uint32_t *const stw = L.stage[wv];
-    const uint32_t *st[1] = {stw};
     uint32_t *stws[1] = {stw};
     uint32_t *const row = L.rows[wv] + lane * D9_ROW;   // this lane's output row
     const uint32_t stride = gridDim.x * NW;
@@ -4662,6 +4564,24 @@ __global__ __launch_bounds__(64) void k_nyb_chunk_dec(const uint8_t *__restrict_
     if (q != expect) *err = 1;
 }
 
+// ------------------------------------------------------------------------------------
+// HBM copy probe (bench.py's reference rate, MI355X_MICROARCH.md's float4 copy): 16-B loads
+// and stores with the nt hint, 4 in flight per lane, 4096 workgroups grid-striding the buffer
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_copy_probe(const uint4 *__restrict__ src, uint4 *__restrict__ dst, uint64_t n16)
+{
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    for (; i + 3 * stride < n16; i += 4 * stride) {
+        uint4 v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = ld_nt(src + i + k * stride);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) st_nt(dst + i + k * stride, v[k]);
+    }
+    for (; i < n16; i += stride) st_nt(dst + i, ld_nt(src + i));
+}
+
 // =====================================================================================
 // host side
 // =====================================================================================
@@ -4687,10 +4607,6 @@ struct dc_ctx {
     uint32_t *d_fixpos;     size_t fixpos_cap;    // decode redo: bit offset of a flagged chunk
     uint64_t last_groups;                         // groups of the last S = 64 decode (redo mask length)
     uint64_t *d_hloc;                             // this context's last histogram (256 u64; hist[] may be all-reduced)
-    uint64_t *d_lbf;        size_t lbf_cap;       // pack: look-back flag per block (k_huff_pack)
-    uint64_t *d_xslot;      size_t xslot_cap;     // pack: boundary-word exchange slot per block boundary
-    uint32_t pack_epoch;                          // pack launches since the flags were last cleared (1..65535)
-    uint32_t *d_claim;                            // pack: block-pair claim counters (2, alternating by epoch)
     const dc_dtable *plan_table;                  // the table and device total of the last plan
     uint64_t *plan_total;
     void *d_scr;            size_t scr_cap;       // per-wave garbage sinks of the decoders
@@ -4795,9 +4711,7 @@ static int ctx_create(dc_ctx **out, int device, void *stream, bool own)
     c->d_errd = c->d_errp + 128;
     if (hipMalloc((void **)&c->d_hflag, 4096) != hipSuccess || hipMemset(c->d_hflag, 0, 4096) != hipSuccess ||
         hipMalloc((void **)&c->d_hloc, 256 * sizeof(uint64_t)) != hipSuccess ||
-        hipMemset(c->d_hloc, 0, 256 * sizeof(uint64_t)) != hipSuccess ||
-        hipMalloc((void **)&c->d_claim, 2 * sizeof(uint32_t)) != hipSuccess ||
-        hipMemset(c->d_claim, 0, 2 * sizeof(uint32_t)) != hipSuccess) {
+        hipMemset(c->d_hloc, 0, 256 * sizeof(uint64_t)) != hipSuccess) {
         free(c);
         return DC_E_HIP;
     }
@@ -4838,9 +4752,6 @@ void dc_ctx_destroy(dc_ctx *c)
     if (c->d_errp) (void)hipFree(c->d_errp);
     if (c->d_hflag) (void)hipFree(c->d_hflag);
     if (c->d_hloc) (void)hipFree(c->d_hloc);
-    if (c->d_claim) (void)hipFree(c->d_claim);
-    if (c->d_lbf) (void)hipFree(c->d_lbf);
-    if (c->d_xslot) (void)hipFree(c->d_xslot);
     if (c->d_queue) (void)hipFree(c->d_queue);
     if (c->d_fix) (void)hipFree(c->d_fix);
     if (c->d_fixlist) (void)hipFree(c->d_fixlist);
@@ -4949,6 +4860,14 @@ int dc_memset(dc_ctx *c, void *d, int v, size_t bytes)
 {
     if (!bytes) return DC_OK;
     HIPCHK(hipMemsetAsync(d, v, bytes, c->stream));
+    return DC_OK;
+}
+int dc_copy_probe(dc_ctx *c, const void *d_src, void *d_dst, uint64_t bytes)
+{
+    if (!c || (bytes && (!d_src || !d_dst)) || (bytes & 15) || (((uintptr_t)d_src | (uintptr_t)d_dst) & 15)) return DC_E_ARG;
+    if (!bytes) return DC_OK;
+    const uint64_t n16 = bytes / 16, wgs = (n16 + 255) / 256;
+    LAUNCH(c, "copy_probe", k_copy_probe, wgs < 4096 ? wgs : 4096, 256, (const uint4 *)d_src, (uint4 *)d_dst, n16);
     return DC_OK;
 }
 
@@ -5077,33 +4996,46 @@ int dc_huff_encode_plan(dc_ctx *c, const uint8_t *d_in, uint64_t n, int M, int n
     return DC_OK;
 }
 
+// The per-block exclusive bit offsets of the last histogram's input under c->plan_table into
+// c->d_off (nblocks + 1 entries), and with d_words set the zeroed block-boundary words the
+// pack OR-merges into: two launches (one more above PLAN_MAX_WG workgroups of blocks)
+static int plan_offsets(dc_ctx *c, int *err, int *err_next, uint64_t bit_base, const uint64_t *d_base,
+                        uint32_t *d_words, uint64_t words_cap)
+{
+    const uint64_t nb = nblocks_of(c->hist_n);
+    if (ensure((void **)&c->d_off, &c->off_cap, (nb + 1) * sizeof(uint64_t))) return DC_E_HIP;
+    if (nb == 0) {
+        HIPCHK(hipMemsetAsync(c->d_off, 0, sizeof(uint64_t), c->stream));
+        return DC_OK;
+    }
+    const uint64_t nwg = (nb + PLAN_WG_BLOCKS - 1) / PLAN_WG_BLOCKS;
+    if (nwg <= PLAN_MAX_WG) {
+        if (ensure((void **)&c->d_plan, &c->plan_cap, (nb + nwg + 64) * sizeof(uint32_t))) return DC_E_HIP;
+        uint32_t *loc = c->d_plan, *tot = c->d_plan + nb + 32;
+        LAUNCH(c, "block_bits", k_block_local, nwg, 256, (const uint16_t *)c->d_bh, nb, c->plan_table, loc, tot, err);
+        LAUNCH(c, "block_scan", k_block_final_wide, nwg, 256, (const uint32_t *)loc, (const uint32_t *)tot, nb,
+               (uint32_t)nwg, c->d_off, c->d_meta + 15, err_next, bit_base, d_base, d_words, words_cap);
+    } else {
+        LAUNCH(c, "block_bits", k_block_bits, (nb + 3) / 4, 256, (const uint16_t *)c->d_bh, nb, c->plan_table,
+               c->d_off, err);
+        LAUNCH(c, "block_scan", k_block_scan, 1, 1024, c->d_off, nb, c->d_meta + 15, err_next);
+        if (d_words)
+            LAUNCH(c, "zero_bounds", k_zero_bounds, (nb + 1 + 255) / 256, 256, (const uint64_t *)c->d_off, nb, bit_base,
+                   d_base, d_words, words_cap);
+    }
+    return DC_OK;
+}
+
 int dc_huff_plan_offsets(dc_ctx *c, uint64_t *h_off, uint64_t max_entries, uint64_t *h_n)
 {
-    // inspection only: the per-block exclusive bit offsets (the pack computes them itself, by
-    // its look-back), recomputed here by the two plan kernels
+    // inspection (synchronising): the offsets of the last plan, recomputed by the plan kernels
     if (!c || !c->plan_ok || !c->plan_table) return DC_E_STATE;
     const uint64_t nb = nblocks_of(c->hist_n);
     if (h_n) *h_n = nb + 1;
     const uint64_t k = nb + 1 < max_entries ? nb + 1 : max_entries;
-    if (ensure((void **)&c->d_off, &c->off_cap, (nb + 1) * sizeof(uint64_t))) return DC_E_HIP;
-    if (nb == 0) {
-        HIPCHK(hipMemsetAsync(c->d_off, 0, sizeof(uint64_t), c->stream));
-    } else {
-        const uint64_t nwg = (nb + PLAN_WG_BLOCKS - 1) / PLAN_WG_BLOCKS;
-        int *const scratch_err = c->d_err + 12;   // not a plan slot: the flags of the real plan stay
-        if (nwg <= PLAN_MAX_WG) {
-            if (ensure((void **)&c->d_plan, &c->plan_cap, (nb + nwg + 64) * sizeof(uint32_t))) return DC_E_HIP;
-            uint32_t *loc = c->d_plan, *tot = c->d_plan + nb + 32;
-            LAUNCH(c, "block_bits", k_block_local, nwg, 256, (const uint16_t *)c->d_bh, nb, c->plan_table, loc, tot,
-                   scratch_err);
-            LAUNCH(c, "block_scan", k_block_final_wide, nwg, 256, (const uint32_t *)loc, (const uint32_t *)tot, nb,
-                   (uint32_t)nwg, c->d_off, c->d_meta + 15, scratch_err);
-        } else {
-            LAUNCH(c, "block_bits", k_block_bits, (nb + 3) / 4, 256, (const uint16_t *)c->d_bh, nb, c->plan_table,
-                   c->d_off, scratch_err);
-            LAUNCH(c, "block_scan", k_block_scan, 1, 1024, c->d_off, nb, c->d_meta + 15, scratch_err);
-        }
-    }
+    int *const scratch_err = c->d_err + 12;   // not a plan slot: the flags of the real plan stay
+    const int r = plan_offsets(c, scratch_err, scratch_err, 0, nullptr, nullptr, 0);
+    if (r != DC_OK) return r;
     if (k) {
         HIPCHK(hipMemcpyAsync(h_off, c->d_off, k * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
@@ -5131,17 +5063,6 @@ static bool sync_ok(uint32_t S) { return S >= 16 && S <= DC_SYNC_MAX && (S & (S 
 uint64_t dc_huff_sync_chunks(uint64_t n, uint32_t S) { return S ? (n + S - 1) / S : 0; }
 uint64_t dc_huff_sync_groups(uint64_t n, uint32_t S) { return (dc_huff_sync_chunks(n, S) + DC_SYNC_GROUP - 1) / DC_SYNC_GROUP; }
 
-// zeroed on (re)allocation: the look-back flags of epoch 0 are never current, and the
-// exchange slots are empty between launches
-static int ensure_zeroed(dc_ctx *c, void **p, size_t *cap, size_t bytes, bool *fresh)
-{
-    const size_t before = *cap;
-    void *const old = *p;
-    if (ensure(p, cap, bytes)) return DC_E_HIP;
-    *fresh = (*p != old || *cap != before);
-    if (*fresh) HIPCHK(hipMemsetAsync(*p, 0, *cap, c->stream));
-    return DC_OK;
-}
 
 static int pack_impl(dc_ctx *c, const uint8_t *d_in, uint64_t n, const dc_dtable *d_table, uint64_t bit_base,
                      const uint64_t *d_base, uint32_t *d_words, uint64_t words_cap, uint64_t *d_sync_base,
@@ -5153,30 +5074,15 @@ static int pack_impl(dc_ctx *c, const uint8_t *d_in, uint64_t n, const dc_dtable
     if (d_sync_len && !sync_ok(sync_syms)) return DC_E_ARG;
     const uint64_t nb = nblocks_of(n);
     if (nb == 0) return DC_OK;
-    bool fresh = false, fresh2 = false;
-    if (ensure_zeroed(c, (void **)&c->d_lbf, &c->lbf_cap, ((nb + 1) / 2) * sizeof(uint64_t), &fresh) ||
-        ensure_zeroed(c, (void **)&c->d_xslot, &c->xslot_cap, (nb + 1) * sizeof(uint64_t), &fresh2))
-        return DC_E_HIP;
-    if (fresh) {   // epochs restart: so do the claim counters
-        c->pack_epoch = 0;
-        HIPCHK(hipMemsetAsync(c->d_claim, 0, 2 * sizeof(uint32_t), c->stream));
-    }
-    if (++c->pack_epoch > 0xFFFFu) {   // the 16-bit epoch wraps: every flag is cleared once
-        HIPCHK(hipMemsetAsync(c->d_lbf, 0, c->lbf_cap, c->stream));
-        HIPCHK(hipMemsetAsync(c->d_claim, 0, 2 * sizeof(uint32_t), c->stream));
-        c->pack_epoch = 1;
-    }
-    // workgroups enough to keep every CU busy (4 resident per CU), but never more than pairs:
-    // each one claims pairs of blocks until none is left
-    // (r1, static dealing: 16384 workgroups ran 1 GiB C2 in 0.452 ms against 0.481 at 4096,
-    // 0.469 at 32768, 0.504 at 1024)
-    const uint64_t pairs = (nb + 1) / 2;
-    const uint64_t gmax = c->opt_pack_grid ? c->opt_pack_grid : pairs;
-    const uint64_t grid = pairs < gmax ? pairs : gmax;
-    // + workgroup 0: the decoder tables (k_huff_table leaves them to the pack's idle CU time)
-    LAUNCH(c, "huff_pack", k_huff_pack, grid + 1, 256, d_in, n, d_table, (const uint16_t *)c->d_bh,
-           (const uint64_t *)c->plan_total, bit_base, d_base, d_words, d_sync_base, d_sync_len, sync_syms, nb, words_cap,
-           plan_err(c), 1, c->d_lbf, c->pack_epoch, c->d_xslot, c->d_claim);
+    // the blocks' offsets, and the boundary words zeroed (the plan's error flags: its slot)
+    const int r = plan_offsets(c, plan_err(c), plan_err_next(c), bit_base, d_base, d_words, words_cap);
+    if (r != DC_OK) return r;
+    // two blocks per workgroup (grid-stride) + workgroup 0: the decoder tables (k_huff_table
+    // leaves them to the pack's idle CU time)
+    const uint64_t gmax = c->opt_pack_grid ? c->opt_pack_grid : (nb + 1) / 2;
+    const uint64_t grid = nb < gmax ? nb : gmax;
+    LAUNCH(c, "huff_pack", k_huff_pack, grid + 1, 256, d_in, n, d_table, (const uint64_t *)c->d_off, bit_base, d_base,
+           d_words, d_sync_base, d_sync_len, sync_syms, nb, words_cap, plan_err(c), 1);
     c->dec_fresh = d_table;   // workgroup 0 built the decoder tables
     return DC_OK;
 }

@@ -195,6 +195,11 @@ class Codec:
         check("dc_huff_decode", self.L.dc_huff_decode(self.ctx, _ptr(words), bit_base, words.numel(), _ptr(base),
                                                       _ptr(lens), sync_syms, n, _ptr(tab), _ptr(out)))
 
+    def copy_probe(self, src, dst):
+        """dc_copy_probe: a float4 device-to-device copy (the HBM reference rate of bench.py)."""
+        check("dc_copy_probe", self.L.dc_copy_probe(self.ctx, _ptr(src), _ptr(dst), min(src.numel() * src.element_size(),
+                                                                                       dst.numel() * dst.element_size())))
+
     def decode_status(self):
         return int(self.L.dc_huff_decode_status(self.ctx))
 

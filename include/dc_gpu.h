@@ -131,6 +131,9 @@ int dc_free(void *d_ptr);
 int dc_memcpy_h2d(dc_ctx *ctx, void *d_dst, const void *h_src, size_t bytes);
 int dc_memcpy_d2h(dc_ctx *ctx, void *h_dst, const void *d_src, size_t bytes);
 int dc_memset(dc_ctx *ctx, void *d_dst, int value, size_t bytes);
+/* HBM reference rate: a float4 (16-B) device-to-device copy of `bytes` (multiple of 16,
+ * 16-B aligned), nt loads and stores, 4096 workgroups (bench.py's copy probe) */
+int dc_copy_probe(dc_ctx *ctx, const void *d_src, void *d_dst, uint64_t bytes);
 
 /* ---- Huffman, device-resident stages ------------------------------------------------- */
 /* (1) byte histogram of d_in[0..n) -> d_hist[256] (u64). Keeps per-block histograms in
