@@ -2193,7 +2193,6 @@ static __device__ __forceinline__ void d8_issue(uint4 (&v)[NC][5], const D8Geo<N
 // resets the heads for the next launch on the stream.
 #define D8_STATIC_PCT 60
 #define D8_QSTRIDE 1024   /* u32 between heads */
-#define D8_FIX_CNT (9 * D8_QSTRIDE)                /* chunks listed for the exact redo        */
 #define D8_QWORDS (11 * D8_QSTRIDE)
 #define D8_WSCR (2 * 4096 + 66 * 8 + 512)            /* per-wave scratch of the decoders (bytes)  */
 #define D8_SCRATCH_WAVES 4096                        /* waves with a scratch slot (both kernels)  */
@@ -2284,7 +2283,6 @@ static __device__ void d8_stale_exit(int *__restrict__ err, uint32_t *__restrict
 {
     const int t = threadIdx.x;
     if (t == 0) atomicOr(err, 1);
-    if (blockIdx.x == 0 && t == 0) queue[D8_FIX_CNT] = 0u;
     const uint64_t ngroups = ((n + 63) / 64 + DC_SYNC_GROUP - 1) / DC_SYNC_GROUP;
     for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + t; g < ngroups; g += (uint64_t)gridDim.x * blockDim.x)
         fix_mask[g] = 0ull;
@@ -2327,7 +2325,6 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode8(const uint32_t *__rest
         __syncthreads();
         for (int sy = tt; sy < 256; sy += NW * 64)
             if (T->nbits[sy] == 8u) inv[T->code[sy] & 255u] = (uint16_t)sy;
-        if (blockIdx.x == 0 && tt == 0) queue[D8_FIX_CNT] = 0u;
         __syncthreads();
         const uint8_t *const ib = reinterpret_cast<const uint8_t *>(in);
         const uint64_t nthr = (uint64_t)gridDim.x * NW * 64, me = (uint64_t)blockIdx.x * NW * 64 + tt;
@@ -2373,7 +2370,6 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode8(const uint32_t *__rest
     for (int i = t; i < (1 << D8_LUT_BITS); i += NT) L.lut[i] = (uint16_t)(4u | ((i & 255u) << 8));
 #endif
     if (t == 0) L.exhausted = 0;
-    if (blockIdx.x == 0 && t == 0) queue[D8_FIX_CNT] = 0u;   // k_huff_fix_list's counter (runs after)
     __syncthreads();
 
     // the launcher guarantees n < 2^37 (chunk and tuple indices fit 32 bits)
@@ -2603,7 +2599,6 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode9(const uint32_t *__rest
         reinterpret_cast<uint2 *>(L.dlut2)[i] = reinterpret_cast<const uint2 *>(T->dlut2)[i];
     const uint32_t K2 = (uint32_t)T->dlut2_k, kmask = (1u << K2) - 1;
     if (t == 0) L.exhausted = 0;
-    if (blockIdx.x == 0 && t == 0) queue[D8_FIX_CNT] = 0u;   // k_huff_fix_list's counter (runs after)
     __syncthreads();
 
     const uint32_t nchunks = (uint32_t)((n + S - 1) / S);
@@ -2742,10 +2737,8 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode9(const uint32_t *__rest
     }
 }
 
-// Exact decode of the chunks k_huff_decode8 flagged (fix_mask: a bit per chunk, fix_pos: the
-// chunk's first bit), compacted into one list by k_huff_fix_list: one chunk per lane, decoded
-// from its span staged in LDS; the 12-bit table and the canonical tables for longer codes
-// (d8_long's rule) are all in LDS.
+// The exact redo's LDS: the 14-bit table, its second level and the canonical tables of longer
+// codes (d8_long's rule), and a span row per lane.
 #ifndef D8F_WAVES
 #define D8F_WAVES 16   /* 16 x 24-word rows: 0.113 -> 0.091 ms on 1 GiB C2 vs 12 x 32 */
 #endif
@@ -2789,83 +2782,46 @@ static __device__ __noinline__ uint32_t d8_long_lds(uint32_t lo, uint32_t hi, co
     return 0u;
 }
 
-// The flagged chunks as one compact list (chunk indices, any order), so the fixup deals
-// them out in full rounds of 64, evenly over its waves. A 1024-thread workgroup covers 16
-// windows of 64 groups and reserves its room with ONE atomic on `cnt` (a single word
-// saturates near 88 atomics/us: one per wave cost 50 us on 1 GiB). (Dealing whole windows
-// to the fixup's waves instead left them 1 or 2 windows of ~100 chunks each: 2.3x max/mean.)
-__global__ __launch_bounds__(1024) void k_huff_fix_list(const uint64_t *__restrict__ fix_mask, uint32_t ngroups,
-                                                        uint32_t nchunks, uint32_t *__restrict__ list,
-                                                        uint32_t *__restrict__ cnt, int *__restrict__ err_next)
-{
-    __shared__ uint32_t s_w[16];
-    __shared__ uint32_t s_base;
-    if (blockIdx.x == 0 && threadIdx.x < 4) err_next[threadIdx.x] = 0;   // the next decode's error slot
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint32_t g = blockIdx.x * 1024 + threadIdx.x;
-    uint64_t m = g < ngroups ? fix_mask[g] : 0ull;
-    const uint64_t c0 = (uint64_t)g * DC_SYNC_GROUP;   // chunks past the end are never redone
-    if (c0 + DC_SYNC_GROUP > nchunks) m = c0 >= nchunks ? 0ull : m & ((1ull << (nchunks - c0)) - 1);
-    const uint32_t c = (uint32_t)__popcll(m);
-    const uint32_t incl = wave_scan_incl(c);
-    if (lane == 63) s_w[wv] = incl;
-    __syncthreads();
-    uint32_t before = 0, all = 0;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-        const uint32_t x = s_w[q];
-        before += q < wv ? x : 0u;
-        all += x;
-    }
-    if (all == 0) return;   // uniform over the workgroup
-    if (threadIdx.x == 0) s_base = atomicAdd(cnt, all);
-    __syncthreads();
-    uint32_t e = s_base + before + incl - c;
-    while (m) {
-        list[e++] = (uint32_t)c0 + (uint32_t)__builtin_ctzll(m);
-        m &= m - 1;
-    }
-}
-
-// Exact decode of the chunks k_huff_decode8 flagged (fix_pos: the chunk's first bit, from
-// word_base), listed by k_huff_fix_list. Persistent, D8F_WAVES waves per CU; wave w takes
-// rounds w, w + P, ... of 64 list items (one chunk per lane). Per wave a pipeline: while round
-// A decodes from its LDS rows, the spans of round B are in flight into registers and the
-// start positions of round C too. Per symbol a branch-free two-level lookup (the fast
-// decoder's 14-bit table, then the second level on the next K bits: both always read, the
-// first entry's length selects) and a canonical search only for codes past the second level.
-// Output leaves as one u32 per 4 symbols straight to HBM (26 MB on 1 GiB C2: L2 request rate
-// is no concern here).
+// Exact decode of the chunks k_huff_decode8 flagged (fix_mask: a bit per chunk, fix_pos: the
+// chunk's first bit, from word_base), in one launch. Workgroup b takes an equal share of the
+// groups' masks, a window of 1024 at a time (one per thread): popcounts, a workgroup scan, and
+// the window's flagged chunks listed in LDS; its waves take the list in rounds of 64 (one
+// chunk per lane): wave w rounds w, w + 16, ... While round A decodes from its LDS rows, the
+// spans of round B are in flight into registers and the start position of round C too. Per
+// symbol a two-level lookup (the fast decoder's 14-bit table, then the second level on the
+// next K bits only when a lane needs it) and a canonical search only for codes past the
+// second level. Output leaves as one u32 per 4 symbols straight to HBM (26 MB on 1 GiB C2).
+// (r2 listed the chunks in a launch of its own, k_huff_fix_list: 0.008 ms + a launch gap on
+// 1 GiB C2; a flagged chunk falls in any group with the same odds, so equal shares of the
+// groups are equal shares of the work, ~12 rounds per workgroup of 16 waves on C2.)
+#define D8F_LIST 2048   /* listed chunks per pass (LDS) */
 __global__ __launch_bounds__(D8F_WAVES * 64) void k_huff_decode8_fix(const uint32_t *__restrict__ in, uint64_t n,
                                                                     uint64_t nwords, const dc_dtable *__restrict__ T,
                                                                     uint8_t *__restrict__ out, int *__restrict__ err,
-                                                                    const uint32_t *__restrict__ list,
+                                                                    const uint64_t *__restrict__ fix_mask,
                                                                     const uint64_t *__restrict__ fix_pos,
-                                                                    uint32_t *__restrict__ queue)
+                                                                    int *__restrict__ err_next)
 {
     constexpr uint32_t S = 64;
+    constexpr int NT = D8F_WAVES * 64;
     __shared__ FixLds F;
+    __shared__ uint32_t s_list[D8F_LIST];
+    __shared__ uint32_t s_wsum[D8F_WAVES];
     const int t = threadIdx.x, lane = t & 63, wv = __builtin_amdgcn_readfirstlane(t >> 6);
-#ifdef DC_DIAG
-    D8_STAMP(f0);
-    unsigned long long f_dec = 0, f_rounds = 0, f_wait = 0, f_first = 0;
-#endif
-    // rounds of 64 list items: wave wid takes rounds wid, wid + P, ...; the first two rounds'
-    // chunks and positions are requested before the table copy, so their latency overlaps it
-    // written by k_huff_fix_list (an earlier launch): a plain scalar load
-    const uint32_t total = ((const __attribute__((address_space(4))) uint32_t *)queue)[D8_FIX_CNT];
-    const uint32_t nrounds = (total + 63) / 64;
-    const uint32_t wstride = gridDim.x * D8F_WAVES;
-    uint32_t ra = blockIdx.x * D8F_WAVES + wv;   // round of A; B and C follow by the stride
-    auto item_ok = [&](uint32_t r) -> bool { return r < nrounds && r * 64 + (uint32_t)lane < total; };
-    auto chunk_of = [&](uint32_t r) -> uint32_t { return item_ok(r) ? list[r * 64 + lane] : ~0u; };
+    if (blockIdx.x == 0 && t < 4) err_next[t] = 0;   // the next decode's error slot
+    const uint32_t nchunks = (uint32_t)((n + S - 1) / S);
+    const uint32_t ngroups = (nchunks + DC_SYNC_GROUP - 1) / DC_SYNC_GROUP;
+    const uint32_t g0 = (uint32_t)((uint64_t)ngroups * blockIdx.x / gridDim.x);
+    const uint32_t g1 = (uint32_t)((uint64_t)ngroups * (blockIdx.x + 1) / gridDim.x);
     const uint32_t K2 = (uint32_t)T->dlut2_k, kmask = (1u << K2) - 1;
-    uint32_t cha, chb;
-    {   // the tables into LDS: their loads first, then the first two rounds' list items (in
-        // flight during the stores); their positions, which depend on them, after the barrier
-        // (the positions' dependent loads issued before the copy held its stores back: 29k of a
-        // wave's 121k cycles, r2 diag)
-        constexpr int NT = D8F_WAVES * 64;
+    auto window_mask = [&](uint32_t g) -> uint64_t {   // chunks past the end are never redone
+        uint64_t m = g < g1 ? fix_mask[g] : 0ull;
+        const uint64_t c0 = (uint64_t)g * DC_SYNC_GROUP;
+        if (c0 + DC_SYNC_GROUP > nchunks) m = c0 >= nchunks ? 0ull : m & ((1ull << (nchunks - c0)) - 1);
+        return m;
+    };
+    uint64_t mk = window_mask(g0 + t);   // the first window's masks, in flight during the table copy
+    {   // the tables into LDS: all loads first, then the stores
         static_assert((1 << D8F_LUT_BITS) / 8 <= 2 * NT && DC_LUT2_CAP / 4 <= 2 * NT && DC_MAX_SYMS <= NT &&
                       DC_MAX_DIGITS + 1 <= NT, "one copy pass");
         const uint4 *l1 = reinterpret_cast<const uint4 *>(T->dlut14);
@@ -2877,8 +2833,6 @@ __global__ __launch_bounds__(D8F_WAVES * 64) void k_huff_decode8_fix(const uint3
         const bool cn = t <= DC_MAX_DIGITS;
         const uint32_t fi = cn ? T->first[t] : 0u, co = cn ? T->count[t] : 0u, sa = cn ? T->start[t] : 0u;
         const uint64_t li = t < 33 ? T->lim[t] : 0ull;
-        cha = chunk_of(ra);
-        chb = chunk_of(ra + wstride);
         reinterpret_cast<uint4 *>(F.lut)[t] = a0;
         if (t + NT < N1) reinterpret_cast<uint4 *>(F.lut)[t + NT] = a1;
         if (t < N2) reinterpret_cast<uint2 *>(F.lut2)[t] = b0;
@@ -2887,17 +2841,10 @@ __global__ __launch_bounds__(D8F_WAVES * 64) void k_huff_decode8_fix(const uint3
         if (cn) { F.first[t] = fi; F.count[t] = co; F.start[t] = sa; }
         if (t < 33) F.lim[t] = li;
     }
-    uint64_t posa = fix_pos[cha != ~0u ? cha : 0u];
-    uint64_t posb = fix_pos[chb != ~0u ? chb : 0u];
-    __syncthreads();
     const int nary = T->n_ary, w = T->w;
     const bool pow2 = (nary & (nary - 1)) == 0;
     uint32_t *row = F.rows[wv] + lane * (D8F_ROW + 1);
     int bad = 0;
-
-#ifdef DC_DIAG
-    D8_STAMP(f1);
-#endif
     // a span's 16-B aligned first word (clamped so that a whole row can be read)
     auto row_base = [&](uint64_t pos) -> uint64_t {
         const uint64_t lim = nwords > D8F_ROW ? (nwords - D8F_ROW) & ~3ull : 0ull;
@@ -2918,104 +2865,111 @@ __global__ __launch_bounds__(D8F_WAVES * 64) void k_huff_decode8_fix(const uint3
             row[4 * k + 3] = brev8(v[k].w);
         }
     };
-    uint4 sv[D8F_ROW / 4];
-#ifdef DC_DIAG
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    D8_STAMP(fp0);
-    const unsigned long long f_pos = fp0 - f1;
-#endif
-    if (ra < nrounds) load_row(sv, row_base(posa));
-    while (ra < nrounds) {
-        // stage round A's spans, then start round B's spans and round C's positions
-        const uint64_t a0 = row_base(posa);
-#ifdef DC_DIAG
-        D8_STAMP(fw0);
-#endif
-        put_row(sv);
-#ifdef DC_DIAG
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        D8_STAMP(fw1);
-        f_wait += fw1 - fw0;
-        if (f_rounds == 0) f_first = fw1 - f1;
-#endif
-        load_row(sv, row_base(posb));
-        const uint32_t chc = chunk_of(ra + 2 * wstride);
-        const uint64_t posc = fix_pos[chc != ~0u ? chc : 0u];
-        // decode round A
-        // (a listed chunk is < nchunks by construction; the clamp keeps a corrupt list from
-        // writing past the output)
-        const bool valid = cha != ~0u && (uint64_t)cha * S < n;
-        const uint64_t s0 = (uint64_t)(valid ? cha : 0u) * S;
-        const uint32_t cntc = valid ? (uint32_t)((n - s0 < S) ? n - s0 : S) : 0u;
-        uint32_t c = (uint32_t)(posa - (a0 << 5));
-        uint64_t rb = a0;   // word of `in` at row word 0
-#ifdef DC_DIAG
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        D8_STAMP(f2);
-#endif
-        uint4 *const o128 = reinterpret_cast<uint4 *>(out + s0);
-        for (uint32_t p = 0; p < (cntc + 15) / 16; ++p) {
-          uint32_t ov[4];
+    for (uint32_t wb = g0; wb < g1; wb += NT) {
+        // this window's flagged chunks: the thread of group g lists its chunks after those of
+        // the groups before it
+        const uint32_t c = (uint32_t)__popcll(mk);
+        const uint32_t incl = wave_scan_incl(c);
+        if (lane == 63) s_wsum[wv] = incl;
+        __syncthreads();   // (also: the table copy, the previous window's rounds)
+        uint32_t before = 0, total = 0;
 #pragma unroll
-          for (int q4 = 0; q4 < 4; ++q4) {
-            const uint32_t q = 4 * p + q4;
-            // 4 codes take <= 128 bits (+ 64 of window): re-stage a row that runs short
-            if (c >= 32 * (D8F_ROW - 6)) {
-                const uint32_t adv = (c >> 5) & ~3u;
-                rb += adv;
-                c -= adv * 32;
-                const uint64_t nq = rb < nwords ? (nwords - rb) / 4 : 0ull;
-#pragma unroll 1
-                for (int k = 0; k < D8F_ROW / 4; ++k) {   // rolled: no second set of row registers
-                    const uint4 v = (uint64_t)k < nq ? reinterpret_cast<const uint4 *>(in + rb)[k] : make_uint4(0u, 0u, 0u, 0u);
-                    row[4 * k] = brev8(v.x);
-                    row[4 * k + 1] = brev8(v.y);
-                    row[4 * k + 2] = brev8(v.z);
-                    row[4 * k + 3] = brev8(v.w);
-                }
-            }
-            uint32_t ob = 0;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const uint32_t a = c >> 5;
-                const uint32_t lo = __builtin_amdgcn_alignbit(row[a + 1], row[a], c);
-                uint32_t e = F.lut[lo & ((1u << D8F_LUT_BITS) - 1)];
-                if (__builtin_amdgcn_ballot_w64((e & 255u) == 0u)) {   // the second level, only when a lane needs it
-                    const uint32_t i2 = min(((e >> 8) << K2) | ((lo >> DC_LUT_BITS) & kmask), (uint32_t)DC_LUT2_CAP - 1);
-                    const uint32_t e2 = F.lut2[(e & 255u) ? 0u : i2];
-                    e = (e & 255u) ? e : e2;
-                }
-                if (e == 0) {   // past the second level (rare): canonical search
-                    const uint32_t hi = __builtin_amdgcn_alignbit(row[a + 2], row[a + 1], c);
-                    e = d8_long_lds(lo, hi, F, nary, w, pow2);
-                    // the stream's partial last chunk decodes past its end: no error there
-                    bad |= (e == 0 && 4 * q + k < cntc);
-                }
-                ob |= ((e >> 8) & 255u) << (8 * k);
-                c += e & 255u;
-            }
-            ov[q4] = ob;
-          }
-          if (16 * p + 16 <= cntc) o128[p] = make_uint4(ov[0], ov[1], ov[2], ov[3]);
-          else   // the stream's partial last chunk
-            for (uint32_t k = 0; 16 * p + k < cntc; ++k) out[s0 + 16 * p + k] = (uint8_t)(ov[k >> 2] >> (8 * (k & 3)));
+        for (int q = 0; q < D8F_WAVES; ++q) {
+            const uint32_t x = s_wsum[q];
+            before += q < wv ? x : 0u;
+            total += x;
         }
-#ifdef DC_DIAG
-        D8_STAMP(f3);
-        f_dec += f3 - f2;
-        ++f_rounds;
-#endif
-        ra += wstride;
-        cha = chb; posa = posb;
-        chb = chc; posb = posc;
+        const uint64_t m_me = mk;
+        const uint32_t c0 = (wb + (uint32_t)t) * DC_SYNC_GROUP;
+        if (wb + NT < g1) mk = window_mask(wb + NT + t);   // the next window's masks, in flight
+        for (uint32_t part = 0; part < total; part += D8F_LIST) {   // (one part unless > 2048 chunks)
+            {
+                uint32_t e = before + incl - c;
+                uint64_t m = m_me;
+                while (m) {
+                    if (e >= part && e < part + D8F_LIST) s_list[e - part] = c0 + (uint32_t)__builtin_ctzll(m);
+                    ++e;
+                    m &= m - 1;
+                }
+            }
+            __syncthreads();
+            const uint32_t cnt = min(total - part, (uint32_t)D8F_LIST), nrounds = (cnt + 63) / 64;
+            auto chunk_of = [&](uint32_t r) -> uint32_t {
+                return r < nrounds && r * 64 + (uint32_t)lane < cnt ? s_list[r * 64 + lane] : ~0u;
+            };
+            uint32_t ra = (uint32_t)wv;   // round of A; B and C follow by the stride
+            uint32_t cha = chunk_of(ra), chb = chunk_of(ra + D8F_WAVES);
+            uint64_t posa = fix_pos[cha != ~0u ? cha : 0u];
+            uint64_t posb = fix_pos[chb != ~0u ? chb : 0u];
+            uint4 sv[D8F_ROW / 4];
+            if (ra < nrounds) load_row(sv, row_base(posa));
+            while (ra < nrounds) {
+                // stage round A's spans, then start round B's spans and round C's positions
+                const uint64_t a0 = row_base(posa);
+                put_row(sv);
+                load_row(sv, row_base(posb));
+                const uint32_t chc = chunk_of(ra + 2 * D8F_WAVES);
+                const uint64_t posc = fix_pos[chc != ~0u ? chc : 0u];
+                // decode round A (the clamp keeps a corrupt mask from writing past the output)
+                const bool valid = cha != ~0u && (uint64_t)cha * S < n;
+                const uint64_t s0 = (uint64_t)(valid ? cha : 0u) * S;
+                const uint32_t cntc = valid ? (uint32_t)((n - s0 < S) ? n - s0 : S) : 0u;
+                uint32_t cb = (uint32_t)(posa - (a0 << 5));
+                uint64_t rb = a0;   // word of `in` at row word 0
+                uint4 *const o128 = reinterpret_cast<uint4 *>(out + s0);
+                for (uint32_t p = 0; p < (cntc + 15) / 16; ++p) {
+                    uint32_t ov[4];
+#pragma unroll
+                    for (int q4 = 0; q4 < 4; ++q4) {
+                        const uint32_t q = 4 * p + q4;
+                        // 4 codes take <= 128 bits (+ 64 of window): re-stage a row that runs short
+                        if (cb >= 32 * (D8F_ROW - 6)) {
+                            const uint32_t adv = (cb >> 5) & ~3u;
+                            rb += adv;
+                            cb -= adv * 32;
+                            const uint64_t nq = rb < nwords ? (nwords - rb) / 4 : 0ull;
+#pragma unroll 1
+                            for (int k = 0; k < D8F_ROW / 4; ++k) {   // rolled: no second set of row registers
+                                const uint4 v = (uint64_t)k < nq ? reinterpret_cast<const uint4 *>(in + rb)[k] : make_uint4(0u, 0u, 0u, 0u);
+                                row[4 * k] = brev8(v.x);
+                                row[4 * k + 1] = brev8(v.y);
+                                row[4 * k + 2] = brev8(v.z);
+                                row[4 * k + 3] = brev8(v.w);
+                            }
+                        }
+                        uint32_t ob = 0;
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) {
+                            const uint32_t a = cb >> 5;
+                            const uint32_t lo = __builtin_amdgcn_alignbit(row[a + 1], row[a], cb);
+                            uint32_t e = F.lut[lo & ((1u << D8F_LUT_BITS) - 1)];
+                            if (__builtin_amdgcn_ballot_w64((e & 255u) == 0u)) {   // the second level, only when a lane needs it
+                                const uint32_t i2 = min(((e >> 8) << K2) | ((lo >> DC_LUT_BITS) & kmask), (uint32_t)DC_LUT2_CAP - 1);
+                                const uint32_t e2 = F.lut2[(e & 255u) ? 0u : i2];
+                                e = (e & 255u) ? e : e2;
+                            }
+                            if (e == 0) {   // past the second level (rare): canonical search
+                                const uint32_t hi = __builtin_amdgcn_alignbit(row[a + 2], row[a + 1], cb);
+                                e = d8_long_lds(lo, hi, F, nary, w, pow2);
+                                // the stream's partial last chunk decodes past its end: no error there
+                                bad |= (e == 0 && 4 * q + k < cntc);
+                            }
+                            ob |= ((e >> 8) & 255u) << (8 * k);
+                            cb += e & 255u;
+                        }
+                        ov[q4] = ob;
+                    }
+                    if (16 * p + 16 <= cntc) o128[p] = make_uint4(ov[0], ov[1], ov[2], ov[3]);
+                    else   // the stream's partial last chunk
+                        for (uint32_t k = 0; 16 * p + k < cntc; ++k) out[s0 + 16 * p + k] = (uint8_t)(ov[k >> 2] >> (8 * (k & 3)));
+                }
+                ra += D8F_WAVES;
+                cha = chb; posa = posb;
+                chb = chc; posb = posc;
+            }
+            __syncthreads();   // the list is rewritten by the next part or window
+        }
     }
-#ifdef DC_DIAG
-    D8_STAMP(f4);
-    if (lane == 0) {
-        unsigned long long *gg = g_d8diag + (blockIdx.x * D8F_WAVES + wv) * 4;
-        gg[0] = f4 - f0; gg[1] = (f1 - f0) | (f_pos << 32); gg[2] = f_dec; gg[3] = f_rounds | (f_wait << 8) | (f_first << 36);
-    }
-#endif
     if (bad) atomicOr(err, 1);
 }
 
@@ -3257,6 +3211,19 @@ __constant__ uint8_t c_static_rank[256];   // " etaoins" -> 0..7, else 0xFF (ini
 
 static __device__ __forceinline__ bool is_lower(uint32_t b) { return b >= 'a' && b <= 'z'; }
 
+// The static dictionary " etaoins" (initialize_dictionary, nybble_compression.c:540-563) as the
+// bytes of one u64, entry k in byte k: the rank of x is the position of the zero byte of
+// dict ^ (x * 0x01..01) (the lowest flagged byte of the SWAR zero test is exact), 0xFF when
+// absent. (A __constant__ byte table cost one divergent load per element.)
+#define NYB_DICT 0x736e696f61746520ull
+static __device__ __forceinline__ uint32_t static_rank(uint32_t x)
+{
+    constexpr uint64_t ones = 0x0101010101010101ull;
+    const uint64_t t = NYB_DICT ^ (ones * (uint64_t)x);
+    const uint64_t z = (t - ones) & ~t & (ones << 7);
+    return z ? (uint32_t)__builtin_ctzll(z) >> 3 : 0xFFu;
+}
+
 // A lane's 16 elements read their bytes from one window of 20 bytes: window byte r = stream
 // byte g0 - 1 + r, g0 = the byte of the lane's first element (element j <-> byte j + FSM_OFF).
 // Lanes' windows start 16 bytes apart, so the misalignment m of the window start is the same
@@ -3341,9 +3308,22 @@ static __device__ __forceinline__ Fsm elem_fsm(const FsmWin &W, int k, uint64_t 
 
 // the lane's 16 ranks (adaptive nybble: aux.rk, element-indexed and 16-B aligned at j0), or
 // the static dictionary's ranks of the window bytes
+// the static ranks in LDS (one byte per value, filled by the workgroup: fsm_rank_table):
+// random reads of 64 dwords, mostly broadcasts on text (the SWAR search of the dictionary, a
+// 64-bit multiply and zero test per element, made the tile count kernel VALU-bound: 0.68 ->
+// 0.94 ms per GiB)
+static __device__ __forceinline__ void fsm_rank_table(uint8_t *s_rank)
+{
+    if (threadIdx.x < 64) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v |= static_rank(4u * threadIdx.x + q) << (8 * q);
+        reinterpret_cast<uint32_t *>(s_rank)[threadIdx.x] = v;
+    }
+}
 template <int M>
 static __device__ __forceinline__ void fsm_ranks(const FsmWin &W, const FsmAux &aux, uint64_t j0, uint64_t nelem,
-                                                 uint32_t (&rk)[16])
+                                                 uint32_t (&rk)[16], const uint8_t *s_rank)
 {
     if (M != M_NYB_ENC) return;
     if (aux.rk) {
@@ -3360,7 +3340,7 @@ static __device__ __forceinline__ void fsm_ranks(const FsmWin &W, const FsmAux &
         for (int k = 0; k < 16; ++k) rk[k] = (w4[k >> 2] >> (8 * (k & 3))) & 255u;
     } else {
 #pragma unroll
-        for (int k = 0; k < 16; ++k) rk[k] = c_static_rank[W.b(k + 1)];
+        for (int k = 0; k < 16; ++k) rk[k] = s_rank[W.b(k + 1)];
     }
 }
 
@@ -3369,7 +3349,9 @@ __global__ __launch_bounds__(256) void k_fsm_tiles(const uint8_t *__restrict__ i
                                                    uint64_t nelem, uint4 *__restrict__ summ, FsmAux aux)
 {
     __shared__ uint4 s_f[FSM_SUB][4];   // wave totals per chunk
+    __shared__ __attribute__((aligned(4))) uint8_t s_rank[256];
     const int t = threadIdx.x;
+    if (M == M_NYB_ENC && !aux.rk) { fsm_rank_table(s_rank); __syncthreads(); }
     // chunk c of the tile: elements [c * 4096 + 16 t, +16) for lane t (coalesced per chunk);
     // all chunks' windows are loaded before any is walked
     FsmWin W[FSM_SUB];
@@ -3383,7 +3365,7 @@ __global__ __launch_bounds__(256) void k_fsm_tiles(const uint8_t *__restrict__ i
         Fsm f = fsm_id();
         if (j0 < nelem) {
             uint32_t rk[16];
-            fsm_ranks<M>(W[c], aux, j0, nelem, rk);
+            fsm_ranks<M>(W[c], aux, j0, nelem, rk, s_rank);
 #pragma unroll
             for (int k = 0; k < 16; ++k)
                 if (j0 + k < nelem) f = fsm_then(f, elem_fsm<M>(W[c], k, len, j0 + k, M == M_NYB_ENC ? rk[k] : 0u));
@@ -3513,12 +3495,15 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
                                                    const uint64_t *__restrict__ meta, uint8_t *__restrict__ out,
                                                    FsmAux aux)
 {
+    static_assert(M == M_NYB_ENC || M == M_NYB_DEC || M == M_NYB_DBODY, "nybble modes (the small codec: k_small_write)");
     // the tile's output (<= 2 bytes per element) is staged in LDS, s_out[x] = out[o_al + x]
     // with o_al the 16-B granule of its first byte, then stored as whole uint4s (bytes only in
     // the two granules shared with the neighbouring tiles)
     __shared__ uint4 s_f[FSM_SUB][4];   // wave totals per chunk
     __shared__ __attribute__((aligned(16))) uint8_t s_out[2 * FSM_TILE + 32];
+    __shared__ __attribute__((aligned(4))) uint8_t s_rank[256];
     const int t = threadIdx.x;
+    if (M == M_NYB_ENC && !aux.rk) fsm_rank_table(s_rank);
     const bool nyb_whole = M == M_NYB_ENC && aux.whole;
     const bool enc = FsmMode<M>::enc || nyb_whole;
     const uint64_t body = (M == M_NYB_ENC) ? meta[0] + (aux.is_last ? meta[1] : 0) : meta[0];
@@ -3537,6 +3522,9 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
         else if (M == M_SMALL_ENC) { out[0] = 8; out[1] = in[0]; }
         else { out[0] = in[1]; }
     }
+    for (uint32_t i = (uint32_t)t; i < (2 * FSM_TILE + 32) / 16; i += 256)   // the stage is OR-merged into
+        reinterpret_cast<uint4 *>(s_out)[i] = make_uint4(0u, 0u, 0u, 0u);
+    if (M == M_NYB_ENC && !aux.rk) __syncthreads();   // s_rank (the stage: ordered by the scan's barrier)
     FsmWin W_[FSM_SUB];
 #pragma unroll
     for (int c = 0; c < FSM_SUB; ++c)
@@ -3552,7 +3540,7 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
         Fsm f = fsm_id();
         if (j0 < nelem) {
             uint32_t rk[16];
-            fsm_ranks<M>(W_[c], aux, j0, nelem, rk);
+            fsm_ranks<M>(W_[c], aux, j0, nelem, rk, s_rank);
 #pragma unroll
             for (int k = 0; k < 16; ++k)
                 if (j0 + k < nelem) f = fsm_then(f, elem_fsm<M>(W_[c], k, len, j0 + k, M == M_NYB_ENC ? rk[k] : 0u));
@@ -3591,76 +3579,76 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
     // granule of the tile's first byte, relative to out (negative when out is unaligned and
     // the tile starts in out's first granule)
     const int64_t o_al = (int64_t)((((uintptr_t)(out + o_tile)) & ~(uintptr_t)15) - (uintptr_t)out);
-#define so(o) s_out[(uint32_t)((int64_t)(o) - o_al)]   /* staged out[o] */
-    const uint8_t *tbl = (const uint8_t *)(aux.tokens ? "\x80\x81\x82\x83\x84\x85\x86\x87" : " etaoins");
+    // Each lane's output is one contiguous run (its elements in order): the bytes are computed
+    // branch-free per element (count 0-2, value, next state) and packed into a 64-bit
+    // accumulator, whose complete dwords are OR-ed into the zeroed LDS stage (dwords shared
+    // with the neighbouring lanes' runs merge without ordering). (r2 stored each byte into the
+    // stage under per-element branches: 2.0 ms per GiB of nybble encode.)
+    // hit table: " etaoins" as one u64, or the token bytes 0x80 | rank (aux.tokens)
+    const uint64_t tblv = aux.tokens ? 0x8786858483828180ull : NYB_DICT;
+    uint32_t *const s_out32 = reinterpret_cast<uint32_t *>(s_out);
 #pragma unroll
     for (int c = 0; c < FSM_SUB; ++c) {
         const uint64_t j0 = (uint64_t)blockIdx.x * FSM_TILE + (uint64_t)c * 4096 + (uint64_t)t * 16;
+        if (j0 >= nelem) continue;
         const FsmWin &W = W_[c];
-        uint64_t o = o_c[c];
+        const uint64_t o0 = o_c[c];
         uint32_t s = st_c[c];
         uint32_t rk[16];
-        if (j0 < nelem) fsm_ranks<M>(W, aux, j0, nelem, rk);
-        if (j0 < nelem) {
+        fsm_ranks<M>(W, aux, j0, nelem, rk, s_rank);
+        const uint32_t P = (uint32_t)((int64_t)o0 - o_al);   // stage byte of the lane's first output
+        uint32_t di = P >> 2, nb = 8u * (P & 3u);
+        uint64_t acc = 0;
+        const uint32_t kend = nelem - j0 < 16 ? (uint32_t)(nelem - j0) : 16u;
 #pragma unroll
-            for (int k = 0; k < 16; ++k) {
+        for (int k = 0; k < 16; ++k) {
+            const bool in_range = (uint32_t)k < kend;
+            const uint32_t x = W.b(k + 1);
+            uint32_t val, cnt, sn;
+            if (M == M_NYB_ENC) {
+                const uint32_t r = rk[k];
+                const bool hit = r != 0xFF;
+                // the rank of the pending hit (the element before): this lane's, or the one
+                // before the lane (a rank of the previous window byte, or the shard's carried one)
                 const uint64_t j = j0 + k;
-                if (j >= nelem) break;
-                const uint32_t x = W.b(k + 1);
-                if (M == M_NYB_ENC) {
-                    const uint64_t i = j + 1;
-                    const uint32_t r = rk[k];
-                    if (r != 0xFF) {
-                        if (s == 1) {
-                            const uint32_t rp = k ? rk[k - 1] : (j ? (aux.rk ? (uint32_t)aux.rk[j - 1]
-                                                                            : (uint32_t)c_static_rank[W.b(0)])
-                                                                   : aux.pend_rank);
-                            so(o++) = (uint8_t)(((8u | rp) << 4) | (8u | r));
-                            s = 0;
-                        } else {
-                            s = 1;
-                            if (aux.is_last && i == len - 1) out[o] = (uint8_t)x;   // odd tail (:1000-1009)
-                        }
-                    } else {
-                        if (s == 1) { so(o++) = (uint8_t)W.b(k); so(o++) = (uint8_t)x; }
-                        else so(o++) = (uint8_t)x;
-                        s = 0;
-                    }
-                } else if (M == M_NYB_DEC || M == M_NYB_DBODY) {
-                    const uint64_t kk = M == M_NYB_DBODY ? j : j + 2;
-                    const uint32_t h = x >> 4, l = x & 15;
-                    const uint32_t nxt = (kk + 1 < len) ? (W.b(k + 2) >> 4) : 0u;
-                    if (s == 0) {
-                        if (h & 8) {
-                            so(o++) = tbl[h & 7];
-                            if (l & 8) { so(o++) = tbl[l & 7]; s = 0; }
-                            else { so(o++) = (uint8_t)(((l & 7) << 4) + nxt); s = 1; }
-                        } else {
-                            so(o++) = (uint8_t)x;
-                            s = 0;
-                        }
-                    } else {
-                        if (l & 8) { so(o++) = tbl[l & 7]; s = 0; }
-                        else { so(o++) = (uint8_t)(((l & 7) << 4) + nxt); s = 1; }
-                    }
-                } else if (FsmMode<M>::small_enc) {
-                    const uint64_t i = j + 1;
-                    const bool second = (M == M_SMALL_BODY1 || i >= 2) && W.b(k) == ' ' && is_lower(x);
-                    if (!second) {
-                        const uint32_t nx = W.b(k + 2);
-                        if (x == ' ' && i + 1 < len && is_lower(nx)) so(o++) = (uint8_t)(0x80 + nx);
-                        else so(o++) = (uint8_t)x;
-                    }
-                } else {
-                    if (x >= 0x80) { so(o++) = ' '; so(o++) = (uint8_t)(x - 0x80); }
-                    else so(o++) = (uint8_t)x;
+                const uint32_t rp = k ? rk[k - 1]
+                                      : (j ? (aux.rk ? (uint32_t)aux.rk[j - 1] : (uint32_t)s_rank[W.b(0)]) : aux.pend_rank);
+                const uint32_t pair = (((8u | rp) << 4) | (8u | r)) & 255u;
+                cnt = hit ? s : 1u + s;
+                val = hit ? (s ? pair : 0u) : (s ? (W.b(k) | (x << 8)) : x);   // (no bits when cnt = 0)
+                sn = hit ? (s ^ 1u) : 0u;
+                if (hit && !s && aux.is_last && j + 1 == len - 1 && in_range)   // odd tail (:1000-1009)
+                    out[o0 + ((nb + 32u * (di - (P >> 2)) - 8u * (P & 3u)) >> 3)] = (uint8_t)x;
+            } else {   // M_NYB_DEC / M_NYB_DBODY: compressed byte x, state s = "at the low nybble"
+                const uint64_t kk = M == M_NYB_DBODY ? j0 + k : j0 + k + 2;
+                const uint32_t h = x >> 4, l = x & 15u;
+                const uint32_t nxt = (kk + 1 < len) ? (W.b(k + 2) >> 4) : 0u;
+                const uint32_t lo_b = (l & 8u) ? (uint32_t)(tblv >> (8u * (l & 7u))) & 255u : ((l & 7u) << 4) + nxt;
+                const uint32_t lo_s = (l & 8u) ? 0u : 1u;
+                const uint32_t hi_b = (uint32_t)(tblv >> (8u * (h & 7u))) & 255u;
+                const bool two = !s && (h & 8u);
+                val = s ? lo_b : (two ? (hi_b | (lo_b << 8)) : x);
+                cnt = two ? 2u : 1u;
+                sn = (s || two) ? lo_s : 0u;
+            }
+            if (in_range) {
+                acc |= (uint64_t)val << nb;
+                nb += 8u * cnt;
+                s = sn;
+            }
+            if (k & 1) {   // <= 32 bits per 2 elements: at most one complete dword
+                if (nb >= 32u) {
+                    atomicOr(&s_out32[di], (uint32_t)acc);
+                    acc >>= 32;
+                    nb -= 32u;
+                    ++di;
                 }
             }
         }
+        if (nb) atomicOr(&s_out32[di], (uint32_t)acc);
     }
     __syncthreads();
     // store [o_tile, end): whole granules as uint4, the first and last granule bytewise
-#undef so
     const int64_t end = (int64_t)s_end, beg = (int64_t)o_tile;
     if (end > beg) {
         const int64_t ng = (end - o_al + 15) / 16;
@@ -4603,7 +4591,6 @@ struct dc_ctx {
     const dc_dtable *dec_fresh;                   // decoder tables current: this context's last pack built them
     uint32_t *d_queue;                            // decode tuple scheduler heads (D8Sched)
     uint32_t *d_fix;        size_t fix_cap;       // decode redo: a u64 chunk mask per group
-    uint32_t *d_fixlist;    size_t fixlist_cap;   // decode redo: flagged chunk indices, compacted
     uint32_t *d_fixpos;     size_t fixpos_cap;    // decode redo: bit offset of a flagged chunk
     uint64_t last_groups;                         // groups of the last S = 64 decode (redo mask length)
     uint64_t *d_hloc;                             // this context's last histogram (256 u64; hist[] may be all-reduced)
@@ -4754,7 +4741,6 @@ void dc_ctx_destroy(dc_ctx *c)
     if (c->d_hloc) (void)hipFree(c->d_hloc);
     if (c->d_queue) (void)hipFree(c->d_queue);
     if (c->d_fix) (void)hipFree(c->d_fix);
-    if (c->d_fixlist) (void)hipFree(c->d_fixlist);
     if (c->d_fixpos) (void)hipFree(c->d_fixpos);
     if (c->d_scr) (void)hipFree(c->d_scr);
     if (c->d_meta) (void)hipFree(c->d_meta);
@@ -5190,12 +5176,8 @@ static int decode_impl(dc_ctx *c, const uint32_t *d_words, uint64_t bit_base, co
         }
 #undef D8_LAUNCH
         c->last_groups = groups;
-        if (ensure((void **)&c->d_fixlist, &c->fixlist_cap, (groups * 64 + 64) * sizeof(uint32_t))) return DC_E_HIP;
-        const uint64_t nchunks = (n + 63) / 64;
-        LAUNCH(c, "huff_fix_list", k_huff_fix_list, (groups + 1023) / 1024, 1024, (const uint64_t *)c->d_fix,
-               (uint32_t)groups, (uint32_t)nchunks, c->d_fixlist, c->d_queue + D8_FIX_CNT, derr_next);
         LAUNCH(c, "huff_decode_fix", k_huff_decode8_fix, 256, D8F_WAVES * 64, d_words, n, words, d_table, d_out,
-               derr, (const uint32_t *)c->d_fixlist, (const uint64_t *)c->d_fixpos, c->d_queue);
+               derr, (const uint64_t *)c->d_fix, (const uint64_t *)c->d_fixpos, derr_next);
         return DC_OK;
     }
     const uint64_t wgs = (groups + DEC_WAVES - 1) / DEC_WAVES;

@@ -7,7 +7,7 @@ from collections import defaultdict
 
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
 want = ("k_hist_blocks", "k_huff_pack", "k_huff_decode", "k_huff_decode_fix", "k_huff_table",
-        "k_block_local", "k_block_final", "k_huff_fix_list", "k_zero_bounds")
+        "k_block_local", "k_block_final", "k_zero_bounds")
 vals = defaultdict(lambda: defaultdict(list))
 for f in sorted(glob.glob(os.path.join(root, "p*", "run_counter_collection.csv"))):
     per = defaultdict(float)
@@ -17,13 +17,13 @@ for f in sorted(glob.glob(os.path.join(root, "p*", "run_counter_collection.csv")
             k = "k_huff_decode_fix"
         elif k.startswith("k_huff_decode"):   # k_huff_decode8<NW, NC> is the decode launch
             k = "k_huff_decode"
-        if k not in want:
+        if k not in want and not (os.environ.get("PMC_ALL") and k.startswith("k_")):
             continue
         key = (k, r["Dispatch_Id"], r["Counter_Name"])
         per[key] += float(r["Counter_Value"])
     for (k, d, c), v in per.items():
         vals[k][c].append(v)
-for k in want:
+for k in (list(want) + sorted(set(vals) - set(want))):
     if k not in vals:
         continue
     print(k)
