@@ -89,7 +89,7 @@ def main():
         return main_nybble(a, dev, rank, world)
     n = a.size
     _phase(rank, "device up")
-    x = synth.device_text(a.cfg, n, seed=input_seed(a.cfg, rank), device=dev)
+    x = bench_input(a.cfg, n, input_seed(a.cfg, rank), dev)
     torch.cuda.synchronize()
     _phase(rank, "input generated")
     c = Codec(local)   # launches on torch's current stream
@@ -318,7 +318,7 @@ def main_nybble(a, dev, rank, world):
     from data_compression_amd.device import Codec
     n = a.size
     modify = a.mode == "adaptive"
-    x = synth.device_text("C1", n, seed=0xC1 + 7919 * rank, device=dev)
+    x = bench_input("C1", n, 0xC1 + 7919 * rank, dev)
     torch.cuda.synchronize()
     c = Codec(dev.index or 0)
     comp_buf = torch.empty(n + 2, dtype=torch.uint8, device=dev)
@@ -465,6 +465,17 @@ def cpu_baseline_nybble(x, a, modify):
     r["encode_GBps"] = round(m / (t1 - t0) / 1e9, 4)
     r["decode_GBps"] = round(m / (t2 - t1) / 1e9, 4)
     return r
+
+
+def bench_input(cfg, n, seed, dev):
+    """The synthetic input, generated on the device (synth.device_text). DC_BENCH_SYNTH=host
+    generates it with the numpy generator instead and copies it over: for rehearsals whose
+    ranks share one GPU, where several processes' torch generation at once stalled inside
+    torch (tools/synth_stall.py)."""
+    from data_compression_amd import synth
+    if os.environ.get("DC_BENCH_SYNTH") == "host":
+        return torch.from_numpy(synth.GENERATORS[cfg](n, seed=seed)).to(dev)
+    return synth.device_text(cfg, n, seed=seed, device=dev)
 
 
 def input_seed(cfg, rank):

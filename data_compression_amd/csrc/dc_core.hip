@@ -2914,34 +2914,41 @@ __global__ __launch_bounds__(D8F_WAVES * 64) void k_huff_decode8_fix(const uint3
                 const bool valid = cha != ~0u && (uint64_t)cha * S < n;
                 const uint64_t s0 = (uint64_t)(valid ? cha : 0u) * S;
                 const uint32_t cntc = valid ? (uint32_t)((n - s0 < S) ? n - s0 : S) : 0u;
-                uint32_t cb = (uint32_t)(posa - (a0 << 5));
+                // the lane's window: row words wa, wa + 1, wa + 2 in registers, bit sh of the first;
+                // a symbol reads only the table (r2 read two row words per symbol, a second LDS
+                // round trip on its chain); the word after moves in when a code crosses a word
+                const uint32_t cb0 = (uint32_t)(posa - (a0 << 5));
+                uint32_t wa = cb0 >> 5, sh = cb0 & 31u;
                 uint64_t rb = a0;   // word of `in` at row word 0
+                // 4 codes move the window <= 4 words (reads up to row word wa + 6): re-stage the
+                // row further on when it runs short (the window registers stay valid)
+                auto restage = [&]() {
+                    const uint32_t adv = wa & ~3u;
+                    rb += adv;
+                    wa -= adv;
+                    const uint64_t nq = rb < nwords ? (nwords - rb) / 4 : 0ull;
+#pragma unroll 1
+                    for (int k = 0; k < D8F_ROW / 4; ++k) {   // rolled: no second set of row registers
+                        const uint4 v = (uint64_t)k < nq ? reinterpret_cast<const uint4 *>(in + rb)[k] : make_uint4(0u, 0u, 0u, 0u);
+                        row[4 * k] = brev8(v.x);
+                        row[4 * k + 1] = brev8(v.y);
+                        row[4 * k + 2] = brev8(v.z);
+                        row[4 * k + 3] = brev8(v.w);
+                    }
+                };
+                if (wa >= D8F_ROW - 6) restage();   // (a row clamped at the buffer's end)
+                uint32_t w0 = row[wa], w1 = row[wa + 1], w2 = row[wa + 2];
                 uint4 *const o128 = reinterpret_cast<uint4 *>(out + s0);
                 for (uint32_t p = 0; p < (cntc + 15) / 16; ++p) {
                     uint32_t ov[4];
 #pragma unroll
                     for (int q4 = 0; q4 < 4; ++q4) {
                         const uint32_t q = 4 * p + q4;
-                        // 4 codes take <= 128 bits (+ 64 of window): re-stage a row that runs short
-                        if (cb >= 32 * (D8F_ROW - 6)) {
-                            const uint32_t adv = (cb >> 5) & ~3u;
-                            rb += adv;
-                            cb -= adv * 32;
-                            const uint64_t nq = rb < nwords ? (nwords - rb) / 4 : 0ull;
-#pragma unroll 1
-                            for (int k = 0; k < D8F_ROW / 4; ++k) {   // rolled: no second set of row registers
-                                const uint4 v = (uint64_t)k < nq ? reinterpret_cast<const uint4 *>(in + rb)[k] : make_uint4(0u, 0u, 0u, 0u);
-                                row[4 * k] = brev8(v.x);
-                                row[4 * k + 1] = brev8(v.y);
-                                row[4 * k + 2] = brev8(v.z);
-                                row[4 * k + 3] = brev8(v.w);
-                            }
-                        }
+                        if (wa >= D8F_ROW - 6) restage();
                         uint32_t ob = 0;
 #pragma unroll
                         for (int k = 0; k < 4; ++k) {
-                            const uint32_t a = cb >> 5;
-                            const uint32_t lo = __builtin_amdgcn_alignbit(row[a + 1], row[a], cb);
+                            const uint32_t lo = __builtin_amdgcn_alignbit(w1, w0, sh);
                             uint32_t e = F.lut[lo & ((1u << D8F_LUT_BITS) - 1)];
                             if (__builtin_amdgcn_ballot_w64((e & 255u) == 0u)) {   // the second level, only when a lane needs it
                                 const uint32_t i2 = min(((e >> 8) << K2) | ((lo >> DC_LUT_BITS) & kmask), (uint32_t)DC_LUT2_CAP - 1);
@@ -2949,13 +2956,19 @@ __global__ __launch_bounds__(D8F_WAVES * 64) void k_huff_decode8_fix(const uint3
                                 e = (e & 255u) ? e : e2;
                             }
                             if (e == 0) {   // past the second level (rare): canonical search
-                                const uint32_t hi = __builtin_amdgcn_alignbit(row[a + 2], row[a + 1], cb);
-                                e = d8_long_lds(lo, hi, F, nary, w, pow2);
+                                e = d8_long_lds(lo, __builtin_amdgcn_alignbit(w2, w1, sh), F, nary, w, pow2);
                                 // the stream's partial last chunk decodes past its end: no error there
                                 bad |= (e == 0 && 4 * q + k < cntc);
                             }
                             ob |= ((e >> 8) & 255u) << (8 * k);
-                            cb += e & 255u;
+                            sh += e & 255u;   // <= 32 bits: at most one word on
+                            if (sh >= 32u) {
+                                sh -= 32u;
+                                w0 = w1;
+                                w1 = w2;
+                                w2 = row[wa + 3];
+                                ++wa;
+                            }
                         }
                         ov[q4] = ob;
                     }
@@ -3344,6 +3357,92 @@ static __device__ __forceinline__ void fsm_ranks(const FsmWin &W, const FsmAux &
     }
 }
 
+// ---- the nybble transducers' states, 16 elements at once (bit k = element k of a lane) ----
+// Both machines are two-state, and a lane's 16 states follow from its element flags by one
+// 32-bit add: a carry is generated where an element forces state 1, killed where it forces 0
+// and propagated where the state carries over, so with A = generate | propagate and
+// B = generate, A + B + s0 carries c_{k-1} = (sum ^ propagate) bit k into element k, which is
+// its state s_k (bit 16: the state after the lane). (r2 composed the 16 elements' transition
+// functions one after another: ~30 VALU per element in the count pass, ~74 in the writer.)
+// bit `bit` of the lane's window bytes 1..16 (element k = window byte k + 1)
+static __device__ __forceinline__ uint32_t fsm_byte_bits(const FsmWin &W, int bit)
+{
+    uint32_t m = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t X = __builtin_amdgcn_alignbyte(W.w[q + 1], W.w[q], 1);   // bytes 4q+1..4q+4
+        uint32_t b = (X >> bit) & 0x01010101u;
+        b = (b | (b >> 7) | (b >> 14) | (b >> 21)) & 15u;
+        m |= b << (4 * q);
+    }
+    return m;
+}
+// the states from s0, bit k = s_k (k <= 16); g, p: generate and propagate masks (disjoint)
+static __device__ __forceinline__ uint32_t fsm_carry_states(uint32_t g, uint32_t p, uint32_t s0)
+{
+    return ((g | p) + g + s0) ^ p;
+}
+// decode (s = "at the low nybble"): s' = (s | h) & !l, h / l = bits 7 / 3 of the byte;
+// elements outside `valid` keep the state. Returns the states (bits 0..16).
+static __device__ __forceinline__ uint32_t nyb_dec_states(uint32_t H, uint32_t L, uint32_t valid, uint32_t s0)
+{
+    const uint32_t g = H & ~L & valid, p = (~H & ~L & valid) | (~valid & 0xFFFFu);
+    return fsm_carry_states(g, p, s0);
+}
+// encode (s = "a hit nybble is pending"): a hit toggles the state, a miss clears it. With P_k
+// the parity of the hits before k, s_k = P_k ^ (P at the last miss before k, or s0): the value
+// at the last miss is carried forward through the hits (a carry generated at a miss where
+// P = 1, killed at one where P = 0). Returns the states (bits 0..16).
+static __device__ __forceinline__ uint32_t nyb_enc_states(uint32_t Hm, uint32_t valid, uint32_t s0)
+{
+    Hm &= valid;       // (window bytes past the stream may read as hits)
+    uint32_t X = Hm;   // inclusive prefix parity
+    X ^= X << 1;
+    X ^= X << 2;
+    X ^= X << 4;
+    X ^= X << 8;
+    const uint32_t P = (X << 1) & 0x1FFFFu;   // exclusive: bit k = parity of hits before k
+    const uint32_t miss = ~Hm & valid;
+    const uint32_t g = miss & P, p = Hm | (~valid & 0xFFFFu);
+    return (P ^ fsm_carry_states(g, p, s0)) & 0x1FFFFu;
+}
+// the lane's composition (both entry states): counts and exit states
+template <int M>
+static __device__ __forceinline__ Fsm nyb_lane_fsm(uint32_t A, uint32_t B, uint32_t valid)
+{
+    Fsm f;
+    if (M == M_NYB_ENC) {   // A = hit mask
+        A &= valid;
+        const uint32_t miss = ~A & valid;
+        const uint32_t S0 = nyb_enc_states(A, valid, 0u), S1 = nyb_enc_states(A, valid, 1u);
+        f.c0 = __popc(A & S0 & 0xFFFFu) + __popc(miss) + __popc(miss & S0);
+        f.c1 = __popc(A & S1 & 0xFFFFu) + __popc(miss) + __popc(miss & S1);
+        f.s0 = (S0 >> 16) & 1u;
+        f.s1 = (S1 >> 16) & 1u;
+    } else {                // A = high-nybble flags, B = low-nybble flags
+        const uint32_t S0 = nyb_dec_states(A, B, valid, 0u), S1 = nyb_dec_states(A, B, valid, 1u);
+        f.c0 = __popc(valid) + __popc(valid & A & ~S0);
+        f.c1 = __popc(valid) + __popc(valid & A & ~S1);
+        f.s0 = (S0 >> 16) & 1u;
+        f.s1 = (S1 >> 16) & 1u;
+    }
+    return f;
+}
+// the lane's flag masks: encode, the hit mask of its ranks; decode, bits 7 and 3 of its bytes
+template <int M>
+static __device__ __forceinline__ void nyb_lane_flags(const FsmWin &W, const uint32_t (&rk)[16], uint32_t &A, uint32_t &B)
+{
+    if (M == M_NYB_ENC) {
+        A = 0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) A |= (rk[k] != 0xFFu ? 1u : 0u) << k;
+        B = 0;
+    } else {
+        A = fsm_byte_bits(W, 7);
+        B = fsm_byte_bits(W, 3);
+    }
+}
+
 template <int M>
 __global__ __launch_bounds__(256) void k_fsm_tiles(const uint8_t *__restrict__ in, uint64_t len,
                                                    uint64_t nelem, uint4 *__restrict__ summ, FsmAux aux)
@@ -3364,11 +3463,11 @@ __global__ __launch_bounds__(256) void k_fsm_tiles(const uint8_t *__restrict__ i
         const uint64_t j0 = (uint64_t)blockIdx.x * FSM_TILE + (uint64_t)c * 4096 + (uint64_t)t * 16;
         Fsm f = fsm_id();
         if (j0 < nelem) {
-            uint32_t rk[16];
+            uint32_t rk[16], A, B;
             fsm_ranks<M>(W[c], aux, j0, nelem, rk, s_rank);
-#pragma unroll
-            for (int k = 0; k < 16; ++k)
-                if (j0 + k < nelem) f = fsm_then(f, elem_fsm<M>(W[c], k, len, j0 + k, M == M_NYB_ENC ? rk[k] : 0u));
+            nyb_lane_flags<M>(W[c], rk, A, B);
+            const uint32_t valid = nelem - j0 >= 16 ? 0xFFFFu : (1u << (uint32_t)(nelem - j0)) - 1u;
+            f = nyb_lane_fsm<M>(A, B, valid);
         }
         const Fsm inc = fsm_wave_scan_incl(f, t & 63);
         if ((t & 63) == 63) s_f[c][t >> 6] = fsm_pack(inc);
@@ -3534,16 +3633,18 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
     // every chunk through LDS (one barrier)
     const int lane = t & 63, wid = t >> 6;
     Fsm ex[FSM_SUB];   // lanes before this one in the wave, per chunk
+    uint32_t fa[FSM_SUB], fb[FSM_SUB], fvalid[FSM_SUB];   // the lane's element flags (nyb_lane_flags)
 #pragma unroll
     for (int c = 0; c < FSM_SUB; ++c) {
         const uint64_t j0 = (uint64_t)blockIdx.x * FSM_TILE + (uint64_t)c * 4096 + (uint64_t)t * 16;
+        fa[c] = fb[c] = 0u;
+        fvalid[c] = j0 >= nelem ? 0u : nelem - j0 >= 16 ? 0xFFFFu : (1u << (uint32_t)(nelem - j0)) - 1u;
         Fsm f = fsm_id();
         if (j0 < nelem) {
             uint32_t rk[16];
             fsm_ranks<M>(W_[c], aux, j0, nelem, rk, s_rank);
-#pragma unroll
-            for (int k = 0; k < 16; ++k)
-                if (j0 + k < nelem) f = fsm_then(f, elem_fsm<M>(W_[c], k, len, j0 + k, M == M_NYB_ENC ? rk[k] : 0u));
+            nyb_lane_flags<M>(W_[c], rk, fa[c], fb[c]);
+            f = nyb_lane_fsm<M>(fa[c], fb[c], fvalid[c]);
         }
         const Fsm inc = fsm_wave_scan_incl(f, lane);
         if (lane == 63) s_f[c][wid] = fsm_pack(inc);
@@ -3593,7 +3694,9 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
         if (j0 >= nelem) continue;
         const FsmWin &W = W_[c];
         const uint64_t o0 = o_c[c];
-        uint32_t s = st_c[c];
+        // every element's state at once, from the lane's entry state
+        const uint32_t S = M == M_NYB_ENC ? nyb_enc_states(fa[c], fvalid[c], st_c[c])
+                                          : nyb_dec_states(fa[c], fb[c], fvalid[c], st_c[c]);
         uint32_t rk[16];
         fsm_ranks<M>(W, aux, j0, nelem, rk, s_rank);
         const uint32_t P = (uint32_t)((int64_t)o0 - o_al);   // stage byte of the lane's first output
@@ -3604,7 +3707,8 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
         for (int k = 0; k < 16; ++k) {
             const bool in_range = (uint32_t)k < kend;
             const uint32_t x = W.b(k + 1);
-            uint32_t val, cnt, sn;
+            const uint32_t s = (S >> k) & 1u;
+            uint32_t val, cnt;
             if (M == M_NYB_ENC) {
                 const uint32_t r = rk[k];
                 const bool hit = r != 0xFF;
@@ -3616,7 +3720,6 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
                 const uint32_t pair = (((8u | rp) << 4) | (8u | r)) & 255u;
                 cnt = hit ? s : 1u + s;
                 val = hit ? (s ? pair : 0u) : (s ? (W.b(k) | (x << 8)) : x);   // (no bits when cnt = 0)
-                sn = hit ? (s ^ 1u) : 0u;
                 if (hit && !s && aux.is_last && j + 1 == len - 1 && in_range)   // odd tail (:1000-1009)
                     out[o0 + ((nb + 32u * (di - (P >> 2)) - 8u * (P & 3u)) >> 3)] = (uint8_t)x;
             } else {   // M_NYB_DEC / M_NYB_DBODY: compressed byte x, state s = "at the low nybble"
@@ -3624,17 +3727,14 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
                 const uint32_t h = x >> 4, l = x & 15u;
                 const uint32_t nxt = (kk + 1 < len) ? (W.b(k + 2) >> 4) : 0u;
                 const uint32_t lo_b = (l & 8u) ? (uint32_t)(tblv >> (8u * (l & 7u))) & 255u : ((l & 7u) << 4) + nxt;
-                const uint32_t lo_s = (l & 8u) ? 0u : 1u;
                 const uint32_t hi_b = (uint32_t)(tblv >> (8u * (h & 7u))) & 255u;
                 const bool two = !s && (h & 8u);
                 val = s ? lo_b : (two ? (hi_b | (lo_b << 8)) : x);
                 cnt = two ? 2u : 1u;
-                sn = (s || two) ? lo_s : 0u;
             }
             if (in_range) {
                 acc |= (uint64_t)val << nb;
                 nb += 8u * cnt;
-                s = sn;
             }
             if (k & 1) {   // <= 32 bits per 2 elements: at most one complete dword
                 if (nb >= 32u) {
@@ -4047,18 +4147,32 @@ __global__ __launch_bounds__(256) void k_mtf_walk(const uint8_t *__restrict__ in
         s_L[c][t] = MODE ? entry[tile].L[c] : 0ull;
         if (MODE) cnts |= (uint64_t)entry[tile].cnt[c] << (4 * c);
     }
-    // bytes [e0, e1] in aligned 16-B pieces: byte e0 is the first context
-    const uintptr_t a0 = (uintptr_t)(in + e0), a1 = (uintptr_t)(in + e1);
+    // 16 elements per step: their bytes in[e + 1 .. e + 16] cut from two aligned granules by one
+    // uniform byte shift (the next step's first granule is this step's second), ranks leave as
+    // one 16-B store per step (r2 stored 4 ranks at a time at 4-KiB-strided lanes: 3.9 ms per
+    // GiB for this pass against 1.6 for the summary pass)
     uint32_t prev = in[e0];
-    uint32_t acc = 0;   // MODE 1: ranks of the current 4-element group
-    for (uintptr_t q = a0 & ~(uintptr_t)15; q <= a1; q += 16) {
-        const uint4 v = *(const uint4 *)q;
-        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    const uintptr_t p0 = (uintptr_t)(in + e0 + 1), end = (uintptr_t)(in + len);
+    const uint32_t sh = (uint32_t)(p0 & 15u), dq = sh >> 2, db = sh & 3u;   // uniform over the lanes
+    uintptr_t g = p0 & ~(uintptr_t)15;
+    uint4 ga = g < end ? *(const uint4 *)g : make_uint4(0u, 0u, 0u, 0u);
+    for (uint64_t e = e0; e < e1; e += 16) {
+        const uint4 gb = g + 16 < end ? *(const uint4 *)(g + 16) : make_uint4(0u, 0u, 0u, 0u);
+        const uint32_t d8[8] = {ga.x, ga.y, ga.z, ga.w, gb.x, gb.y, gb.z, gb.w};
+        uint32_t X[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {   // dwords dq + j, dq + j + 1 (dq uniform: selects)
+            uint32_t lo = d8[j], hi = d8[j + 1];
+#pragma unroll
+            for (int k = 1; k < 4; ++k) { lo = dq == (uint32_t)k ? d8[j + k] : lo; hi = dq == (uint32_t)k ? d8[j + k + 1] : hi; }
+            X[j] = __builtin_amdgcn_alignbyte(hi, lo, db);
+        }
+        const uint32_t cnt16 = e1 - e < 16 ? (uint32_t)(e1 - e) : 16u;
+        uint32_t R[4] = {0u, 0u, 0u, 0u};   // MODE 1: the step's ranks (0..7, 0xFF a miss)
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
-            const uintptr_t a = q + k;
-            if (a <= a0 || a > a1) continue;
-            const uint32_t x = (w[k >> 2] >> (8 * (k & 3))) & 255u;
+            if ((uint32_t)k >= cnt16) break;
+            const uint32_t x = (X[k >> 2] >> (8 * (k & 3))) & 255u;
             const uint32_t c = (prev >> 3) & 15u;
             uint64_t L = s_L[c][t];
             uint32_t n = (uint32_t)(cnts >> (4 * c)) & 15u;
@@ -4066,15 +4180,14 @@ __global__ __launch_bounds__(256) void k_mtf_walk(const uint8_t *__restrict__ in
             s_L[c][t] = L;
             cnts = (cnts & ~(15ull << (4 * c))) | ((uint64_t)n << (4 * c));
             prev = x;
-            if (MODE) {
-                const uint64_t e = (uint64_t)(a - (uintptr_t)in) - 1;
-                acc |= (uint32_t)(r < 0 ? 0xFF : r) << (8 * (e & 3));
-                if ((e & 3) == 3) { *(uint32_t *)(rk + e - 3) = acc; acc = 0; }
-                else if (e + 1 == e1) {   // ragged end of the stream (tiles are multiples of 4)
-                    for (uint64_t u = e & ~3ull; u <= e; ++u) rk[u] = (uint8_t)(acc >> (8 * (u & 3)));
-                }
-            }
+            if (MODE) R[k >> 2] |= (uint32_t)(r < 0 ? 0xFF : r) << (8 * (k & 3));
         }
+        if (MODE) {
+            if (cnt16 == 16) *reinterpret_cast<uint4 *>(rk + e) = make_uint4(R[0], R[1], R[2], R[3]);
+            else for (uint32_t k = 0; k < cnt16; ++k) rk[e + k] = (uint8_t)(R[k >> 2] >> (8 * (k & 3)));   // ragged end
+        }
+        ga = gb;
+        g += 16;
     }
     if (!MODE) {
         for (int c = 0; c < 16; ++c) {

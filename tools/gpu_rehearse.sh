@@ -16,5 +16,7 @@ run() {   # N PORT LOG extra-args...
   grep -E "rank [0-9]\]" $LOG | tail -8
   return $rc
 }
-run 2 29511 gpurun_out/${TAG}_gloo2_C2.log || exit 1
-run 4 29512 gpurun_out/${TAG}_gloo4_C2.log || { for f in gpurun_out/trace_rank*.log; do echo "== $f"; tail -30 $f; done; exit 1; }
+run 2 29511 gpurun_out/${TAG}_gloo2_C2.log --gather-reps 1 || exit 1
+# 4 ranks: the input generated on the host (DC_BENCH_SYNTH=host): four processes' torch
+# generation at once on one GPU stalled in r2/r3 (tools/synth_stall.py isolates it)
+DC_BENCH_SYNTH=host run 4 29512 gpurun_out/${TAG}_gloo4_C2.log --gather-reps 1 || { for f in gpurun_out/trace_rank*.log; do echo "== $f"; tail -12 $f; done; exit 1; }
