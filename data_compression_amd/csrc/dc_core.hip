@@ -4414,13 +4414,65 @@ static __device__ __forceinline__ uint32_t adec_step_s(uint32_t t, u64x16 &lists
     return v;
 }
 
+// The same step in scalar instructions only, the 16 lists pinned in s[64:95] (list c in
+// s[64 + 2c : 65 + 2c], read and written M0-relative: s_movrels / s_movreld): ~27 SALU per
+// byte and no vector-scalar crossing. (Compiled from adec_step_s, the lists went to VGPRs
+// under s_set_gpr_idx with a v_readfirstlane per byte: ~170 cycles per byte, 12.4 MB/s.)
+// The keep mask is made in here from the inline constant -1: handed in as an "s" operand, the
+// constant 0xFFFFFFFFFFFFFF00 became s_mov_b64 with a 32-bit literal that the hardware
+// zero-extends, and every move past rank 3 lost its top bytes (tools/ubench/adec_asm.hip).
+typedef uint32_t u32x32 __attribute__((ext_vector_type(32)));
+static __device__ __forceinline__ uint32_t adec_step_asm(uint32_t t, u32x32 &lists, uint32_t &ctx, uint64_t h80)
+{
+    uint32_t v;
+    asm volatile(
+        "s_lshl_b32 m0, %[ctx], 1\n\t"
+        "s_mul_i32 s98, %[t], 0x1010101\n\t"             // t in every byte
+        "s_mov_b32 s99, s98\n\t"
+        "s_movrels_b64 s[96:97], s[64:65]\n\t"          // L = list of ctx
+        "s_xor_b64 s[98:99], s[98:99], s[96:97]\n\t"     // x = L ^ t...t
+        "s_sub_u32 s100, s98, 0x1010101\n\t"
+        "s_subb_u32 s101, s99, 0x1010101\n\t"
+        "s_andn2_b64 s[100:101], s[100:101], s[98:99]\n\t"
+        "s_and_b64 s[100:101], s[100:101], %[h80]\n\t"   // a literal's first match (zero byte of x)
+        "s_ff1_i32_b64 s98, s[100:101]\n\t"
+        "s_lshr_b32 s98, s98, 3\n\t"
+        "s_min_u32 s98, s98, 7\n\t"                     // pl (absent: 7, the last entry drops)
+        "s_and_b32 s99, %[t], 7\n\t"                     // ph, a hit's rank
+        "s_bitcmp1_b32 %[t], 7\n\t"
+        "s_cselect_b32 s98, s99, s98\n\t"                // p = hit ? ph : pl
+        "s_lshl_b32 s99, s99, 3\n\t"
+        "s_lshr_b64 s[100:101], s[96:97], s99\n\t"
+        "s_and_b32 s100, s100, 0xff\n\t"                 // vh = the byte at rank ph
+        "s_bitcmp1_b32 %[t], 7\n\t"
+        "s_cselect_b32 %[v], s100, %[t]\n\t"             // v = hit ? vh : t
+        "s_lshl_b32 s99, s98, 3\n\t"
+        "s_lshl_b64 s[100:101], -1, s99\n\t"
+        "s_lshl_b64 s[100:101], s[100:101], 8\n\t"      // keep: bytes above p
+        "s_lshl_b64 s[98:99], s[96:97], 8\n\t"
+        "s_xor_b64 s[98:99], s[98:99], s[96:97]\n\t"
+        "s_andn2_b64 s[98:99], s[98:99], s[100:101]\n\t"
+        "s_xor_b64 s[96:97], s[96:97], s[98:99]\n\t"     // bytes [0, p) move up one
+        "s_or_b32 s96, s96, %[v]\n\t"                    // v to the front (:665-687)
+        "s_movreld_b64 s[64:65], s[96:97]\n\t"
+        "s_bfe_u32 %[ctx], %[v], 0x40003"                  // the next context: v >> 3
+        : [lists] "+{s[64:95]}"(lists), [ctx] "+s"(ctx), [v] "=&s"(v)
+        : [t] "s"(t), [h80] "s"(h80)
+        : "s96", "s97", "s98", "s99", "s100", "s101", "scc");
+    return v;
+}
+
 // out[0] is the first byte, out[1..n) the tokens of pass 1; all replaced in place
 __global__ __launch_bounds__(64) void k_nyb_resolve_s(uint8_t *__restrict__ out, uint64_t n)
 {
     const int lane = (int)threadIdx.x;
-    u64x16 lists;
+    const uint64_t h80 = 0x8080808080808080ull;
+    u32x32 lists;
 #pragma unroll
-    for (int c = 0; c < 16; ++c) lists[c] = mtf_init_word();
+    for (int c = 0; c < 16; ++c) {
+        lists[2 * c] = (uint32_t)mtf_init_word();
+        lists[2 * c + 1] = (uint32_t)(mtf_init_word() >> 32);
+    }
     uint32_t ctx = ((uint32_t)__builtin_amdgcn_readfirstlane((int)out[0]) >> 3) & 15u;
     const uint64_t k0 = min((uint64_t)((64 - (((uintptr_t)out + 1) & 63)) & 63) + 1, n);
     const uint64_t nblk = (n - k0) / 64, k1 = k0 + 64 * nblk;
@@ -4430,7 +4482,7 @@ __global__ __launch_bounds__(64) void k_nyb_resolve_s(uint8_t *__restrict__ out,
         const uint32_t tv = (uint64_t)lane < m ? out[ka + lane] : 0u;
         uint32_t ov = 0;
         for (uint32_t i = 0; i < (uint32_t)m; ++i) {
-            const uint32_t v = adec_step_s((uint32_t)__builtin_amdgcn_readlane((int)tv, (int)i), lists, ctx);
+            const uint32_t v = adec_step_asm((uint32_t)__builtin_amdgcn_readlane((int)tv, (int)i), lists, ctx, h80);
             ov = lane == (int)i ? v : ov;
         }
         if ((uint64_t)lane < m) out[ka + lane] = (uint8_t)ov;
@@ -4450,7 +4502,7 @@ __global__ __launch_bounds__(64) void k_nyb_resolve_s(uint8_t *__restrict__ out,
             for (int j = 0; j < 16; ++j) {
                 uint32_t w = 0;
 #pragma unroll
-                for (int q = 0; q < 4; ++q) w |= adec_step_s((T[j] >> (8 * q)) & 255u, lists, ctx) << (8 * q);
+                for (int q = 0; q < 4; ++q) w |= adec_step_asm((T[j] >> (8 * q)) & 255u, lists, ctx, h80) << (8 * q);
                 ADEC_PUT(dw, w, j);
             }
             if (lane < 16) reinterpret_cast<uint32_t *>(out + k0 + 64 * b)[lane] = dw;
