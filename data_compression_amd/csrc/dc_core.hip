@@ -2808,6 +2808,10 @@ __global__ __launch_bounds__(D8F_WAVES * 64) void k_huff_decode8_fix(const uint3
     __shared__ uint32_t s_list[D8F_LIST];
     __shared__ uint32_t s_wsum[D8F_WAVES];
     const int t = threadIdx.x, lane = t & 63, wv = __builtin_amdgcn_readfirstlane(t >> 6);
+    D8_STAMP(f_begin);
+#ifdef DC_DIAG
+    unsigned long long f_list = 0, f_first = 0, f_dec = 0, f_wait = 0, f_rounds = 0;
+#endif
     if (blockIdx.x == 0 && t < 4) err_next[t] = 0;   // the next decode's error slot
     const uint32_t nchunks = (uint32_t)((n + S - 1) / S);
     const uint32_t ngroups = (nchunks + DC_SYNC_GROUP - 1) / DC_SYNC_GROUP;
@@ -2893,6 +2897,9 @@ __global__ __launch_bounds__(D8F_WAVES * 64) void k_huff_decode8_fix(const uint3
                 }
             }
             __syncthreads();
+#ifdef DC_DIAG
+            if (!f_list) f_list = __builtin_amdgcn_s_memtime() - f_begin;
+#endif
             const uint32_t cnt = min(total - part, (uint32_t)D8F_LIST), nrounds = (cnt + 63) / 64;
             auto chunk_of = [&](uint32_t r) -> uint32_t {
                 return r < nrounds && r * 64 + (uint32_t)lane < cnt ? s_list[r * 64 + lane] : ~0u;
@@ -2906,6 +2913,14 @@ __global__ __launch_bounds__(D8F_WAVES * 64) void k_huff_decode8_fix(const uint3
             while (ra < nrounds) {
                 // stage round A's spans, then start round B's spans and round C's positions
                 const uint64_t a0 = row_base(posa);
+#ifdef DC_DIAG
+                D8_STAMP(f_w0);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                D8_STAMP(f_w1);
+                f_wait += f_w1 - f_w0;
+                if (!f_first) f_first = f_w1 - f_begin;
+                ++f_rounds;
+#endif
                 put_row(sv);
                 load_row(sv, row_base(posb));
                 const uint32_t chc = chunk_of(ra + 2 * D8F_WAVES);
@@ -2976,6 +2991,10 @@ __global__ __launch_bounds__(D8F_WAVES * 64) void k_huff_decode8_fix(const uint3
                     else   // the stream's partial last chunk
                         for (uint32_t k = 0; 16 * p + k < cntc; ++k) out[s0 + 16 * p + k] = (uint8_t)(ov[k >> 2] >> (8 * (k & 3)));
                 }
+#ifdef DC_DIAG
+                D8_STAMP(f_d1);
+                f_dec += f_d1 - f_w1;
+#endif
                 ra += D8F_WAVES;
                 cha = chb; posa = posb;
                 chb = chc; posb = posc;
@@ -2984,6 +3003,16 @@ __global__ __launch_bounds__(D8F_WAVES * 64) void k_huff_decode8_fix(const uint3
         }
     }
     if (bad) atomicOr(err, 1);
+#ifdef DC_DIAG
+    D8_STAMP(f_end);
+    if (lane == 0 && blockIdx.x < 256) {
+        unsigned long long *gg = g_d8diag + (blockIdx.x * D8F_WAVES + wv) * 4;
+        gg[0] = f_end - f_begin;
+        gg[1] = (f_list & 0xffffffffull) | (f_first << 32);
+        gg[2] = f_dec;
+        gg[3] = (f_rounds & 255) | ((f_wait & ((1ull << 28) - 1)) << 8) | (f_first << 36);
+    }
+#endif
 }
 
 // base64url rendering of a bit range (int2digit alphabet, n_ary_huffman.c:371-378)

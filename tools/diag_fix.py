@@ -30,6 +30,7 @@ pos = (raw[:, 1] >> 32).astype(np.float64)
 rounds = (raw[:, 3] & 255).astype(np.float64)
 wait = ((raw[:, 3] >> 8) & ((1 << 28) - 1)).astype(np.float64)
 first = (raw[:, 3] >> 36).astype(np.float64)
-print(f"fix waves {len(tot)}: total {tot.mean():.0f} cyc (max {tot.max():.0f})  tables {tab.mean():.0f}  "
-      f"decode {dec.mean():.0f} ({dec.sum()/tot.sum():.1%})  rounds {rounds.mean():.2f} (max {rounds.max():.0f})  "
-      f"stage waits {wait.mean():.0f}  first positions at {pos.mean():.0f} (max {pos.max():.0f})  first stage at {first.mean():.0f} (max {first.max():.0f})")
+act = rounds > 0
+print(f"fix waves {len(tot)} (with a round: {act.sum()}): total {tot.mean():.0f} cyc (max {tot.max():.0f})  list ready at {tab.mean():.0f} "
+      f"(max {tab.max():.0f})  decode {dec[act].mean():.0f} per active wave (max {dec.max():.0f})  rounds {rounds.mean():.2f} (max {rounds.max():.0f})  "
+      f"row waits {wait[act].mean():.0f}  first row at {pos[act].mean():.0f} (max {pos.max():.0f})  [s_memtime: shader clock cycles]")
