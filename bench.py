@@ -434,7 +434,7 @@ def main_nybble(a, dev, rank, world):
     else:
         res["decode_sample"] = {"bytes": 16 << 20, "ms": round(dec_sample_ms, 2),
                                 "MBps": round((16 << 20) / (dec_sample_ms * 1e-3) / 1e6, 1),
-                                "path": "tokens (parallel transducer) + k_nyb_resolve (one wave)"}
+                                "path": "tokens (parallel transducer) + control words + k_nyb_resolve_c (one wave)"}
     if rank == 0 and world == 1 and not a.no_cpu:
         res["cpu_baseline"] = cpu_baseline_nybble(x, a, modify)
     if rank == 0:

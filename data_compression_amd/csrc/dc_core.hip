@@ -3732,46 +3732,67 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
         uint32_t di = P >> 2, nb = 8u * (P & 3u);
         uint64_t acc = 0;
         const uint32_t kend = nelem - j0 < 16 ? (uint32_t)(nelem - j0) : 16u;
+        const uint32_t valid = fvalid[c];
+        // (a dword is complete at most once per 2 elements, <= 32 bits: OR-ed into the stage
+        // unconditionally, 0 when it is not complete yet: no branch)
+        auto flush = [&]() {
+            const uint32_t f = nb >= 32u ? 1u : 0u;
+            atomicOr(&s_out32[di], (uint32_t)acc & (0u - f));
+            acc = f ? (acc >> 32) : acc;
+            nb -= 32u * f;
+            di += f;
+        };
+        if (M == M_NYB_ENC) {
+            // masks of the lane's elements: a hit, and the state before it; an element past the
+            // input counts as a hit in state 0 (no bytes)
+            const uint32_t Hx = (fa[c] & valid) | (~valid & 0xFFFFu), Sx = S & valid;
+            // the rank of the pending hit before element 0: the previous window byte's, or the
+            // shard's carried one
+            const uint32_t rp0 = j0 ? (aux.rk ? (uint32_t)aux.rk[j0 - 1] : (uint32_t)s_rank[W.b(0)]) : aux.pend_rank;
+            if (aux.is_last && len >= 2 && len - 2 >= j0 && len - 2 < j0 + kend) {
+                // odd tail (:1000-1009): the stream's last element a hit left pending: its byte,
+                // raw, after the bytes of the elements before it
+                const uint32_t kt = (uint32_t)(len - 2 - j0);
+                if (((Hx & ~Sx) >> kt) & 1u) {
+                    const uint32_t below = (1u << kt) - 1u;
+                    const uint32_t before = __popc(~Hx & below) + __popc(Sx & below);
+                    uint32_t w = W.w[0];   // window byte kt + 1 (a runtime index: selects)
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const bool in_range = (uint32_t)k < kend;
-            const uint32_t x = W.b(k + 1);
-            const uint32_t s = (S >> k) & 1u;
-            uint32_t val, cnt;
-            if (M == M_NYB_ENC) {
-                const uint32_t r = rk[k];
-                const bool hit = r != 0xFF;
-                // the rank of the pending hit (the element before): this lane's, or the one
-                // before the lane (a rank of the previous window byte, or the shard's carried one)
-                const uint64_t j = j0 + k;
-                const uint32_t rp = k ? rk[k - 1]
-                                      : (j ? (aux.rk ? (uint32_t)aux.rk[j - 1] : (uint32_t)s_rank[W.b(0)]) : aux.pend_rank);
-                const uint32_t pair = (((8u | rp) << 4) | (8u | r)) & 255u;
-                cnt = hit ? s : 1u + s;
-                val = hit ? (s ? pair : 0u) : (s ? (W.b(k) | (x << 8)) : x);   // (no bits when cnt = 0)
-                if (hit && !s && aux.is_last && j + 1 == len - 1 && in_range)   // odd tail (:1000-1009)
-                    out[o0 + ((nb + 32u * (di - (P >> 2)) - 8u * (P & 3u)) >> 3)] = (uint8_t)x;
-            } else {   // M_NYB_DEC / M_NYB_DBODY: compressed byte x, state s = "at the low nybble"
-                const uint64_t kk = M == M_NYB_DBODY ? j0 + k : j0 + k + 2;
+                    for (uint32_t q = 1; q < 5; ++q) w = ((kt + 1) >> 2) == q ? W.w[q] : w;
+                    out[o0 + before] = (uint8_t)(w >> (8 * ((kt + 1) & 3)));
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const uint32_t x = W.b(k + 1), prev = W.b(k);
+                const uint32_t h = (Hx >> k) & 1u, s = (Sx >> k) & 1u;
+                const uint32_t rq = (k ? rk[k - 1] : rp0) & 7u;
+                const uint32_t pair = 0x88u | (rq << 4) | (rk[k] & 7u);   // the pending hit, then this one
+                const uint32_t lit = s ? (prev | (x << 8)) : x;           // (the pending hit's byte raw, then this)
+                const uint32_t val = h ? (pair & (0u - s)) : lit;
+                acc |= (uint64_t)val << nb;
+                nb += 8u * (1u - h + s);
+                if (k & 1) flush();
+            }
+        } else {   // M_NYB_DEC / M_NYB_DBODY: compressed byte x, state s = "at the low nybble"
+            // elements whose next byte is inside the stream (the literal's second nybble)
+            const uint64_t kk0 = M == M_NYB_DBODY ? j0 : j0 + 2;
+            const uint32_t nxt_ok = kk0 + 1 >= len ? 0u : (len - kk0 - 1 >= 16 ? 0xFFFFu : (1u << (uint32_t)(len - kk0 - 1)) - 1u);
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const uint32_t x = W.b(k + 1);
+                const uint32_t s = (S >> k) & 1u;
                 const uint32_t h = x >> 4, l = x & 15u;
-                const uint32_t nxt = (kk + 1 < len) ? (W.b(k + 2) >> 4) : 0u;
+                const uint32_t nxt = ((nxt_ok >> k) & 1u) ? (W.b(k + 2) >> 4) : 0u;
                 const uint32_t lo_b = (l & 8u) ? (uint32_t)(tblv >> (8u * (l & 7u))) & 255u : ((l & 7u) << 4) + nxt;
                 const uint32_t hi_b = (uint32_t)(tblv >> (8u * (h & 7u))) & 255u;
                 const bool two = !s && (h & 8u);
-                val = s ? lo_b : (two ? (hi_b | (lo_b << 8)) : x);
-                cnt = two ? 2u : 1u;
-            }
-            if (in_range) {
+                uint32_t val = s ? lo_b : (two ? (hi_b | (lo_b << 8)) : x);
+                const uint32_t in_range = (valid >> k) & 1u;
+                val &= 0u - in_range;
                 acc |= (uint64_t)val << nb;
-                nb += 8u * cnt;
-            }
-            if (k & 1) {   // <= 32 bits per 2 elements: at most one complete dword
-                if (nb >= 32u) {
-                    atomicOr(&s_out32[di], (uint32_t)acc);
-                    acc >>= 32;
-                    nb -= 32u;
-                    ++di;
-                }
+                nb += in_range * (two ? 16u : 8u);
+                if (k & 1) flush();
             }
         }
         if (nb) atomicOr(&s_out32[di], (uint32_t)acc);
@@ -4443,54 +4464,35 @@ static __device__ __forceinline__ uint32_t adec_step_s(uint32_t t, u64x16 &lists
     return v;
 }
 
-// The same step in scalar instructions only, the 16 lists pinned in s[64:95] (list c in
-// s[64 + 2c : 65 + 2c], read and written M0-relative: s_movrels / s_movreld): ~27 SALU per
-// byte and no vector-scalar crossing. (Compiled from adec_step_s, the lists went to VGPRs
-// under s_set_gpr_idx with a v_readfirstlane per byte: ~170 cycles per byte, 12.4 MB/s.)
-// The keep mask is made in here from the inline constant -1: handed in as an "s" operand, the
-// constant 0xFFFFFFFFFFFFFF00 became s_mov_b64 with a 32-bit literal that the hardware
-// zero-extends, and every move past rank 3 lost its top bytes (tools/ubench/adec_asm.hip).
+// The exact step (the reference's search for a literal in its list) over the 16 lists as 32
+// dwords. r3's first form pinned them in s[64:95] and touched them M0-relative in inline asm
+// (s_movrels / s_movreld, ~28 SALU per byte, 16.3 MB/s); the fast resolve below keeps that
+// addressing. Two things learnt there: a 64-bit constant handed to the asm as an "s" operand
+// (0xFFFFFFFFFFFFFF00) became s_mov_b64 with a 32-bit literal that the hardware zero-extends,
+// so masks are made from the inline constant -1 (tools/ubench/adec_asm.hip traced it); and
+// fixed scratch pairs must avoid s100-s101, which gfx950 reserves (compiler-chosen operands).
 typedef uint32_t u32x32 __attribute__((ext_vector_type(32)));
 static __device__ __forceinline__ uint32_t adec_step_asm(uint32_t t, u32x32 &lists, uint32_t &ctx, uint64_t h80)
 {
-    uint32_t v;
-    asm volatile(
-        "s_lshl_b32 m0, %[ctx], 1\n\t"
-        "s_mul_i32 s98, %[t], 0x1010101\n\t"             // t in every byte
-        "s_mov_b32 s99, s98\n\t"
-        "s_movrels_b64 s[96:97], s[64:65]\n\t"          // L = list of ctx
-        "s_xor_b64 s[98:99], s[98:99], s[96:97]\n\t"     // x = L ^ t...t
-        "s_sub_u32 s100, s98, 0x1010101\n\t"
-        "s_subb_u32 s101, s99, 0x1010101\n\t"
-        "s_andn2_b64 s[100:101], s[100:101], s[98:99]\n\t"
-        "s_and_b64 s[100:101], s[100:101], %[h80]\n\t"   // a literal's first match (zero byte of x)
-        "s_ff1_i32_b64 s98, s[100:101]\n\t"
-        "s_lshr_b32 s98, s98, 3\n\t"
-        "s_min_u32 s98, s98, 7\n\t"                     // pl (absent: 7, the last entry drops)
-        "s_and_b32 s99, %[t], 7\n\t"                     // ph, a hit's rank
-        "s_bitcmp1_b32 %[t], 7\n\t"
-        "s_cselect_b32 s98, s99, s98\n\t"                // p = hit ? ph : pl
-        "s_lshl_b32 s99, s99, 3\n\t"
-        "s_lshr_b64 s[100:101], s[96:97], s99\n\t"
-        "s_and_b32 s100, s100, 0xff\n\t"                 // vh = the byte at rank ph
-        "s_bitcmp1_b32 %[t], 7\n\t"
-        "s_cselect_b32 %[v], s100, %[t]\n\t"             // v = hit ? vh : t
-        "s_lshl_b32 s99, s98, 3\n\t"
-        "s_lshl_b64 s[100:101], -1, s99\n\t"
-        "s_lshl_b64 s[100:101], s[100:101], 8\n\t"      // keep: bytes above p
-        "s_lshl_b64 s[98:99], s[96:97], 8\n\t"
-        "s_xor_b64 s[98:99], s[98:99], s[96:97]\n\t"
-        "s_andn2_b64 s[98:99], s[98:99], s[100:101]\n\t"
-        "s_xor_b64 s[96:97], s[96:97], s[98:99]\n\t"     // bytes [0, p) move up one
-        "s_or_b32 s96, s96, %[v]\n\t"                    // v to the front (:665-687)
-        "s_movreld_b64 s[64:65], s[96:97]\n\t"
-        "s_bfe_u32 %[ctx], %[v], 0x40003"                  // the next context: v >> 3
-        : [lists] "+{s[64:95]}"(lists), [ctx] "+s"(ctx), [v] "=&s"(v)
-        : [t] "s"(t), [h80] "s"(h80)
-        : "s96", "s97", "s98", "s99", "s100", "s101", "scc");
+    // (the exact step, also the fast resolve's fallback: plain code, the lists indexed by the
+    // uniform context; a hand-scheduled form with fixed scratch pairs clobbered s100-s101,
+    // which gfx950 reserves)
+    const uint64_t L = ((uint64_t)lists[2 * ctx + 1] << 32) | lists[2 * ctx];
+    const uint64_t ones = 0x0101010101010101ull;
+    const uint32_t ph = t & 7u;
+    const uint32_t vh = (uint32_t)(L >> (8u * ph)) & 255u;
+    const uint64_t x = L ^ (ones * (uint64_t)t);
+    const uint64_t z = (x - ones) & ~x & h80;
+    const uint32_t pl = z ? (uint32_t)__builtin_ctzll(z) >> 3 : 7u;
+    const bool hit = (t & 0x80u) != 0;
+    const uint32_t v = hit ? vh : t, p = hit ? ph : pl;
+    const uint64_t keep = (~0ull << (8u * p)) << 8;              // bytes above p stay
+    const uint64_t N = (L ^ ((L ^ (L << 8)) & ~keep)) | (uint64_t)v;   // move to front (:665-687)
+    lists[2 * ctx] = (uint32_t)N;
+    lists[2 * ctx + 1] = (uint32_t)(N >> 32);
+    ctx = (v >> 3) & 15u;
     return v;
 }
-
 // out[0] is the first byte, out[1..n) the tokens of pass 1; all replaced in place
 __global__ __launch_bounds__(64) void k_nyb_resolve_s(uint8_t *__restrict__ out, uint64_t n)
 {
@@ -4540,6 +4542,148 @@ __global__ __launch_bounds__(64) void k_nyb_resolve_s(uint8_t *__restrict__ out,
         }
     }
     edge(k1, n);
+}
+
+// Fourth form (the product path since r3b): what a token gives without the lists is
+// computed beforehand, in parallel (k_nyb_adec_ctl, one dword per token), and the sequential
+// step is scalar instructions on the 16 lists in s[64:95]: the list by M0 from the byte
+// before (s_bfe of its bits 2..6: M0 = 2c + a don't-care bit the 64-bit s_movrels ignores,
+// tools/ubench/movrels.hip); a hit's byte by one s_bfe_u64 of the list (width 8 at 8p); the
+// move to front by the mask of the bytes past p. A literal still needs update_context's
+// search (:674-682): the encoder writes a pending hit raw when a miss follows it, so a
+// literal can be in its list (the r3 tokens showed it at 1 in ~30 symbols of the bench text).
+// It takes a uniform branch: hits 15 scalar instructions, literals 26, against 28 for every
+// byte in k_nyb_resolve_s's form.
+// ctl[i] for the token at out position k0 + i: bits 5:0 the S_BFE_U64 offset 8p, bits 22:16
+// its width (8 for a hit, 0 for a literal), bits 31:24 the literal.
+__global__ __launch_bounds__(256) void k_nyb_adec_ctl(const uint8_t *__restrict__ tok, uint64_t k0, uint64_t k1,
+                                                      uint32_t *__restrict__ ctl)
+{
+    for (uint64_t i = k0 + (uint64_t)blockIdx.x * 256 + threadIdx.x; i < k1; i += (uint64_t)gridDim.x * 256) {
+        const uint32_t t = tok[i];
+        ctl[i - k0] = (t & 0x80u) ? (0x80000u | (8u * (t & 7u))) : ((t << 24) | 56u);
+    }
+}
+
+static __device__ __forceinline__ uint32_t adec_step_c(u32x32 &lists, uint32_t &vprev, uint32_t c)
+{
+    uint32_t v, T;
+    uint64_t N;   // (compiler-chosen scratch; the fixed pairs s96-s99 stay clear of s100-s101,
+                  //  which gfx950 reserves; M0 is used by nothing else in these kernels)
+    asm volatile(
+        "s_bfe_u32 m0, %[vp], 0x50002\n\t"             // 2c (+ bit 2 of the byte: ignored)
+        "s_lshr_b32 %[v], %[c], 24\n\t"                // the literal (0 for a hit)
+        "s_bitcmp1_b32 %[c], 19\n\t"                   // a hit (width 8)?
+        "s_movrels_b64 s[96:97], s[64:65]\n\t"          // L = the list of context c (2 instructions after M0)
+        "s_cbranch_scc1 .Lhit%=\n\t"
+        // a literal: its position in L (update_context's search, :674-682), 7 when absent
+        "s_mul_i32 s98, %[v], 0x1010101\n\t"
+        "s_xor_b32 s99, s98, s97\n\t"
+        "s_xor_b32 s98, s98, s96\n\t"
+        "s_sub_u32 %[T], s98, 0x1010101\n\t"
+        "s_andn2_b32 %[T], %[T], s98\n\t"
+        "s_and_b32 s98, %[T], 0x80808080\n\t"           // zero bytes of the low half (the lowest exact)
+        "s_sub_u32 %[T], s99, 0x1010101\n\t"
+        "s_andn2_b32 %[T], %[T], s99\n\t"
+        "s_and_b32 s99, %[T], 0x80808080\n\t"
+        "s_ff1_i32_b64 %[T], s[98:99]\n\t"
+        "s_lshr_b32 %[T], %[T], 3\n\t"
+        "s_min_u32 %[T], %[T], 7\n\t"
+        "s_lshl_b32 %[T], %[T], 3\n\t"
+        "s_lshl_b64 %[N], -1, %[T]\n\t"
+        "s_branch .Ljoin%=\n"
+        ".Lhit%=:\n\t"
+        "s_bfe_u64 s[98:99], s[96:97], %[c]\n\t"       // a hit: the byte at its rank
+        "s_or_b32 %[v], %[v], s98\n\t"
+        "s_lshl_b64 %[N], -1, %[c]\n"
+        ".Ljoin%=:\n\t"
+        "s_lshl_b64 %[N], %[N], 8\n\t"                 // the bytes past p (they stay)
+        "s_lshl_b64 s[98:99], s[96:97], 8\n\t"
+        "s_andn2_b64 s[98:99], s[98:99], %[N]\n\t"     // bytes 0..p-1 move up one
+        "s_and_b64 s[96:97], s[96:97], %[N]\n\t"
+        "s_or_b64 s[96:97], s[96:97], s[98:99]\n\t"
+        "s_or_b32 s96, s96, %[v]\n\t"                  // v to the front (:665-687)
+        "s_movreld_b64 s[64:65], s[96:97]"
+        : [lists] "+{s[64:95]}"(lists), [v] "=&s"(v), [N] "=&s"(N), [T] "=&s"(T)
+        : [vp] "s"(vprev), [c] "s"(c)
+        : "s96", "s97", "s98", "s99", "scc");
+    vprev = v;
+    return v;
+}
+
+// the same step, also a compiler barrier for memory: the scalar loads written after it are
+// issued after it (scalar loads complete out of order, so waiting for one waits for all: the
+// next group's load must leave only after the current group's wait)
+static __device__ __forceinline__ uint32_t adec_step_c_fence(u32x32 &lists, uint32_t &vprev, uint32_t c)
+{
+    const uint32_t v = adec_step_c(lists, vprev, c);
+    asm volatile("" ::: "memory");
+    return v;
+}
+
+#define ADEC_PUTB(dst, val, k) asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(dst) : "s"(val), "i"(k))
+
+// one wave resolves the tokens of out[k0, k1) in place from ctl[0, k1 - k0); state[0..31] the
+// 16 lists, state[32] the byte before k0 (first: the initial lists and out[k0 - 1])
+__global__ __launch_bounds__(64) void k_nyb_resolve_c(uint8_t *__restrict__ out, uint64_t k0, uint64_t k1,
+                                                      const uint32_t *__restrict__ ctl, uint32_t *__restrict__ state,
+                                                      int first)
+{
+    const int lane = (int)threadIdx.x;
+    u32x32 lists;
+    uint32_t vprev;
+    if (first) {
+#pragma unroll
+        for (int c = 0; c < 16; ++c) {
+            lists[2 * c] = (uint32_t)mtf_init_word();
+            lists[2 * c + 1] = (uint32_t)(mtf_init_word() >> 32);
+        }
+        vprev = (uint32_t)__builtin_amdgcn_readfirstlane((int)out[k0 - 1]);
+    } else {
+        c_u32 *st = (c_u32 *)state;
+#pragma unroll
+        for (int q = 0; q < 32; ++q) lists[q] = st[q];
+        vprev = st[32];
+    }
+    c_u32 *cw = (c_u32 *)ctl;
+    const uint64_t m = k1 - k0, nfull = m / 64;
+    if (nfull) {
+        uint32_t A[16], B[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) A[q] = cw[q];
+        for (uint64_t b = 0; b < nfull; ++b) {
+            uint32_t ov = 0;   // lane k: the byte of token 64b + k
+            c_u32 *blk = cw + 64 * b;
+#pragma unroll
+            for (int g = 0; g < 4; g += 2) {
+                // group g in A (its load waited for by the first step), g + 1 into B meanwhile
+                ADEC_PUTB(ov, adec_step_c_fence(lists, vprev, A[0]), 16 * g);
+#pragma unroll
+                for (int q = 0; q < 16; ++q) B[q] = blk[16 * (g + 1) + q];
+#pragma unroll
+                for (int k = 1; k < 16; ++k) ADEC_PUTB(ov, adec_step_c(lists, vprev, A[k]), 16 * g + k);
+                ADEC_PUTB(ov, adec_step_c_fence(lists, vprev, B[0]), 16 * g + 16);
+                // then group g + 2 (the next block's first group after g = 2; past the end: reread)
+                c_u32 *nx = (g + 2 < 4) ? blk + 16 * (g + 2) : (b + 1 < nfull ? blk + 64 : blk);
+#pragma unroll
+                for (int q = 0; q < 16; ++q) A[q] = nx[q];
+#pragma unroll
+                for (int k = 1; k < 16; ++k) ADEC_PUTB(ov, adec_step_c(lists, vprev, B[k]), 16 * g + 16 + k);
+            }
+            out[k0 + 64 * b + lane] = (uint8_t)ov;
+        }
+    }
+    uint32_t ov = 0;   // the last < 64 tokens, one at a time
+    for (uint64_t i = 64 * nfull; i < m; ++i) {
+        const uint32_t v = adec_step_c(lists, vprev, cw[i]);
+        ov = (uint64_t)lane == i - 64 * nfull ? v : ov;
+    }
+    if ((uint64_t)lane < m - 64 * nfull) out[k0 + 64 * nfull + lane] = (uint8_t)ov;
+    if (lane == 0) {
+#pragma unroll
+        for (int q = 0; q < 32; ++q) state[q] = lists[q];
+        state[32] = vprev;
+    }
 }
 
 __global__ __launch_bounds__(64) void k_nyb_adec(const uint8_t *__restrict__ in, uint64_t len,
@@ -4796,6 +4940,8 @@ struct dc_ctx {
     uint64_t *d_entry;      size_t entry_cap;
     MtfSum *d_mtf;          size_t mtf_cap;       // adaptive nybble: tile summaries + entries, all levels
     uint8_t *d_rk;          size_t rk_cap;        // adaptive nybble: rank per element
+    uint32_t *d_actl;       size_t actl_cap;      // adaptive nybble decode: control words of a segment
+    uint32_t *d_astate;                           // adaptive nybble decode: lists + byte between segments
     const uint8_t *rk_in; uint64_t rk_len;        // identity of the input the ranks belong to
     const uint8_t *fsm_in; uint64_t fsm_len, fsm_nelem; int fsm_mode;   // input of the last transducer plan
     uint8_t *d_kscr;        size_t kscr_cap;      // chunked nybble: per-chunk streams before packing
@@ -4811,7 +4957,8 @@ struct dc_ctx {
     uint32_t opt_hist_pf;         // histogram: blocks of loads in flight ahead (1..2, 0 = default 2)
     uint32_t *d_hflag;            // histogram accumulator (256 u64) + done counter, zero between launches
     uint32_t opt_decode_variant;  // fast decoder: 0 one code per lookup (k_huff_decode8), 1 up to 3 (k_huff_decode9)
-    uint32_t opt_adec_v1;         // adaptive nybble decode: 1 = the one-pass k_nyb_adec (A/B)
+    uint32_t opt_adec_v1;         // adaptive nybble decode: 0 control words + k_nyb_resolve_c, 1 = the one-pass
+                                  // k_nyb_adec, 2 = r2's k_nyb_resolve, 3 = k_nyb_resolve_s (A/B)
     // timing
     int timing;
     int nev;
@@ -4942,6 +5089,8 @@ void dc_ctx_destroy(dc_ctx *c)
     if (c->d_entry) (void)hipFree(c->d_entry);
     if (c->d_mtf) (void)hipFree(c->d_mtf);
     if (c->d_rk) (void)hipFree(c->d_rk);
+    if (c->d_actl) (void)hipFree(c->d_actl);
+    if (c->d_astate) (void)hipFree(c->d_astate);
     if (c->d_kscr) (void)hipFree(c->d_kscr);
     if (c->d_klens) (void)hipFree(c->d_klens);
     if (c->h_pinned) (void)hipHostFree(c->h_pinned);
@@ -4976,7 +5125,7 @@ int dc_ctx_set_option(dc_ctx *c, int option, int64_t value)
         c->opt_decode_variant = (uint32_t)value;
         return DC_OK;
     case DC_OPT_NYB_ADEC_V1:
-        if (value < 0 || value > 2) return DC_E_ARG;
+        if (value < 0 || value > 3) return DC_E_ARG;
         c->opt_adec_v1 = (uint32_t)value;
         return DC_OK;
     case DC_OPT_HIST_PREFETCH:
@@ -5585,6 +5734,25 @@ static int mtf_run(dc_ctx *c, const uint8_t *d_in, uint64_t len, const MtfSum *h
     return DC_OK;
 }
 
+// The adaptive decode's resolve (k_nyb_resolve_c) over the tokens in out[1, n), in segments
+// of ADEC_SEG tokens (a control dword each).
+#define ADEC_SEG (16ull << 20)
+static int adec_fast(dc_ctx *c, uint8_t *d_out, uint64_t n)
+{
+    const uint64_t seg = std::min<uint64_t>(n - 1, ADEC_SEG);
+    if (ensure((void **)&c->d_actl, &c->actl_cap, (seg + 64) * sizeof(uint32_t))) return DC_E_HIP;
+    if (!c->d_astate && hipMalloc(&c->d_astate, 64 * sizeof(uint32_t)) != hipSuccess) return DC_E_HIP;
+    for (uint64_t k0 = 1; k0 < n; k0 += ADEC_SEG) {
+        const uint64_t k1 = std::min<uint64_t>(k0 + ADEC_SEG, n);
+        const uint64_t grid = std::min<uint64_t>((k1 - k0 + 255) / 256, 8192);
+        LAUNCH(c, "nyb_adec_ctl", k_nyb_adec_ctl, grid, 256, (const uint8_t *)d_out, k0, k1, c->d_actl);
+        LAUNCH(c, "nyb_resolve", k_nyb_resolve_c, 1, 64, d_out, k0, k1, (const uint32_t *)c->d_actl, c->d_astate,
+               k0 == 1 ? 1 : 0);
+    }
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return DC_OK;
+}
+
 static MtfSum mtf_initial()   // initialize_dictionary (nybble_compression.c:546-562)
 {
     MtfSum s;
@@ -5819,9 +5987,11 @@ int dc_nyb_decompress(dc_ctx *c, const uint8_t *d_in, uint64_t m, int modify, ui
         // tokens by the static transducer (parallel), then one wave resolves them in place
         r = fsm_run<M_NYB_DEC>(c, d_in, m, m - 2, d_out, h_len, "nyb_tok_tiles", FsmAux{nullptr, 0, 0, 1, 1, 1});
         if (r) return r;
-        if (*h_len > 1) {
-            if (c->opt_adec_v1 == 2) LAUNCH(c, "nyb_resolve", k_nyb_resolve, 1, 64, d_out, *h_len);   // A/B: r2's
-            else LAUNCH(c, "nyb_resolve", k_nyb_resolve_s, 1, 64, d_out, *h_len);
+        const uint64_t n = *h_len;
+        if (n > 1 && c->opt_adec_v1 == 0) return adec_fast(c, d_out, n);   // control words + k_nyb_resolve_c
+        if (n > 1) {
+            if (c->opt_adec_v1 == 2) LAUNCH(c, "nyb_resolve", k_nyb_resolve, 1, 64, d_out, n);   // A/B: r2's
+            else LAUNCH(c, "nyb_resolve", k_nyb_resolve_s, 1, 64, d_out, n);
         }
         HIPCHK(hipStreamSynchronize(c->stream));
         return DC_OK;

@@ -678,12 +678,13 @@ def test_nybble_encode_parallel_vs_oracle(torch_cuda, codec, modify):
                 assert np.array_equal(back.cpu().numpy(), x), (kind, x.size)
 
 
-@pytest.mark.parametrize("v1", [False, True])
+@pytest.mark.parametrize("v1", [0, 1, 3])
 def test_nybble_adaptive_decode_edges(torch_cuda, codec, v1):
-    """Adaptive decode (tokens by the static transducer, then k_nyb_resolve in place; v1 = the
-    one-pass k_nyb_adec): every output size 1..200 and block-boundary sizes, output buffers
-    at every offset mod 64 (the resolve kernel's guarded first and last blocks), against the
-    reference restatement."""
+    """Adaptive decode (tokens by the static transducer, then the resolve in place: 0 = control
+    words + k_nyb_resolve_c + the re-encode check, 3 = the exact k_nyb_resolve_s, 1 = the
+    one-pass k_nyb_adec): every output size 1..200 and block-boundary sizes, output buffers at
+    every offset mod 64 (the resolve kernels' first and last blocks), against the reference
+    restatement."""
     torch = torch_cuda
     from data_compression_amd import synth
     codec.set_option("nyb_adec_v1", int(v1))
@@ -701,6 +702,37 @@ def test_nybble_adaptive_decode_edges(torch_cuda, codec, v1):
             assert got.cpu().numpy().tobytes() == want, (n, off)
             tail = big[off + len(want):].cpu().numpy()
             assert (big[:off].cpu().numpy() == 0xEE).all() and (tail[: 2 * len(ref) - len(want)] == 0xEE).all(), n
+    finally:
+        codec.set_option("nyb_adec_v1", 0)
+
+
+@pytest.mark.parametrize("v1", [0, 3])
+def test_nybble_adaptive_decode_any_stream(torch_cuda, codec, v1):
+    """Adaptive decode of arbitrary streams (random nybbles after the 0xAF header, and the
+    encoder's streams with one byte changed to a literal that is in its list, which the
+    reference decoder moves from where it is), for the control-word resolve and the plain-code
+    one, against the reference restatement."""
+    torch = torch_cuda
+    from data_compression_amd import synth
+    codec.set_option("nyb_adec_v1", v1)
+    try:
+        rng = np.random.default_rng(23)
+        for n in [3, 4, 17, 64, 65, 66, 130, 1000, 4097, 70_001]:
+            for kind in ("random", "low", "patched"):
+                if kind == "patched":
+                    ref = bytearray(orc.nybble_compress(synth.english_like(n, seed=n).tobytes(), True))
+                    if ref[0] != 0xAF or len(ref) < 4:
+                        continue
+                    k = 2 + int(rng.integers(0, len(ref) - 2))
+                    ref[k] = 0x65   # a literal 'e' nybble pair where the stream had something else
+                    comp = bytes(ref)
+                else:
+                    body = rng.integers(0, 256 if kind == "random" else 128, size=n, dtype=np.uint8)
+                    comp = bytes([0xAF]) + body.tobytes()
+                want = orc.nybble_decompress(comp, True)
+                t = torch.from_numpy(np.frombuffer(comp, np.uint8).copy()).cuda()
+                got = codec.nyb_decompress(t, True).cpu().numpy().tobytes()
+                assert got == want, (n, kind)
     finally:
         codec.set_option("nyb_adec_v1", 0)
 
