@@ -3775,24 +3775,31 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
                 if (k & 1) flush();
             }
         } else {   // M_NYB_DEC / M_NYB_DBODY: compressed byte x, state s = "at the low nybble"
-            // elements whose next byte is inside the stream (the literal's second nybble)
-            const uint64_t kk0 = M == M_NYB_DBODY ? j0 : j0 + 2;
-            const uint32_t nxt_ok = kk0 + 1 >= len ? 0u : (len - kk0 - 1 >= 16 ? 0xFFFFu : (1u << (uint32_t)(len - kk0 - 1)) - 1u);
+            // (r2's element loop: per element branches measured 1-3% faster here than the
+            // encoder's branch-free form, same-box A/B tools/gpu_r3n.sh)
 #pragma unroll
             for (int k = 0; k < 16; ++k) {
                 const uint32_t x = W.b(k + 1);
                 const uint32_t s = (S >> k) & 1u;
+                const uint64_t kk = M == M_NYB_DBODY ? j0 + k : j0 + k + 2;
                 const uint32_t h = x >> 4, l = x & 15u;
-                const uint32_t nxt = ((nxt_ok >> k) & 1u) ? (W.b(k + 2) >> 4) : 0u;
+                const uint32_t nxt = (kk + 1 < len) ? (W.b(k + 2) >> 4) : 0u;
                 const uint32_t lo_b = (l & 8u) ? (uint32_t)(tblv >> (8u * (l & 7u))) & 255u : ((l & 7u) << 4) + nxt;
                 const uint32_t hi_b = (uint32_t)(tblv >> (8u * (h & 7u))) & 255u;
                 const bool two = !s && (h & 8u);
-                uint32_t val = s ? lo_b : (two ? (hi_b | (lo_b << 8)) : x);
-                const uint32_t in_range = (valid >> k) & 1u;
-                val &= 0u - in_range;
-                acc |= (uint64_t)val << nb;
-                nb += in_range * (two ? 16u : 8u);
-                if (k & 1) flush();
+                const uint32_t val = s ? lo_b : (two ? (hi_b | (lo_b << 8)) : x);
+                if ((uint32_t)k < kend) {
+                    acc |= (uint64_t)val << nb;
+                    nb += two ? 16u : 8u;
+                }
+                if (k & 1) {
+                    if (nb >= 32u) {
+                        atomicOr(&s_out32[di], (uint32_t)acc);
+                        acc >>= 32;
+                        nb -= 32u;
+                        ++di;
+                    }
+                }
             }
         }
         if (nb) atomicOr(&s_out32[di], (uint32_t)acc);
