@@ -2495,6 +2495,11 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode8(const uint32_t *__rest
             *pp = (uint64_t)cur.wo[j] * 32 + cur.lead[j] + cur.off[j];   // chunk start, bits from word_base
             uint64_t *mp = g < ngroups ? fix_mask + g : reinterpret_cast<uint64_t *>(dummy) + 64;
             *mp = m;
+            // the first flagged chunk's start also beside the masks (fix_mask + ngroups: the redo
+            // reads it with them, coalesced, instead of gathering its fix_pos line)
+            const uint32_t f = (uint32_t)__builtin_ctzll(m | (1ull << 63));
+            uint64_t *fp = g < ngroups ? fix_mask + ngroups + g : reinterpret_cast<uint64_t *>(dummy) + 65;
+            *fp = (uint64_t)cur.wo[j] * 32 + cur.lead[j] + (uint32_t)__builtin_amdgcn_readlane((int)cur.off[j], (int)f);
         }
         // next tuple: stage it (its spans are in v), then start the loads of the one after
         tp = t1;
@@ -2718,6 +2723,9 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode9(const uint32_t *__rest
             *pp = (uint64_t)cur.wo[0] * 32 + cur.lead[0] + cur.off[0];
             uint64_t *mp = gg < ngroups ? fix_mask + gg : reinterpret_cast<uint64_t *>(dummy) + 64;
             *mp = m;
+            const uint32_t f = (uint32_t)__builtin_ctzll(m | (1ull << 63));   // (as k_huff_decode8)
+            uint64_t *fp = gg < ngroups ? fix_mask + ngroups + gg : reinterpret_cast<uint64_t *>(dummy) + 65;
+            *fp = (uint64_t)cur.wo[0] * 32 + cur.lead[0] + (uint32_t)__builtin_amdgcn_readlane((int)cur.off[0], (int)f);
         }
         tp = t1;
         t1 = t2;
@@ -2743,7 +2751,7 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode9(const uint32_t *__rest
 #define D8F_WAVES 16   /* 16 x 24-word rows: 0.113 -> 0.091 ms on 1 GiB C2 vs 12 x 32 */
 #endif
 #ifndef D8F_ROW
-#define D8F_ROW 24   /* words of a lane's staged span (longer chunks re-stage it further on) */
+#define D8F_ROW 20   /* words of a lane's staged span (longer chunks re-stage it further on; r2-r3: 24) */
 #endif
 static_assert(offsetof(dc_dtable, dlut14) % 16 == 0 && offsetof(dc_dtable, dlut15) % 16 == 0 && offsetof(dc_dtable, dlut2) % 8 == 0,
               "table copies");
@@ -2794,7 +2802,7 @@ static __device__ __noinline__ uint32_t d8_long_lds(uint32_t lo, uint32_t hi, co
 // (r2 listed the chunks in a launch of its own, k_huff_fix_list: 0.008 ms + a launch gap on
 // 1 GiB C2; a flagged chunk falls in any group with the same odds, so equal shares of the
 // groups are equal shares of the work, ~12 rounds per workgroup of 16 waves on C2.)
-#define D8F_LIST 2048   /* listed chunks per pass (LDS) */
+#define D8F_LIST 1024   /* listed chunks per pass (LDS) */
 __global__ __launch_bounds__(D8F_WAVES * 64) void k_huff_decode8_fix(const uint32_t *__restrict__ in, uint64_t n,
                                                                     uint64_t nwords, const dc_dtable *__restrict__ T,
                                                                     uint8_t *__restrict__ out, int *__restrict__ err,
@@ -2806,6 +2814,7 @@ __global__ __launch_bounds__(D8F_WAVES * 64) void k_huff_decode8_fix(const uint3
     constexpr int NT = D8F_WAVES * 64;
     __shared__ FixLds F;
     __shared__ uint32_t s_list[D8F_LIST];
+    __shared__ uint64_t s_pos[D8F_LIST];   // a listed chunk's start when it is its group's first, else ~0
     __shared__ uint32_t s_wsum[D8F_WAVES];
     const int t = threadIdx.x, lane = t & 63, wv = __builtin_amdgcn_readfirstlane(t >> 6);
     D8_STAMP(f_begin);
@@ -2824,7 +2833,10 @@ __global__ __launch_bounds__(D8F_WAVES * 64) void k_huff_decode8_fix(const uint3
         if (c0 + DC_SYNC_GROUP > nchunks) m = c0 >= nchunks ? 0ull : m & ((1ull << (nchunks - c0)) - 1);
         return m;
     };
+    const uint64_t *const fix_first = fix_mask + ngroups;   // (k_huff_decode8: the first flagged chunk's start)
+    auto window_first = [&](uint32_t g) -> uint64_t { return fix_first[g < g1 ? g : g0]; };
     uint64_t mk = window_mask(g0 + t);   // the first window's masks, in flight during the table copy
+    uint64_t fk = window_first(g0 + t);
     {   // the tables into LDS: all loads first, then the stores
         static_assert((1 << D8F_LUT_BITS) / 8 <= 2 * NT && DC_LUT2_CAP / 4 <= 2 * NT && DC_MAX_SYMS <= NT &&
                       DC_MAX_DIGITS + 1 <= NT, "one copy pass");
@@ -2883,15 +2895,22 @@ __global__ __launch_bounds__(D8F_WAVES * 64) void k_huff_decode8_fix(const uint3
             before += q < wv ? x : 0u;
             total += x;
         }
-        const uint64_t m_me = mk;
+        const uint64_t m_me = mk, f_me = fk;
         const uint32_t c0 = (wb + (uint32_t)t) * DC_SYNC_GROUP;
-        if (wb + NT < g1) mk = window_mask(wb + NT + t);   // the next window's masks, in flight
+        if (wb + NT < g1) {   // the next window's masks, in flight
+            mk = window_mask(wb + NT + t);
+            fk = window_first(wb + NT + t);
+        }
         for (uint32_t part = 0; part < total; part += D8F_LIST) {   // (one part unless > 2048 chunks)
             {
                 uint32_t e = before + incl - c;
-                uint64_t m = m_me;
+                uint64_t m = m_me, fpos = f_me;
                 while (m) {
-                    if (e >= part && e < part + D8F_LIST) s_list[e - part] = c0 + (uint32_t)__builtin_ctzll(m);
+                    if (e >= part && e < part + D8F_LIST) {
+                        s_list[e - part] = c0 + (uint32_t)__builtin_ctzll(m);
+                        s_pos[e - part] = fpos;
+                    }
+                    fpos = ~0ull;
                     ++e;
                     m &= m - 1;
                 }
@@ -2904,10 +2923,17 @@ __global__ __launch_bounds__(D8F_WAVES * 64) void k_huff_decode8_fix(const uint3
             auto chunk_of = [&](uint32_t r) -> uint32_t {
                 return r < nrounds && r * 64 + (uint32_t)lane < cnt ? s_list[r * 64 + lane] : ~0u;
             };
+            // a chunk's start: from the list when it is its group's first flagged chunk, else
+            // gathered from fix_pos (always a load: of line 0 when not needed, no branch)
+            auto pos_of = [&](uint32_t r, uint32_t ch) -> uint64_t {
+                const uint64_t p = r < nrounds && r * 64 + (uint32_t)lane < cnt ? s_pos[r * 64 + lane] : 0ull;
+                const uint64_t q = fix_pos[(p == ~0ull && ch != ~0u) ? ch : 0u];
+                return p == ~0ull ? q : p;
+            };
             uint32_t ra = (uint32_t)wv;   // round of A; B and C follow by the stride
             uint32_t cha = chunk_of(ra), chb = chunk_of(ra + D8F_WAVES);
-            uint64_t posa = fix_pos[cha != ~0u ? cha : 0u];
-            uint64_t posb = fix_pos[chb != ~0u ? chb : 0u];
+            uint64_t posa = pos_of(ra, cha);
+            uint64_t posb = pos_of(ra + D8F_WAVES, chb);
             uint4 sv[D8F_ROW / 4];
             if (ra < nrounds) load_row(sv, row_base(posa));
             while (ra < nrounds) {
@@ -2924,7 +2950,7 @@ __global__ __launch_bounds__(D8F_WAVES * 64) void k_huff_decode8_fix(const uint3
                 put_row(sv);
                 load_row(sv, row_base(posb));
                 const uint32_t chc = chunk_of(ra + 2 * D8F_WAVES);
-                const uint64_t posc = fix_pos[chc != ~0u ? chc : 0u];
+                const uint64_t posc = pos_of(ra + 2 * D8F_WAVES, chc);
                 // decode round A (the clamp keeps a corrupt mask from writing past the output)
                 const bool valid = cha != ~0u && (uint64_t)cha * S < n;
                 const uint64_t s0 = (uint64_t)(valid ? cha : 0u) * S;
@@ -5516,7 +5542,7 @@ static int decode_impl(dc_ctx *c, const uint32_t *d_words, uint64_t bit_base, co
         // LDS (the 8 x 4 split measured 0.89 vs 0.70 ms on 1 GiB C2: spills)
         const uint32_t spct = c->opt_d8_static;   // clamped to 0..100 by dc_ctx_set_option
         const uint64_t tuples = (groups + 1) / 2;   // 2 chains (groups) per wave
-        if (ensure((void **)&c->d_fix, &c->fix_cap, (groups + 64) * sizeof(uint64_t)) ||
+        if (ensure((void **)&c->d_fix, &c->fix_cap, (2 * groups + 64) * sizeof(uint64_t)) ||   // masks, first starts
             ensure((void **)&c->d_fixpos, &c->fixpos_cap, (groups * 64 + 64) * sizeof(uint64_t)))
             return DC_E_HIP;
         if (ensure((void **)&c->d_scr, &c->scr_cap, (size_t)D8_SCRATCH_WAVES * D8_WSCR)) return DC_E_HIP;
