@@ -4938,13 +4938,6 @@ __global__ __launch_bounds__(256) void k_copy_probe(const uint4 *__restrict__ sr
 {
     const uint64_t stride = (uint64_t)gridDim.x * 256;
     uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    for (; i + 3 * stride < n16; i += 4 * stride) {
-        uint4 v[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) v[k] = ld_nt(src + i + k * stride);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) st_nt(dst + i + k * stride, v[k]);
-    }
     for (; i < n16; i += stride) st_nt(dst + i, ld_nt(src + i));
 }
 
@@ -5235,8 +5228,10 @@ int dc_copy_probe(dc_ctx *c, const void *d_src, void *d_dst, uint64_t bytes)
 {
     if (!c || (bytes && (!d_src || !d_dst)) || (bytes & 15) || (((uintptr_t)d_src | (uintptr_t)d_dst) & 15)) return DC_E_ARG;
     if (!bytes) return DC_OK;
+    // grid 16384 (r3g measured 4096 x 4 uint4 per lane at 4.47 TB/s on 1 GiB, 16384 at 5.26;
+    // tools/ubench/gap2.hip: 16384 with 1 uint4 per lane and step 5.44, a read-only pass 6.35)
     const uint64_t n16 = bytes / 16, wgs = (n16 + 255) / 256;
-    LAUNCH(c, "copy_probe", k_copy_probe, wgs < 4096 ? wgs : 4096, 256, (const uint4 *)d_src, (uint4 *)d_dst, n16);
+    LAUNCH(c, "copy_probe", k_copy_probe, wgs < 16384 ? wgs : 16384, 256, (const uint4 *)d_src, (uint4 *)d_dst, n16);
     return DC_OK;
 }
 
