@@ -4605,45 +4605,53 @@ __global__ __launch_bounds__(256) void k_nyb_adec_ctl(const uint8_t *__restrict_
     }
 }
 
+// STEP_C_ASM(W): the step's text; W is inserted right after the join, where v is final (the
+// block loop puts v_writelane there: issued after the s_movreld it drew a compiler s_nop)
+#define STEP_C_ASM_X(W, V, VP, C, SFX)                                                                         \
+        "s_lshr_b32 %[" V "], %[" C "], 24\n\t"                /* the literal (0 for a hit); first, so   \
+                                                          the previous s_movreld is not followed \
+                                                          by an M0 write (a compiler s_nop) */  \
+        "s_bfe_u32 m0, %[" VP "], 0x50002\n\t"             /* 2c (+ bit 2 of the byte: ignored) */  \
+        "s_bitcmp1_b32 %[" C "], 23\n\t"                   /* a literal: search its position */     \
+        "s_movrels_b64 s[96:97], s[64:65]\n\t"          /* L = the list of context c */          \
+        "s_cbranch_scc0 .Lhit%=" SFX "\n\t"                                                           \
+        "s_mul_i32 s98, %[" V "], 0x1010101\n\t"           /* (update_context's search :674-682) */ \
+        "s_xor_b32 s99, s98, s97\n\t"                                                          \
+        "s_xor_b32 s98, s98, s96\n\t"                                                          \
+        "s_sub_u32 %[T], s98, 0x1010101\n\t"                                                   \
+        "s_andn2_b32 %[T], %[T], s98\n\t"                                                      \
+        "s_and_b32 s98, %[T], 0x80808080\n\t"          /* zero bytes of the low half */         \
+        "s_sub_u32 %[T], s99, 0x1010101\n\t"                                                   \
+        "s_andn2_b32 %[T], %[T], s99\n\t"                                                      \
+        "s_and_b32 s99, %[T], 0x80808080\n\t"                                                  \
+        "s_ff1_i32_b64 %[T], s[98:99]\n\t"                                                     \
+        "s_lshr_b32 %[T], %[T], 3\n\t"                                                         \
+        "s_min_u32 %[T], %[T], 7\n\t"                  /* absent: 7, the last entry drops */    \
+        "s_lshl_b32 %[T], %[T], 3\n\t"                                                         \
+        "s_lshl_b64 %[N], -1, %[T]\n\t"                                                        \
+        "s_branch .Ljoin%=" SFX "\n"                                                                  \
+        ".Lhit%=" SFX ":\n\t"                                                                         \
+        "s_bfe_u64 s[98:99], s[96:97], %[" C "]\n\t"       /* a hit: the byte at its rank */        \
+        "s_or_b32 %[" V "], %[" V "], s98\n\t"                                                         \
+        "s_lshl_b64 %[N], -1, %[" C "]\n"                                                          \
+        ".Ljoin%=" SFX ":\n\t"                                                                        \
+        W                                                                                      \
+        "s_lshl_b64 %[N], %[N], 8\n\t"                 /* the bytes past p (they stay) */       \
+        "s_lshl_b64 s[98:99], s[96:97], 8\n\t"                                                 \
+        "s_andn2_b64 s[98:99], s[98:99], %[N]\n\t"     /* bytes 0..p-1 move up one */           \
+        "s_and_b64 s[96:97], s[96:97], %[N]\n\t"                                               \
+        "s_or_b64 s[96:97], s[96:97], s[98:99]\n\t"                                            \
+        "s_or_b32 s96, s96, %[" V "]\n\t"                  /* v to the front (:665-687) */          \
+        "s_movreld_b64 s[64:65], s[96:97]"
+
+#define STEP_C_ASM(W) STEP_C_ASM_X(W, "v", "vp", "c", "")
+
 static __device__ __forceinline__ uint32_t adec_step_c(u32x32 &lists, uint32_t &vprev, uint32_t c)
 {
     uint32_t v, T;
     uint64_t N;   // (compiler-chosen scratch; the fixed pairs s96-s99 stay clear of s100-s101,
                   //  which gfx950 reserves; M0 is used by nothing else in these kernels)
-    asm volatile(
-        "s_bfe_u32 m0, %[vp], 0x50002\n\t"             // 2c (+ bit 2 of the byte: ignored)
-        "s_lshr_b32 %[v], %[c], 24\n\t"                // the literal (0 for a hit)
-        "s_bitcmp1_b32 %[c], 23\n\t"                   // a literal that may be in its list?
-        "s_movrels_b64 s[96:97], s[64:65]\n\t"          // L = the list of context c (2 instructions after M0)
-        "s_cbranch_scc0 .Lhit%=\n\t"
-        // a literal: its position in L (update_context's search, :674-682), 7 when absent
-        "s_mul_i32 s98, %[v], 0x1010101\n\t"
-        "s_xor_b32 s99, s98, s97\n\t"
-        "s_xor_b32 s98, s98, s96\n\t"
-        "s_sub_u32 %[T], s98, 0x1010101\n\t"
-        "s_andn2_b32 %[T], %[T], s98\n\t"
-        "s_and_b32 s98, %[T], 0x80808080\n\t"           // zero bytes of the low half (the lowest exact)
-        "s_sub_u32 %[T], s99, 0x1010101\n\t"
-        "s_andn2_b32 %[T], %[T], s99\n\t"
-        "s_and_b32 s99, %[T], 0x80808080\n\t"
-        "s_ff1_i32_b64 %[T], s[98:99]\n\t"
-        "s_lshr_b32 %[T], %[T], 3\n\t"
-        "s_min_u32 %[T], %[T], 7\n\t"
-        "s_lshl_b32 %[T], %[T], 3\n\t"
-        "s_lshl_b64 %[N], -1, %[T]\n\t"
-        "s_branch .Ljoin%=\n"
-        ".Lhit%=:\n\t"
-        "s_bfe_u64 s[98:99], s[96:97], %[c]\n\t"       // a hit: the byte at its rank (a miss: 0, p = 7)
-        "s_or_b32 %[v], %[v], s98\n\t"
-        "s_lshl_b64 %[N], -1, %[c]\n"
-        ".Ljoin%=:\n\t"
-        "s_lshl_b64 %[N], %[N], 8\n\t"                 // the bytes past p (they stay)
-        "s_lshl_b64 s[98:99], s[96:97], 8\n\t"
-        "s_andn2_b64 s[98:99], s[98:99], %[N]\n\t"     // bytes 0..p-1 move up one
-        "s_and_b64 s[96:97], s[96:97], %[N]\n\t"
-        "s_or_b64 s[96:97], s[96:97], s[98:99]\n\t"
-        "s_or_b32 s96, s96, %[v]\n\t"                  // v to the front (:665-687)
-        "s_movreld_b64 s[64:65], s[96:97]"
+    asm volatile(STEP_C_ASM("")
         : [lists] "+{s[64:95]}"(lists), [v] "=&s"(v), [N] "=&s"(N), [T] "=&s"(T)
         : [vp] "s"(vprev), [c] "s"(c)
         : "s96", "s97", "s98", "s99", "scc");
@@ -4651,17 +4659,50 @@ static __device__ __forceinline__ uint32_t adec_step_c(u32x32 &lists, uint32_t &
     return v;
 }
 
-// the same step, also a compiler barrier for memory: the scalar loads written after it are
-// issued after it (scalar loads complete out of order, so waiting for one waits for all: the
-// next group's load must leave only after the current group's wait)
-static __device__ __forceinline__ uint32_t adec_step_c_fence(u32x32 &lists, uint32_t &vprev, uint32_t c)
+// four steps in one statement (between two asm statements the compiler puts an s_nop: it
+// cannot see that the next one's first instruction is no hazard after the s_movreld)
+#define STEP_WL(V, KK) "v_writelane_b32 %[ov], %[" V "], %[" KK "]\n\t"
+template <int K>
+static __device__ __forceinline__ void adec_step_cw4(u32x32 &lists, uint32_t &vprev, const uint32_t *c, uint32_t &ov)
 {
-    const uint32_t v = adec_step_c(lists, vprev, c);
-    asm volatile("" ::: "memory");
-    return v;
+    uint32_t v0, v1, v2, v3, T;
+    uint64_t N;
+    asm volatile(STEP_C_ASM_X(STEP_WL("v0", "k0"), "v0", "vp", "c0", "a") "\n\t"
+                 STEP_C_ASM_X(STEP_WL("v1", "k1"), "v1", "v0", "c1", "b") "\n\t"
+                 STEP_C_ASM_X(STEP_WL("v2", "k2"), "v2", "v1", "c2", "c") "\n\t"
+                 STEP_C_ASM_X(STEP_WL("v3", "k3"), "v3", "v2", "c3", "d")
+        : [lists] "+{s[64:95]}"(lists), [v0] "=&s"(v0), [v1] "=&s"(v1), [v2] "=&s"(v2), [v3] "=&s"(v3),
+          [N] "=&s"(N), [T] "=&s"(T), [ov] "+v"(ov)
+        : [vp] "s"(vprev), [c0] "s"(c[0]), [c1] "s"(c[1]), [c2] "s"(c[2]), [c3] "s"(c[3]),
+          [k0] "i"(K), [k1] "i"(K + 1), [k2] "i"(K + 2), [k3] "i"(K + 3)
+        : "s96", "s97", "s98", "s99", "scc");
+    vprev = v3;
 }
 
-#define ADEC_PUTB(dst, val, k) asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(dst) : "s"(val), "i"(k))
+
+// a 64-token block: group G from A (loaded), group G + 1 into B while it runs (its load
+// issued after the first steps' wait), and so on: G = 0, 2
+template <int G>
+static __device__ __forceinline__ void adec_block(u32x32 &lists, uint32_t &vprev, uint32_t (&A)[16], uint32_t (&B)[16],
+                                                  c_u32 *blk, c_u32 *next_blk, uint32_t &ov)
+{
+    adec_step_cw4<16 * G>(lists, vprev, A, ov);
+    asm volatile("" ::: "memory");   // group G + 1's load leaves after the wait for group G
+#pragma unroll
+    for (int q = 0; q < 16; ++q) B[q] = blk[16 * (G + 1) + q];
+    adec_step_cw4<16 * G + 4>(lists, vprev, A + 4, ov);
+    adec_step_cw4<16 * G + 8>(lists, vprev, A + 8, ov);
+    adec_step_cw4<16 * G + 12>(lists, vprev, A + 12, ov);
+    adec_step_cw4<16 * G + 16>(lists, vprev, B, ov);
+    asm volatile("" ::: "memory");
+    c_u32 *nx = (G + 2 < 4) ? blk + 16 * (G + 2) : next_blk;   // group G + 2, or the next block's first
+#pragma unroll
+    for (int q = 0; q < 16; ++q) A[q] = nx[q];
+    adec_step_cw4<16 * G + 20>(lists, vprev, B + 4, ov);
+    adec_step_cw4<16 * G + 24>(lists, vprev, B + 8, ov);
+    adec_step_cw4<16 * G + 28>(lists, vprev, B + 12, ov);
+    if (G == 0) adec_block<2>(lists, vprev, A, B, blk, next_blk, ov);
+}
 
 // one wave resolves the tokens of out[k0, k1) in place from ctl[0, k1 - k0); state[0..31] the
 // 16 lists, state[32] the byte before k0 (first: the initial lists and out[k0 - 1])
@@ -4694,22 +4735,7 @@ __global__ __launch_bounds__(64) void k_nyb_resolve_c(uint8_t *__restrict__ out,
         for (uint64_t b = 0; b < nfull; ++b) {
             uint32_t ov = 0;   // lane k: the byte of token 64b + k
             c_u32 *blk = cw + 64 * b;
-#pragma unroll
-            for (int g = 0; g < 4; g += 2) {
-                // group g in A (its load waited for by the first step), g + 1 into B meanwhile
-                ADEC_PUTB(ov, adec_step_c_fence(lists, vprev, A[0]), 16 * g);
-#pragma unroll
-                for (int q = 0; q < 16; ++q) B[q] = blk[16 * (g + 1) + q];
-#pragma unroll
-                for (int k = 1; k < 16; ++k) ADEC_PUTB(ov, adec_step_c(lists, vprev, A[k]), 16 * g + k);
-                ADEC_PUTB(ov, adec_step_c_fence(lists, vprev, B[0]), 16 * g + 16);
-                // then group g + 2 (the next block's first group after g = 2; past the end: reread)
-                c_u32 *nx = (g + 2 < 4) ? blk + 16 * (g + 2) : (b + 1 < nfull ? blk + 64 : blk);
-#pragma unroll
-                for (int q = 0; q < 16; ++q) A[q] = nx[q];
-#pragma unroll
-                for (int k = 1; k < 16; ++k) ADEC_PUTB(ov, adec_step_c(lists, vprev, B[k]), 16 * g + 16 + k);
-            }
+            adec_block<0>(lists, vprev, A, B, blk, (b + 1 < nfull) ? blk + 64 : blk, ov);
             out[k0 + 64 * b + lane] = (uint8_t)ov;
         }
     }
