@@ -3768,6 +3768,9 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
             nb -= 32u * f;
             di += f;
         };
+#ifdef DC_DIAG_FSMW_NOLOOP   // timing ablation only: no element loop (garbage output)
+        if (M == M_NYB_ENC) { atomicOr(&s_out32[di], (uint32_t)S ^ valid); continue; }
+#endif
         if (M == M_NYB_ENC) {
             // masks of the lane's elements: a hit, and the state before it; an element past the
             // input counts as a hit in state 0 (no bytes)
