@@ -41,6 +41,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)   # ~1 ms each: amortises the bracketing syncs
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--prewarm", type=int, default=40,
+                    help="untimed steps before the W warmup steps: the GPU reaches its steady clocks "
+                         "only after ~20-30 ms of load (tools/step_probe.py, profiles/r3w_step_probe.log: "
+                         "after 5 warmup steps the first timed steps ran 1.15 -> 1.03 ms, steady 1.02)")
     ap.add_argument("--cfg", default="C2")
     ap.add_argument("--frontend", action="store_true",
                     help="C5 pipeline: small_compression.c front-end, then n-ary Huffman (dist.ShardedSmall)")
@@ -136,7 +140,7 @@ def main():
         decode()
 
     _phase(rank, "buffers ready")
-    for _ in range(a.warmup):
+    for _ in range(a.prewarm + a.warmup):   # the same count on every rank (steps hold collectives)
         step()
     torch.cuda.synchronize()
     _phase(rank, "warmup done")
@@ -260,6 +264,7 @@ def main():
         "n_gpus": world,
         "steps": a.steps,
         "warmup": a.warmup,
+        "prewarm": a.prewarm,
         "ms_per_step": round(ms_step, 4),
         "higher_is_better": True,
         "scaling": "weak",
@@ -336,7 +341,7 @@ def main_nybble(a, dev, rank, world):
         if not modify:
             decode()
 
-    for _ in range(a.warmup):
+    for _ in range(a.prewarm + a.warmup):   # the same count on every rank (steps hold collectives)
         step()
     torch.cuda.synchronize()
     if world > 1:
@@ -408,7 +413,7 @@ def main_nybble(a, dev, rank, world):
     res = {
         "metric": NYB_METRIC if not modify else NYB_METRIC.replace("encode+decode", "encode"),
         "value": round(world * n / (ms_step * 1e-3) / 1e9, 2),
-        "unit": "GB/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+        "unit": "GB/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup, "prewarm": a.prewarm,
         "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "u8", "data": "synthetic",
         "config": {"workload": f"nybble {'adaptive (nybble_compress)' if modify else 'static (compress_bytestring)'}"
