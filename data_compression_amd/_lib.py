@@ -99,6 +99,8 @@ def _declare_core(L):
         "dc_huff_pack_async": ([vp, P, u64, P, u64, P, u64, P, P, u32], i32),
         "dc_huff_pack_async_dev": ([vp, P, u64, P, P, P, u64, P, P, u32], i32),
         "dc_huff_pack_status": ([vp, P], i32),
+        "dc_huff_plan_gen": ([vp], u32),
+        "dc_huff_pack_status_gen": ([vp, P, u32], i32),
         "dc_huff_plan_offsets": ([vp, P, u64, C.POINTER(u64)], i32),
         "dc_huff_block_hist": ([vp, P, u64], i32),
         "dc_huff_decode": ([vp, P, u64, u64, P, P, u32, u64, P, P], i32),

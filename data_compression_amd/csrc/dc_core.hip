@@ -13,6 +13,8 @@
 #include <string.h>
 #include <stdlib.h>
 
+#include <atomic>
+
 #include "dc_gpu.h"
 
 #define DC_VERSION "dc-mi355x 0.1 (gfx950)"
@@ -1839,6 +1841,7 @@ static __device__ uint32_t d8_long(uint32_t lo, uint32_t hi, const dc_dtable *__
     return 0u;
 }
 
+#ifdef DC_AB_KERNELS   // multi_entry (k_huff_decode9's table): A/B alternative, diagnostic builds only (tools/diag_build.sh)
 // Multi-symbol lookup table of k_huff_decode9 (built into its LDS by every workgroup): up to
 // 3 whole codes at the start of a DC_MULTI_BITS-bit LSB-first window, by the canonical search
 // of d8_long repeated after each code while the window holds it. Symbols in bytes 0..2 (the
@@ -1861,6 +1864,8 @@ static __device__ __forceinline__ uint32_t multi_entry(uint32_t x, const dc_dtab
     }
     return cnt ? syms | (used << 24) | (cnt << 28) : 0u;
 }
+
+#endif  // DC_AB_KERNELS
 
 // any chunk, any count, exact: words read from HBM (MSB-first bytes; reads clamped to the
 // nwords of the buffer), bytes written one by one
@@ -2543,6 +2548,7 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode8(const uint32_t *__rest
 #endif
 }
 
+#ifdef DC_AB_KERNELS   // k_huff_decode9: A/B alternative, diagnostic builds only (tools/diag_build.sh)
 // ------------------------------------------------------------------------------------
 // (H8) fast decoder, multi-symbol form (S = 64; same schedule, staging, sync index, output
 // layout and redo protocol as k_huff_decode8, one chain per wave). A lookup in the 13-bit
@@ -2744,6 +2750,8 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode9(const uint32_t *__rest
             for (int h = 0; h <= 8; ++h) atomicExch(queue + h * D8_QSTRIDE, 0u);
     }
 }
+
+#endif  // DC_AB_KERNELS
 
 // The exact redo's LDS: the 14-bit table, its second level and the canonical tables of longer
 // codes (d8_long's rule), and a span row per lane.
@@ -4390,8 +4398,11 @@ static __device__ __forceinline__ void adec_flush(uint32_t w, uintptr_t OA, uint
 //     Tokens arrive by scalar loads one 64-byte block ahead; the 64 bytes of a block are
 //     assembled in SGPRs at static positions (the loop is unrolled over the block) and leave
 //     as 16 dwords of one VGPR.
-typedef __attribute__((address_space(4))) const uint32_t c_u32;   // scalar (s_load) reads
 
+typedef __attribute__((address_space(4))) const uint32_t c_u32;   // scalar (s_load) reads
+typedef uint32_t u32x32 __attribute__((ext_vector_type(32)));   // the 16 lists as 32 SGPR dwords
+
+#ifdef DC_AB_KERNELS   // k_nyb_resolve: A/B alternative, diagnostic builds only (tools/diag_build.sh)
 // one token -> its byte, with the list touch. The list of context c lives in VGPR lane c
 // (Llo, Hhi); all else is wave-uniform (SGPRs). Move to front (update_context :665-687) of
 // the entry at p (a hit: its rank; a literal: its position, or 7 when absent, so the last
@@ -4474,6 +4485,9 @@ __global__ __launch_bounds__(64) void k_nyb_resolve(uint8_t *__restrict__ out, u
     edge(k1, n);
 }
 
+#endif  // DC_AB_KERNELS
+
+#ifdef DC_AB_KERNELS   // k_nyb_resolve_s: A/B alternative, diagnostic builds only (tools/diag_build.sh)
 // Third form of pass 2 (the product path since r3): the 16 lists stay in SGPRs. They are one
 // wave-uniform vector of 16 u64; the uniform context index selects one by s_movrels_b64 and
 // the touched list goes back by s_movreld_b64 (M0-relative SGPR addressing), so a byte is
@@ -4507,7 +4521,6 @@ static __device__ __forceinline__ uint32_t adec_step_s(uint32_t t, u64x16 &lists
 // (0xFFFFFFFFFFFFFF00) became s_mov_b64 with a 32-bit literal that the hardware zero-extends,
 // so masks are made from the inline constant -1 (tools/ubench/adec_asm.hip traced it); and
 // fixed scratch pairs must avoid s100-s101, which gfx950 reserves (compiler-chosen operands).
-typedef uint32_t u32x32 __attribute__((ext_vector_type(32)));
 static __device__ __forceinline__ uint32_t adec_step_asm(uint32_t t, u32x32 &lists, uint32_t &ctx, uint64_t h80)
 {
     // (the exact step, also the fast resolve's fallback: plain code, the lists indexed by the
@@ -4580,6 +4593,8 @@ __global__ __launch_bounds__(64) void k_nyb_resolve_s(uint8_t *__restrict__ out,
     edge(k1, n);
 }
 
+#endif  // DC_AB_KERNELS
+
 // Fourth form (the product path since r3b): what a token gives without the lists is
 // computed beforehand, in parallel (k_nyb_adec_ctl, one dword per token), and the sequential
 // step is scalar instructions on the 16 lists in s[64:95]: the list by M0 from the byte
@@ -4649,13 +4664,19 @@ __global__ __launch_bounds__(256) void k_nyb_adec_ctl(const uint8_t *__restrict_
 
 #define STEP_C_ASM(W) STEP_C_ASM_X(W, "v", "vp", "c", "")
 
+// M0 is compiler-reserved: an "m0" clobber is not honoured (hipcc warns that reserved
+// registers on the clobber list may not be preserved), so every statement that writes M0
+// saves it on entry and restores it before it ends (cdna_hip_programming.md §5.7): whatever
+// the compiler keeps in M0 survives the statement
+#define M0_SAVE "s_mov_b32 %[m0keep], m0\n\t"
+#define M0_RESTORE "\n\ts_mov_b32 m0, %[m0keep]"
 static __device__ __forceinline__ uint32_t adec_step_c(u32x32 &lists, uint32_t &vprev, uint32_t c)
 {
-    uint32_t v, T;
+    uint32_t v, T, m0keep;
     uint64_t N;   // (compiler-chosen scratch; the fixed pairs s96-s99 stay clear of s100-s101,
-                  //  which gfx950 reserves; M0 is used by nothing else in these kernels)
-    asm volatile(STEP_C_ASM("")
-        : [lists] "+{s[64:95]}"(lists), [v] "=&s"(v), [N] "=&s"(N), [T] "=&s"(T)
+                  //  which gfx950 reserves)
+    asm volatile(M0_SAVE STEP_C_ASM("") M0_RESTORE
+        : [lists] "+{s[64:95]}"(lists), [v] "=&s"(v), [N] "=&s"(N), [T] "=&s"(T), [m0keep] "=&s"(m0keep)
         : [vp] "s"(vprev), [c] "s"(c)
         : "s96", "s97", "s98", "s99", "scc");
     vprev = v;
@@ -4668,14 +4689,16 @@ static __device__ __forceinline__ uint32_t adec_step_c(u32x32 &lists, uint32_t &
 template <int K>
 static __device__ __forceinline__ void adec_step_cw4(u32x32 &lists, uint32_t &vprev, const uint32_t *c, uint32_t &ov)
 {
-    uint32_t v0, v1, v2, v3, T;
+    uint32_t v0, v1, v2, v3, T, m0keep;
     uint64_t N;
-    asm volatile(STEP_C_ASM_X(STEP_WL("v0", "k0"), "v0", "vp", "c0", "a") "\n\t"
+    asm volatile(M0_SAVE
+                 STEP_C_ASM_X(STEP_WL("v0", "k0"), "v0", "vp", "c0", "a") "\n\t"
                  STEP_C_ASM_X(STEP_WL("v1", "k1"), "v1", "v0", "c1", "b") "\n\t"
                  STEP_C_ASM_X(STEP_WL("v2", "k2"), "v2", "v1", "c2", "c") "\n\t"
                  STEP_C_ASM_X(STEP_WL("v3", "k3"), "v3", "v2", "c3", "d")
+                 M0_RESTORE
         : [lists] "+{s[64:95]}"(lists), [v0] "=&s"(v0), [v1] "=&s"(v1), [v2] "=&s"(v2), [v3] "=&s"(v3),
-          [N] "=&s"(N), [T] "=&s"(T), [ov] "+v"(ov)
+          [N] "=&s"(N), [T] "=&s"(T), [ov] "+v"(ov), [m0keep] "=&s"(m0keep)
         : [vp] "s"(vprev), [c0] "s"(c[0]), [c1] "s"(c[1]), [c2] "s"(c[2]), [c3] "s"(c[3]),
           [k0] "i"(K), [k1] "i"(K + 1), [k2] "i"(K + 2), [k3] "i"(K + 3)
         : "s96", "s97", "s98", "s99", "scc");
@@ -4755,6 +4778,7 @@ __global__ __launch_bounds__(64) void k_nyb_resolve_c(uint8_t *__restrict__ out,
     }
 }
 
+#ifdef DC_AB_KERNELS   // k_nyb_adec: the one-pass decoder, A/B only
 __global__ __launch_bounds__(64) void k_nyb_adec(const uint8_t *__restrict__ in, uint64_t len,
                                                  uint8_t *__restrict__ out, uint64_t *__restrict__ meta)
 {
@@ -4827,6 +4851,7 @@ __global__ __launch_bounds__(64) void k_nyb_adec(const uint8_t *__restrict__ in,
     adec_flush(ow, OA, ob, ob + o, lane);
     if (lane == 0) meta[0] = o;
 }
+#endif  // DC_AB_KERNELS
 
 
 __global__ __launch_bounds__(64) void k_nyb_chunk_enc(const uint8_t *__restrict__ in, uint64_t n, uint32_t K,
@@ -4961,7 +4986,11 @@ __global__ __launch_bounds__(64) void k_nyb_chunk_dec(const uint8_t *__restrict_
 
 // ------------------------------------------------------------------------------------
 // HBM copy probe (bench.py's reference rate, MI355X_MICROARCH.md's float4 copy): 16-B loads
-// and stores with the nt hint, 4 in flight per lane, 4096 workgroups grid-striding the buffer
+// and stores with the nt hint, one uint4 per lane and one workgroup per 4 KiB (the full grid:
+// 262144 workgroups on 1 GiB). r4 shapes (tools/ubench/copy_shapes.hip,
+// profiles/r4a_copy_shapes.log): this shape 6.34 TB/s; grid-striding 4096-32768 workgroups
+// with one uint4 per lane and step 4.57-4.69 (r3's probe, 16384, read 5.40 in the bench);
+// 4 uint4 per lane and step at 32768 workgroups 6.24
 // ------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_copy_probe(const uint4 *__restrict__ src, uint4 *__restrict__ dst, uint64_t n16)
 {
@@ -4988,7 +5017,8 @@ struct dc_ctx {
     // takes the next slot, which a kernel of the call before cleared (no memset launch)
     int *d_errp, *d_errd;
     uint32_t gen_p, gen_d;
-    const dc_dtable *dec_fresh;                   // decoder tables current: this context's last pack built them
+    const dc_dtable *dec_fresh;                   // decoder tables current: this context's last pack built them,
+    uint64_t dec_fresh_gen;                       // ... while g_table_gen had this value (see table_written)
     uint32_t *d_queue;                            // decode tuple scheduler heads (D8Sched)
     uint32_t *d_fix;        size_t fix_cap;       // decode redo: a u64 chunk mask per group
     uint32_t *d_fixpos;     size_t fixpos_cap;    // decode redo: bit offset of a flagged chunk
@@ -5030,6 +5060,28 @@ struct dc_ctx {
 };
 
 #define HIPCHK(x) do { if ((x) != hipSuccess) return DC_E_HIP; } while (0)
+
+// Decoder-table freshness. A pack builds the decoder tables of its table (its workgroup 0),
+// so the decode after it skips k_dec_tables. The skip is keyed on the table's address AND on
+// a process-wide generation that every table write through this library bumps (any context:
+// k_huff_table, the fused encode plan): a table rebuilt since at the same address, e.g. a
+// recycled buffer filled by another context, is never taken for the packed one. (Keyed on the
+// address alone, such a table skipped the rebuild and its decode reported a stream error.)
+static std::atomic<uint64_t> g_table_gen{1};
+static void table_written(dc_ctx *c)
+{
+    c->dec_fresh = nullptr;
+    g_table_gen.fetch_add(1, std::memory_order_relaxed);
+}
+static void dec_tables_built(dc_ctx *c, const dc_dtable *t)
+{
+    c->dec_fresh = t;
+    c->dec_fresh_gen = g_table_gen.load(std::memory_order_relaxed);
+}
+static bool dec_tables_fresh(const dc_ctx *c, const dc_dtable *t)
+{
+    return c->dec_fresh == t && c->dec_fresh_gen == g_table_gen.load(std::memory_order_relaxed);
+}
 
 static int ensure(void **p, size_t *cap, size_t bytes)
 {
@@ -5182,12 +5234,20 @@ int dc_ctx_set_option(dc_ctx *c, int option, int64_t value)
         if (value != 0 && value != 1) return DC_E_ARG;
         c->opt_decode_general = (uint32_t)value;
         return DC_OK;
-    case DC_OPT_DECODE_VARIANT:
+    case DC_OPT_DECODE_VARIANT:   // 1: k_huff_decode9, in DC_AB_KERNELS builds only
+#ifdef DC_AB_KERNELS
         if (value < 0 || value > 1) return DC_E_ARG;
+#else
+        if (value != 0) return DC_E_ARG;
+#endif
         c->opt_decode_variant = (uint32_t)value;
         return DC_OK;
-    case DC_OPT_NYB_ADEC_V1:
+    case DC_OPT_NYB_ADEC_V1:   // 1-3: the A/B resolves, in DC_AB_KERNELS builds only
+#ifdef DC_AB_KERNELS
         if (value < 0 || value > 3) return DC_E_ARG;
+#else
+        if (value != 0) return DC_E_ARG;
+#endif
         c->opt_adec_v1 = (uint32_t)value;
         return DC_OK;
     case DC_OPT_HIST_PREFETCH:
@@ -5257,10 +5317,11 @@ int dc_copy_probe(dc_ctx *c, const void *d_src, void *d_dst, uint64_t bytes)
 {
     if (!c || (bytes && (!d_src || !d_dst)) || (bytes & 15) || (((uintptr_t)d_src | (uintptr_t)d_dst) & 15)) return DC_E_ARG;
     if (!bytes) return DC_OK;
-    // grid 16384 (r3g measured 4096 x 4 uint4 per lane at 4.47 TB/s on 1 GiB, 16384 at 5.26;
-    // tools/ubench/gap2.hip: 16384 with 1 uint4 per lane and step 5.44, a read-only pass 6.35)
+    // the full grid, one uint4 per lane (6.34 TB/s on 1 GiB, k_copy_probe's comment); grid-
+    // stride beyond 2^31 - 1 workgroups (32 TiB)
     const uint64_t n16 = bytes / 16, wgs = (n16 + 255) / 256;
-    LAUNCH(c, "copy_probe", k_copy_probe, wgs < 16384 ? wgs : 16384, 256, (const uint4 *)d_src, (uint4 *)d_dst, n16);
+    LAUNCH(c, "copy_probe", k_copy_probe, wgs < 0x7fffffffull ? wgs : 0x7fffffffull, 256, (const uint4 *)d_src,
+           (uint4 *)d_dst, n16);
     return DC_OK;
 }
 
@@ -5305,7 +5366,7 @@ static int table_common(dc_ctx *c, const uint64_t *d_freq, int is_hist, const in
                         int nary, dc_dtable *d_table)
 {
     if (!c || !d_table || M < 0 || M >= DC_MAX_SYMS || nary < 2 || nary > 256) return DC_E_ARG;
-    c->dec_fresh = nullptr;
+    table_written(c);
     LAUNCH(c, "huff_table", k_huff_table, 1, 256, d_freq, is_hist, d_len, M, nary, d_table, (dc_tree *)nullptr,
            (const uint64_t *)nullptr, (uint64_t *)nullptr, (int *)nullptr, (int *)nullptr);
     return DC_OK;
@@ -5314,7 +5375,7 @@ static int table_common(dc_ctx *c, const uint64_t *d_freq, int is_hist, const in
 int dc_huff_tree(dc_ctx *c, const uint64_t *d_freq, int M, int nary, dc_dtable *d_table, dc_tree *d_tree)
 {
     if (!c || !d_freq || !d_table || !d_tree || M < 0 || M >= DC_MAX_SYMS || nary < 2 || nary > 256) return DC_E_ARG;
-    c->dec_fresh = nullptr;
+    table_written(c);
     LAUNCH(c, "huff_tree", k_huff_table, 1, 256, d_freq, 0, (const int32_t *)nullptr, M, nary, d_table, d_tree,
            (const uint64_t *)nullptr, (uint64_t *)nullptr, (int *)nullptr, (int *)nullptr);
     return DC_OK;
@@ -5365,7 +5426,8 @@ int dc_huff_plan(dc_ctx *c, const dc_dtable *d_table, uint64_t *d_total_bits)
     if (!c->hist_in && c->hist_n) return DC_E_STATE;
     ++c->gen_p;   // this plan's error slot (cleared by the plan before; the next one is cleared below)
     // the payload bits of this context's last histogram under d_table (and the missing-code
-    // flag): one 256-thread launch; the blocks' offsets are the pack's own look-back
+    // flag): one 256-thread launch; the blocks' offsets come from the plan kernels the pack
+    // launches first (plan_offsets: k_block_local + k_block_final_wide)
     LAUNCH(c, "plan_total", k_plan_total, 1, 256, (const uint64_t *)c->d_hloc, d_table, d_total_bits, plan_err(c),
            plan_err_next(c));
     c->plan_table = d_table;
@@ -5379,7 +5441,7 @@ int dc_huff_encode_plan(dc_ctx *c, const uint8_t *d_in, uint64_t n, int M, int n
 {
     if (!c || !d_table || !d_total_bits || M < 0 || M >= DC_MAX_SYMS || nary < 2 || nary > 256) return DC_E_ARG;
     ++c->gen_p;
-    c->dec_fresh = nullptr;
+    table_written(c);
     const int r = hist_impl(c, d_in, n, d_hist,
                             HistFuse{d_table, M, nary, d_total_bits, plan_err(c), plan_err_next(c)});
     if (r != DC_OK) { --c->gen_p; return r; }
@@ -5476,7 +5538,7 @@ static int pack_impl(dc_ctx *c, const uint8_t *d_in, uint64_t n, const dc_dtable
     const uint64_t grid = nb < gmax ? nb : gmax;
     LAUNCH(c, "huff_pack", k_huff_pack, grid + 1, 256, d_in, n, d_table, (const uint64_t *)c->d_off, bit_base, d_base,
            d_words, d_sync_base, d_sync_len, sync_syms, nb, words_cap, plan_err(c), 1);
-    c->dec_fresh = d_table;   // workgroup 0 built the decoder tables
+    dec_tables_built(c, d_table);   // workgroup 0 built the decoder tables
     return DC_OK;
 }
 
@@ -5495,10 +5557,22 @@ int dc_huff_pack_async_dev(dc_ctx *c, const uint8_t *d_in, uint64_t n, const dc_
     return pack_impl(c, d_in, n, d_table, 0, d_bit_base, d_words, words_cap, d_sync_base, d_sync_len, sync_syms);
 }
 
+uint32_t dc_huff_plan_gen(dc_ctx *c) { return c ? c->gen_p : 0u; }
+
 int dc_huff_pack_status(dc_ctx *c, const dc_dtable *d_table)
 {
+    if (!c) return DC_E_ARG;
+    return dc_huff_pack_status_gen(c, d_table, c->gen_p);
+}
+
+int dc_huff_pack_status_gen(dc_ctx *c, const dc_dtable *d_table, uint32_t gen)
+{
+    if (!c) return DC_E_ARG;
+    // the plan's own slot; 32 slots rotate, and plan gen + 1's slot is cleared by plan gen:
+    // a plan more than 30 plans back has lost its flags
+    if ((uint32_t)(c->gen_p - gen) > 30u) return DC_E_STATE;
     int v[3] = {0, 0, 0};
-    HIPCHK(hipMemcpyAsync(v, plan_err(c), 3 * sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(v, c->d_errp + 4 * (gen & 31u), 3 * sizeof(int), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     if (v[0]) {
         const int st = dc_huff_table_status(c, d_table, nullptr);
@@ -5560,7 +5634,7 @@ static int decode_impl(dc_ctx *c, const uint32_t *d_words, uint64_t bit_base, co
     int *const derr = dec_err(c), *const derr_next = dec_err_next(c);
     // the decoder tables, unless this context's last pack built them for this table (no launch
     // then; a table rebuilt elsewhere since reads dec_ready 0 in the decoder: a stream error)
-    if (c->dec_fresh != d_table) LAUNCH(c, "dec_tables", k_dec_tables, 1, 256, const_cast<dc_dtable *>(d_table), derr);
+    if (!dec_tables_fresh(c, d_table)) LAUNCH(c, "dec_tables", k_dec_tables, 1, 256, const_cast<dc_dtable *>(d_table), derr);
     if (S == 64 && n < (1ull << 37) && words < (1ull << 31) && !c->opt_decode_general) {
         // 12 waves x 2 chains, one workgroup per CU: the stage and the 14-bit table fill the
         // LDS (the 8 x 4 split measured 0.89 vs 0.70 ms on 1 GiB C2: spills)
@@ -5574,11 +5648,14 @@ static int decode_impl(dc_ctx *c, const uint32_t *d_words, uint64_t bit_base, co
         LAUNCH(c, "huff_decode", (k_huff_decode8<NW_, NC_>), (tuples + NW_ - 1) / NW_ < 256 ? (tuples + NW_ - 1) / NW_ : 256, \
                NW_ * 64, d_words, bit_base, d_base, d_sync_base, d_sync_len, n, words, d_table, d_out, derr,       \
                c->d_queue, spct, (uint64_t *)c->d_fix, (uint64_t *)c->d_fixpos, (uint8_t *)c->d_scr)
+#ifdef DC_AB_KERNELS
         if (c->opt_decode_variant == 1) {   // multi-symbol lookups, one group per wave
             LAUNCH(c, "huff_decode", k_huff_decode9<12>, groups < 256 * 12 ? (groups + 11) / 12 : 256, 12 * 64,
                    d_words, bit_base, d_base, d_sync_base, d_sync_len, n, words, d_table, d_out, derr, c->d_queue,
                    spct, (uint64_t *)c->d_fix, (uint64_t *)c->d_fixpos, (uint8_t *)c->d_scr);
-        } else {   // one code per lookup, 11 waves x 2 chains (the 15-bit table takes 64 KiB of LDS)
+        } else
+#endif
+        {   // one code per lookup, 11 waves x 2 chains (the 15-bit table takes 64 KiB of LDS)
             D8_LAUNCH(11, 2);
         }
 #undef D8_LAUNCH
@@ -6041,6 +6118,7 @@ int dc_nyb_decompress(dc_ctx *c, const uint8_t *d_in, uint64_t m, int modify, ui
     if (type == 0xAF) {
         if (m < 2) { *h_len = 0; return DC_OK; }
         if (!modify) return fsm_run<M_NYB_DEC>(c, d_in, m, m - 2, d_out, h_len, "nyb_dec_tiles");
+#ifdef DC_AB_KERNELS
         if (c->opt_adec_v1 == 1) {   // A/B only: the one-pass single-wave decoder
             LAUNCH(c, "nyb_adec", k_nyb_adec, 1, 64, d_in, m, d_out, c->d_meta);
             HIPCHK(hipMemcpyAsync(c->h_pinned, c->d_meta, sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
@@ -6048,15 +6126,18 @@ int dc_nyb_decompress(dc_ctx *c, const uint8_t *d_in, uint64_t m, int modify, ui
             *h_len = c->h_pinned[0];
             return DC_OK;
         }
+#endif
         // tokens by the static transducer (parallel), then one wave resolves them in place
         r = fsm_run<M_NYB_DEC>(c, d_in, m, m - 2, d_out, h_len, "nyb_tok_tiles", FsmAux{nullptr, 0, 0, 1, 1, 1});
         if (r) return r;
         const uint64_t n = *h_len;
         if (n > 1 && c->opt_adec_v1 == 0) return adec_fast(c, d_out, n);   // control words + k_nyb_resolve_c
+#ifdef DC_AB_KERNELS
         if (n > 1) {
             if (c->opt_adec_v1 == 2) LAUNCH(c, "nyb_resolve", k_nyb_resolve, 1, 64, d_out, n);   // A/B: r2's
             else LAUNCH(c, "nyb_resolve", k_nyb_resolve_s, 1, 64, d_out, n);
         }
+#endif
         HIPCHK(hipStreamSynchronize(c->stream));
         return DC_OK;
     }

@@ -181,8 +181,15 @@ class Codec:
               self.L.dc_huff_pack_async(self.ctx, _ptr(x), x.numel(), _ptr(tab), bit_base, _ptr(words),
                                         words.numel(), _ptr(base), _ptr(lens), S))
 
-    def pack_status(self, tab):
-        return int(self.L.dc_huff_pack_status(self.ctx, _ptr(tab)))
+    def pack_status(self, tab, gen=None):
+        """Outcome of the last plan + pack (gen=None), or of the plan whose plan_gen() was gen."""
+        if gen is None:
+            return int(self.L.dc_huff_pack_status(self.ctx, _ptr(tab)))
+        return int(self.L.dc_huff_pack_status_gen(self.ctx, _ptr(tab), gen))
+
+    def plan_gen(self) -> int:
+        """Identity of the last plan on this context (dc_huff_plan_gen), for pack_status(gen=)."""
+        return int(self.L.dc_huff_plan_gen(self.ctx))
 
     def decode(self, words, bit_base, sync, sync_syms, n, tab, out):
         """bit_base: an int, or a one-element int64 device tensor (dc_huff_decode_dev)."""

@@ -46,6 +46,8 @@ class ShardStream:
     n: int                   # symbols in this shard
     table: torch.Tensor      # device code table (identical on every rank)
     totals: torch.Tensor = None   # the ranks' payload bits (device), when bit_base is a tensor
+    total: torch.Tensor = None    # this shard's payload bits (device), as planned
+    plan_gen: int = None          # the engine's plan identity (pack_status of THIS encode)
 
 
 class ShardedHuffman:
@@ -127,22 +129,24 @@ class ShardedHuffman:
             words = self.e.alloc_words(base, bits)
         if sync is None:
             sync = self.e.alloc_sync(n, sync_syms)
+        gen = self.e.plan_gen()   # this encode's plan: finalize() reads its own pack status
         self.e.pack_async(x, tab, base, words, sync, sync_syms)
         return ShardStream(words, base, bits if bits is not None else -1, sync, sync_syms, n, tab,
-                           totals if not isinstance(base, int) else None)
+                           totals if not isinstance(base, int) else None, tot, gen)
 
     def finalize(self, s: ShardStream):
         """Host values of the bit offset and payload bit count (one host read) if encode()
         left them on the device, and the pack's outcome: with the offset on the device, a
         preallocated `words` too small for bit_base % 32 + bits (size it with
         words_needed(31, bits)) makes the kernels write nothing, which is raised here
-        rather than gathered as an empty stream."""
+        rather than gathered as an empty stream. The status and bit count are this stream's
+        own (its plan's slot and total), whatever the engine encoded after it."""
         if s.totals is not None:
             tv = s.totals.cpu().tolist()
             s.bit_base, s.bits, s.totals = int(sum(tv[: self.rank])), int(tv[self.rank]), None
         elif s.bits < 0:
-            s.bits = int(self.e.plan_total())
-        st = self.e.pack_status(s.table)
+            s.bits = int(s.total.item()) if s.total is not None else int(self.e.plan_total())
+        st = self.e.pack_status(s.table, s.plan_gen)
         if st != 0:
             raise RuntimeError(f"rank {self.rank}: pack failed with status {st} (dc_huff_pack_status)")
         return s

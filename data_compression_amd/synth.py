@@ -185,7 +185,6 @@ def device_text(cfg: str, n: int, seed: int, device):
     cdf = torch.from_numpy(np.cumsum(p)).to(device)
     g = torch.Generator(device=device).manual_seed(seed)
     avg = float((lens * p).sum())
-    col = torch.arange(arr.shape[1], device=device)[None, :]
     out = torch.empty(n, dtype=torch.uint8, device=device)
     filled = 0
     while filled < n:
@@ -193,7 +192,16 @@ def device_text(cfg: str, n: int, seed: int, device):
         ntok = int(want / avg * 1.05) + 64
         u = torch.rand(ntok, generator=g, device=device, dtype=torch.float64)
         ids = torch.clamp(torch.searchsorted(cdf, u), max=len(lens) - 1)
-        chunk = tok[ids][col < tlen[ids][:, None]]
+        # the sampled tokens' bytes, concatenated: a flat gather (token of each output byte by
+        # repeat_interleave, its column = position - the token's exclusive offset). The same
+        # bytes as the 2-D boolean-mask index tok[ids][col < tlen[ids][:, None]] it replaces,
+        # which hung when 4 processes ran it at once on one GPU (tools/synth_stall.py)
+        tl = tlen[ids].to(torch.int64)
+        total = int(tl.sum())
+        start = torch.cumsum(tl, 0) - tl
+        which = torch.repeat_interleave(torch.arange(ntok, device=device), tl, output_size=total)
+        pos = torch.arange(total, device=device) - start[which]
+        chunk = tok[ids[which], pos]
         take = min(chunk.numel(), n - filled)
         out[filled : filled + take] = chunk[:take]
         filled += take

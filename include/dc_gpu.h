@@ -133,7 +133,8 @@ int dc_memcpy_h2d(dc_ctx *ctx, void *d_dst, const void *h_src, size_t bytes);
 int dc_memcpy_d2h(dc_ctx *ctx, void *h_dst, const void *d_src, size_t bytes);
 int dc_memset(dc_ctx *ctx, void *d_dst, int value, size_t bytes);
 /* HBM reference rate: a float4 (16-B) device-to-device copy of `bytes` (multiple of 16,
- * 16-B aligned), nt loads and stores, 4096 workgroups (bench.py's copy probe) */
+ * 16-B aligned), nt loads and stores, one uint4 per lane over the full grid (one 256-thread
+ * workgroup per 4 KiB; bench.py's copy probe) */
 int dc_copy_probe(dc_ctx *ctx, const void *d_src, void *d_dst, uint64_t bytes);
 
 /* ---- Huffman, device-resident stages ------------------------------------------------- */
@@ -157,7 +158,9 @@ int dc_huff_tree(dc_ctx *ctx, const uint64_t *d_freq, int max_symbol_value, int 
 int dc_tree_depths(dc_ctx *ctx, const int32_t *d_parent, int list_length, int leaves, int32_t *d_depth);
 /* (3) the encode plan of the input of the last dc_huff_hist under d_table: its payload bit
  *     count into *d_total_bits (device u64) and the missing-code flag (dc_huff_pack_status).
- *     The per-block offsets are the pack's own (a decoupled look-back inside k_huff_pack). */
+ *     The per-block bit offsets are computed at pack time by two plan kernels before the
+ *     pack (k_block_local: bits per 32 KiB block and a scan per 64 blocks; k_block_final_wide:
+ *     the absolute offsets, and the zeroing of the payload words two blocks share). */
 int dc_huff_plan(dc_ctx *ctx, const dc_dtable *d_table, uint64_t *d_total_bits);
 /* (1+2+3 fused) histogram, table and plan of d_in[0..n) in ONE launch: the histogram's last
  *     workgroup builds the table (as dc_huff_table) and the plan total (as dc_huff_plan) from
@@ -195,6 +198,11 @@ int dc_huff_pack_async_dev(dc_ctx *ctx, const uint8_t *d_in, uint64_t n, const d
                            const uint64_t *d_bit_base, uint32_t *d_words, uint64_t words_cap,
                            uint64_t *d_sync_base, uint16_t *d_sync_len, uint32_t sync_syms);
 int dc_huff_pack_status(dc_ctx *ctx, const dc_dtable *d_table);
+/* the outcome of one particular plan + pack: gen = dc_huff_plan_gen() read right after its
+ * plan (dc_huff_plan / dc_huff_encode_plan), so later encodes on the context do not answer
+ * for it. DC_E_STATE when more than 30 plans have run since (its flags are recycled). */
+uint32_t dc_huff_plan_gen(dc_ctx *ctx);
+int dc_huff_pack_status_gen(dc_ctx *ctx, const dc_dtable *d_table, uint32_t gen);
 /* Status word written by the table / plan kernels (host-synchronising read). */
 int dc_huff_table_status(dc_ctx *ctx, const dc_dtable *d_table, int32_t *max_bits);
 /* (5) decode n symbols. d_words/bit_base and the sync index as written by pack. The

@@ -74,8 +74,11 @@ class CpuEngine:
         sync[0][: len(base)] = torch.from_numpy(base.astype(np.int64))
         sync[1][: len(lens)] = torch.from_numpy(lens.view(np.int16))
 
-    def pack_status(self, tab):
+    def pack_status(self, tab, gen=None):
         return 0   # the oracle pack above either writes the whole stream or raises
+
+    def plan_gen(self):
+        return 0
 
     def decode(self, words, bit_base, sync, S, n, tab, out):
         bit_base = int(bit_base)

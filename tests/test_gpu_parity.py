@@ -510,6 +510,16 @@ def test_decode_error_slots_and_stale_tables(torch_cuda, codec):
     assert codec.decode_status() == 0 and torch.equal(out, xt)
 
 
+def _set_or_skip(c, name, value):
+    """Select an A/B variant; the product library only has variant 0 (the alternatives are
+    compiled in DC_AB_KERNELS diagnostic builds, tools/diag_build.sh)."""
+    from data_compression_amd._lib import DcError
+    try:
+        c.set_option(name, value)
+    except DcError:
+        pytest.skip(f"{name}={value}: A/B kernels not in this build (DC_AB_KERNELS)")
+
+
 @pytest.mark.parametrize("variant", [0, 1])
 def test_decode_stale_tables_after_larger_decode(torch_cuda, variant):
     """a decode that finds its tables stale must leave the redo stage
@@ -522,7 +532,7 @@ def test_decode_stale_tables_after_larger_decode(torch_cuda, variant):
     from data_compression_amd.device import Codec
     c = Codec(0)
     other = Codec(0)
-    c.set_option("decode_variant", variant)
+    _set_or_skip(c, "decode_variant", variant)
     big = torch.from_numpy(_chain_stream(20, 5)).cuda()   # codes past the 15-bit table: many redo chunks
     enc = c.encode(big, n_ary=2, sync_syms=64)
     out = torch.empty_like(big)
@@ -530,8 +540,12 @@ def test_decode_stale_tables_after_larger_decode(torch_cuda, variant):
     assert c.decode_status() == 0 and torch.equal(out, big)
     assert variant == 1 or c.decode_redo_count() > 0
     small = torch.from_numpy(synth.enwik_like(70_001, seed=33)).cuda()
+    # another context's table (decoder tables never built: dec_ready 0), made BEFORE the encode
+    # below and copied over the encode's table by plain bytes afterwards: the library sees no
+    # table write after c's pack, so c keeps its tables for fresh and the decoder must catch it
+    stale = other.table(other.hist(torch.from_numpy(synth.uniform_bytes(4096, seed=4)).cuda()), 2)
     enc_s = c.encode(small, n_ary=2, sync_syms=64)
-    other.table(other.hist(torch.from_numpy(synth.uniform_bytes(4096, seed=4)).cuda()), 2, out=enc_s["table"])
+    enc_s["table"].copy_(stale)
     guard = torch.full((small.numel() + 4096,), 0xA5, dtype=torch.uint8, device=small.device)
     c.decode_into(enc_s, guard[: small.numel()])
     assert c.decode_status() != 0
@@ -543,13 +557,59 @@ def test_decode_stale_tables_after_larger_decode(torch_cuda, variant):
         assert c.decode_status() == 0 and torch.equal(o, x)
 
 
+def test_decode_table_rewritten_at_same_address(torch_cuda, codec):
+    """the decoder tables a pack built are reused only while no table has
+    been written since (process-wide generation, not the address alone). A new table written
+    by another context into the buffer this context just packed with, and a stream under it
+    (packed by the oracle, so no device pack builds its decoder tables), decodes exactly."""
+    torch = torch_cuda
+    from data_compression_amd import synth
+    from data_compression_amd.device import Codec
+    other = Codec(0)
+    x1 = torch.from_numpy(synth.enwik_like(300_000, seed=91)).cuda()
+    enc1 = codec.encode(x1, n_ary=2, sync_syms=64)   # codec's pack built this table's decoder tables
+    T = enc1["table"]
+    x2 = synth.english_like(200_003, seed=92)
+    other.table(other.hist(torch.from_numpy(x2).cuda()), 2, out=T)   # same address, new table
+    L, el, ev, code, nb, mx = _oracle_encode(x2, 2)
+    payload, bits, idx = orc.huff_pack(x2, code, nb, sync_syms=64)
+    words = torch.zeros(codec.words_needed(0, bits), dtype=torch.int32, device="cuda")
+    words.view(torch.uint8)[: len(payload)] = torch.from_numpy(payload).cuda()
+    lens = np.diff(np.append(idx, np.uint64(bits))).astype(np.int16)
+    bases = idx[::64].astype(np.int64)
+    sync = (torch.from_numpy(bases).cuda(), torch.from_numpy(lens).cuda())
+    out = torch.empty(x2.size, dtype=torch.uint8, device="cuda")
+    codec.decode(words, 0, sync, 64, x2.size, T, out)
+    assert codec.decode_status() == 0 and np.array_equal(out.cpu().numpy(), x2)
+
+
+def test_sharded_finalize_reads_its_own_plan(torch_cuda, codec):
+    """finalize() of a stream reports that stream's pack outcome, not the
+    latest encode's. Stream A into a words buffer far too small (the kernels write nothing and
+    flag A's plan slot), then stream B encoded normally on the same context: finalize(A)
+    raises, finalize(B) passes and B round-trips."""
+    torch = torch_cuda
+    from data_compression_amd import synth
+    from data_compression_amd.dist import ShardedHuffman
+    sh = ShardedHuffman(codec)
+    xa = torch.from_numpy(synth.enwik_like(200_000, seed=5)).cuda()
+    xb = torch.from_numpy(synth.enwik_like(150_000, seed=6)).cuda()
+    tiny = torch.zeros(64, dtype=torch.int32, device="cuda")
+    sa = sh.encode(xa, 2, 64, words=tiny, sync=codec.alloc_sync(xa.numel(), 64))
+    sb = sh.encode(xb, 2, 64)
+    with pytest.raises(RuntimeError):
+        sh.finalize(sa)
+    sh.finalize(sb)
+    assert torch.equal(sh.decode(sb), xb)
+
+
 @pytest.mark.parametrize("variant", [0, 1])
 def test_decode_variants(torch_cuda, codec, variant):
     """The fast decoder's variants (0: one code per 15-bit lookup; 1: up to 3 per 13-bit
     lookup) on text, Zipf and flat bytes at n = 2, 3, 16, ragged sizes: exact round trips."""
     torch = torch_cuda
     from data_compression_amd import synth
-    codec.set_option("decode_variant", variant)
+    _set_or_skip(codec, "decode_variant", variant)
     try:
         for x, n_ary in ((synth.enwik_like(3 << 20, seed=61), 2), (synth.zipf_bytes((2 << 20) + 5, seed=62), 2),
                          (synth.english_like(1_000_003, seed=63), 3), (synth.enwik_like(777_777, seed=64), 16),
@@ -687,7 +747,7 @@ def test_nybble_adaptive_decode_edges(torch_cuda, codec, v1):
     restatement."""
     torch = torch_cuda
     from data_compression_amd import synth
-    codec.set_option("nyb_adec_v1", int(v1))
+    _set_or_skip(codec, "nyb_adec_v1", int(v1))
     try:
         rng = np.random.default_rng(17)
         sizes = list(range(1, 201)) + [255, 256, 257, 4095, 4096, 4097, 65536 + 63, 200_001]
@@ -714,7 +774,7 @@ def test_nybble_adaptive_decode_any_stream(torch_cuda, codec, v1):
     one, against the reference restatement."""
     torch = torch_cuda
     from data_compression_amd import synth
-    codec.set_option("nyb_adec_v1", v1)
+    _set_or_skip(codec, "nyb_adec_v1", v1)
     try:
         rng = np.random.default_rng(23)
         for n in [3, 4, 17, 64, 65, 66, 130, 1000, 4097, 70_001]:
