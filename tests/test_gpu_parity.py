@@ -486,8 +486,8 @@ def test_decode_corrupt_stream_reports(torch_cuda, codec):
 def test_decode_error_slots_and_stale_tables(torch_cuda, codec):
     """Error flags live in per-call rotating slots (no clearing launch): an error stays with
     its own call. A decode right after this context's pack skips the decoder-table launch; a
-    table rebuilt since by another context reads dec_ready 0 in the decoder: reported as a
-    stream error, never silent garbage. Every later call is clean again."""
+    table whose bytes were replaced since (not through the library) reads dec_ready 0 in the
+    decoder: reported as a stream error, never silent garbage. Every later call is clean again."""
     torch = torch_cuda
     from data_compression_amd import synth
     from data_compression_amd.device import Codec
@@ -499,8 +499,13 @@ def test_decode_error_slots_and_stale_tables(torch_cuda, codec):
         enc = codec.encode(xt, n_ary=2, sync_syms=64)
         codec.decode_into(enc, out)
         assert codec.decode_status() == 0 and torch.equal(out, xt)
+    # a table rewritten behind the library's back (plain bytes of another context's table,
+    # built BEFORE the encode, so no table write follows the pack): the decoder sees its
+    # dec_ready 0 and reports it (a table written through the library since the pack makes
+    # the decode rebuild the decoder tables instead: test_decode_table_rewritten_at_same_address)
+    stale = other.table(other.hist(torch.from_numpy(synth.uniform_bytes(4096, seed=3)).cuda()), 2)
     enc = codec.encode(xt, n_ary=2, sync_syms=64)
-    other.table(other.hist(torch.from_numpy(synth.uniform_bytes(4096, seed=3)).cuda()), 2, out=enc["table"])
+    enc["table"].copy_(stale)
     codec.decode_into(enc, out)
     assert codec.decode_status() != 0   # stale decoder tables: reported
     enc = codec.encode(xt, n_ary=2, sync_syms=64)
