@@ -14,7 +14,6 @@
 #include <stdlib.h>
 
 #include <atomic>
-#include <type_traits>
 
 #include "dc_gpu.h"
 
@@ -1144,8 +1143,7 @@ __global__ void k_zero_bounds(const uint64_t *__restrict__ off, uint64_t nblocks
 // and over ranges of 4-16 blocks per workgroup, 0.45-0.50 ms, against 0.373 for this pack after
 // the plan launches: a look-back costs ~2 us per agent-scope round trip, and ranges of blocks
 // long enough to hide it leave the last dispatch round unbalanced.)
-template <int FUSE>   // 1: one table lookup per byte (code and length), parts accumulated in registers
-__global__ __launch_bounds__(256, 4) void k_huff_pack(const uint8_t *__restrict__ in, uint64_t n,
+__global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ in, uint64_t n,
                                                    const dc_dtable *__restrict__ T,
                                                    const uint64_t *__restrict__ block_off, uint64_t bit_base,
                                                    const uint64_t *__restrict__ d_base, uint32_t *__restrict__ out, uint64_t *__restrict__ sync_base,
@@ -1266,123 +1264,6 @@ __global__ __launch_bounds__(256, 4) void k_huff_pack(const uint8_t *__restrict_
             // bits takes the per-code flush loop instead (exact, rare on text).
             const int lane = t & 63, wid = t >> 6;
             const uint32_t nwa = sh + nw_blk;
-            const uint64_t org = (blk_first_word - sh) << 5;   // absolute bit of stage bit 0
-            const uint32_t cm = sync_syms >> 4;                 // lanes per sync chunk
-            uint64_t run = blk_abs;   // absolute bit where piece k starts
-            // OR a right-justified run of nb <= 64 bits into the stage at bit pos (<= 3 words)
-            // Branch-free: the run left-justified in 64 bits has zeros below it, so the
-            // words it does not reach receive 0 (a no-op OR; some lane of a wave needs each
-            // of the 3 ORs anyway, so skipping them per lane saved no LDS cycle and cost
-            // compares and exec-mask branches). nb == 0 only for an all-zero acc (absent
-            // symbols have code 0), where the unmasked shift by 64 & 63 = 0 is harmless.
-            auto emit = [&](uint64_t acc, uint32_t nb, uint32_t pos) {
-                const uint64_t al = acc << ((64u - nb) & 63u);
-                const uint32_t hi = (uint32_t)(al >> 32), lo = (uint32_t)al, r = pos & 31u, wi = pos >> 5;
-                atomicOr(&s_stage[wi], hi >> r);
-                atomicOr(&s_stage[wi + 1], __builtin_amdgcn_alignbit(hi, lo, r));
-                atomicOr(&s_stage[wi + 2], __builtin_amdgcn_alignbit(lo, 0u, r));
-            };
-            // sync index entries of piece k (chunk bits = inclusive scan at the chunk's last
-            // lane - exclusive at its first), As = the piece's absolute start bit
-            auto sync_put = [&](int k, uint32_t Ikk, uint32_t Tkk, uint64_t As) {
-                if (sync_len == nullptr) return;
-                const uint64_t p = blk_start + (uint64_t)k * PACK_TILE + (uint64_t)t * 16;
-                const uint32_t last = (cm == 4) ? (uint32_t)__builtin_amdgcn_update_dpp(0, (int)Ikk, 0xff, 0xf, 0xf, false)
-                                                : (uint32_t)__shfl((int)Ikk, lane | (int)(cm - 1), 64);
-                if ((p & (uint64_t)(sync_syms - 1)) == 0) {
-                    sync_len[p >> slog] = (uint16_t)(last - (Ikk - Tkk));
-                    if ((p & ((uint64_t)sync_syms * DC_SYNC_GROUP - 1)) == 0)
-                        sync_base[p >> (slog + DC_SYNC_GROUP_LOG)] = As;
-                }
-            };
-            if (FUSE && !qmode) {
-                // one lookup per byte: each part (8 codes, or 4 in quarter mode) is gathered
-                // into a 64-bit register while its length is summed, the input's registers
-                // die, and after the scan the parts are OR-ed into the stage (pass A's 1-byte
-                // length lookups, about a third of the pack's LDS cycles, are gone). A part of
-                // more than 64 bits re-reads its piece and codes it code by code.
-                auto fused = [&](auto QC) {
-                    constexpr int Q = decltype(QC)::value, CP = 16 / Q;   // parts per piece, codes per part
-                    uint64_t acc[PACK_PIECES][Q];
-                    uint32_t plen[PACK_PIECES];    // part lengths, 8 bits each (<= 128: 4 codes x 32)
-                    uint32_t Tk[PACK_PIECES], Ik[PACK_PIECES];
-                    uint32_t ovf = 0;              // bit k: piece k has a part of > 64 bits
-#pragma unroll
-                    for (int k = 0; k < PACK_PIECES; ++k) {
-                        uint32_t w4[4] = {blkv[k].x, blkv[k].y, blkv[k].z, blkv[k].w};
-                        // opaque: no lookup address is computed before its piece (hoisted, they
-                        // all stayed live: 618 VGPRs of spills)
-                        asm volatile("" : "+v"(w4[0]), "+v"(w4[1]), "+v"(w4[2]), "+v"(w4[3]));
-                        uint32_t pl = 0, tk = 0;
-#pragma unroll
-                        for (int q = 0; q < Q; ++q) {
-                            uint64_t a = 0;
-                            uint32_t l = 0;
-#pragma unroll
-                            for (int i = q * CP; i < q * CP + CP; ++i) {
-                                const uint2 e = s_tab[(w4[i >> 2] >> (8 * (i & 3))) & 255u];
-                                a = (a << e.y) | e.x;
-                                l += e.y;
-                            }
-                            // opaque: the part is built here, not sunk below the scan's barrier
-                            // (sunk, all 128 table entries stayed live)
-                            asm volatile("" : "+v"(a));
-                            acc[k][q] = a;
-                            ovf |= (l > 64u ? 1u : 0u) << k;
-                            __builtin_amdgcn_sched_barrier(0);   // one part's 8 lookups in flight
-                            if (Q == 2) pl |= min(l, 255u) << (16 * q);
-                            else pl |= min(l, 255u) << (8 * q);
-                            tk += l;
-                        }
-                        plen[k] = pl;
-                        Tk[k] = tk;
-                        __builtin_amdgcn_sched_barrier(0);   // one piece's lookups in flight at a time
-                    }
-#pragma unroll
-                    for (int k = 0; k < PACK_PIECES; ++k) Ik[k] = wave_scan_incl(Tk[k]);
-                    if (lane == 63) {
-#pragma unroll
-                        for (int k = 0; k < PACK_PIECES; ++k) s_tot[k][wid] = Ik[k];
-                    }
-                    lds_barrier();
-#pragma unroll
-                    for (int k = 0; k < PACK_PIECES; ++k) {
-                        uint32_t wo = 0, kt = 0;
-#pragma unroll
-                        for (int w = 0; w < 4; ++w) {
-                            const uint32_t v = s_tot[k][w];
-                            wo += (w < wid) ? v : 0u;
-                            kt += v;
-                        }
-                        const uint64_t As = run + wo + (Ik[k] - Tk[k]);
-                        run += kt;
-                        sync_put(k, Ik[k], Tk[k], As);
-                        uint32_t pos = (uint32_t)(As - org);
-                        // (wave-uniform choice: a divergent per-lane fallback cost SGPR spills)
-                        if (__ballot((ovf >> k) & 1u) == 0) {
-#pragma unroll
-                            for (int q = 0; q < Q; ++q) {
-                                const uint32_t l = Q == 2 ? (plen[k] >> (16 * q)) & 0xFFFFu : (plen[k] >> (8 * q)) & 255u;
-                                emit(acc[k][q], l, pos);
-                                pos += l;
-                            }
-                        } else {   // rare: a part of > 64 bits in the wave: code by code from the bytes
-                            const uint4 v = LD_PACK(reinterpret_cast<const uint4 *>(in + blk_start + (uint64_t)k * PACK_TILE +
-                                                                                     (uint64_t)t * 16));
-                            const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll 1
-                            for (int i = 0; i < 16; ++i) {
-                                const uint2 e = s_tab[(w4[i >> 2] >> (8 * (i & 3))) & 255u];
-                                emit(e.x, e.y, pos);
-                                pos += e.y;
-                            }
-                        }
-                    }
-                };
-                // (quarter mode, 4 parts per piece, took 64 accumulator VGPRs and spilled: it
-                // keeps the two-pass code below)
-                fused(std::integral_constant<int, 2>{});
-            } else {
             uint32_t Tk[PACK_PIECES], Hk[PACK_PIECES], Ik[PACK_PIECES];
 #pragma unroll
             for (int k = 0; k < PACK_PIECES; ++k) {
@@ -1403,6 +1284,9 @@ __global__ __launch_bounds__(256, 4) void k_huff_pack(const uint8_t *__restrict_
                 for (int k = 0; k < PACK_PIECES; ++k) s_tot[k][wid] = Ik[k];
             }
             lds_barrier();
+            const uint64_t org = (blk_first_word - sh) << 5;   // absolute bit of stage bit 0
+            const uint32_t cm = sync_syms >> 4;                 // lanes per sync chunk
+            uint64_t run = blk_abs;   // absolute bit where piece k starts
 #pragma unroll
             for (int k = 0; k < PACK_PIECES; ++k) {
                 uint32_t wo = 0, kt = 0;
@@ -1414,11 +1298,34 @@ __global__ __launch_bounds__(256, 4) void k_huff_pack(const uint8_t *__restrict_
                 }
                 const uint64_t As = run + wo + (Ik[k] - Tk[k]);
                 run += kt;
-                sync_put(k, Ik[k], Tk[k], As);
+                const uint64_t p = blk_start + (uint64_t)k * PACK_TILE + (uint64_t)t * 16;
+                if (sync_len != nullptr) {
+                    // chunk bits = inclusive scan at the chunk's last lane - exclusive at its first
+                    const uint32_t last = (cm == 4) ? (uint32_t)__builtin_amdgcn_update_dpp(0, (int)Ik[k], 0xff, 0xf, 0xf, false)
+                                                    : (uint32_t)__shfl((int)Ik[k], lane | (int)(cm - 1), 64);
+                    if ((p & (uint64_t)(sync_syms - 1)) == 0) {
+                        sync_len[p >> slog] = (uint16_t)(last - (Ik[k] - Tk[k]));
+                        if ((p & ((uint64_t)sync_syms * DC_SYNC_GROUP - 1)) == 0)
+                            sync_base[p >> (slog + DC_SYNC_GROUP_LOG)] = As;
+                    }
+                }
                 uint32_t w4[4] = {blkv[k].x, blkv[k].y, blkv[k].z, blkv[k].w};
                 // opaque copy: stops the compiler from keeping pass A's lookup addresses live
                 asm volatile("" : "+v"(w4[0]), "+v"(w4[1]), "+v"(w4[2]), "+v"(w4[3]));
                 const uint32_t rel = (uint32_t)(As - org);
+                // OR a right-justified run of nb <= 64 bits into the stage at bit pos (<= 3 words)
+                // Branch-free: the run left-justified in 64 bits has zeros below it, so the
+                // words it does not reach receive 0 (a no-op OR; some lane of a wave needs each
+                // of the 3 ORs anyway, so skipping them per lane saved no LDS cycle and cost
+                // compares and exec-mask branches). nb == 0 only for an all-zero acc (absent
+                // symbols have code 0), where the unmasked shift by 64 & 63 = 0 is harmless.
+                auto emit = [&](uint64_t acc, uint32_t nb, uint32_t pos) {
+                    const uint64_t al = acc << ((64u - nb) & 63u);
+                    const uint32_t hi = (uint32_t)(al >> 32), lo = (uint32_t)al, r = pos & 31u, wi = pos >> 5;
+                    atomicOr(&s_stage[wi], hi >> r);
+                    atomicOr(&s_stage[wi + 1], __builtin_amdgcn_alignbit(hi, lo, r));
+                    atomicOr(&s_stage[wi + 2], __builtin_amdgcn_alignbit(lo, 0u, r));
+                };
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
                     const uint32_t Th = h ? Tk[k] - Hk[k] : Hk[k];
@@ -1464,7 +1371,6 @@ __global__ __launch_bounds__(256, 4) void k_huff_pack(const uint8_t *__restrict_
                 }
                 __builtin_amdgcn_sched_barrier(0);   // keep the pieces' lookups from being hoisted
             }
-            }   // !FUSE
             lds_barrier();
             // stage word sh = the block's first word, shared with the previous block; the last
             // word is shared with the next one when the block ends inside it: those two are
@@ -1598,381 +1504,6 @@ __global__ __launch_bounds__(256, 4) void k_huff_pack(const uint8_t *__restrict_
         __syncthreads();
     }
 }
-
-// ------------------------------------------------------------------------------------
-// (H7) pack, r4 form (the default): persistent workgroups of 4 compute waves + 1 loader
-// wave, 2 per CU (71 KiB of LDS each). The loader streams the workgroup's next full block
-// into LDS by LDS-DMA (global_load_lds_dwordx4, nt) while the compute waves code the current
-// one from registers, and fetches that block's bit offsets, so the compute waves issue no
-// global load inside the loop: their only vector-memory operations are the output stores,
-// which nothing waits for. (k_huff_pack loads each block's input into registers at its start,
-// behind the previous block's stores in the wave's in-order vmcnt; HBM read was in flight only
-// during those load phases, while the other 3 workgroups of the CU coded.) The compute code
-// per block is k_huff_pack's; the loader mirrors its barriers (lds_barrier: no vmcnt drain, so
-// its DMA stays in flight across them) and waits for its DMA only before the next block.
-// ------------------------------------------------------------------------------------
-typedef __attribute__((address_space(4))) const uint64_t c_u64;   // scalar (s_load) reads
-#define PK2_CW 4                          /* compute waves: k_huff_pack's 256-thread block code */
-#define PK2_THREADS (PK2_CW * 64 + 64)    /* + the loader wave */
-#define DEC_BUILD_BARRIERS 8              /* __syncthreads() in dec_tables_build (the loader mirrors them) */
-
-struct Pk2Lds {
-    __attribute__((aligned(16))) uint32_t in_buf[DC_BLOCK_BYTES / 4];   // next full block (LDS-DMA target)
-    __attribute__((aligned(16))) uint32_t stage[PACK_BLK_WORDS + 4];    // +4: emit's no-op ORs past the end
-    uint2 tab[256];
-    uint8_t nb8[256];
-    uint32_t scan[4];
-    uint32_t tot[PACK_PIECES][4];
-};
-static_assert(sizeof(DecBuildLds) <= sizeof(((Pk2Lds *)0)->in_buf), "decoder-table builder uses in_buf");
-
-// one 32 KiB block into LDS: 32 x 1 KiB LDS-DMA by the loader wave, 4 per asm statement (M0 =
-// the LDS destination, written and restored in the statement: cdna_hip_programming.md §5.7;
-// a SALU write of M0 needs one wait state before an LDS-DMA). Hidden from the compiler's
-// waitcnt bookkeeping on purpose: the loader waits for it with its own vmcnt(0), and the
-// compute waves, which issue none, get no vmcnt wait at their in_buf reads.
-static __device__ __forceinline__ void pk2_dma_block(const uint8_t *src_block, uint32_t *in_buf, int lane)
-{
-    const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void *)in_buf;
-    // (the instruction's immediate offset would move the LDS address too, so each 1 KiB piece
-    // gets its own address register and M0 steps by 1 KiB, as the compiler's own lowering does)
-#pragma unroll
-    for (int s = 0; s < DC_BLOCK_BYTES / 4096; ++s) {
-        const uint8_t *g = src_block + s * 4096 + lane * 16;
-        uint32_t keep;
-        asm volatile("s_mov_b32 %0, m0\n\t"
-                     "s_mov_b32 m0, %5\n\ts_nop 0\n\t"
-                     "global_load_lds_dwordx4 %1, off nt\n\t"
-                     "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
-                     "global_load_lds_dwordx4 %2, off nt\n\t"
-                     "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
-                     "global_load_lds_dwordx4 %3, off nt\n\t"
-                     "s_add_u32 m0, m0, 0x400\n\ts_nop 0\n\t"
-                     "global_load_lds_dwordx4 %4, off nt\n\t"
-                     "s_mov_b32 m0, %0"
-                     : "=&s"(keep)
-                     : "v"(g), "v"(g + 1024), "v"(g + 2048), "v"(g + 3072), "s"(lds0 + (uint32_t)s * 4096u)
-                     : "memory", "scc");
-    }
-}
-
-// where block b lies and which path codes it (the compute waves and the loader both derive it,
-// the loader to mirror the barrier count)
-struct Pk2Blk {
-    uint64_t blk_start, blk_end, s_excl, s_bits, blk_abs, blk_first_word;
-    uint32_t nw_blk, sh, ntiles;
-    bool full, fast;
-};
-static __device__ __forceinline__ Pk2Blk pk2_block(uint64_t b, uint64_t n, uint64_t s_excl, uint64_t s_next,
-                                                   uint64_t bit_base, uint64_t word_base, bool vec_out)
-{
-    Pk2Blk k;
-    k.blk_start = b * (uint64_t)DC_BLOCK_BYTES;
-    k.full = k.blk_start + DC_BLOCK_BYTES <= n;
-    k.blk_end = k.full ? k.blk_start + DC_BLOCK_BYTES : n;
-    k.s_excl = s_excl;
-    k.s_bits = s_next - s_excl;
-    k.blk_abs = bit_base + s_excl;
-    k.blk_first_word = k.blk_abs >> 5;
-    k.nw_blk = (uint32_t)(((k.blk_abs & 31) + k.s_bits + 31) >> 5);
-    k.sh = vec_out ? (uint32_t)((k.blk_first_word - word_base) & 3) : 0u;
-    k.fast = k.full && k.nw_blk + k.sh <= PACK_BLK_WORDS;
-    k.ntiles = (uint32_t)((k.blk_end - k.blk_start + PACK_TILE - 1) / PACK_TILE);
-    return k;
-}
-
-__global__ __launch_bounds__(PK2_THREADS) void k_huff_pack2(const uint8_t *__restrict__ in, uint64_t n,
-                                                            const dc_dtable *__restrict__ T,
-                                                            const uint64_t *__restrict__ block_off, uint64_t bit_base,
-                                                            const uint64_t *__restrict__ d_base, uint32_t *__restrict__ out,
-                                                            uint64_t *__restrict__ sync_base, uint16_t *__restrict__ sync_len,
-                                                            uint32_t sync_syms, uint64_t nblocks, uint64_t words_cap,
-                                                            int *__restrict__ err, int build_dec)
-{
-    __shared__ Pk2Lds S;
-    const int t = threadIdx.x, lane = t & 63;
-    // wave-uniform by construction (readfirstlane): the loop's branches and the block offsets'
-    // scalar loads stay uniform
-    const bool loader = __builtin_amdgcn_readfirstlane(t >> 6) >= PK2_CW;
-    if (build_dec && blockIdx.x == 0) {   // workgroup 0: the decoder tables, beside the pack
-        if (T->status == DC_OK) {
-            if (!loader) dec_tables_build(const_cast<dc_dtable *>(T), *reinterpret_cast<DecBuildLds *>(S.in_buf));
-            else
-                for (int i = 0; i < DEC_BUILD_BARRIERS; ++i) lds_barrier();
-        }
-        return;
-    }
-    const uint64_t bx = blockIdx.x - (uint64_t)build_dec, gstride = gridDim.x - (uint64_t)build_dec;
-    if (d_base) bit_base += *d_base;
-    const uint64_t total = block_off[nblocks];
-    if (err[0] != 0) return;
-    if (((bit_base & 31) + total + 31) / 32 > words_cap) {
-        if (t == 0) err[2] = 1;   // (pack status: DC_E_CAPACITY)
-        return;
-    }
-    const bool vec_out = ((uintptr_t)out & 15) == 0;
-    const uint64_t word_base = bit_base >> 5;
-    const uint32_t slog = sync_syms ? (uint32_t)__builtin_ctz(sync_syms) : 0u;
-    const bool qmode = 2 * total > 11 * n;
-    if (loader) {   // the first block's input
-        if (bx < nblocks && bx * (uint64_t)DC_BLOCK_BYTES + DC_BLOCK_BYTES <= n) {
-            pk2_dma_block(in + bx * (uint64_t)DC_BLOCK_BYTES, S.in_buf, lane);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-    } else {
-        S.tab[t] = make_uint2(T->code[t], T->nbits[t]);
-        S.nb8[t] = (uint8_t)T->nbits[t];
-        for (uint32_t i = 4u * t; i < PACK_BLK_WORDS + 4; i += 4u * PK2_CW * 64)
-            *reinterpret_cast<uint4 *>(&S.stage[i]) = make_uint4(0u, 0u, 0u, 0u);
-    }
-    lds_barrier();   // A (first block)
-    c_u64 *const soff = (c_u64 *)block_off;   // scalar loads: lgkmcnt, never behind the stores' vmcnt
-    for (uint64_t b = bx; b < nblocks; b += gstride) {
-        const Pk2Blk K = pk2_block(b, n, soff[b], soff[b + 1], bit_base, word_base, vec_out);
-        if (loader) {
-            // the compute waves' barriers for this block: fast path 2, tile path 6 per tile + 2;
-            // the next block's DMA goes out after the first (in_buf has been read by then)
-            const uint32_t nbar = K.fast ? 2u : 6u * K.ntiles + 2u;
-            lds_barrier();
-            const uint64_t bn = b + gstride;
-            if (bn < nblocks && bn * (uint64_t)DC_BLOCK_BYTES + DC_BLOCK_BYTES <= n)
-                pk2_dma_block(in + bn * (uint64_t)DC_BLOCK_BYTES, S.in_buf, lane);
-            for (uint32_t i = 1; i < nbar; ++i) lds_barrier();
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            lds_barrier();   // A (next block)
-            continue;
-        }
-        uint4 blkv[PACK_PIECES];
-        if (K.full) {
-#pragma unroll
-            for (int k = 0; k < PACK_PIECES; ++k)
-                blkv[k] = *reinterpret_cast<const uint4 *>(&S.in_buf[(k * PACK_TILE + t * 16) / 4]);
-        }
-        const uint64_t blk_start = K.blk_start, blk_end = K.blk_end, blk_abs = K.blk_abs;
-        const uint64_t blk_first_word = K.blk_first_word;
-        const uint32_t nw_blk = K.nw_blk, sh = K.sh;
-        if (K.fast) {
-            const int wid = t >> 6;
-            const uint32_t nwa = sh + nw_blk;
-            uint32_t Tk[PACK_PIECES], Hk[PACK_PIECES], Ik[PACK_PIECES];
-#pragma unroll
-            for (int k = 0; k < PACK_PIECES; ++k) {
-                const uint32_t w4[4] = {blkv[k].x, blkv[k].y, blkv[k].z, blkv[k].w};
-                uint32_t s0 = 0, s1 = 0;
-#pragma unroll
-                for (int i = 0; i < 8; ++i) s0 += S.nb8[(w4[i >> 2] >> (8 * (i & 3))) & 255u];
-#pragma unroll
-                for (int i = 8; i < 16; ++i) s1 += S.nb8[(w4[i >> 2] >> (8 * (i & 3))) & 255u];
-                Hk[k] = s0;
-                Tk[k] = s0 + s1;
-                __builtin_amdgcn_sched_barrier(0);
-            }
-#pragma unroll
-            for (int k = 0; k < PACK_PIECES; ++k) Ik[k] = wave_scan_incl(Tk[k]);
-            if (lane == 63) {
-#pragma unroll
-                for (int k = 0; k < PACK_PIECES; ++k) S.tot[k][wid] = Ik[k];
-            }
-            lds_barrier();   // F1
-            const uint64_t org = (blk_first_word - sh) << 5;
-            const uint32_t cm = sync_syms >> 4;
-            uint64_t run = blk_abs;
-#pragma unroll
-            for (int k = 0; k < PACK_PIECES; ++k) {
-                uint32_t wo = 0, kt = 0;
-#pragma unroll
-                for (int w = 0; w < 4; ++w) {
-                    const uint32_t v = S.tot[k][w];
-                    wo += (w < wid) ? v : 0u;
-                    kt += v;
-                }
-                const uint64_t As = run + wo + (Ik[k] - Tk[k]);
-                run += kt;
-                const uint64_t p = blk_start + (uint64_t)k * PACK_TILE + (uint64_t)t * 16;
-                if (sync_len != nullptr) {
-                    const uint32_t last = (cm == 4) ? (uint32_t)__builtin_amdgcn_update_dpp(0, (int)Ik[k], 0xff, 0xf, 0xf, false)
-                                                    : (uint32_t)__shfl((int)Ik[k], lane | (int)(cm - 1), 64);
-                    if ((p & (uint64_t)(sync_syms - 1)) == 0) {
-                        sync_len[p >> slog] = (uint16_t)(last - (Ik[k] - Tk[k]));
-                        if ((p & ((uint64_t)sync_syms * DC_SYNC_GROUP - 1)) == 0)
-                            sync_base[p >> (slog + DC_SYNC_GROUP_LOG)] = As;
-                    }
-                }
-                uint32_t w4[4] = {blkv[k].x, blkv[k].y, blkv[k].z, blkv[k].w};
-                asm volatile("" : "+v"(w4[0]), "+v"(w4[1]), "+v"(w4[2]), "+v"(w4[3]));
-                const uint32_t rel = (uint32_t)(As - org);
-                auto emit = [&](uint64_t acc, uint32_t nb, uint32_t pos) {
-                    const uint64_t al = acc << ((64u - nb) & 63u);
-                    const uint32_t hi = (uint32_t)(al >> 32), lo = (uint32_t)al, r = pos & 31u, wi = pos >> 5;
-                    atomicOr(&S.stage[wi], hi >> r);
-                    atomicOr(&S.stage[wi + 1], __builtin_amdgcn_alignbit(hi, lo, r));
-                    atomicOr(&S.stage[wi + 2], __builtin_amdgcn_alignbit(lo, 0u, r));
-                };
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const uint32_t Th = h ? Tk[k] - Hk[k] : Hk[k];
-                    const uint32_t pos = h ? rel + Hk[k] : rel;
-                    if (!qmode && Th <= 64u) {
-                        uint64_t acc = 0;
-#pragma unroll
-                        for (int i = 8 * h; i < 8 * h + 8; ++i) {
-                            const uint2 e = S.tab[(w4[i >> 2] >> (8 * (i & 3))) & 255u];
-                            acc = (acc << e.y) | e.x;
-                        }
-                        emit(acc, Th, pos);
-                    } else {
-                        uint32_t pp = pos;
-#pragma unroll 1
-                        for (int qq = 0; qq < 2; ++qq) {
-                            uint2 e[4];
-                            uint32_t nq = 0;
-#pragma unroll
-                            for (int i = 0; i < 4; ++i) {
-                                const int bi = 8 * h + 4 * qq + i;
-                                const uint32_t wv = qq ? w4[2 * h + 1] : w4[2 * h];
-                                e[i] = S.tab[(wv >> (8 * (bi & 3))) & 255u];
-                                nq += e[i].y;
-                            }
-                            if (nq <= 64u) {
-                                uint64_t acc = 0;
-#pragma unroll
-                                for (int i = 0; i < 4; ++i) acc = (acc << e[i].y) | e[i].x;
-                                emit(acc, nq, pp);
-                                pp += nq;
-                            } else {
-#pragma unroll
-                                for (int i = 0; i < 4; ++i) { emit(e[i].x, e[i].y, pp); pp += e[i].y; }
-                            }
-                        }
-                    }
-                }
-                __builtin_amdgcn_sched_barrier(0);
-            }
-            lds_barrier();   // F2
-            const uint32_t last_plain = ((run & 31) != 0) ? nwa - 1 : nwa;
-            uint32_t *dst = out + (blk_first_word - word_base) - sh;
-            if (vec_out) {
-                const uint32_t nq = last_plain >> 2;
-                for (uint32_t q = 1 + t; q < nq; q += PK2_CW * 64) {
-                    uint4 *const sq = reinterpret_cast<uint4 *>(&S.stage[4 * q]);
-                    const uint4 v = *sq;
-                    *sq = make_uint4(0u, 0u, 0u, 0u);
-                    uint4 *const d4 = reinterpret_cast<uint4 *>(dst + 4 * q);
-                    __builtin_nontemporal_store(bswap32(v.x), &d4->x);
-                    __builtin_nontemporal_store(bswap32(v.y), &d4->y);
-                    __builtin_nontemporal_store(bswap32(v.z), &d4->z);
-                    __builtin_nontemporal_store(bswap32(v.w), &d4->w);
-                }
-                const uint32_t hend = last_plain < 4u ? last_plain : 4u;
-                if (t < 4 && (uint32_t)t > sh && (uint32_t)t < hend) { dst[t] = bswap32(S.stage[t]); S.stage[t] = 0u; }
-                const uint32_t tb = nq > 0 ? 4 * nq : 4u;
-                if (t >= 8 && t < 12 && tb + (t - 8) < last_plain) {
-                    dst[tb + (t - 8)] = bswap32(S.stage[tb + (t - 8)]);
-                    S.stage[tb + (t - 8)] = 0u;
-                }
-            } else {
-                for (uint32_t i = t + 1; i < last_plain; i += PK2_CW * 64) { dst[i] = bswap32(S.stage[i]); S.stage[i] = 0u; }
-            }
-            if (t == 0) {
-                atomicOr(&dst[sh], bswap32(S.stage[sh]));
-                S.stage[sh] = 0u;
-            }
-            if (t == 64 && last_plain < nwa && nw_blk > 1) {
-                atomicOr(&dst[nwa - 1], bswap32(S.stage[nwa - 1]));
-                S.stage[nwa - 1] = 0u;
-            }
-        } else {
-            // blocks whose output exceeds the stage, and a partial last block: k_huff_pack's
-            // tile loop (6 barriers per 4 KiB tile + 2: the loader mirrors them)
-            const bool full = K.full;
-            uint64_t tile_abs = blk_abs;
-#pragma unroll
-            for (int k = 0; k < PACK_PIECES; ++k) {
-                const uint64_t tile = blk_start + (uint64_t)k * PACK_TILE;
-                if (tile >= blk_end) break;
-                const uint64_t p = tile + (uint64_t)t * 16;
-                const int cnt = (p + 16 <= blk_end) ? 16 : (p < blk_end ? (int)(blk_end - p) : 0);
-                uint32_t bytes4[4] = {0u, 0u, 0u, 0u};
-                if (full) {
-                    bytes4[0] = blkv[k].x; bytes4[1] = blkv[k].y; bytes4[2] = blkv[k].z; bytes4[3] = blkv[k].w;
-                } else {
-                    for (int i = 0; i < cnt; ++i) bytes4[i >> 2] |= (uint32_t)in[p + i] << (8 * (i & 3));
-                }
-                uint32_t code[16], nb[16];
-                uint32_t T_bits = 0;
-#pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    const uint2 e = S.tab[(bytes4[i >> 2] >> (8 * (i & 3))) & 255u];
-                    code[i] = e.x;
-                    nb[i] = (i < cnt) ? e.y : 0u;
-                    T_bits += nb[i];
-                }
-                uint32_t tile_bits;
-                const uint32_t pre = wg_scan_excl_u32(T_bits, S.scan, &tile_bits);
-                const uint64_t TB = tile_abs >> 5;
-                const uint64_t As = tile_abs + pre;
-                const uint64_t Ae = As + T_bits;
-                if (sync_len != nullptr) {
-                    uint32_t cb = T_bits;
-                    for (uint32_t d = 1; d < (sync_syms >> 4); d <<= 1) cb += __shfl_xor(cb, (int)d, 64);
-                    if (cnt > 0 && (p & (uint64_t)(sync_syms - 1)) == 0) {
-                        sync_len[p >> slog] = (uint16_t)cb;
-                        if ((p & ((uint64_t)sync_syms * DC_SYNC_GROUP - 1)) == 0)
-                            sync_base[p >> (slog + DC_SYNC_GROUP_LOG)] = As;
-                    }
-                }
-                const uint32_t ws = (uint32_t)((As >> 5) - TB);
-                if (ws != 0) S.stage[ws] = 0u;
-                if (t == PK2_CW * 64 - 1) {
-                    const uint32_t we = (uint32_t)((Ae >> 5) - TB);
-                    if (we != 0) S.stage[we] = 0u;
-                }
-                __syncthreads();
-                if (T_bits > 0) {
-                    uint64_t acc = 0;
-                    uint32_t nacc = (uint32_t)(As & 31);
-                    uint32_t wi = ws;
-                    bool first = true;
-#pragma unroll
-                    for (int i = 0; i < 16; ++i) {
-                        if (nb[i]) {
-                            acc = (acc << nb[i]) | code[i];
-                            nacc += nb[i];
-                            if (nacc >= 32) {
-                                nacc -= 32;
-                                const uint32_t word = (uint32_t)(acc >> nacc);
-                                if (first) atomicOr(&S.stage[wi], word);
-                                else S.stage[wi] = word;
-                                first = false;
-                                ++wi;
-                            }
-                        }
-                    }
-                    if (nacc > 0) atomicOr(&S.stage[wi], (uint32_t)(acc << (32 - nacc)));
-                }
-                __syncthreads();
-                const uint64_t tile_end_abs = tile_abs + tile_bits;
-                const uint32_t nfull = (uint32_t)((tile_end_abs >> 5) - TB);
-                for (uint32_t i = t; i < nfull; i += PK2_CW * 64) {
-                    const uint64_t gw = TB + i;
-                    if (gw == blk_first_word) atomicOr(&out[gw - word_base], bswap32(S.stage[i]));
-                    else out[gw - word_base] = bswap32(S.stage[i]);
-                }
-                __syncthreads();
-                if (t == 0) S.stage[0] = (tile_end_abs & 31) ? S.stage[nfull] : 0u;
-                tile_abs = tile_end_abs;
-                __syncthreads();
-            }
-            if (t == 0 && (tile_abs & 31)) atomicOr(&out[(tile_abs >> 5) - word_base], bswap32(S.stage[0]));
-            __syncthreads();
-            for (uint32_t i = 4u * t; i < PACK_BLK_WORDS + 4; i += 4u * PK2_CW * 64)
-                *reinterpret_cast<uint4 *>(&S.stage[i]) = make_uint4(0u, 0u, 0u, 0u);
-            __syncthreads();
-        }
-        lds_barrier();   // A (next block): stage zeroed, the loader's next block landed
-    }
-}
-
 
 // ------------------------------------------------------------------------------------
 // (H8) decode. The stream is cut into chunks of S symbols (sync index: u16 bit length per
@@ -2579,6 +2110,7 @@ extern "C" int dc_diag_read(void *h, size_t bytes)
 #define D8_STAMP(v)
 #endif
 
+typedef __attribute__((address_space(4))) const uint64_t c_u64;   // scalar (s_load) reads
 
 template <int NC>
 struct D8Meta { uint32_t len[NC]; uint64_t base[NC]; };   // sync index of one tuple: len per lane, base uniform
@@ -5517,8 +5049,6 @@ struct dc_ctx {
     uint32_t opt_hist_pf;         // histogram: blocks of loads in flight ahead (1..2, 0 = default 2)
     uint32_t *d_hflag;            // histogram accumulator (256 u64) + done counter, zero between launches
     uint32_t opt_decode_variant;  // fast decoder: 0 one code per lookup (k_huff_decode8), 1 up to 3 (k_huff_decode9)
-    uint32_t opt_pack_variant;    // pack: 0 k_huff_pack, 1 the loader-wave persistent k_huff_pack2 (A/B)
-    int ncu;                      // compute units of the device (persistent grids)
     uint32_t opt_adec_v1;         // adaptive nybble decode: 0 control words + k_nyb_resolve_c, 1 = the one-pass
                                   // k_nyb_adec, 2 = r2's k_nyb_resolve, 3 = k_nyb_resolve_s (A/B)
     // timing
@@ -5633,15 +5163,12 @@ static int ctx_create(dc_ctx **out, int device, void *stream, bool own)
         return DC_E_HIP;
     }
     c->opt_d8_static = D8_STATIC_PCT;
-    if (hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || c->ncu <= 0)
-        c->ncu = 256;
     {   // A/B knobs of tools/ab_env.sh and tools/dec_ab.py, read once per context and clamped
         const char *e;
         if ((e = getenv("DC_HIST_GRID"))) (void)dc_ctx_set_option(c, DC_OPT_HIST_GRID, atoll(e));
         if ((e = getenv("DC_PACK_GRID"))) (void)dc_ctx_set_option(c, DC_OPT_PACK_GRID, atoll(e));
         if ((e = getenv("DC_D8_STATIC"))) (void)dc_ctx_set_option(c, DC_OPT_DECODE_STATIC_PCT, atoll(e));
         if ((e = getenv("DC_DECODE_V7"))) (void)dc_ctx_set_option(c, DC_OPT_DECODE_GENERAL, atoll(e) != 0);
-        if ((e = getenv("DC_PACK_VARIANT"))) (void)dc_ctx_set_option(c, DC_OPT_PACK_VARIANT, atoll(e));
     }
     if (g_rank_uploaded != device) {
         uint8_t rank[256];
@@ -5722,10 +5249,6 @@ int dc_ctx_set_option(dc_ctx *c, int option, int64_t value)
         if (value != 0) return DC_E_ARG;
 #endif
         c->opt_adec_v1 = (uint32_t)value;
-        return DC_OK;
-    case DC_OPT_PACK_VARIANT:
-        if (value < 0 || value > 2) return DC_E_ARG;
-        c->opt_pack_variant = (uint32_t)value;
         return DC_OK;
     case DC_OPT_HIST_PREFETCH:
         if (value < 0 || value > 2) return DC_E_ARG;
@@ -6009,25 +5532,12 @@ static int pack_impl(dc_ctx *c, const uint8_t *d_in, uint64_t n, const dc_dtable
     // the blocks' offsets, and the boundary words zeroed (the plan's error flags: its slot)
     const int r = plan_offsets(c, plan_err(c), plan_err_next(c), bit_base, d_base, d_words, words_cap);
     if (r != DC_OK) return r;
-    if (c->opt_pack_variant == 1) {
-        // persistent: 2 workgroups (4 compute waves + 1 loader) per CU, workgroup 0 builds the
-        // decoder tables and the others stride over the blocks
-        const uint64_t gmax = c->opt_pack_grid ? c->opt_pack_grid : (uint64_t)(2 * c->ncu) - 1;
-        const uint64_t grid = nb < gmax ? nb : gmax;
-        LAUNCH(c, "huff_pack", k_huff_pack2, grid + 1, PK2_THREADS, d_in, n, d_table, (const uint64_t *)c->d_off, bit_base,
-               d_base, d_words, d_sync_base, d_sync_len, sync_syms, nb, words_cap, plan_err(c), 1);
-    } else {
-        // two blocks per workgroup (grid-stride) + workgroup 0: the decoder tables
-        // (k_huff_table leaves them to the pack's idle CU time)
-        const uint64_t gmax = c->opt_pack_grid ? c->opt_pack_grid : (nb + 1) / 2;
-        const uint64_t grid = nb < gmax ? nb : gmax;
-        if (c->opt_pack_variant == 2)
-            LAUNCH(c, "huff_pack", k_huff_pack<1>, grid + 1, 256, d_in, n, d_table, (const uint64_t *)c->d_off, bit_base,
-                   d_base, d_words, d_sync_base, d_sync_len, sync_syms, nb, words_cap, plan_err(c), 1);
-        else
-            LAUNCH(c, "huff_pack", k_huff_pack<0>, grid + 1, 256, d_in, n, d_table, (const uint64_t *)c->d_off, bit_base,
-                   d_base, d_words, d_sync_base, d_sync_len, sync_syms, nb, words_cap, plan_err(c), 1);
-    }
+    // two blocks per workgroup (grid-stride) + workgroup 0: the decoder tables (k_huff_table
+    // leaves them to the pack's idle CU time)
+    const uint64_t gmax = c->opt_pack_grid ? c->opt_pack_grid : (nb + 1) / 2;
+    const uint64_t grid = nb < gmax ? nb : gmax;
+    LAUNCH(c, "huff_pack", k_huff_pack, grid + 1, 256, d_in, n, d_table, (const uint64_t *)c->d_off, bit_base, d_base,
+           d_words, d_sync_base, d_sync_len, sync_syms, nb, words_cap, plan_err(c), 1);
     dec_tables_built(c, d_table);   // workgroup 0 built the decoder tables
     return DC_OK;
 }
