@@ -230,129 +230,6 @@ __global__ __launch_bounds__(256) void k_hist_blocks(const uint8_t *__restrict__
     }
 }
 
-// (H1) r4 histogram: ONE 1024-thread workgroup per CU (16 waves, where k_hist_blocks fits 2 x 4
-// waves by its 64 KiB of counters per workgroup). The same 64 KiB counter layout (dword bin*64
-// + lane: conflict-free ds_add_u32 per byte, one v_perm for its address), 4 waves per 8-bit field
-// (waves w, w+4, w+8, w+12 share field w & 3: a lane sees 32 bytes of a 32 KiB block, so a field
-// grows by <= 128 per block and the running-difference read stays exact). The block's counts are
-// read by all 1024 threads: thread t takes bin t >> 2, quarter t & 3 of its 64 columns (16
-// dwords, rotated so the 16 lanes of a ds_read_b128 group hit 16 distinct bank quads), and the
-// quad's 4 partial counts are summed by DPP. PF blocks of loads in flight ahead of the counting.
-template <int PF>
-__global__ __launch_bounds__(1024) void k_hist16(const uint8_t *__restrict__ in, uint64_t n, uint64_t nblocks,
-                                                 uint16_t *__restrict__ bh, uint64_t *__restrict__ hist,
-                                                 uint64_t *__restrict__ hacc, uint32_t *__restrict__ hdone,
-                                                 uint64_t *__restrict__ hloc, HistFuse fuse)
-{
-    __shared__ __attribute__((aligned(16))) uint32_t cnt[256 * 64];
-    __shared__ uint32_t s_last;
-    __shared__ uint64_t s_h[256];
-    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-    const uint32_t inc = 1u << (8 * (wv & 3));
-    const uint32_t lane4 = 4u * (uint32_t)lane;
-    char *const cbase = reinterpret_cast<char *>(cnt);
-    for (int i = t; i < 256 * 16; i += 1024) reinterpret_cast<uint4 *>(cnt)[i] = make_uint4(0u, 0u, 0u, 0u);
-    __syncthreads();
-    const int bin = t >> 2, qq = t & 3;
-    const uint64_t nfull = n / DC_BLOCK_BYTES;
-    uint64_t total = 0;          // bin's count over this workgroup's blocks (threads with qq == 0)
-    uint32_t prevc[16];
-#pragma unroll
-    for (int q = 0; q < 16; ++q) prevc[q] = 0u;
-    uint4 v[PF][2];
-    uint64_t b = blockIdx.x;
-#pragma unroll
-    for (int f = 0; f < PF; ++f) {
-        const uint64_t bf = b + (uint64_t)f * gridDim.x;
-        if (bf < nfull) {
-            const uint4 *p = reinterpret_cast<const uint4 *>(in + bf * (uint64_t)DC_BLOCK_BYTES) + t;
-            v[f][0] = LD_HIST(p);
-            v[f][1] = LD_HIST(p + 1024);
-        }
-    }
-    for (; b < nblocks; b += gridDim.x) {
-        if (b < nfull) {
-            const uint4 cur[2] = {v[0][0], v[0][1]};
-#pragma unroll
-            for (int f = 0; f + 1 < PF; ++f) { v[f][0] = v[f + 1][0]; v[f][1] = v[f + 1][1]; }
-            const uint64_t nb = b + (uint64_t)PF * gridDim.x;
-            if (nb < nfull) {
-                const uint4 *p = reinterpret_cast<const uint4 *>(in + nb * (uint64_t)DC_BLOCK_BYTES) + t;
-                v[PF - 1][0] = LD_HIST(p);
-                v[PF - 1][1] = LD_HIST(p + 1024);
-            }
-#pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                const uint32_t w4[4] = {cur[k].x, cur[k].y, cur[k].z, cur[k].w};
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const uint32_t addr = __builtin_amdgcn_perm(w4[j], lane4, 0x0c0c0000u | ((4u + q) << 8));
-                        atomicAdd(reinterpret_cast<uint32_t *>(cbase + addr), inc);
-                    }
-                }
-            }
-        } else {
-            const uint64_t base = b * (uint64_t)DC_BLOCK_BYTES;
-            for (uint64_t i = base + t; i < n; i += 1024) atomicAdd(&cnt[in[i] * 64 + lane], inc);
-        }
-        __syncthreads();
-        // bin `bin`, columns [16 qq, 16 qq + 16) as 4 uint4 (slot rotated by the bin), minus
-        // their values after the previous block; v_dot4 adds the four wave fields
-        const uint4 *row = reinterpret_cast<const uint4 *>(&cnt[bin * 64 + qq * 16]);
-        uint32_t acc = 0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint4 d = row[(k + bin) & 3];
-            const uint32_t dn[4] = {d.x, d.y, d.z, d.w};
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const uint32_t x = dn[q], diff = x - prevc[4 * k + q];
-                acc = __builtin_amdgcn_udot4(diff, 0x01010101u, acc, false);
-                prevc[4 * k + q] = x;
-            }
-        }
-        // the quad's 4 partials (lanes 4 bin .. 4 bin + 3): row_shr 1 and 2 within the quad
-        acc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)acc, 0x111, 0xf, 0xf, false);   // row_shr:1
-        acc += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)acc, 0x112, 0xf, 0xf, false);   // row_shr:2
-        // lane 4 bin + 3 now holds the sum of its quad (row_shr stays inside each row of 16)
-        if (qq == 3) {
-            bh[b * 256 + bin] = (uint16_t)acc;
-            total += acc;
-        }
-        __syncthreads();
-    }
-    // as k_hist_blocks: this workgroup's totals into the accumulator, the last workgroup out moves
-    // it to hist[] (release/acquire counter hand-off, cdna_hip_programming.md §6 Guideline 16)
-    if (qq == 3 && total) atomicAdd(reinterpret_cast<unsigned long long *>(&hacc[bin]), total);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (t == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const bool last = __hip_atomic_fetch_add(hdone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                          gridDim.x - 1;
-        if (last) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        s_last = last;
-    }
-    __syncthreads();
-    if (!s_last || t >= 256) return;   // (waves that end leave the workgroup's barriers: 4 waves remain)
-    const uint64_t hv = atomicExch(reinterpret_cast<unsigned long long *>(&hacc[t]), 0ull);
-    hist[t] = hv;
-    hloc[t] = hv;
-    if (t == 0) atomicExch(hdone, 0u);
-    if (fuse.T) {
-        s_h[t] = hv;
-        __syncthreads();
-        huff_table_body(*reinterpret_cast<TblLds *>(cnt), s_h, 1, nullptr, fuse.M, fuse.nary, fuse.T, nullptr, s_h,
-                        fuse.d_total, fuse.perr, fuse.perr_next);
-    }
-}
-
 // ------------------------------------------------------------------------------------
 // (H2-H6) code table: n-ary Huffman lengths + canonical n-ary codes + packed bit codes
 // + decode tables. One workgroup.
@@ -5172,7 +5049,6 @@ struct dc_ctx {
     uint32_t opt_hist_pf;         // histogram: blocks of loads in flight ahead (1..2, 0 = default 2)
     uint32_t *d_hflag;            // histogram accumulator (256 u64) + done counter, zero between launches
     uint32_t opt_decode_variant;  // fast decoder: 0 one code per lookup (k_huff_decode8), 1 up to 3 (k_huff_decode9)
-    uint32_t opt_hist_variant;    // histogram: 0 k_hist_blocks (2 x 4 waves per CU), 1 k_hist16 (16 waves per CU)
     uint32_t opt_adec_v1;         // adaptive nybble decode: 0 control words + k_nyb_resolve_c, 1 = the one-pass
                                   // k_nyb_adec, 2 = r2's k_nyb_resolve, 3 = k_nyb_resolve_s (A/B)
     // timing
@@ -5293,8 +5169,6 @@ static int ctx_create(dc_ctx **out, int device, void *stream, bool own)
         if ((e = getenv("DC_PACK_GRID"))) (void)dc_ctx_set_option(c, DC_OPT_PACK_GRID, atoll(e));
         if ((e = getenv("DC_D8_STATIC"))) (void)dc_ctx_set_option(c, DC_OPT_DECODE_STATIC_PCT, atoll(e));
         if ((e = getenv("DC_DECODE_V7"))) (void)dc_ctx_set_option(c, DC_OPT_DECODE_GENERAL, atoll(e) != 0);
-        if ((e = getenv("DC_HIST_VARIANT"))) (void)dc_ctx_set_option(c, DC_OPT_HIST_VARIANT, atoll(e));
-        if ((e = getenv("DC_HIST_PF"))) (void)dc_ctx_set_option(c, DC_OPT_HIST_PREFETCH, atoll(e));
     }
     if (g_rank_uploaded != device) {
         uint8_t rank[256];
@@ -5375,10 +5249,6 @@ int dc_ctx_set_option(dc_ctx *c, int option, int64_t value)
         if (value != 0) return DC_E_ARG;
 #endif
         c->opt_adec_v1 = (uint32_t)value;
-        return DC_OK;
-    case DC_OPT_HIST_VARIANT:
-        if (value < 0 || value > 1) return DC_E_ARG;
-        c->opt_hist_variant = (uint32_t)value;
         return DC_OK;
     case DC_OPT_HIST_PREFETCH:
         if (value < 0 || value > 2) return DC_E_ARG;
@@ -5481,14 +5351,6 @@ static int hist_impl(dc_ctx *c, const uint8_t *d_in, uint64_t n, uint64_t *d_his
     // 0.176 ms against 0.179 with one; before the nt loads one was best, 0.1995 vs 0.2022 ms)
     uint64_t *const hacc = reinterpret_cast<uint64_t *>(c->d_hflag);
     uint32_t *const hdone = c->d_hflag + 512;
-    if (c->opt_hist_variant == 1) {   // one 16-wave workgroup per CU
-        const uint64_t g16 = c->opt_hist_grid ? c->opt_hist_grid : 256u;
-        const uint64_t grid16 = nb < g16 ? nb : g16;
-        if (c->opt_hist_pf == 1)
-            LAUNCH(c, "hist_blocks", k_hist16<2>, grid16, 1024, d_in, n, nb, c->d_bh, d_hist, hacc, hdone, c->d_hloc, fuse);
-        else LAUNCH(c, "hist_blocks", k_hist16<4>, grid16, 1024, d_in, n, nb, c->d_bh, d_hist, hacc, hdone, c->d_hloc, fuse);
-        return DC_OK;
-    }
     if (c->opt_hist_pf == 1)
         LAUNCH(c, "hist_blocks", k_hist_blocks<1>, grid, 256, d_in, n, nb, c->d_bh, d_hist, hacc, hdone, c->d_hloc, fuse);
     else LAUNCH(c, "hist_blocks", k_hist_blocks<2>, grid, 256, d_in, n, nb, c->d_bh, d_hist, hacc, hdone, c->d_hloc, fuse);

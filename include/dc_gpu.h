@@ -117,13 +117,10 @@ enum {
     DC_OPT_HIST_PREFETCH = 5,     /* histogram: 32 KiB blocks in flight ahead, 1..2, 0 = 2 */
     DC_OPT_DECODE_VARIANT = 6,    /* fast decoder: 0 one code per lookup (k_huff_decode8),
                                      1 up to 3 codes per lookup (k_huff_decode9) */
-    DC_OPT_NYB_ADEC_V1 = 7,       /* adaptive nybble decode: 0 tokens + control words + the
+    DC_OPT_NYB_ADEC_V1 = 7        /* adaptive nybble decode: 0 tokens + control words + the
                                      SGPR-list resolve (k_nyb_resolve_c); 1 the one-pass
                                      single-wave k_nyb_adec; 2 tokens + r2's VGPR-list resolve;
-                                     3 tokens + the plain-code resolve (k_nyb_resolve_s) (A/B;
-                                     1-3 only in DC_AB_KERNELS builds) */
-    DC_OPT_HIST_VARIANT = 9       /* histogram: 0 two 4-wave workgroups per CU (k_hist_blocks),
-                                     1 one 16-wave workgroup per CU (k_hist16); env DC_HIST_VARIANT */
+                                     3 tokens + the plain-code resolve (k_nyb_resolve_s) (A/B) */
 };
 int dc_ctx_set_option(dc_ctx *ctx, int option, int64_t value);
 const char *dc_version(void);
