@@ -91,6 +91,7 @@ def _declare_core(L):
         "dc_huff_table_status": ([vp, P, C.POINTER(C.c_int32)], i32),
         "dc_huff_plan": ([vp, P, P], i32),
         "dc_huff_encode_plan": ([vp, P, u64, i32, i32, P, P, P], i32),
+        "dc_huff_table_plan": ([vp, P, i32, i32, P, P], i32),
         "dc_copy_probe": ([vp, P, P, u64], i32),
         "dc_huff_pack": ([vp, P, u64, P, u64, P, u64, P, P, u32], i32),
         "dc_huff_sync_chunks": ([u64, u32], u64),

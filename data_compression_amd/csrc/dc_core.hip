@@ -5436,6 +5436,22 @@ int dc_huff_plan(dc_ctx *c, const dc_dtable *d_table, uint64_t *d_total_bits)
     return DC_OK;
 }
 
+int dc_huff_table_plan(dc_ctx *c, const uint64_t *d_hist, int M, int nary, dc_dtable *d_table, uint64_t *d_total_bits)
+{
+    if (!c || !d_hist || !d_table || !d_total_bits || M < 0 || M >= DC_MAX_SYMS || nary < 2 || nary > 256) return DC_E_ARG;
+    if (!c->hist_in && c->hist_n) return DC_E_STATE;
+    ++c->gen_p;   // this plan's error slot (the table kernel clears the next one)
+    table_written(c);
+    // the table of d_hist (e.g. the all-reduced histogram of every shard) and, in the same
+    // launch, the payload bits of THIS context's last histogram under it (huff_table_body's plan)
+    LAUNCH(c, "huff_table", k_huff_table, 1, 256, d_hist, 1, (const int32_t *)nullptr, M, nary, d_table,
+           (dc_tree *)nullptr, (const uint64_t *)c->d_hloc, d_total_bits, plan_err(c), plan_err_next(c));
+    c->plan_table = d_table;
+    c->plan_total = d_total_bits;
+    c->plan_ok = true;
+    return DC_OK;
+}
+
 int dc_huff_encode_plan(dc_ctx *c, const uint8_t *d_in, uint64_t n, int M, int nary, uint64_t *d_hist,
                         dc_dtable *d_table, uint64_t *d_total_bits)
 {

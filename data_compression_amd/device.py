@@ -147,6 +147,16 @@ class Codec:
         self._last_total = total
         return hist, table, total
 
+    def table_plan(self, hist, n_ary: int, max_symbol_value: int = 258, out=None, total=None):
+        """table of `hist` + the plan of this context's last hist() under it, one launch
+        (dc_huff_table_plan: a shard's encode after the all-reduce). Returns (table, total)."""
+        table = out if out is not None else self._t(self.table_bytes)
+        total = total if total is not None else self._t(1, torch.int64)
+        check("dc_huff_table_plan", self.L.dc_huff_table_plan(self.ctx, _ptr(hist), max_symbol_value, n_ary,
+                                                              _ptr(table), _ptr(total)))
+        self._last_total = total
+        return table, total
+
     def plan_total(self) -> int:
         return int(self._last_total.item())
 

@@ -92,17 +92,26 @@ class ShardedHuffman:
             hist, tab, total = self.e.encode_plan(x, n_ary, hist=hist, table=table, total=total)
             return tab, total, None
         hist = self.e.hist(x, out=hist) if hist is not None else self.e.hist(x)
+        fused = hasattr(self.e, "table_plan")   # table + this shard's plan in one launch
         if self.table_mode == "broadcast" and self.world > 1:
             self._reduce_to_src(hist)
-            if self.rank == self.table_src:
-                tab = self.e.table(hist, n_ary, out=table) if table is not None else self.e.table(hist, n_ary)
+            if self.rank == self.table_src and fused:   # table + its own plan, one launch
+                tab, total = self.e.table_plan(hist, n_ary, out=table, total=total)
+                self._broadcast_table(tab)
             else:
-                tab = table if table is not None else self.e.alloc_table()
-            self._broadcast_table(tab)
+                if self.rank == self.table_src:
+                    tab = self.e.table(hist, n_ary, out=table) if table is not None else self.e.table(hist, n_ary)
+                else:
+                    tab = table if table is not None else self.e.alloc_table()
+                self._broadcast_table(tab)
+                total = self.e.plan(tab, total=total) if total is not None else self.e.plan(tab)
         else:
             self._all_reduce(hist)
-            tab = self.e.table(hist, n_ary, out=table) if table is not None else self.e.table(hist, n_ary)
-        total = self.e.plan(tab, total=total) if total is not None else self.e.plan(tab)
+            if fused:
+                tab, total = self.e.table_plan(hist, n_ary, out=table, total=total)
+            else:
+                tab = self.e.table(hist, n_ary, out=table) if table is not None else self.e.table(hist, n_ary)
+                total = self.e.plan(tab, total=total) if total is not None else self.e.plan(tab)
         totals = self._all_gather_scalar(total) if self.world > 1 else None
         return tab, total, totals
 

@@ -162,6 +162,11 @@ int dc_tree_depths(dc_ctx *ctx, const int32_t *d_parent, int list_length, int le
  *     pack (k_block_local: bits per 32 KiB block and a scan per 64 blocks; k_block_final_wide:
  *     the absolute offsets, and the zeroing of the payload words two blocks share). */
 int dc_huff_plan(dc_ctx *ctx, const dc_dtable *d_table, uint64_t *d_total_bits);
+/* (2+3 fused) the table of d_hist (dc_huff_table) and the plan of this context's last
+ *     dc_huff_hist under it (dc_huff_plan) in ONE launch: a sharded encode's step after the
+ *     all-reduce of the histograms (the table of the global histogram, the bits of the shard). */
+int dc_huff_table_plan(dc_ctx *ctx, const uint64_t *d_hist, int max_symbol_value, int n_ary, dc_dtable *d_table,
+                       uint64_t *d_total_bits);
 /* (1+2+3 fused) histogram, table and plan of d_in[0..n) in ONE launch: the histogram's last
  *     workgroup builds the table (as dc_huff_table) and the plan total (as dc_huff_plan) from
  *     the histogram it holds. The single-stream encoder's path (a sharded encode must reduce

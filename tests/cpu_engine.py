@@ -48,6 +48,11 @@ class CpuEngine:
         self._total = int((h * tab["nb"].astype(np.int64)).sum())
         return torch.tensor([self._total], dtype=torch.int64)
 
+    def table_plan(self, hist, n_ary, out=None, total=None):
+        """dc_huff_table_plan: the table of hist and this engine's last hist() planned under it."""
+        tab = self.table(hist, n_ary, out=out)
+        return tab, self.plan(tab, total=total)
+
     def plan_total(self):
         return self._total
 
