@@ -3767,15 +3767,6 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
         uint64_t acc = 0;
         const uint32_t kend = nelem - j0 < 16 ? (uint32_t)(nelem - j0) : 16u;
         const uint32_t valid = fvalid[c];
-        // (a dword is complete at most once per 2 elements, <= 32 bits: OR-ed into the stage
-        // unconditionally, 0 when it is not complete yet: no branch)
-        auto flush = [&]() {
-            const uint32_t f = nb >= 32u ? 1u : 0u;
-            atomicOr(&s_out32[di], (uint32_t)acc & (0u - f));
-            acc = f ? (acc >> 32) : acc;
-            nb -= 32u * f;
-            di += f;
-        };
 #ifdef DC_DIAG_FSMW_NOLOOP   // timing ablation only: no element loop (garbage output)
         if (M == M_NYB_ENC) { atomicOr(&s_out32[di], (uint32_t)S ^ valid); continue; }
 #endif
@@ -3799,21 +3790,33 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
                     out[o0 + before] = (uint8_t)(w >> (8 * ((kt + 1) & 3)));
                 }
             }
+            // Each element's 0-2 bytes go straight into the stage at their own offset (the count
+            // of bytes before them: a running sum, no serial shift-accumulate): 1 - h + s bytes,
+            // the first = s ? (h ? pair : prev) : x, the second (a miss after a pending hit) = x.
+            // Every byte of the tile's output is written exactly once (no zeroed stage, no ORs).
+            // (r3's 64-bit accumulator with a dword flush every 2 elements: ~26 VALU per element,
+            // the kernel VALU-issue bound at 1.28 ms per GiB)
+            uint8_t *const so = s_out + P;
+            uint32_t pos = 0;
 #pragma unroll
             for (int k = 0; k < 16; ++k) {
                 const uint32_t x = W.b(k + 1), prev = W.b(k);
-                const uint32_t h = (Hx >> k) & 1u, s = (Sx >> k) & 1u;
+                const bool h = (Hx >> k) & 1u, s = (Sx >> k) & 1u;
                 const uint32_t rq = (k ? rk[k - 1] : rp0) & 7u;
                 const uint32_t pair = 0x88u | (rq << 4) | (rk[k] & 7u);   // the pending hit, then this one
-                const uint32_t lit = s ? (prev | (x << 8)) : x;           // (the pending hit's byte raw, then this)
-                const uint32_t val = h ? (pair & (0u - s)) : lit;
-                acc |= (uint64_t)val << nb;
-                nb += 8u * (1u - h + s);
-                if (k & 1) flush();
+                const uint32_t b1 = s ? (h ? pair : prev) : x;
+                if (!h || s) so[pos] = (uint8_t)b1;
+                if (!h && s) so[pos + 1] = (uint8_t)x;
+                pos += (h ? 0u : 1u) + (s ? 1u : 0u);
             }
+            nb = 0;   // (nothing left in the accumulator)
         } else {   // M_NYB_DEC / M_NYB_DBODY: compressed byte x, state s = "at the low nybble"
             // (r2's element loop: per element branches measured 1-3% faster here than the
             // encoder's branch-free form, same-box A/B tools/gpu_r3n.sh)
+            // each element's 1-2 bytes straight into the stage at their running offset (as the
+            // encoder above: no shift-accumulate chain, every output byte written once)
+            uint8_t *const so = s_out + P;
+            uint32_t pos = 0;
 #pragma unroll
             for (int k = 0; k < 16; ++k) {
                 const uint32_t x = W.b(k + 1);
@@ -3824,18 +3827,10 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
                 const uint32_t lo_b = (l & 8u) ? (uint32_t)(tblv >> (8u * (l & 7u))) & 255u : ((l & 7u) << 4) + nxt;
                 const uint32_t hi_b = (uint32_t)(tblv >> (8u * (h & 7u))) & 255u;
                 const bool two = !s && (h & 8u);
-                const uint32_t val = s ? lo_b : (two ? (hi_b | (lo_b << 8)) : x);
                 if ((uint32_t)k < kend) {
-                    acc |= (uint64_t)val << nb;
-                    nb += two ? 16u : 8u;
-                }
-                if (k & 1) {
-                    if (nb >= 32u) {
-                        atomicOr(&s_out32[di], (uint32_t)acc);
-                        acc >>= 32;
-                        nb -= 32u;
-                        ++di;
-                    }
+                    so[pos] = (uint8_t)(s ? lo_b : (two ? hi_b : x));
+                    if (two) so[pos + 1] = (uint8_t)lo_b;
+                    pos += two ? 2u : 1u;
                 }
             }
         }
