@@ -381,6 +381,27 @@ def main_nybble(a, dev, rank, world):
         dec_sample_ms = (time.perf_counter() - t) * 1e3
         ok = bool(torch.equal(ys, xs))
         dec_ms = None
+        # the many-stream throughput path (dc_nyb_decompress_batch, one lane per stream): the
+        # first 256 MiB as independent 4 KiB streams (each the reference's nybble_compress of its
+        # bytes, as the DCNK container holds them), decoded from their concatenation + offsets
+        KB = 4096
+        xb = x[: min(n, 256 << 20)]
+        cont = c.nyb_compress_chunked(xb, True, KB)
+        nch = (xb.numel() + KB - 1) // KB
+        offs = cont[32: 32 + 8 * (nch + 1)].view(torch.int64).clone()
+        pay = cont[32 + 8 * (nch + 1):]
+        yb, _ = c.nyb_decompress_batch(pay, offs, True, out_cap=xb.numel())
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        reps = 5
+        for _ in range(reps):
+            yb, _ = c.nyb_decompress_batch(pay, offs, True, out_cap=xb.numel())
+        torch.cuda.synchronize()
+        bt = (time.perf_counter() - t) / reps
+        ok = ok and bool(torch.equal(yb, xb))
+        dec_batch = {"streams": int(nch), "stream_bytes": KB, "bytes": int(xb.numel()), "ms": round(bt * 1e3, 3),
+                     "GBps": round(xb.numel() / bt / 1e9, 2),
+                     "path": "dc_nyb_decompress_batch: one lane per independent stream (lengths, scan, decode)"}
     else:
         dec_ms = timed(decode, a.profile_steps)
         ok = bool(torch.equal(st["y"], x))
@@ -440,6 +461,7 @@ def main_nybble(a, dev, rank, world):
         res["decode_sample"] = {"bytes": 16 << 20, "ms": round(dec_sample_ms, 2),
                                 "MBps": round((16 << 20) / (dec_sample_ms * 1e-3) / 1e6, 1),
                                 "path": "tokens (parallel transducer) + control words + k_nyb_resolve_c (one wave)"}
+        res["decode_batch"] = dec_batch
     if rank == 0 and world == 1 and not a.no_cpu:
         res["cpu_baseline"] = cpu_baseline_nybble(x, a, modify)
     if rank == 0:

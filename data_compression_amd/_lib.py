@@ -121,6 +121,7 @@ def _declare_core(L):
         "dc_nyb_compress_chunked": ([vp, P, u64, i32, u32, P, u64, C.POINTER(u64)], i32),
         "dc_nyb_chunked_info": ([vp, P, u64, C.POINTER(u64), C.POINTER(i32), C.POINTER(u32)], i32),
         "dc_nyb_decompress_chunked": ([vp, P, u64, P, u64, C.POINTER(u64)], i32),
+        "dc_nyb_decompress_batch": ([vp, P, P, u64, i32, P, u64, P, C.POINTER(u64)], i32),
         "dc_nyb_mtf_summary": ([vp, P, u64, P, P], i32),
         "dc_nyb_body_plan": ([vp, P, u64, i32, P, P], i32),
         "dc_nyb_body_write": ([vp, P, u64, i32, i32, i32, P, C.POINTER(u64), C.POINTER(i32)], i32),

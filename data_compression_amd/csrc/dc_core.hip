@@ -3664,6 +3664,7 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
     __shared__ uint4 s_f[FSM_SUB][4];   // wave totals per chunk
     __shared__ __attribute__((aligned(16))) uint8_t s_out[2 * FSM_TILE + 32];
     __shared__ __attribute__((aligned(4))) uint8_t s_rank[256];
+    __shared__ __attribute__((aligned(4))) uint8_t s_dump[4 * 256];   // a lane's unused byte stores
     const int t = threadIdx.x;
     if (M == M_NYB_ENC && !aux.rk) fsm_rank_table(s_rank);
     const bool nyb_whole = M == M_NYB_ENC && aux.whole;
@@ -3796,18 +3797,24 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
             // Every byte of the tile's output is written exactly once (no zeroed stage, no ORs).
             // (r3's 64-bit accumulator with a dword flush every 2 elements: ~26 VALU per element,
             // the kernel VALU-issue bound at 1.28 ms per GiB)
+            // (no branches: a byte an element does not write goes to this lane's dump slot, so
+            // both stores issue unconditionally, with no exec-mask juggling per element)
             uint8_t *const so = s_out + P;
+            uint8_t *const dump = s_dump + 4 * t;
+            const uint32_t C1 = ~Hx | Sx, C2 = ~Hx & Sx;   // element writes its first / second byte
             uint32_t pos = 0;
 #pragma unroll
             for (int k = 0; k < 16; ++k) {
                 const uint32_t x = W.b(k + 1), prev = W.b(k);
-                const bool h = (Hx >> k) & 1u, s = (Sx >> k) & 1u;
+                const uint32_t hm = 0u - ((Hx >> k) & 1u), sm = 0u - ((Sx >> k) & 1u);   // all-ones masks
                 const uint32_t rq = (k ? rk[k - 1] : rp0) & 7u;
                 const uint32_t pair = 0x88u | (rq << 4) | (rk[k] & 7u);   // the pending hit, then this one
-                const uint32_t b1 = s ? (h ? pair : prev) : x;
-                if (!h || s) so[pos] = (uint8_t)b1;
-                if (!h && s) so[pos + 1] = (uint8_t)x;
-                pos += (h ? 0u : 1u) + (s ? 1u : 0u);
+                // s ? (h ? pair : prev) : x, as bit selects (a ternary became a branch)
+                const uint32_t b1 = (x & ~sm) | (sm & ((pair & hm) | (prev & ~hm)));
+                const uint32_t c1 = (C1 >> k) & 1u, c2 = (C2 >> k) & 1u;
+                *(c1 ? so + pos : dump) = (uint8_t)b1;
+                *(c2 ? so + pos + 1 : dump + 1) = (uint8_t)x;
+                pos += c1 + c2;
             }
             nb = 0;   // (nothing left in the accumulator)
         } else {   // M_NYB_DEC / M_NYB_DBODY: compressed byte x, state s = "at the low nybble"
@@ -3816,6 +3823,7 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
             // each element's 1-2 bytes straight into the stage at their running offset (as the
             // encoder above: no shift-accumulate chain, every output byte written once)
             uint8_t *const so = s_out + P;
+            uint8_t *const dump = s_dump + 4 * t;
             uint32_t pos = 0;
 #pragma unroll
             for (int k = 0; k < 16; ++k) {
@@ -3824,14 +3832,13 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
                 const uint64_t kk = M == M_NYB_DBODY ? j0 + k : j0 + k + 2;
                 const uint32_t h = x >> 4, l = x & 15u;
                 const uint32_t nxt = (kk + 1 < len) ? (W.b(k + 2) >> 4) : 0u;
-                const uint32_t lo_b = (l & 8u) ? (uint32_t)(tblv >> (8u * (l & 7u))) & 255u : ((l & 7u) << 4) + nxt;
+                const uint32_t lm = 0u - ((l >> 3) & 1u);   // a hit in the low nybble (bit selects, no branch)
+                const uint32_t lo_b = ((uint32_t)(tblv >> (8u * (l & 7u))) & 255u & lm) | ((((l & 7u) << 4) + nxt) & ~lm);
                 const uint32_t hi_b = (uint32_t)(tblv >> (8u * (h & 7u))) & 255u;
-                const bool two = !s && (h & 8u);
-                if ((uint32_t)k < kend) {
-                    so[pos] = (uint8_t)(s ? lo_b : (two ? hi_b : x));
-                    if (two) so[pos + 1] = (uint8_t)lo_b;
-                    pos += two ? 2u : 1u;
-                }
+                const bool in = (uint32_t)k < kend, two = in && !s && (h & 8u);
+                *(in ? so + pos : dump) = (uint8_t)(s ? lo_b : (two ? hi_b : x));
+                *(two ? so + pos + 1 : dump + 1) = (uint8_t)lo_b;
+                pos += (in ? 1u : 0u) + (two ? 1u : 0u);
             }
         }
         if (nb) atomicOr(&s_out32[di], (uint32_t)acc);
@@ -4931,6 +4938,54 @@ __global__ __launch_bounds__(256) void k_nyb_chunk_copy(const uint8_t *__restric
 // one lane per chunk: decompress_bytestring (nybble_compression.c:734-817) of the chunk's
 // stream into out + ch*K; a stream that is not a nybble/LITERAL stream of exactly the chunk's
 // length sets *err (bytes >= 0x80 do not round-trip through the reference codec, P8)
+// One lane decodes one whole reference stream (decompress_bytestring, nybble_compression.c:
+// 734-817) of m bytes into exactly `expect` bytes at o; its 16 move-to-front lists are its
+// column of sL (LDS, 8 KiB per 64 lanes). Type dispatch (:744, :799, :806): 0xAF nybbles,
+// ' ' the raw bytes after it, any other type byte (any_type; DCNK chunks are never written so)
+// every byte including the type byte. False: the stream does not decode to `expect` bytes.
+static __device__ bool nyb_lane_decode(const uint8_t *__restrict__ src, uint64_t m, uint64_t expect, int modify,
+                                       bool any_type, uint8_t *__restrict__ o, uint64_t (*sL)[64], int t)
+{
+    if (m == 0) return expect == 0;
+    const uint32_t type = src[0];
+    if (type == ' ') {
+        if (m - 1 != expect) return false;
+        for (uint64_t i = 1; i < m; ++i) o[i - 1] = src[i];
+        return true;
+    }
+    if (type != 0xAF) {
+        if (!any_type || m != expect) return false;
+        for (uint64_t i = 0; i < m; ++i) o[i] = src[i];
+        return true;
+    }
+    if (m < 2) return expect == 0;
+    for (int c = 0; c < 16; ++c) sL[c][t] = mtf_init_word();
+    uint32_t prev = src[1];
+    if (expect == 0) return false;
+    o[0] = (uint8_t)prev;
+    uint64_t q = 1, pos = 2;
+    int offn = 0;
+    while (pos < m) {
+        const uint32_t bb = src[pos];
+        uint32_t nyb, nxt;
+        if (offn == 0) { nyb = bb >> 4; nxt = bb & 15; }
+        else { nyb = bb & 15; nxt = (pos + 1 < m) ? (uint32_t)(src[pos + 1] >> 4) : 0u; }
+        const uint32_t c = (prev >> 3) & 15u;
+        uint64_t L = sL[c][t];
+        uint32_t v;
+        int used;
+        if (nyb & 8) { v = (uint32_t)(L >> (8 * (nyb & 7))) & 255u; used = 1; }
+        else { v = ((nyb & 7) << 4) + nxt; used = 2; }
+        if (modify) { uint32_t cnt = 8; (void)mtf_touch64(L, cnt, v); sL[c][t] = L; }
+        if (q >= expect) return false;
+        o[q++] = (uint8_t)v;
+        prev = v;
+        offn += used;
+        if (offn >= 2) { ++pos; offn -= 2; }
+    }
+    return q == expect;
+}
+
 __global__ __launch_bounds__(64) void k_nyb_chunk_dec(const uint8_t *__restrict__ payload,
                                                       const uint64_t *__restrict__ off, uint64_t total, uint64_t n,
                                                       uint32_t K, uint64_t nchunks, int modify,
@@ -4942,41 +4997,57 @@ __global__ __launch_bounds__(64) void k_nyb_chunk_dec(const uint8_t *__restrict_
     if (ch >= nchunks) return;
     const uint64_t a = off[ch], b = off[ch + 1];
     const uint64_t expect = (n - ch * K < K) ? n - ch * K : K;
-    uint8_t *o = out + ch * K;
     if (b < a || b > total || b - a < 1) { *err = 1; return; }
-    const uint8_t *src = payload + a;
+    if (!nyb_lane_decode(payload + a, b - a, expect, modify, false, out + ch * K, s_L, t)) *err = 1;
+}
+
+// dc_nyb_decompress_batch: the output length of each stream (one lane per stream): the token
+// count of a 0xAF stream plus its first byte (the token structure needs no lists: a nybble with
+// bit 3 set is a 1-nybble hit, any other starts a 2-nybble literal), the bytes after a ' ', or
+// every byte under another type byte; an invalid range (end before start) counts 0 and flags err
+__global__ __launch_bounds__(64) void k_nyb_batch_len(const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_off,
+                                                      uint64_t count, uint64_t *__restrict__ len, uint64_t *__restrict__ err)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * 64 + threadIdx.x;
+    if (i >= count) return;
+    const uint64_t a = in_off[i], b = in_off[i + 1];
+    if (b < a) { len[i] = 0; *err = 1; return; }
     const uint64_t m = b - a;
-    const uint32_t type = src[0];
-    if (type == ' ') {
-        if (m - 1 != expect) { *err = 1; return; }
-        for (uint64_t i = 1; i < m; ++i) o[i - 1] = src[i];
-        return;
+    const uint8_t *src = in + a;
+    uint64_t q = 0;
+    if (m > 0) {
+        const uint32_t type = src[0];
+        if (type == 0xAF) {
+            if (m >= 2) {
+                q = 1;
+                uint64_t pos = 2;
+                int offn = 0;
+                while (pos < m) {
+                    const uint32_t bb = src[pos];
+                    const uint32_t nyb = offn == 0 ? bb >> 4 : bb & 15;
+                    offn += (nyb & 8) ? 1 : 2;
+                    ++q;
+                    if (offn >= 2) { ++pos; offn -= 2; }
+                }
+            }
+        } else {
+            q = type == ' ' ? m - 1 : m;
+        }
     }
-    if (type != 0xAF || m < 2) { *err = 1; return; }
-    for (int c = 0; c < 16; ++c) s_L[c][t] = mtf_init_word();
-    uint32_t prev = src[1];
-    o[0] = (uint8_t)prev;
-    uint64_t q = 1, pos = 2;
-    int offn = 0;
-    while (pos < m) {
-        const uint32_t bb = src[pos];
-        uint32_t nyb, nxt;
-        if (offn == 0) { nyb = bb >> 4; nxt = bb & 15; }
-        else { nyb = bb & 15; nxt = (pos + 1 < m) ? (uint32_t)(src[pos + 1] >> 4) : 0u; }
-        const uint32_t c = (prev >> 3) & 15u;
-        uint64_t L = s_L[c][t];
-        uint32_t v;
-        int used;
-        if (nyb & 8) { v = (uint32_t)(L >> (8 * (nyb & 7))) & 255u; used = 1; }
-        else { v = ((nyb & 7) << 4) + nxt; used = 2; }
-        if (modify) { uint32_t cnt = 8; (void)mtf_touch64(L, cnt, v); s_L[c][t] = L; }
-        if (q >= expect) { *err = 1; return; }
-        o[q++] = (uint8_t)v;
-        prev = v;
-        offn += used;
-        if (offn >= 2) { ++pos; offn -= 2; }
-    }
-    if (q != expect) *err = 1;
+    len[i] = q;
+}
+
+__global__ __launch_bounds__(64) void k_nyb_batch_dec(const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_off,
+                                                      const uint64_t *__restrict__ out_off, uint64_t count, int modify,
+                                                      uint8_t *__restrict__ out, uint64_t *__restrict__ err)
+{
+    __shared__ uint64_t s_L[16][64];
+    const int t = threadIdx.x;
+    const uint64_t i = (uint64_t)blockIdx.x * 64 + t;
+    if (i >= count) return;
+    const uint64_t a = in_off[i], b = in_off[i + 1];
+    if (b < a) return;   // (flagged by k_nyb_batch_len)
+    if (!nyb_lane_decode(in + a, b - a, out_off[i + 1] - out_off[i], modify, true, out + out_off[i], s_L, t)) *err = 1;
 }
 
 // ------------------------------------------------------------------------------------
@@ -6031,6 +6102,36 @@ int dc_nyb_decompress_chunked(dc_ctx *c, const uint8_t *d_in, uint64_t m, uint8_
     HIPCHK(hipMemsetAsync(err, 0, 8, c->stream));
     LAUNCH(c, "nyb_chunk_dec", k_nyb_chunk_dec, (nch + 63) / 64, 64, d_in + head,
            (const uint64_t *)(d_in + NYBK_HEAD), m - head, n, K, nch, modify, d_out, err);
+    HIPCHK(hipMemcpyAsync(c->h_pinned, err, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return c->h_pinned[0] ? DC_E_STREAM : DC_OK;
+}
+
+int dc_nyb_decompress_batch(dc_ctx *c, const uint8_t *d_in, const uint64_t *d_in_off, uint64_t count, int modify,
+                            uint8_t *d_out, uint64_t out_cap, uint64_t *d_out_off, uint64_t *h_total)
+{
+    if (!c || !d_in_off || !d_out_off || !h_total || (count && !d_in)) return DC_E_ARG;
+    *h_total = 0;
+    if (count == 0) {
+        HIPCHK(hipMemsetAsync(d_out_off, 0, sizeof(uint64_t), c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        return DC_OK;
+    }
+    if (ensure((void **)&c->d_klens, &c->klens_cap, count * sizeof(uint64_t))) return DC_E_HIP;
+    uint64_t *err = c->d_meta + 8;
+    HIPCHK(hipMemsetAsync(err, 0, 8, c->stream));
+    const uint64_t grid = (count + 63) / 64;
+    LAUNCH(c, "nyb_batch_len", k_nyb_batch_len, grid, 64, d_in, d_in_off, count, c->d_klens, err);
+    LAUNCH(c, "nyb_batch_scan", k_scan_u64, 1, 1024, (const uint64_t *)c->d_klens, count, d_out_off);
+    HIPCHK(hipMemcpyAsync(c->h_pinned, d_out_off + count, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(c->h_pinned + 1, err, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    const uint64_t total = c->h_pinned[0];
+    if (c->h_pinned[1]) return DC_E_ARG;
+    *h_total = total;
+    if (total > out_cap || (total && !d_out)) return DC_E_CAPACITY;
+    LAUNCH(c, "nyb_batch_dec", k_nyb_batch_dec, grid, 64, d_in, d_in_off, (const uint64_t *)d_out_off, count, modify,
+           d_out, err);
     HIPCHK(hipMemcpyAsync(c->h_pinned, err, 8, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return c->h_pinned[0] ? DC_E_STREAM : DC_OK;

@@ -330,6 +330,20 @@ class Codec:
                                                                             _ptr(out), n.value, C.byref(got)))
         return out[: got.value]
 
+    def nyb_decompress_batch(self, data, offsets, modify: bool, out_cap: int | None = None):
+        """dc_nyb_decompress_batch: streams data[offsets[i]:offsets[i+1]] (device uint8 data,
+        device int64 offsets, count + 1 entries) decoded one lane per stream. Returns
+        (output bytes, output offsets), both device tensors."""
+        count = offsets.numel() - 1
+        out_off = self._t(count + 1, torch.int64)
+        cap = out_cap if out_cap is not None else 2 * data.numel() + 16
+        out = self._t(max(cap, 1))
+        tot = C.c_uint64(0)
+        check("dc_nyb_decompress_batch", self.L.dc_nyb_decompress_batch(self.ctx, _ptr(data), _ptr(offsets), count,
+                                                                        int(modify), _ptr(out), cap, _ptr(out_off),
+                                                                        C.byref(tot)))
+        return out[: tot.value], out_off
+
     def nyb_mtf_summary(self, y):
         """Move-to-front lists after elements y[1..] from empty lists: (lists[16][8], cnt[16])."""
         lists = np.zeros(128, np.uint8)

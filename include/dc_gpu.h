@@ -279,6 +279,17 @@ int dc_nyb_compress_chunked(dc_ctx *ctx, const uint8_t *d_in, uint64_t n, int mo
 int dc_nyb_chunked_info(dc_ctx *ctx, const uint8_t *d_in, uint64_t m, uint64_t *h_n, int *h_modify, uint32_t *h_K);
 int dc_nyb_decompress_chunked(dc_ctx *ctx, const uint8_t *d_in, uint64_t m, uint8_t *d_out, uint64_t out_cap,
                               uint64_t *h_out_len);
+/* Batched decode of many independent reference streams (the throughput path for many
+ * separate nybble_decompress / decompress_bytestring calls, beside the DCNK container): stream i
+ * = d_in[d_in_off[i] .. d_in_off[i+1]) (device u64 offsets, count+1 entries), each a whole
+ * stream as compress_bytestring writes it, decoded as decompress_bytestring(modify) does
+ * (nybble_compression.c:734-817; any type byte but 0xAF / ' ' copies the stream). One lane per
+ * stream (a single stream's adaptive decode is sequential). d_out_off (device, count+1) receives
+ * the output offsets, *h_total the total; DC_E_CAPACITY when it exceeds out_cap (nothing
+ * decoded), DC_E_STREAM when a 0xAF stream's walk leaves its bytes inconsistent, DC_E_ARG for an
+ * offset range that ends before it starts. Synchronising. */
+int dc_nyb_decompress_batch(dc_ctx *ctx, const uint8_t *d_in, const uint64_t *d_in_off, uint64_t count, int modify,
+                            uint8_t *d_out, uint64_t out_cap, uint64_t *d_out_off, uint64_t *h_total);
 /* Shard bodies (data_compression_amd/dist.py ShardedNybble). A shard buffer is
  * d_in[0 .. len): d_in[0] is the context byte (the stream's first byte on the first shard, the
  * previous shard's last byte after it) and the shard's elements are bytes 1 .. len-1, as in

@@ -902,6 +902,35 @@ def test_nybble_chunked_container(torch_cuda, codec, modify):
     assert merge_chunked(per) == whole
 
 
+@pytest.mark.parametrize("modify", [True, False])
+def test_nybble_batch_decode_vs_oracle(torch_cuda, codec, modify):
+    """dc_nyb_decompress_batch (the many-stream throughput path beside DCNK):
+    independent reference streams of mixed sizes, including empty ones, LITERAL-fallback
+    streams (type ' '), streams of other type bytes (copied whole, :806), arbitrary nybble
+    streams and one of every size 1..40, each decoded as the reference restatement does."""
+    torch = torch_cuda
+    from data_compression_amd import synth
+    rng = np.random.default_rng(41)
+    streams = [b""]
+    for n in list(range(1, 41)) + [100, 4095, 4096, 4097, 65_537]:
+        streams.append(orc.nybble_compress(synth.english_like(n, seed=n).tobytes(), modify))
+    streams.append(orc.nybble_compress(bytes(rng.integers(1, 128, size=3000, dtype=np.uint8)), modify))  # often ' '
+    streams.append(bytes([0x41]) + b"raw bytes under another type")
+    streams.append(bytes([0xAF]) + rng.integers(0, 256, size=777, dtype=np.uint8).tobytes())
+    streams.append(bytes([0xAF]))
+    for _ in range(300):
+        n = int(rng.integers(1, 2000))
+        streams.append(orc.nybble_compress(synth.english_like(n, seed=int(rng.integers(1 << 30))).tobytes(), modify))
+    off = np.zeros(len(streams) + 1, np.int64)
+    off[1:] = np.cumsum([len(x) for x in streams])
+    data = np.frombuffer(b"".join(streams), np.uint8).copy()
+    out, out_off = codec.nyb_decompress_batch(torch.from_numpy(data).cuda(), torch.from_numpy(off).cuda(), modify)
+    o, oo = out.cpu().numpy().tobytes(), out_off.cpu().numpy()
+    for i, st in enumerate(streams):
+        want = b"" if st == b"" else orc.nybble_decompress(st, modify) if st[0] != 0xAF or len(st) >= 2 else b""
+        assert o[oo[i]: oo[i + 1]] == want, (i, len(st))
+
+
 def _thread_collectives(sh, tr, r, world, torch):
     """ShardedHuffman collectives over thread ranks (all on one GPU)."""
     def all_reduce(t):
