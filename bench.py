@@ -232,7 +232,9 @@ def main():
     sync_bytes = ngroups * 8 + nchunks * 2
     alg = {"hist_blocks": nh, "huff_pack": nh + payload + sync_bytes, "huff_decode": payload + sync_bytes + nh}
     if a.frontend:   # SURVEY §8(d), as for nybble: the front-end moves N + its output each way
-        alg.update({"small_write": n + nh, "small_dec_write": nh + n, "small_body_tiles": n, "small_dec_tiles": nh})
+        alg.update({"small_write": n + nh, "small_dec_write": nh + n, "small_body_tiles": n, "small_dec_tiles": nh,
+                    # the fused encode (world 1): the input read twice, the payload and index written
+                    "fe_hist_blocks": n, "fe_pack": n + payload + sync_bytes})
     kernels = {}
     for name, v in per.items():
         m = float(np.mean(v))

@@ -29,7 +29,7 @@ i32 = C.c_int
 
 class DcError(RuntimeError):
     NAMES = {-1: "DC_E_ARG", -2: "DC_E_HIP", -3: "DC_E_CODE_TOO_LONG", -4: "DC_E_NOCODE",
-             -5: "DC_E_STATE", -6: "DC_E_CAPACITY", -7: "DC_E_STREAM"}
+             -5: "DC_E_STATE", -6: "DC_E_CAPACITY", -7: "DC_E_STREAM", -8: "DC_E_FALLBACK"}
 
     def __init__(self, fn, rc):
         super().__init__(f"{fn} failed: {self.NAMES.get(rc, rc)}")
@@ -92,6 +92,10 @@ def _declare_core(L):
         "dc_huff_plan": ([vp, P, P], i32),
         "dc_huff_encode_plan": ([vp, P, u64, i32, i32, P, P, P], i32),
         "dc_huff_table_plan": ([vp, P, i32, i32, P, P], i32),
+        "dc_small_huff_plan": ([vp, P, u64, i32, i32, P, P, P], i32),
+        "dc_small_huff_pack_async": ([vp, P, u64, P, u64, P, u64, P, P, u32], i32),
+        "dc_small_huff_symbols": ([vp, C.POINTER(u64)], i32),
+        "dc_small_huff_decode": ([vp, P, u64, u64, P, P, u32, u64, P, P, P, C.POINTER(u64)], i32),
         "dc_copy_probe": ([vp, P, P, u64], i32),
         "dc_huff_pack": ([vp, P, u64, P, u64, P, u64, P, P, u32], i32),
         "dc_huff_sync_chunks": ([u64, u32], u64),

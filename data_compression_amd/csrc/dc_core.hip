@@ -72,6 +72,83 @@ static __device__ __forceinline__ uint32_t wg_scan_excl_u32(uint32_t v, uint32_t
     return base + x - v;
 }
 
+// inclusive wave64 prefix sum in DPP (VALU only: __shfl_up is ds_bpermute, i.e. an LDS
+// instruction queued behind the table reads): row_shr 1/2/4/8 within each row of
+// 16 lanes, then row_bcast:15 and row_bcast:31 across rows (GFX9 DPP)
+static __device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x)
+{
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);   // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);   // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);   // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);   // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);   // row_bcast:15
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);   // row_bcast:31
+    return x;
+}
+
+// SWAR byte tests on a dword (bit 7 of each byte = the test; the kernels are VALU-issue
+// bound, and one 32-bit op here tests 4 bytes: 31 VALU per byte per element rule before)
+static __device__ __forceinline__ uint32_t swar_eq(uint32_t x, uint32_t c4)   // byte == c
+{
+    const uint32_t v = x ^ c4;
+    return ~(((v & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | v) & 0x80808080u;
+}
+static __device__ __forceinline__ uint32_t swar_lower(uint32_t x)   // 'a' <= byte <= 'z'
+{
+    const uint32_t t = x & 0x7F7F7F7Fu;
+    return (t + 0x1F1F1F1Fu) & ~(t + 0x05050505u) & ~x & 0x80808080u;
+}
+
+// ------------------------------------------------------------------------------------
+// C5 front-end fusion (small_compression.c:582-665, then n-ary Huffman of its output M).
+// M = [8, x[0]] then, for g >= 1, x[g], except that ' ' + lowercase letter at g, g + 1 (a pair
+// START at g, g <= n - 2) becomes the one byte 0x80 + letter. Pairs never overlap (the second
+// byte is a letter, never ' '), so the symbol stream is a per-position map of the input with
+// one byte of context each side. The fused kernels read the input x itself and never write
+// M: a pair's symbol is counted and coded at its SECOND position (as x[g] | 0x80: the letter
+// is < 0x80) and the start position carries no symbol (in the pack: a byte value z with no
+// code, 0 bits). The M order is unchanged: nothing lies between a pair's two positions.
+// ------------------------------------------------------------------------------------
+// The shifts run with every lane active: a DPP read of a lane that EXEC disables returns 0,
+// and a select such as `lane == 0 ? a : dpp(x)` was compiled as a branch that ran the DPP
+// with lane 0 off, so lane 1 read 0 (the opaque asm keeps the shift out of any branch).
+static __device__ __forceinline__ uint32_t dpp_wave_shr1(uint32_t x)   // lane l <- lane l - 1 (lane 0: 0)
+{
+    uint32_t r = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x138, 0xf, 0xf, false);
+    asm volatile("" : "+v"(r));
+    return r;
+}
+static __device__ __forceinline__ uint32_t dpp_wave_shl1(uint32_t x)   // lane l <- lane l + 1 (lane 63: 0)
+{
+    uint32_t r = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x130, 0xf, 0xf, false);
+    asm volatile("" : "+v"(r));
+    return r;
+}
+// The dword a lane of the fused kernels loads beside its 16 bytes at p: lane 0 the one
+// holding x[p - 1], lane 63 the one at p + 16 (the lanes between take the byte from their
+// neighbours by DPP wave shifts); others re-read their own first dword (in cache; one
+// unconditional load keeps the compiler's load waits counted)
+static __device__ __forceinline__ uint64_t fe_edge_addr(uint64_t p, int lane, uint64_t n)
+{
+    return lane == 0 ? (p >= 4 ? p - 4 : p) : lane == 63 ? (p + 16 < n ? p + 16 : p) : p;
+}
+// pair starts among the 16 bytes w4 (q = the byte after them, 0 past the input): 0x80 in
+// byte j of st[k] = a START at byte 4k + j
+static __device__ __forceinline__ void fe_pair_starts(const uint32_t (&w4)[4], uint32_t q, uint32_t (&st)[4])
+{
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t nx = __builtin_amdgcn_alignbyte(k < 3 ? w4[k + 1] : q, w4[k], 1u);   // the next bytes
+        st[k] = swar_eq(w4[k], 0x20202020u) & swar_lower(nx);
+    }
+}
+// a start at p - 1 (its byte pb, x[p] = the low byte of w0), which makes x[p] a pair's second
+static __device__ __forceinline__ uint32_t fe_start_before(uint32_t pb, uint32_t w0, uint64_t p)
+{
+    const uint32_t x = w0 & 255u;
+    return (p >= 16 && pb == 0x20u && x >= 'a' && x <= 'z') ? 0x80u : 0u;
+}
+
 // ------------------------------------------------------------------------------------
 // (H1) byte histogram per 32 KiB block.  n_ary_huffman.c:461-493
 // LDS layout: dword (bin*64 + lane) holds four 8-bit counters, one per wave of the
@@ -98,7 +175,11 @@ struct HistFuse {
     int *perr, *perr_next; // plan error slot of this call, and the next one (cleared)
 };
 
-template <int PF>   // full blocks whose loads are in flight ahead of the one being counted
+// PF: full blocks whose loads are in flight ahead of the one being counted. FE (the C5 fused
+// front-end): the histogram is that of the front-end output M, per 32 KiB block of the INPUT:
+// a pair's symbol 0x80 + letter counts at its second position (letter | 0x80), each block's
+// ' ' count loses its pair starts, and block 0 gains the type byte 8 (M[0]).
+template <int PF, bool FE = false>
 __global__ __launch_bounds__(256) void k_hist_blocks(const uint8_t *__restrict__ in, uint64_t n,
                                                      uint64_t nblocks, uint16_t *__restrict__ bh,
                                                      uint64_t *__restrict__ hist, uint64_t *__restrict__ hacc,
@@ -107,6 +188,7 @@ __global__ __launch_bounds__(256) void k_hist_blocks(const uint8_t *__restrict__
 {
     __shared__ __attribute__((aligned(16))) uint32_t cnt[256 * 64];
     __shared__ uint32_t s_last;
+    __shared__ uint32_t s_ps[4];
     __shared__ uint64_t s_h[256];
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const uint32_t inc = 1u << (8 * wv);
@@ -122,34 +204,58 @@ __global__ __launch_bounds__(256) void k_hist_blocks(const uint8_t *__restrict__
     // software pipeline: the next PF full blocks' loads are in flight while this block counts
     // (the LDS counters allow 2 workgroups per CU, so registers up to 256 cost no occupancy)
     uint4 v[PF][8];
+    uint32_t ve[FE ? PF : 1][8];   // FE: the dwords beside each 16 B (fe_edge_addr)
     uint64_t b = blockIdx.x;
+    auto issue = [&](int f, uint64_t bf) {
+        const uint4 *p = reinterpret_cast<const uint4 *>(in + bf * (uint64_t)DC_BLOCK_BYTES) + t;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[f][k] = LD_HIST(p + k * 256);
+        if (FE) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const uint64_t q = bf * (uint64_t)DC_BLOCK_BYTES + (uint64_t)k * 4096 + (uint64_t)t * 16;
+                ve[FE ? f : 0][k] = *reinterpret_cast<const uint32_t *>(in + fe_edge_addr(q, lane, n));
+            }
+        }
+    };
 #pragma unroll
     for (int f = 0; f < PF; ++f) {
         const uint64_t bf = b + (uint64_t)f * gridDim.x;
-        if (bf < nfull) {
-            const uint4 *p = reinterpret_cast<const uint4 *>(in + bf * (uint64_t)DC_BLOCK_BYTES) + t;
-#pragma unroll
-            for (int k = 0; k < 8; ++k) v[f][k] = LD_HIST(p + k * 256);
-        }
+        if (bf < nfull) issue(f, bf);
     }
     for (; b < nblocks; b += gridDim.x) {
+        uint32_t pc = 0;   // FE: pair starts this thread saw in the block
         if (b < nfull) {
             uint4 cur[8];
+            uint32_t ce[8];
 #pragma unroll
-            for (int k = 0; k < 8; ++k) cur[k] = v[0][k];
+            for (int k = 0; k < 8; ++k) { cur[k] = v[0][k]; ce[k] = FE ? ve[0][k] : 0u; }
 #pragma unroll
             for (int f = 0; f + 1 < PF; ++f)
 #pragma unroll
-                for (int k = 0; k < 8; ++k) v[f][k] = v[f + 1][k];
+                for (int k = 0; k < 8; ++k) {
+                    v[f][k] = v[f + 1][k];
+                    if (FE) ve[FE ? f : 0][k] = ve[FE ? f + 1 : 0][k];
+                }
             const uint64_t nb = b + (uint64_t)PF * gridDim.x;
-            if (nb < nfull) {
-                const uint4 *p = reinterpret_cast<const uint4 *>(in + nb * (uint64_t)DC_BLOCK_BYTES) + t;
-#pragma unroll
-                for (int k = 0; k < 8; ++k) v[PF - 1][k] = LD_HIST(p + k * 256);
-            }
+            if (nb < nfull) issue(PF - 1, nb);
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
-                const uint32_t w4[4] = {cur[k].x, cur[k].y, cur[k].z, cur[k].w};
+                uint32_t w4[4] = {cur[k].x, cur[k].y, cur[k].z, cur[k].w};
+                if (FE) {   // pair seconds -> letter | 0x80; count the starts
+                    const uint64_t p = b * (uint64_t)DC_BLOCK_BYTES + (uint64_t)k * 4096 + (uint64_t)t * 16;
+                    const uint32_t pb = lane == 0 ? ce[k] >> 24 : dpp_wave_shr1(w4[3]) >> 24;
+                    const uint32_t qb = lane == 63 ? (p + 16 < n ? ce[k] & 255u : 0u) : dpp_wave_shl1(w4[0]) & 255u;
+                    uint32_t st[4];
+                    fe_pair_starts(w4, qb, st);
+                    if (p == 0) st[0] &= ~0x80u;   // position 0 never starts a pair
+                    const uint32_t s0 = fe_start_before(pb, w4[0], p);
+                    w4[0] |= (st[0] << 8) | s0;
+#pragma unroll
+                    for (int q = 1; q < 4; ++q) w4[q] |= (st[q] << 8) | (st[q - 1] >> 24);
+                    pc += (uint32_t)__popc(st[0]) + (uint32_t)__popc(st[1]) + (uint32_t)__popc(st[2]) +
+                          (uint32_t)__popc(st[3]);
+                }
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
 #pragma unroll
@@ -163,7 +269,20 @@ __global__ __launch_bounds__(256) void k_hist_blocks(const uint8_t *__restrict__
             }
         } else {
             const uint64_t base = b * (uint64_t)DC_BLOCK_BYTES;
-            for (uint64_t i = base + t; i < n; i += 256) atomicAdd(&cnt[in[i] * 64 + lane], inc);
+            for (uint64_t i = base + t; i < n; i += 256) {
+                uint32_t x = in[i];
+                if (FE) {
+                    const bool sec = i >= 2 && in[i - 1] == 0x20 && x >= 'a' && x <= 'z';
+                    const uint32_t nx = i + 1 < n ? in[i + 1] : 0u;
+                    pc += (i >= 1 && x == 0x20u && nx >= 'a' && nx <= 'z') ? 1u : 0u;
+                    x |= sec ? 0x80u : 0u;
+                }
+                atomicAdd(&cnt[x * 64 + lane], inc);
+            }
+        }
+        if (FE) {
+            const uint32_t ws = (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_incl(pc), 63);
+            if (lane == 0) s_ps[wv] = ws;
         }
         __syncthreads();
         // bin t: its 64 lane columns (16-B reads, rotated so a wave's reads spread over all
@@ -186,6 +305,10 @@ __global__ __launch_bounds__(256) void k_hist_blocks(const uint8_t *__restrict__
                 acc = __builtin_amdgcn_udot4(diff, 0x01010101u, acc, false);
                 prevc[4 * k + q] = x;
             }
+        }
+        if (FE) {   // the block's pair starts carry no symbol; block 0 holds the type byte 8
+            if (t == 0x20) acc -= s_ps[0] + s_ps[1] + s_ps[2] + s_ps[3];
+            if (t == 8 && b == 0) acc += 1u;
         }
         bh[b * 256 + t] = (uint16_t)acc;
         total += acc;
@@ -243,20 +366,6 @@ __global__ __launch_bounds__(256) void k_hist_blocks(const uint8_t *__restrict__
 //     leaf for n = 2.
 //   * canonical values (:1540-1568) with the reference's index-M quirks (:1336, :1421).
 // ------------------------------------------------------------------------------------
-// inclusive wave64 prefix sum in DPP (VALU only: __shfl_up is ds_bpermute, i.e. an LDS
-// instruction queued behind the table reads): row_shr 1/2/4/8 within each row of
-// 16 lanes, then row_bcast:15 and row_bcast:31 across rows (GFX9 DPP)
-static __device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x)
-{
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);   // row_shr:1
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);   // row_shr:2
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);   // row_shr:4
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);   // row_shr:8
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);   // row_bcast:15
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);   // row_bcast:31
-    return x;
-}
-
 #ifdef DC_DIAG
 __device__ unsigned long long g_tbldiag[16];
 extern "C" int dc_diag_tbl_read(void *h)
@@ -999,12 +1108,16 @@ __global__ __launch_bounds__(1024) void k_block_scan(uint64_t *__restrict__ bits
 // workgroup totals before it and writes its blocks' absolute offsets.
 #define PLAN_WG_BLOCKS 64
 #define PLAN_MAX_WG 16384   /* workgroup bases in LDS (128 KiB): streams up to 32 GiB per call */
+// With lcnt set (the C5 fused front-end, whose blocks hold a varying number of symbols) it
+// also scans the symbols per block (the sum of its histogram) into lcnt / wgcnt.
 __global__ __launch_bounds__(256) void k_block_local(const uint16_t *__restrict__ bh, uint64_t nblocks,
                                                      const dc_dtable *__restrict__ T, uint32_t *__restrict__ local,
-                                                     uint32_t *__restrict__ wgtot, int *__restrict__ err)
+                                                     uint32_t *__restrict__ wgtot, int *__restrict__ err,
+                                                     uint32_t *__restrict__ lcnt, uint32_t *__restrict__ wgcnt)
 {
     __shared__ uint32_t s_nb[256];
     __shared__ uint32_t s_bits[PLAN_WG_BLOCKS];
+    __shared__ uint32_t s_syms[PLAN_WG_BLOCKS];
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     s_nb[t] = T->nbits[t];
     __syncthreads();
@@ -1021,7 +1134,7 @@ __global__ __launch_bounds__(256) void k_block_local(const uint16_t *__restrict_
     for (int k = 0; k < PLAN_WG_BLOCKS / 4; ++k) {
         const int j = wv * (PLAN_WG_BLOCKS / 4) + k;
         const uint64_t b = b0 + j;
-        uint32_t acc = 0;
+        uint32_t acc = 0, syms = 0;
         if (b < nblocks) {
             const uint2 h = hv[k];
             const uint32_t c[4] = {h.x & 0xFFFFu, h.x >> 16, h.y & 0xFFFFu, h.y >> 16};
@@ -1029,11 +1142,16 @@ __global__ __launch_bounds__(256) void k_block_local(const uint16_t *__restrict_
             for (int q = 0; q < 4; ++q) {
                 const uint32_t nb = s_nb[lane * 4 + q];
                 acc += c[q] * nb;
+                syms += c[q];
                 missing |= (c[q] != 0 && nb == 0);
             }
         }
         acc = (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_incl(acc), 63);   // <= 2^20 per block
         if (lane == 0) s_bits[j] = acc;
+        if (lcnt) {
+            syms = (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_incl(syms), 63);
+            if (lane == 0) s_syms[j] = syms;
+        }
     }
     if (__any(missing) && lane == 0) atomicOr(err, 1);
     __syncthreads();
@@ -1042,6 +1160,11 @@ __global__ __launch_bounds__(256) void k_block_local(const uint16_t *__restrict_
         const uint32_t incl = wave_scan_incl(v);   // <= 2^26 per workgroup
         if (b0 + lane < nblocks) local[b0 + lane] = incl - v;
         if (lane == 63) wgtot[blockIdx.x] = incl;
+    } else if (wv == 1 && lcnt) {
+        const uint32_t v = s_syms[lane];
+        const uint32_t incl = wave_scan_incl(v);   // <= 2^21 per workgroup
+        if (b0 + lane < nblocks) lcnt[b0 + lane] = incl - v;
+        if (lane == 63) wgcnt[blockIdx.x] = incl;
     }
 }
 
@@ -1056,29 +1179,62 @@ __global__ __launch_bounds__(256) void k_block_final_wide(const uint32_t *__rest
                                                           uint32_t nwg, uint64_t *__restrict__ off,
                                                           uint64_t *__restrict__ d_total, int *__restrict__ err_next,
                                                           uint64_t bit_base, const uint64_t *__restrict__ d_base,
-                                                          uint32_t *__restrict__ words, uint64_t words_cap)
+                                                          uint32_t *__restrict__ words, uint64_t words_cap,
+                                                          const uint32_t *__restrict__ lcnt,
+                                                          const uint32_t *__restrict__ wgcnt, uint64_t *__restrict__ msym,
+                                                          uint32_t *__restrict__ sl32, uint32_t slog)
 {
-    __shared__ uint64_t s_w[4];
+    // With lcnt set (C5 fused front-end): msym[b] = the index of block b's first symbol
+    // (msym[nblocks] = all symbols), and the sync-length dword holding the chunk that spans each
+    // block boundary (the last chunk begun before block b, b = 1..nblocks) is zeroed: k_fe_pack
+    // adds the two blocks' parts of it, and of its dword neighbour, atomically.
+    __shared__ uint64_t s_w[4], s_c[4];
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const uint32_t g = blockIdx.x;
     if (g == 0 && t < 4) err_next[t] = 0;   // the next plan's error slot
     const bool last = g + 1 == nwg;
     const uint32_t lim = last ? nwg : g;   // the last workgroup sums everything (the total)
-    uint64_t before = 0, all = 0;
+    uint64_t before = 0, all = 0, cbefore = 0, call = 0;
     for (uint32_t i = t; i < lim; i += 256) {
         const uint64_t v = wgtot[i];
         all += v;
         before += i < g ? v : 0ull;
+        if (lcnt) {
+            const uint64_t cv = wgcnt[i];
+            call += cv;
+            cbefore += i < g ? cv : 0ull;
+        }
     }
 #pragma unroll
     for (int d = 32; d > 0; d >>= 1) {
         before += __shfl_xor(before, d, 64);
         all += __shfl_xor(all, d, 64);
+        if (lcnt) {
+            cbefore += __shfl_xor(cbefore, d, 64);
+            call += __shfl_xor(call, d, 64);
+        }
     }
-    if (lane == 0) s_w[wv] = before;
+    if (lane == 0) { s_w[wv] = before; s_c[wv] = cbefore; }
     __syncthreads();
     const uint64_t base = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+    const uint64_t cbase = s_c[0] + s_c[1] + s_c[2] + s_c[3];
     __syncthreads();
+    if (lcnt) {
+        if (lane == 0) s_c[wv] = call;
+        __syncthreads();
+        const uint64_t ctot = s_c[0] + s_c[1] + s_c[2] + s_c[3];
+        if (t < PLAN_WG_BLOCKS) {
+            const uint64_t b = (uint64_t)g * PLAN_WG_BLOCKS + t;
+            if (b < nblocks) {
+                const uint64_t m = cbase + lcnt[b];
+                msym[b] = m;
+                if (b > 0) sl32[((m - 1) >> slog) >> 1] = 0u;
+            }
+        } else if (t == PLAN_WG_BLOCKS && last) {
+            msym[nblocks] = ctot;
+            sl32[((ctot - 1) >> slog) >> 1] = 0u;
+        }
+    }
     if (last) {
         if (lane == 0) s_w[wv] = all;
         __syncthreads();
@@ -1502,6 +1658,305 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
         for (uint32_t i = 4u * t; i < PACK_BLK_WORDS + 4; i += 1024u)
             *reinterpret_cast<uint4 *>(&s_stage[i]) = make_uint4(0u, 0u, 0u, 0u);
         __syncthreads();
+    }
+}
+
+// C5 fused front-end pack: codes the front-end output M of `in` (see the front-end fusion
+// block above k_hist_blocks) without M ever being written. The blocks are k_huff_pack's: 32 KiB
+// of the INPUT, lane t of wave w coding piece k = input bytes [k*4096 + 16t, +16), whose
+// symbols are the bytes y: x, or letter | 0x80 at a pair's second position, or z (a byte value
+// without a code: 0 bits) at a pair's start and past the input. Block b's bit offset comes
+// from the plan over the FE histograms, its first symbol index msym[b] from the same plan.
+// The sync index (chunks of S symbols of M) is k_huff_pack's format, but chunk starts no longer
+// sit at piece starts: a lane whose piece holds the symbol of index = 0 mod S (at most one:
+// S >= 16) records that symbol's bit offset (bits of the piece before it, tallied in pass B)
+// in a list beside the stage; after pass B the block writes each chunk's length as the
+// difference of consecutive starts. The chunks spanning a block boundary get their two parts
+// by atomic adds into the u32 holding their u16 (zeroed by the plan), and so does the other
+// u16 of that u32. Fallbacks (reported in the plan slot's err[1], nothing written): LITERAL
+// output (M >= n bytes), no free byte value for z, a block whose bits exceed the stage.
+__global__ __launch_bounds__(256) void k_fe_pack(const uint8_t *__restrict__ in, uint64_t n,
+                                                 const dc_dtable *__restrict__ T,
+                                                 const uint64_t *__restrict__ block_off,
+                                                 const uint64_t *__restrict__ msym, uint64_t bit_base,
+                                                 uint32_t *__restrict__ out, uint64_t *__restrict__ sync_base,
+                                                 uint16_t *__restrict__ sync_len, uint32_t sync_syms,
+                                                 uint64_t nblocks, uint64_t words_cap, int *__restrict__ err,
+                                                 int build_dec)
+{
+    __shared__ uint2 s_tab[256];
+    __shared__ uint8_t s_nb8[256];
+    __shared__ __attribute__((aligned(16))) uint32_t s_stage[PACK_BLK_WORDS + 4];
+    __shared__ uint32_t s_tot[PACK_PIECES][4];
+    __shared__ uint32_t s_z;
+    static_assert(sizeof(DecBuildLds) <= sizeof(s_stage), "decoder-table builder uses the stage");
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    if (build_dec && blockIdx.x == 0) {
+        if (T->status == DC_OK)
+            dec_tables_build(const_cast<dc_dtable *>(T), *reinterpret_cast<DecBuildLds *>(s_stage));
+        return;
+    }
+    const uint64_t bx = blockIdx.x - (uint64_t)build_dec, gstride = gridDim.x - (uint64_t)build_dec;
+    const uint64_t total = block_off[nblocks];
+    if (err[0] != 0) return;
+    if (((bit_base & 31) + total + 31) / 32 > words_cap) {
+        if (t == 0) err[2] = 1;
+        return;
+    }
+    const uint32_t nbt = T->nbits[t];
+    s_tab[t] = make_uint2(nbt ? T->code[t] : 0u, nbt);   // z codes as nothing (a code value of a
+    s_nb8[t] = (uint8_t)nbt;                               // length-0 entry would be OR-ed in)
+    if (t == 0) s_z = 256u;
+    for (uint32_t i = 4u * t; i < PACK_BLK_WORDS + 4; i += 1024u)
+        *reinterpret_cast<uint4 *>(&s_stage[i]) = make_uint4(0u, 0u, 0u, 0u);
+    __syncthreads();
+    const uint64_t zb = __ballot(nbt == 0u);   // byte values without a code
+    if (lane == 0 && zb) atomicMin(&s_z, (uint32_t)(t + __builtin_ctzll(zb)));
+    __syncthreads();
+    const uint32_t z = s_z;
+    const uint64_t mtot = msym[nblocks];   // symbols of M (the type byte included)
+    if (z > 255u || mtot >= n) {
+        if (t == 0) err[1] = 1;
+        return;
+    }
+    const bool vec_out = ((uintptr_t)out & 15) == 0;
+    const uint64_t word_base = bit_base >> 5;
+    const uint32_t slog = (uint32_t)__builtin_ctz(sync_syms), S = sync_syms;
+    const uint32_t cbw = (DC_BLOCK_BYTES >> slog) + 2;             // chunk starts a block can hold
+    uint32_t *const s_cb = s_stage + (PACK_BLK_WORDS + 4 - cbw);   // the list sits past the payload
+    const uint32_t lim = PACK_BLK_WORDS - cbw - 4;
+    const bool qmode = 2 * total > 11 * mtot;
+    const uint32_t Z4 = z * 0x01010101u;
+    uint32_t *const sl32 = reinterpret_cast<uint32_t *>(sync_len);
+
+    for (uint64_t b = bx; b < nblocks; b += gstride) {
+        const uint64_t blk_start = b * (uint64_t)DC_BLOCK_BYTES;
+        const bool full = blk_start + DC_BLOCK_BYTES <= n;
+        uint4 blkv[PACK_PIECES];
+        uint32_t ve[PACK_PIECES];
+        if (full) {
+#pragma unroll
+            for (int k = 0; k < PACK_PIECES; ++k) {
+                const uint64_t p = blk_start + (uint64_t)k * PACK_TILE + (uint64_t)t * 16;
+                blkv[k] = LD_PACK(reinterpret_cast<const uint4 *>(in + p));
+                ve[k] = *reinterpret_cast<const uint32_t *>(in + fe_edge_addr(p, lane, n));
+            }
+        } else {   // the stream's last, partial block: bytes past the input read as 0 (the 16-B
+                   // granule holding byte n - 1 is read whole: it lies in the page of that byte)
+#pragma unroll
+            for (int k = 0; k < PACK_PIECES; ++k) {
+                const uint64_t p = blk_start + (uint64_t)k * PACK_TILE + (uint64_t)t * 16;
+                uint4 v = p < n ? LD_PACK(reinterpret_cast<const uint4 *>(in + p)) : make_uint4(0u, 0u, 0u, 0u);
+                if (p + 16 > n) {
+                    uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const int64_t r = (int64_t)n - (int64_t)(p + 4 * q);   // bytes of dword q inside
+                        w[q] &= r <= 0 ? 0u : r >= 4 ? ~0u : ~(~0u << (8 * (uint32_t)r));
+                    }
+                    v = make_uint4(w[0], w[1], w[2], w[3]);
+                }
+                blkv[k] = v;
+                const uint64_t ea = fe_edge_addr(p, lane, n);
+                ve[k] = ea < n ? *reinterpret_cast<const uint32_t *>(in + ea) : 0u;
+            }
+        }
+        const uint64_t s_excl = block_off[b], s_bits = block_off[b + 1] - s_excl;
+        const uint64_t blk_abs = bit_base + s_excl;
+        const uint64_t blk_first_word = blk_abs >> 5;
+        const uint32_t nw_blk = (uint32_t)(((blk_abs & 31) + s_bits + 31) >> 5);
+        const uint32_t sh = vec_out ? (uint32_t)((blk_first_word - word_base) & 3) : 0u;
+        if (nw_blk + sh > lim) {   // uniform: more bits than the stage holds beside the list
+            if (t == 0) err[1] = 2;
+            continue;
+        }
+        const uint64_t m0 = msym[b], m1 = msym[b + 1];
+        const uint64_t cf = (m0 + S - 1) >> slog;   // the first chunk that starts in this block
+        const uint64_t ct = (m1 - 1) >> slog;       // the last one (this block's tail chunk)
+        const uint32_t nc = ct >= cf ? (uint32_t)(ct - cf + 1) : 0u;
+        const uint32_t nwa = sh + nw_blk;
+        // ---- the symbols y, pass A: bit and symbol counts per piece ----
+        // Pk = bits (<= 512) | symbols << 18 (<= 16) | bits of the first half << 23 (<= 256)
+        uint32_t Pk[PACK_PIECES], Ik[PACK_PIECES];
+#pragma unroll
+        for (int k = 0; k < PACK_PIECES; ++k) {
+            const uint64_t p = blk_start + (uint64_t)k * PACK_TILE + (uint64_t)t * 16;
+            uint32_t w4[4] = {blkv[k].x, blkv[k].y, blkv[k].z, blkv[k].w};
+            const uint32_t pb = lane == 0 ? ve[k] >> 24 : dpp_wave_shr1(w4[3]) >> 24;
+            const uint32_t qb = lane == 63 ? (p + 16 < n ? ve[k] & 255u : 0u) : dpp_wave_shl1(w4[0]) & 255u;
+            uint32_t st[4];
+            fe_pair_starts(w4, qb, st);
+            if (p == 0) st[0] &= ~0x80u;   // position 0 never starts a pair
+            uint32_t nul = 0;               // positions without a symbol
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t sec = (st[q] << 8) | (q ? st[q - 1] >> 24 : fe_start_before(pb, w4[0], p));
+                uint32_t m8 = st[q];
+                if (!full) {   // past the input: no symbol
+                    const int64_t v = (int64_t)n - (int64_t)(p + 4 * q);
+                    m8 |= v <= 0 ? 0x80808080u : v >= 4 ? 0u : (0x80808080u << (8 * (uint32_t)v));
+                }
+                nul += (uint32_t)__popc(m8);
+                m8 = (m8 - (m8 >> 7)) | m8;   // 0x80 -> 0xFF per byte
+                w4[q] = (w4[q] & ~m8) | (Z4 & m8) | sec;
+            }
+            blkv[k] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+            uint32_t s0 = 0, s1 = 0;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) s0 += s_nb8[(w4[i >> 2] >> (8 * (i & 3))) & 255u];
+#pragma unroll
+            for (int i = 8; i < 16; ++i) s1 += s_nb8[(w4[i >> 2] >> (8 * (i & 3))) & 255u];
+            Pk[k] = (s0 + s1) | ((16u - nul) << 18) | (s0 << 23);
+            // materialised here: sunk to the scan, the sums kept every piece's 16 lookups live
+            asm volatile("" : "+v"(Pk[k]));
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        // one scan of bits | symbols << 18 (a piece of the workgroup: <= 2^17 bits, 4096 symbols)
+#pragma unroll
+        for (int k = 0; k < PACK_PIECES; ++k) Ik[k] = wave_scan_incl(Pk[k] & 0x7FFFFFu);
+        if (lane == 63) {
+#pragma unroll
+            for (int k = 0; k < PACK_PIECES; ++k) s_tot[k][wid] = Ik[k];
+        }
+        lds_barrier();
+        const uint64_t org = (blk_first_word - sh) << 5;   // absolute bit of stage bit 0
+        auto emit = [&](uint64_t acc, uint32_t nb, uint32_t pos) {   // as in k_huff_pack
+            const uint64_t al = acc << ((64u - nb) & 63u);
+            const uint32_t hi = (uint32_t)(al >> 32), lo = (uint32_t)al, r = pos & 31u, wi = pos >> 5;
+            atomicOr(&s_stage[wi], hi >> r);
+            atomicOr(&s_stage[wi + 1], __builtin_amdgcn_alignbit(hi, lo, r));
+            atomicOr(&s_stage[wi + 2], __builtin_amdgcn_alignbit(lo, 0u, r));
+        };
+        uint64_t run = blk_abs, mrun = m0;
+        if (b == 0) {   // M[0] = the type byte 8 (EIGHT_BIT_PRUNED, small_compression.c:39), chunk 0's start
+            const uint2 h = s_tab[8];
+            if (t == 0) {
+                emit(h.x, h.y, (uint32_t)(blk_abs - org));
+                s_cb[0] = 0u;
+            }
+            run += h.y;
+            mrun += 1;
+        }
+#pragma unroll
+        for (int k = 0; k < PACK_PIECES; ++k) {
+            uint32_t wo = 0, kt = 0, cwo = 0, ckt = 0;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                const uint32_t v = s_tot[k][w], vb = v & 0x3FFFFu, vc = v >> 18;
+                wo += (w < wid) ? vb : 0u;
+                kt += vb;
+                cwo += (w < wid) ? vc : 0u;
+                ckt += vc;
+            }
+            const uint32_t Tk = Pk[k] & 0x3FFFFu, Ck = (Pk[k] >> 18) & 31u, Hk = Pk[k] >> 23;
+            const uint64_t As = run + wo + ((Ik[k] & 0x3FFFFu) - Tk);
+            const uint64_t mi = mrun + cwo + ((Ik[k] >> 18) - Ck);   // index of the piece's first symbol
+            run += kt;
+            mrun += ckt;
+            const uint32_t j0 = (uint32_t)(0ull - mi) & (S - 1);     // symbols before the chunk start
+            const bool has = j0 < Ck;
+            const uint32_t jj = has ? j0 : 0xFFFFu;
+            uint32_t ec = 0, cap = 0;   // symbols seen, bits before the chunk start
+            auto tally = [&](uint32_t l) {
+                ec += l != 0u ? 1u : 0u;
+                cap += ec <= jj ? l : 0u;
+            };
+            uint32_t w4[4] = {blkv[k].x, blkv[k].y, blkv[k].z, blkv[k].w};
+            asm volatile("" : "+v"(w4[0]), "+v"(w4[1]), "+v"(w4[2]), "+v"(w4[3]));
+            const uint32_t rel = (uint32_t)(As - org);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const uint32_t Th = h ? Tk - Hk : Hk;
+                const uint32_t pos = h ? rel + Hk : rel;
+                if (!qmode && Th <= 64u) {
+                    uint64_t acc = 0;
+#pragma unroll
+                    for (int i = 8 * h; i < 8 * h + 8; ++i) {
+                        const uint2 e = s_tab[(w4[i >> 2] >> (8 * (i & 3))) & 255u];
+                        acc = (acc << e.y) | e.x;
+                        tally(e.y);
+                    }
+                    emit(acc, Th, pos);
+                } else {
+                    uint32_t pq = pos;
+#pragma unroll 1
+                    for (int qq = 0; qq < 2; ++qq) {
+                        uint2 e[4];
+                        uint32_t nq = 0;
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            const int bi = 8 * h + 4 * qq + i;
+                            const uint32_t wv = qq ? w4[2 * h + 1] : w4[2 * h];
+                            e[i] = s_tab[(wv >> (8 * (bi & 3))) & 255u];
+                            nq += e[i].y;
+                            tally(e[i].y);
+                        }
+                        if (nq <= 64u) {
+                            uint64_t acc = 0;
+#pragma unroll
+                            for (int i = 0; i < 4; ++i) acc = (acc << e[i].y) | e[i].x;
+                            emit(acc, nq, pq);
+                            pq += nq;
+                        } else {
+#pragma unroll
+                            for (int i = 0; i < 4; ++i) { emit(e[i].x, e[i].y, pq); pq += e[i].y; }
+                        }
+                    }
+                }
+            }
+            if (has) s_cb[(uint32_t)(((mi + j0) >> slog) - cf)] = (uint32_t)(As - blk_abs) + cap;
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        lds_barrier();
+        // ---- store phase: as in k_huff_pack ----
+        const uint32_t last_plain = ((run & 31) != 0) ? nwa - 1 : nwa;
+        uint32_t *dst = out + (blk_first_word - word_base) - sh;
+        if (vec_out) {
+            const uint32_t nq = last_plain >> 2;
+            for (uint32_t q = 1 + t; q < nq; q += 256) {
+                uint4 *const sq = reinterpret_cast<uint4 *>(&s_stage[4 * q]);
+                const uint4 v = *sq;
+                *sq = make_uint4(0u, 0u, 0u, 0u);
+                uint4 *const d4 = reinterpret_cast<uint4 *>(dst + 4 * q);
+                __builtin_nontemporal_store(bswap32(v.x), &d4->x);
+                __builtin_nontemporal_store(bswap32(v.y), &d4->y);
+                __builtin_nontemporal_store(bswap32(v.z), &d4->z);
+                __builtin_nontemporal_store(bswap32(v.w), &d4->w);
+            }
+            const uint32_t hend = last_plain < 4u ? last_plain : 4u;
+            if (t < 4 && (uint32_t)t > sh && (uint32_t)t < hend) { dst[t] = bswap32(s_stage[t]); s_stage[t] = 0u; }
+            const uint32_t tb = nq > 0 ? 4 * nq : 4u;
+            if (t >= 8 && t < 12 && tb + (t - 8) < last_plain) {
+                dst[tb + (t - 8)] = bswap32(s_stage[tb + (t - 8)]);
+                s_stage[tb + (t - 8)] = 0u;
+            }
+        } else {
+            for (uint32_t i = t + 1; i < last_plain; i += 256) { dst[i] = bswap32(s_stage[i]); s_stage[i] = 0u; }
+        }
+        if (t == 0) {
+            atomicOr(&dst[sh], bswap32(s_stage[sh]));
+            s_stage[sh] = 0u;
+        }
+        if (t == 64 && last_plain < nwa && nw_blk > 1) {
+            atomicOr(&dst[nwa - 1], bswap32(s_stage[nwa - 1]));
+            s_stage[nwa - 1] = 0u;
+        }
+        // ---- the sync index: chunk lengths from consecutive starts; group bases ----
+        if (sync_len != nullptr) {
+            const uint64_t hd = m0 > 0 ? ((m0 - 1) >> slog) >> 1 : ~0ull, td = ct >> 1;
+            for (uint32_t i = t; i < nc; i += 256) {
+                const uint32_t a = s_cb[i], e = i + 1 < nc ? s_cb[i + 1] : (uint32_t)s_bits;
+                const uint64_t c = cf + i;
+                if ((c & (DC_SYNC_GROUP - 1)) == 0) sync_base[c >> DC_SYNC_GROUP_LOG] = blk_abs + a;
+                if ((c >> 1) == hd || (c >> 1) == td) atomicAdd(&sl32[c >> 1], (e - a) << (16u * (uint32_t)(c & 1)));
+                else sync_len[c] = (uint16_t)(e - a);
+            }
+            if (t == 255 && (m0 & (S - 1)) != 0) {   // the previous block's tail chunk: the part in this block
+                const uint64_t c = cf - 1;
+                atomicAdd(&sl32[c >> 1], (nc ? s_cb[0] : (uint32_t)s_bits) << (16u * (uint32_t)(c & 1)));
+            }
+        }
+        lds_barrier();
     }
 }
 
@@ -2300,7 +2755,10 @@ static __device__ void d8_stale_exit(int *__restrict__ err, uint32_t *__restrict
 
 // NW waves per workgroup (one workgroup per CU), NC chains per wave: wave w of workgroup b
 // decodes the NC consecutive groups of "tuple" b*NW + w (+ grid stride), lane = chunk.
-template <int NW, int NC>
+// EXP (the C5 decode, dc_small_huff_decode): also the number of symbols >= 0x80 of every group
+// into gexp[group] (each is a front-end pair: two output bytes), so the front-end inverse needs
+// no counting pass of its own; the redo adds those of the chunks it rewrites.
+template <int NW, int NC, bool EXP = false>
 __global__ __launch_bounds__(NW * 64) void k_huff_decode8(const uint32_t *__restrict__ in, uint64_t bit_base, const uint64_t *__restrict__ d_base,
                                                           const uint64_t *__restrict__ sync_base,
                                                           const uint16_t *__restrict__ sync_len, uint64_t n,
@@ -2308,7 +2766,7 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode8(const uint32_t *__rest
                                                           uint8_t *__restrict__ out, int *__restrict__ err,
                                                           uint32_t *__restrict__ queue, uint32_t static_pct,
                                                           uint64_t *__restrict__ fix_mask, uint64_t *__restrict__ fix_pos,
-                                                          uint8_t *__restrict__ scratch)
+                                                          uint8_t *__restrict__ scratch, uint32_t *__restrict__ gexp = nullptr)
 {
     static_assert(NW * NC <= D8_CHAINS && NW <= D8_MAX_WAVES, "stage slots");
     constexpr uint32_t S = 64;
@@ -2320,7 +2778,7 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode8(const uint32_t *__rest
         return;
     }
     if (d_base) bit_base += *d_base;   // device-resident shard offset (dist: no host read)
-    if (T->fixed8 && (bit_base & 127) == 0 && ((uintptr_t)in & 15) == 0 && ((uintptr_t)out & 15) == 0 &&
+    if (!EXP && T->fixed8 && (bit_base & 127) == 0 && ((uintptr_t)in & 15) == 0 && ((uintptr_t)out & 15) == 0 &&
         (n + 3) / 4 <= nwords) {
         // every code 8 bits: output symbol i = the symbol of stream byte bit_base / 8 + i (the
         // words' first byte; bit_base % 128 == 0). No chunk is redone: the fix masks are zeroed.
@@ -2505,6 +2963,14 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode8(const uint32_t *__rest
             const uint32_t f = (uint32_t)__builtin_ctzll(m | (1ull << 63));
             uint64_t *fp = g < ngroups ? fix_mask + ngroups + g : reinterpret_cast<uint64_t *>(dummy) + 65;
             *fp = (uint64_t)cur.wo[j] * 32 + cur.lead[j] + (uint32_t)__builtin_amdgcn_readlane((int)cur.off[j], (int)f);
+            if (EXP) {   // symbols >= 0x80 of the chunks not redone (the redo adds the others)
+                uint32_t e = 0;
+#pragma unroll
+                for (int q = 0; q < 16; ++q) e += (uint32_t)__popc(o[j][q] & 0x80808080u);
+                e = (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_incl(redo ? 0u : e), 63);
+                uint32_t *ep = (lane == 0 && g < ngroups) ? gexp + g : dummy + 132 + lane;
+                *ep = e;
+            }
         }
         // next tuple: stage it (its spans are in v), then start the loads of the one after
         tp = t1;
@@ -2816,7 +3282,7 @@ __global__ __launch_bounds__(D8F_WAVES * 64) void k_huff_decode8_fix(const uint3
                                                                     uint8_t *__restrict__ out, int *__restrict__ err,
                                                                     const uint64_t *__restrict__ fix_mask,
                                                                     const uint64_t *__restrict__ fix_pos,
-                                                                    int *__restrict__ err_next)
+                                                                    int *__restrict__ err_next, uint32_t *__restrict__ gexp = nullptr)
 {
     constexpr uint32_t S = 64;
     constexpr int NT = D8F_WAVES * 64;
@@ -2988,6 +3454,7 @@ __global__ __launch_bounds__(D8F_WAVES * 64) void k_huff_decode8_fix(const uint3
                 if (wa >= D8F_ROW - 6) restage();   // (a row clamped at the buffer's end)
                 uint32_t w0 = row[wa], w1 = row[wa + 1], w2 = row[wa + 2];
                 uint4 *const o128 = reinterpret_cast<uint4 *>(out + s0);
+                uint32_t ex = 0;   // symbols >= 0x80 (gexp)
                 for (uint32_t p = 0; p < (cntc + 15) / 16; ++p) {
                     uint32_t ov[4];
 #pragma unroll
@@ -3024,7 +3491,16 @@ __global__ __launch_bounds__(D8F_WAVES * 64) void k_huff_decode8_fix(const uint3
                     if (16 * p + 16 <= cntc) o128[p] = make_uint4(ov[0], ov[1], ov[2], ov[3]);
                     else   // the stream's partial last chunk
                         for (uint32_t k = 0; 16 * p + k < cntc; ++k) out[s0 + 16 * p + k] = (uint8_t)(ov[k >> 2] >> (8 * (k & 3)));
+                    if (gexp) {
+#pragma unroll
+                        for (int q4 = 0; q4 < 4; ++q4) {
+                            const int rem = (int)cntc - (int)(16 * p) - 4 * q4;   // bytes of ov[q4] inside the chunk
+                            const uint32_t keep = rem <= 0 ? 0u : rem >= 4 ? ~0u : ~(~0u << (8 * rem));
+                            ex += (uint32_t)__popc(ov[q4] & keep & 0x80808080u);
+                        }
+                    }
                 }
+                if (gexp && valid) atomicAdd(gexp + cha / DC_SYNC_GROUP, ex);
 #ifdef DC_DIAG
                 D8_STAMP(f_d1);
                 f_dec += f_d1 - f_w1;
@@ -3913,18 +4389,6 @@ template <int M> static uint64_t sm_ntiles(const uint8_t *in, int off, uint64_t 
     return nelem ? (lead + nelem + SM_TILE - 1) / SM_TILE : 0;
 }
 
-// SWAR byte tests on a dword (bit 7 of each byte = the test; the kernels are VALU-issue
-// bound, and one 32-bit op here tests 4 bytes: 31 VALU per byte per element rule before)
-static __device__ __forceinline__ uint32_t swar_eq(uint32_t x, uint32_t c4)   // byte == c
-{
-    const uint32_t v = x ^ c4;
-    return ~(((v & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | v) & 0x80808080u;
-}
-static __device__ __forceinline__ uint32_t swar_lower(uint32_t x)   // 'a' <= byte <= 'z'
-{
-    const uint32_t t = x & 0x7F7F7F7Fu;
-    return (t + 0x1F1F1F1Fu) & ~(t + 0x05050505u) & ~x & 0x80808080u;
-}
 // bytes k of the dword at tile byte u with u + k >= lim / < lim
 static __device__ __forceinline__ uint32_t swar_ge(uint32_t u, uint32_t lim)
 {
@@ -4003,8 +4467,7 @@ static __device__ __forceinline__ uint2 sm_nb(const SmEdge<M> &E, uint32_t d, in
 {
     // the neighbour lanes' dwords by DPP wave shifts (VALU; the bpermutes they replace were a
     // fifth of the writer's LDS instructions)
-    const uint32_t pu = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)d, 0x138, 0xf, 0xf, false) >> 24;   // wave_shr:1
-    const uint32_t qd = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)d, 0x130, 0xf, 0xf, false) & 255u;  // wave_shl:1
+    const uint32_t pu = dpp_wave_shr1(d) >> 24, qd = dpp_wave_shl1(d) & 255u;
     const uint32_t pe = w > 0 ? E.last[st][w - 1] : st > 0 ? E.last[st - 1][3] : E.before;
     const uint32_t qe = w < 3 ? E.first[st][w + 1] : st + 1 < SM_STEPS ? E.first[st + 1][0] : E.after;
     return make_uint2(lane == 0 ? pe : pu, lane == 63 ? qe : qd);
@@ -4043,6 +4506,27 @@ __global__ __launch_bounds__(256) void k_small_tiles(const uint8_t *__restrict__
         const uint32_t c = s_w[0] + s_w[1] + s_w[2] + s_w[3];
         summ[blockIdx.x] = make_uint4(c, c, 0u, 0u);   // a stateless composition
     }
+}
+
+// The C5 decode's tile summaries without a counting pass (dc_small_huff_decode): the decoder
+// counted the symbols >= 0x80 of every group of 4096 (gexp; S = 64), and a decode tile (8 KiB of
+// the front-end stream, 16-B aligned) is two groups: output bytes = its elements + those
+// symbols (the raw first byte M[1] excluded). Thread 0 also hands the type byte M[0] to the
+// host (meta[8]: only 8 = EIGHT_BIT_PRUNED is decoded this way).
+__global__ __launch_bounds__(256) void k_small_dec_summ(const uint32_t *__restrict__ gexp, uint64_t ngroups,
+                                                        const uint8_t *__restrict__ in, uint64_t len, uint64_t ntiles,
+                                                        uint4 *__restrict__ summ, uint64_t *__restrict__ meta)
+{
+    const uint64_t tile = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (tile == 0) meta[8] = in[0];
+    if (tile >= ntiles) return;
+    constexpr uint64_t TB = SmMode<M_SMALL_DEC>::tile;
+    static_assert(TB == 2 * 64 * DC_SYNC_GROUP, "a decode tile is two groups of S = 64");
+    const uint64_t lo = tile * TB > 2 ? tile * TB : 2, hi = (tile + 1) * TB < len ? (tile + 1) * TB : len;
+    uint32_t c = hi > lo ? (uint32_t)(hi - lo) : 0u;
+    c += gexp[2 * tile] + (2 * tile + 1 < ngroups ? gexp[2 * tile + 1] : 0u);
+    if (tile == 0 && len > 1 && in[1] >= 0x80) c -= 1;   // M[1] = x[0], raw (small_compression.c:587)
+    summ[tile] = make_uint4(c, c, 0u, 0u);
 }
 
 // The writer: lane-contiguous geometry (unlike the count kernel's, whose tile totals are the
@@ -4101,8 +4585,7 @@ __global__ __launch_bounds__(SmMode<M>::wthreads) void k_small_write(const uint8
         if (t == 0) s_before = (T.base - 1 >= 0 && T.base - 1 < (int64_t)len) ? in[T.base - 1] : 0;
         if (t == (int)NT - 1) s_after = (T.base + TILE >= 0 && T.base + TILE < (int64_t)len) ? in[T.base + TILE] : 0;
         __syncthreads();
-        const uint32_t pu = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)d[LD - 1], 0x138, 0xf, 0xf, false) >> 24;   // wave_shr:1
-        const uint32_t qd = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)d[0], 0x130, 0xf, 0xf, false) & 255u;       // wave_shl:1
+        const uint32_t pu = dpp_wave_shr1(d[LD - 1]) >> 24, qd = dpp_wave_shl1(d[0]) & 255u;
         p = lane == 0 ? (w > 0 ? s_last[w - 1] : s_before) : pu;
         q = lane == 63 ? (w + 1 < (int)NW ? s_first[w + 1] : s_after) : qd;
     }
@@ -5078,6 +5561,8 @@ struct dc_ctx {
     uint16_t *d_bh;         size_t bh_cap;        // block histograms (u16 x 256 per block)
     uint64_t *d_off;        size_t off_cap;       // nblocks + 1
     uint32_t *d_plan;       size_t plan_cap;      // plan: per-block local offsets + workgroup totals
+    uint64_t *d_msym;       size_t msym_cap;      // C5 fused front-end: first symbol index per block (+ total)
+    uint32_t *d_gexp;       size_t gexp_cap;      // C5 decode: symbols >= 0x80 per group (dc_small_huff_decode)
     int *d_err;                                   // [8] text parse
     // error flags of plan/pack and of decode in rotating slots (32 x 4 ints each): every call
     // takes the next slot, which a kernel of the call before cleared (no memset launch)
@@ -5106,6 +5591,7 @@ struct dc_ctx {
     uint64_t *d_klens;      size_t klens_cap;     // chunked nybble: stream length per chunk
     uint64_t *h_pinned;                           // pinned host scalars
     const uint8_t *hist_in; uint64_t hist_n;      // identity of the last dc_huff_hist input
+    bool hist_fe;                                 // ... histogram of its C5 front-end output (dc_small_huff_plan)
     bool plan_ok;
     // tuning options (dc_ctx_set_option; initial values from the environment, read once here)
     uint32_t opt_hist_grid;       // histogram workgroups (0: default 512)
@@ -5256,6 +5742,8 @@ void dc_ctx_destroy(dc_ctx *c)
     if (c->d_bh) (void)hipFree(c->d_bh);
     if (c->d_off) (void)hipFree(c->d_off);
     if (c->d_plan) (void)hipFree(c->d_plan);
+    if (c->d_msym) (void)hipFree(c->d_msym);
+    if (c->d_gexp) (void)hipFree(c->d_gexp);
     if (c->d_err) (void)hipFree(c->d_err);
     if (c->d_errp) (void)hipFree(c->d_errp);
     if (c->d_hflag) (void)hipFree(c->d_hflag);
@@ -5394,7 +5882,7 @@ int dc_copy_probe(dc_ctx *c, const void *d_src, void *d_dst, uint64_t bytes)
 // ---- Huffman -----------------------------------------------------------------------
 static uint64_t nblocks_of(uint64_t n) { return (n + DC_BLOCK_BYTES - 1) / DC_BLOCK_BYTES; }
 
-static int hist_impl(dc_ctx *c, const uint8_t *d_in, uint64_t n, uint64_t *d_hist, HistFuse fuse)
+static int hist_impl(dc_ctx *c, const uint8_t *d_in, uint64_t n, uint64_t *d_hist, HistFuse fuse, bool fe = false)
 {
     if (!c || !d_hist || (n && !d_in)) return DC_E_ARG;
     if (((uintptr_t)d_in) & 15) return DC_E_ARG;
@@ -5402,7 +5890,14 @@ static int hist_impl(dc_ctx *c, const uint8_t *d_in, uint64_t n, uint64_t *d_his
     if (ensure((void **)&c->d_bh, &c->bh_cap, (nb ? nb : 1) * 256 * sizeof(uint16_t))) return DC_E_HIP;
     c->hist_in = d_in;
     c->hist_n = n;
+    c->hist_fe = fe;
     c->plan_ok = false;
+    if (fe) {   // n >= 2 (dc_small_huff_plan)
+        const uint64_t grid = nb < 512u ? nb : 512u;
+        LAUNCH(c, "fe_hist_blocks", (k_hist_blocks<1, true>), grid, 256, d_in, n, nb, c->d_bh, d_hist,
+               reinterpret_cast<uint64_t *>(c->d_hflag), c->d_hflag + 512, c->d_hloc, fuse);
+        return DC_OK;
+    }
     if (nb == 0) {
         HIPCHK(hipMemsetAsync(d_hist, 0, 256 * sizeof(uint64_t), c->stream));
         HIPCHK(hipMemsetAsync(c->d_hloc, 0, 256 * sizeof(uint64_t), c->stream));
@@ -5536,22 +6031,36 @@ int dc_huff_encode_plan(dc_ctx *c, const uint8_t *d_in, uint64_t n, int M, int n
 // The per-block exclusive bit offsets of the last histogram's input under c->plan_table into
 // c->d_off (nblocks + 1 entries), and with d_words set the zeroed block-boundary words the
 // pack OR-merges into: two launches (one more above PLAN_MAX_WG workgroups of blocks)
+// With sl32 set (C5 fused front-end, k_fe_pack): also the symbol index of each block's first
+// symbol into c->d_msym, and the sync-length dwords of the chunks spanning block boundaries
+// zeroed (S = 1 << slog); one plan launch pair as well, at most PLAN_MAX_WG workgroups.
 static int plan_offsets(dc_ctx *c, int *err, int *err_next, uint64_t bit_base, const uint64_t *d_base,
-                        uint32_t *d_words, uint64_t words_cap)
+                        uint32_t *d_words, uint64_t words_cap, uint32_t *sl32 = nullptr, uint32_t slog = 0)
 {
     const uint64_t nb = nblocks_of(c->hist_n);
     if (ensure((void **)&c->d_off, &c->off_cap, (nb + 1) * sizeof(uint64_t))) return DC_E_HIP;
     if (nb == 0) {
+        if (sl32) return DC_E_ARG;
         HIPCHK(hipMemsetAsync(c->d_off, 0, sizeof(uint64_t), c->stream));
         return DC_OK;
     }
     const uint64_t nwg = (nb + PLAN_WG_BLOCKS - 1) / PLAN_WG_BLOCKS;
     if (nwg <= PLAN_MAX_WG) {
-        if (ensure((void **)&c->d_plan, &c->plan_cap, (nb + nwg + 64) * sizeof(uint32_t))) return DC_E_HIP;
+        if (ensure((void **)&c->d_plan, &c->plan_cap, 2 * (nb + nwg + 64) * sizeof(uint32_t))) return DC_E_HIP;
         uint32_t *loc = c->d_plan, *tot = c->d_plan + nb + 32;
-        LAUNCH(c, "block_bits", k_block_local, nwg, 256, (const uint16_t *)c->d_bh, nb, c->plan_table, loc, tot, err);
+        uint32_t *lcnt = nullptr, *wgcnt = nullptr;
+        if (sl32) {
+            if (ensure((void **)&c->d_msym, &c->msym_cap, (nb + 1) * sizeof(uint64_t))) return DC_E_HIP;
+            lcnt = c->d_plan + nb + nwg + 64;
+            wgcnt = lcnt + nb + 32;
+        }
+        LAUNCH(c, "block_bits", k_block_local, nwg, 256, (const uint16_t *)c->d_bh, nb, c->plan_table, loc, tot, err,
+               lcnt, wgcnt);
         LAUNCH(c, "block_scan", k_block_final_wide, nwg, 256, (const uint32_t *)loc, (const uint32_t *)tot, nb,
-               (uint32_t)nwg, c->d_off, c->d_meta + 15, err_next, bit_base, d_base, d_words, words_cap);
+               (uint32_t)nwg, c->d_off, c->d_meta + 15, err_next, bit_base, d_base, d_words, words_cap,
+               (const uint32_t *)lcnt, (const uint32_t *)wgcnt, c->d_msym, sl32, slog);
+    } else if (sl32) {
+        return DC_E_ARG;
     } else {
         LAUNCH(c, "block_bits", k_block_bits, (nb + 3) / 4, 256, (const uint16_t *)c->d_bh, nb, c->plan_table,
                c->d_off, err);
@@ -5606,7 +6115,7 @@ static int pack_impl(dc_ctx *c, const uint8_t *d_in, uint64_t n, const dc_dtable
                      uint16_t *d_sync_len, uint32_t sync_syms)
 {
     if (!c || !d_table || !d_words) return DC_E_ARG;
-    if (d_in != c->hist_in || n != c->hist_n || !c->plan_ok || !c->plan_total) return DC_E_STATE;
+    if (d_in != c->hist_in || n != c->hist_n || c->hist_fe || !c->plan_ok || !c->plan_total) return DC_E_STATE;
     if ((d_sync_base != nullptr) != (d_sync_len != nullptr)) return DC_E_ARG;
     if (d_sync_len && !sync_ok(sync_syms)) return DC_E_ARG;
     const uint64_t nb = nblocks_of(n);
@@ -5639,6 +6148,52 @@ int dc_huff_pack_async_dev(dc_ctx *c, const uint8_t *d_in, uint64_t n, const dc_
     return pack_impl(c, d_in, n, d_table, 0, d_bit_base, d_words, words_cap, d_sync_base, d_sync_len, sync_syms);
 }
 
+// ---- C5 fused front-end encode (k_hist_blocks<.., true> + plan + k_fe_pack) -------------
+int dc_small_huff_plan(dc_ctx *c, const uint8_t *d_in, uint64_t n, int M, int nary, uint64_t *d_hist,
+                       dc_dtable *d_table, uint64_t *d_total_bits)
+{
+    if (!c || !d_table || !d_total_bits || !d_hist || M < 255 || M >= DC_MAX_SYMS || nary < 2 || nary > 256) return DC_E_ARG;
+    if (n < 2) return DC_E_FALLBACK;   // the front-end output of < 2 bytes is LITERAL
+    ++c->gen_p;
+    table_written(c);
+    const int r = hist_impl(c, d_in, n, d_hist, HistFuse{d_table, M, nary, d_total_bits, plan_err(c), plan_err_next(c)},
+                            true);
+    if (r != DC_OK) { --c->gen_p; return r; }
+    c->plan_table = d_table;
+    c->plan_total = d_total_bits;
+    c->plan_ok = true;
+    return DC_OK;
+}
+
+int dc_small_huff_pack_async(dc_ctx *c, const uint8_t *d_in, uint64_t n, const dc_dtable *d_table, uint64_t bit_base,
+                             uint32_t *d_words, uint64_t words_cap, uint64_t *d_sync_base, uint16_t *d_sync_len,
+                             uint32_t sync_syms)
+{
+    if (!c || !d_table || !d_words || !d_sync_base || !d_sync_len || !sync_ok(sync_syms)) return DC_E_ARG;
+    if (((uintptr_t)d_sync_len) & 3) return DC_E_ARG;
+    if (d_in != c->hist_in || n != c->hist_n || !c->hist_fe || !c->plan_ok || !c->plan_total) return DC_E_STATE;
+    const uint64_t nb = nblocks_of(n);
+    const int r = plan_offsets(c, plan_err(c), plan_err_next(c), bit_base, nullptr, d_words, words_cap,
+                               reinterpret_cast<uint32_t *>(d_sync_len), (uint32_t)__builtin_ctz(sync_syms));
+    if (r != DC_OK) return r;
+    const uint64_t gmax = c->opt_pack_grid ? c->opt_pack_grid : (nb + 1) / 2;
+    const uint64_t grid = nb < gmax ? nb : gmax;
+    LAUNCH(c, "fe_pack", k_fe_pack, grid + 1, 256, d_in, n, d_table, (const uint64_t *)c->d_off,
+           (const uint64_t *)c->d_msym, bit_base, d_words, d_sync_base, d_sync_len, sync_syms, nb, words_cap,
+           plan_err(c), 1);
+    dec_tables_built(c, d_table);
+    return DC_OK;
+}
+
+int dc_small_huff_symbols(dc_ctx *c, uint64_t *h_m)
+{
+    if (!c || !h_m) return DC_E_ARG;
+    if (!c->hist_fe || !c->d_msym || !c->hist_n) return DC_E_STATE;
+    HIPCHK(hipMemcpyAsync(h_m, c->d_msym + nblocks_of(c->hist_n), sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return DC_OK;
+}
+
 uint32_t dc_huff_plan_gen(dc_ctx *c) { return c ? c->gen_p : 0u; }
 
 int dc_huff_pack_status(dc_ctx *c, const dc_dtable *d_table)
@@ -5660,6 +6215,7 @@ int dc_huff_pack_status_gen(dc_ctx *c, const dc_dtable *d_table, uint32_t gen)
         const int st = dc_huff_table_status(c, d_table, nullptr);
         return st ? st : DC_E_NOCODE;
     }
+    if (v[1]) return DC_E_FALLBACK;   // k_fe_pack: the fused path does not apply
     return v[2] ? DC_E_CAPACITY : DC_OK;
 }
 
@@ -5701,9 +6257,11 @@ uint32_t dc_huff_choose_sync(uint64_t n, uint64_t total_bits)
     return (64.0 * 64.0 * avg / 8.0 <= 4200.0) ? 64u : 32u;
 }
 
+// d_gexp (C5, dc_small_huff_decode): symbols >= 0x80 per group of 64 chunks, from the fast
+// decoder and its redo (S = 64 only: DC_E_ARG otherwise)
 static int decode_impl(dc_ctx *c, const uint32_t *d_words, uint64_t bit_base, const uint64_t *d_base, uint64_t words,
                        const uint64_t *d_sync_base, const uint16_t *d_sync_len, uint32_t S, uint64_t n,
-                       const dc_dtable *d_table, uint8_t *d_out)
+                       const dc_dtable *d_table, uint8_t *d_out, uint32_t *d_gexp = nullptr)
 {
     if (!c || !d_table || (n && (!d_words || !d_sync_base || !d_sync_len || !d_out))) return DC_E_ARG;
     if (!sync_ok(S)) return DC_E_ARG;
@@ -5717,7 +6275,9 @@ static int decode_impl(dc_ctx *c, const uint32_t *d_words, uint64_t bit_base, co
     // the decoder tables, unless this context's last pack built them for this table (no launch
     // then; a table rebuilt elsewhere since reads dec_ready 0 in the decoder: a stream error)
     if (!dec_tables_fresh(c, d_table)) LAUNCH(c, "dec_tables", k_dec_tables, 1, 256, const_cast<dc_dtable *>(d_table), derr);
-    if (S == 64 && n < (1ull << 37) && words < (1ull << 31) && !c->opt_decode_general) {
+    const bool fast8 = S == 64 && n < (1ull << 37) && words < (1ull << 31) && !c->opt_decode_general;
+    if (d_gexp && !fast8) return DC_E_ARG;
+    if (fast8) {
         // 12 waves x 2 chains, one workgroup per CU: the stage and the 14-bit table fill the
         // LDS (the 8 x 4 split measured 0.89 vs 0.70 ms on 1 GiB C2: spills)
         const uint32_t spct = c->opt_d8_static;   // clamped to 0..100 by dc_ctx_set_option
@@ -5737,13 +6297,17 @@ static int decode_impl(dc_ctx *c, const uint32_t *d_words, uint64_t bit_base, co
                    spct, (uint64_t *)c->d_fix, (uint64_t *)c->d_fixpos, (uint8_t *)c->d_scr);
         } else
 #endif
-        {   // one code per lookup, 11 waves x 2 chains (the 15-bit table takes 64 KiB of LDS)
+        if (d_gexp) {   // (C5) with the symbols >= 0x80 per group
+            LAUNCH(c, "huff_decode", (k_huff_decode8<11, 2, true>), (tuples + 10) / 11 < 256 ? (tuples + 10) / 11 : 256,
+                   11 * 64, d_words, bit_base, d_base, d_sync_base, d_sync_len, n, words, d_table, d_out, derr,
+                   c->d_queue, spct, (uint64_t *)c->d_fix, (uint64_t *)c->d_fixpos, (uint8_t *)c->d_scr, d_gexp);
+        } else {   // one code per lookup, 11 waves x 2 chains (the 15-bit table takes 64 KiB of LDS)
             D8_LAUNCH(11, 2);
         }
 #undef D8_LAUNCH
         c->last_groups = groups;
         LAUNCH(c, "huff_decode_fix", k_huff_decode8_fix, 256, D8F_WAVES * 64, d_words, n, words, d_table, d_out,
-               derr, (const uint64_t *)c->d_fix, (const uint64_t *)c->d_fixpos, derr_next);
+               derr, (const uint64_t *)c->d_fix, (const uint64_t *)c->d_fixpos, derr_next, d_gexp);
         return DC_OK;
     }
     const uint64_t wgs = (groups + DEC_WAVES - 1) / DEC_WAVES;
@@ -5842,10 +6406,12 @@ int dc_huff_base64url(dc_ctx *c, const uint32_t *d_words, uint64_t bit_base, uin
 // ---- byte-stream transducer codecs --------------------------------------------------
 // tiles + scan (from state aux.s_init) + write; h_plan (optional) gets the whole composition
 // (c0, c1, s0, s1) for shard plans; write = false stops after the scan
+// gexp (M_SMALL_DEC only, dc_small_huff_decode): the tile summaries from the decoder's counts
+// (k_small_dec_summ) instead of the counting pass
 template <int M>
 static int fsm_run(dc_ctx *c, const uint8_t *d_in, uint64_t len, uint64_t nelem, uint8_t *d_out, uint64_t *h_len,
                    const char *name, FsmAux aux = FsmAux{nullptr, 0, 0, 1, 1}, uint64_t *h_plan = nullptr,
-                   bool write = true)
+                   bool write = true, const uint32_t *gexp = nullptr, uint64_t ngroups = 0)
 {
     const uint64_t ntiles = SmMode<M>::fast ? sm_ntiles<M>(d_in, FsmOff<M>::v, nelem) : (nelem + FSM_TILE - 1) / FSM_TILE;
     const uint64_t nt = ntiles ? ntiles : 1;
@@ -5865,7 +6431,10 @@ static int fsm_run(dc_ctx *c, const uint8_t *d_in, uint64_t len, uint64_t nelem,
         HIPCHK(hipMemcpyAsync(c->d_summ, idn, sizeof(uint4), hipMemcpyHostToDevice, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
     } else {
-        if constexpr (SmMode<M>::fast) LAUNCH(c, name, k_small_tiles<M>, ntiles, 256, d_in, len, nelem, c->d_summ);
+        if (M == M_SMALL_DEC && gexp)
+            LAUNCH(c, "small_dec_summ", k_small_dec_summ, (ntiles + 255) / 256, 256, gexp, ngroups, d_in, len, ntiles,
+                   c->d_summ, c->d_meta);
+        else if constexpr (SmMode<M>::fast) LAUNCH(c, name, k_small_tiles<M>, ntiles, 256, d_in, len, nelem, c->d_summ);
         else LAUNCH(c, name, k_fsm_tiles<M>, ntiles, 256, d_in, len, nelem, c->d_summ, aux);
         LAUNCH(c, "fsm_scan_up", k_fsm_scan_up, ng, FSM_GROUP, c->d_summ, ntiles, gsum);
         LAUNCH(c, "fsm_scan", k_fsm_scan, 1, 1024, (const uint4 *)gsum, ng, c->d_entry, c->d_meta, aux.s_init);
@@ -5879,8 +6448,9 @@ static int fsm_run(dc_ctx *c, const uint8_t *d_in, uint64_t len, uint64_t nelem,
             LAUNCH(c, FsmMode<M>::wname, k_fsm_write<M>, wgrid, 256, d_in, len, nelem, (const uint64_t *)c->d_entry,
                    (const uint4 *)c->d_summ, (const uint64_t *)c->d_meta, d_out, aux);
     }
-    HIPCHK(hipMemcpyAsync(c->h_pinned, c->d_meta, 6 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(c->h_pinned, c->d_meta, 9 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
+    if (gexp && c->h_pinned[8] != 8) return DC_E_STREAM;   // (dc_small_huff_decode: not a type-8 stream)
     if (h_plan) for (int k = 0; k < 4; ++k) h_plan[k] = c->h_pinned[2 + k];
     c->fsm_in = write ? nullptr : d_in; c->fsm_len = len; c->fsm_nelem = nelem; c->fsm_mode = M;
     const bool nyb = M == M_NYB_ENC;
@@ -6303,6 +6873,25 @@ int dc_small_decompress_body(dc_ctx *c, const uint8_t *d_in, uint64_t m, uint8_t
     if (!c || !d_out || !h_len || (m && !d_in)) return DC_E_ARG;
     if (m == 0) { *h_len = 0; return DC_OK; }
     return fsm_run<M_SMALL_DBODY>(c, d_in, m, m, d_out, h_len, "small_dbody_tiles");
+}
+
+int dc_small_huff_decode(dc_ctx *c, const uint32_t *d_words, uint64_t bit_base, uint64_t words,
+                         const uint64_t *d_sync_base, const uint16_t *d_sync_len, uint32_t S, uint64_t m,
+                         const dc_dtable *d_table, uint8_t *d_m, uint8_t *d_out, uint64_t *h_len)
+{
+    if (!c || !d_m || !d_out || !h_len) return DC_E_ARG;
+    if (S != 64 || m < 2 || ((uintptr_t)d_m & 15) || c->opt_decode_general) {   // the two stages as they are
+        const int r = decode_impl(c, d_words, bit_base, nullptr, words, d_sync_base, d_sync_len, S, m, d_table, d_m);
+        return r ? r : dc_small_decompress(c, d_m, m, d_out, h_len);
+    }
+    const uint64_t groups = dc_huff_sync_groups(m, 64);
+    if (ensure((void **)&c->d_gexp, &c->gexp_cap, (groups + 2) * sizeof(uint32_t))) return DC_E_HIP;
+    int r = decode_impl(c, d_words, bit_base, nullptr, words, d_sync_base, d_sync_len, 64, m, d_table, d_m, c->d_gexp);
+    if (r) return r;
+    r = fsm_run<M_SMALL_DEC>(c, d_m, m, m - 2, d_out, h_len, "small_dec_tiles", FsmAux{nullptr, 0, 0, 1, 1}, nullptr,
+                             true, c->d_gexp, groups);
+    if (r == DC_E_STREAM) return dc_small_decompress(c, d_m, m, d_out, h_len);   // not a type-8 stream
+    return r;
 }
 
 int dc_small_decompress(dc_ctx *c, const uint8_t *d_in, uint64_t m, uint8_t *d_out, uint64_t *h_len)

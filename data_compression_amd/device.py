@@ -445,6 +445,82 @@ class Codec:
     def decode_into(self, enc, out):
         self.decode(enc["words"], enc["bit_base"], enc["sync"], enc["S"], enc["n"], enc["table"], out)
 
+    # ---- C5 fused front-end encode (small_compression.c front-end, then Huffman; one pass) -----
+    def small_huff_plan(self, x, n_ary: int = 16, max_symbol_value: int = 258, hist=None, table=None, total=None):
+        """dc_small_huff_plan: histogram of the front-end output of x (never written), table and
+        plan total in one launch. Returns (hist, table, total); DcError DC_E_FALLBACK for n < 2."""
+        hist = hist if hist is not None else self._t(256, torch.int64)
+        table = table if table is not None else self._t(self.table_bytes)
+        total = total if total is not None else self._t(1, torch.int64)
+        check("dc_small_huff_plan", self.L.dc_small_huff_plan(self.ctx, _ptr(x), x.numel(), max_symbol_value, n_ary,
+                                                              _ptr(hist), _ptr(table), _ptr(total)))
+        self._last_total = total
+        return hist, table, total
+
+    def small_huff_pack_async(self, x, tab, bit_base, words, sync, sync_syms):
+        base, lens = sync
+        check("dc_small_huff_pack_async",
+              self.L.dc_small_huff_pack_async(self.ctx, _ptr(x), x.numel(), _ptr(tab), bit_base, _ptr(words),
+                                              words.numel(), _ptr(base), _ptr(lens), sync_syms))
+
+    def small_huff_symbols(self) -> int:
+        v = C.c_uint64(0)
+        check("dc_small_huff_symbols", self.L.dc_small_huff_symbols(self.ctx, C.byref(v)))
+        return int(v.value)
+
+    def small_huff_encode(self, x, n_ary: int = 16, sync_syms: int = 64, bit_base: int = 0, words=None, sync=None):
+        """The C5 encode of device bytes x: the front-end (small_compression.c:582-665) and the
+        n-ary Huffman code of its output M in one pass over x, M never written. Returns the
+        dict of encode() for M ("n" = symbols of M) with "fused": True, bit-identical to
+        small_compress + encode. When the fused path does not apply (DC_E_FALLBACK: LITERAL
+        output, every byte value present in M, an over-long block) the two stages run and
+        "fused" is False. words / sync: optional preallocated buffers (sync for n + 1 symbols)."""
+        n = x.numel()
+        try:
+            hist, tab, total = self.small_huff_plan(x, n_ary)
+        except DcError as e:
+            if e.rc != -8:
+                raise
+            return self._small_huff_two_stage(x, n_ary, sync_syms, bit_base)
+        bits = int(total.item())
+        need = self.words_needed(bit_base, bits)
+        if words is None or words.numel() < need:
+            words = self._t(need, torch.int32)
+        sync = sync if sync is not None else self.alloc_sync(n + 1, sync_syms)
+        self.small_huff_pack_async(x, tab, bit_base, words, sync, sync_syms)
+        st = self.pack_status(tab)
+        if st == -8:
+            return self._small_huff_two_stage(x, n_ary, sync_syms, bit_base)
+        check("dc_small_huff_pack_async", st)
+        return {"hist": hist, "table": tab, "bits": bits, "words": words, "sync": sync, "S": sync_syms,
+                "bit_base": bit_base, "n": self.small_huff_symbols(), "fused": True}
+
+    def _small_huff_two_stage(self, x, n_ary, sync_syms, bit_base):
+        fe = self._t(x.numel() + 64)
+        m = C.c_uint64(0)
+        check("dc_small_compress", self.L.dc_small_compress(self.ctx, _ptr(x), x.numel(), _ptr(fe), C.byref(m)))
+        enc = self.encode(fe[: m.value], n_ary=n_ary, sync_syms=sync_syms, bit_base=bit_base)
+        enc["fused"] = False
+        return enc
+
+    def small_huff_decode(self, enc, out=None, mbuf=None):
+        """Huffman decode of M, then the front-end inverse (dc_small_huff_decode: the inverse
+        takes the decoder's per-group counts instead of a counting pass of its own): the input
+        bytes, a view of out (>= 2 * enc["n"] bytes) when given. mbuf: optional buffer for M."""
+        m = enc["n"]
+        mbuf = mbuf if mbuf is not None else self._t(max(m, 1) + 16)
+        out = self._dec_out(mbuf[: m], out)
+        n = C.c_uint64(0)
+        base, lens = enc["sync"]
+        bb = enc["bit_base"]
+        if hasattr(bb, "data_ptr"):   # (device-resident offset: the two stages)
+            self.decode(enc["words"], bb, enc["sync"], enc["S"], m, enc["table"], mbuf)
+            return self.small_decompress(mbuf[: m], out=out)
+        check("dc_small_huff_decode", self.L.dc_small_huff_decode(
+            self.ctx, _ptr(enc["words"]), bb, enc["words"].numel(), _ptr(base), _ptr(lens), enc["S"], m,
+            _ptr(enc["table"]), _ptr(mbuf), _ptr(out), C.byref(n)))
+        return out[: n.value]
+
     # ---- allocation helpers (the engine interface used by dist.ShardedHuffman) -----------
     def alloc_words(self, bit_base: int, bits: int):
         return self._t(self.words_needed(bit_base, bits), torch.int32)

@@ -358,16 +358,64 @@ class ShardedSmall:
             w.wait()
 
     def encode(self, x, n_ary: int = 16, sync_syms: int = 64):
+        if self.world == 1 and hasattr(self.e, "small_huff_plan") and x.numel() >= 2:
+            s = self._encode_fused(x, n_ary, sync_syms)
+            if s is not None:
+                return s
         seg, literal = self.frontend(x, sync_syms)
         s = self.h.encode(seg, n_ary=n_ary, sync_syms=sync_syms)
         s.literal = literal
         return s
 
+    def _encode_fused(self, x, n_ary, S):
+        """World size 1: the front-end and the Huffman code in one pass over x, the front-end
+        output never written (dc_small_huff_plan + dc_small_huff_pack_async): the stream equals
+        frontend() + ShardedHuffman.encode() bit for bit. None when the fused path does not
+        apply (LITERAL output, every byte value present, DC_E_FALLBACK): the caller runs the
+        two stages. Buffers are kept across calls of the same size."""
+        from ._lib import DcError
+        n = x.numel()
+        key = (n, S)
+        buf = getattr(self, "_fbuf", None)
+        if buf is None or buf["key"] != key:
+            buf = self._fbuf = {"key": key, "hist": self.e._t(256, torch.int64), "tab": self.e.alloc_table(),
+                                "total": self.e._t(1, torch.int64), "sync": self.e.alloc_sync(n + 1, S),
+                                "words": None}
+        try:
+            _, tab, tot = self.e.small_huff_plan(x, n_ary, hist=buf["hist"], table=buf["tab"], total=buf["total"])
+        except DcError as err:
+            if err.rc != -8:
+                raise
+            return None
+        bits = int(tot.item())
+        need = self.e.words_needed(0, bits)
+        if buf["words"] is None or buf["words"].numel() < need:
+            buf["words"] = self.e._t(need + need // 16, torch.int32)
+        gen = self.e.plan_gen()
+        self.e.small_huff_pack_async(x, tab, 0, buf["words"], buf["sync"], S)
+        st = self.e.pack_status(tab, gen)
+        if st == -8:
+            return None
+        if st != 0:
+            raise RuntimeError(f"dc_small_huff_pack_async failed with status {st}")
+        s = ShardStream(buf["words"], 0, bits, buf["sync"], S, self.e.small_huff_symbols(), tab, None, tot, gen)
+        s.literal = False
+        return s
+
     def decode(self, s, out=None):
         """out: optional buffer of >= 2 * s.n bytes for the front-end inverse (the result is a
         view of it, or of the Huffman output when a later rank's segment is LITERAL)."""
-        seg = self.h.decode(s)[: s.n]
         kw = {} if out is None else {"out": out}
+        if self.world == 1 and not s.literal and hasattr(self.e, "small_huff_decode") and isinstance(s.bit_base, int):
+            # world 1: the decoder counts the pair symbols per group, and the front-end inverse
+            # takes those counts (dc_small_huff_decode: no counting pass over the decoded stream)
+            enc = {"words": s.words, "bit_base": s.bit_base, "sync": s.sync, "S": s.sync_syms, "n": s.n,
+                   "table": s.table}
+            mb = getattr(self, "_mbuf", None)
+            if mb is None or mb.numel() < s.n + 16:
+                mb = self._mbuf = self.e.alloc_bytes(s.n + 16)
+            return self.e.small_huff_decode(enc, mbuf=mb, **kw)
+        seg = self.h.decode(s)[: s.n]
         if self.rank == 0:
             return self.e.small_decompress(seg, **kw)
         return seg if s.literal else self.e.small_decompress_body(seg, **kw)

@@ -33,7 +33,8 @@ enum {
     DC_E_NOCODE = -4,        /* the input holds a byte that has no code */
     DC_E_STATE = -5,         /* stage called out of order (e.g. pack before hist of that input) */
     DC_E_CAPACITY = -6,      /* output buffer too small */
-    DC_E_STREAM = -7         /* corrupt compressed stream */
+    DC_E_STREAM = -7,        /* corrupt compressed stream */
+    DC_E_FALLBACK = -8       /* the fused C5 path does not apply to this input: run the two stages */
 };
 
 #define DC_BLOCK_BYTES 32768u   /* encoder block: one histogram + one bit offset each */
@@ -208,6 +209,35 @@ int dc_huff_pack_status(dc_ctx *ctx, const dc_dtable *d_table);
  * for it. DC_E_STATE when more than 30 plans have run since (its flags are recycled). */
 uint32_t dc_huff_plan_gen(dc_ctx *ctx);
 int dc_huff_pack_status_gen(dc_ctx *ctx, const dc_dtable *d_table, uint32_t gen);
+/* C5 fused front-end encode (small_compression.c:582-665 front-end, then n-ary Huffman of its
+ * output M), without M ever written to memory: the stream and sync index are exactly those of
+ * dc_small_compress followed by dc_huff_encode_plan + dc_huff_pack_async on M (the same payload
+ * bits, the same sync chunks of S symbols of M), from the input bytes d_in (16-B aligned, n >= 2).
+ * (1-3) the histogram of M per 32 KiB block of the input, the table and the plan total in one
+ *     launch (as dc_huff_encode_plan);
+ * (4) two plan launches (block bit offsets, each block's first symbol index, the sync-length
+ *     words of chunks spanning block boundaries zeroed) and the pack. d_sync_len (4-B aligned)
+ *     and d_sync_base are required, sized for dc_small_huff_symbols() symbols: at most n + 1.
+ * dc_huff_pack_status then returns DC_E_FALLBACK (nothing usable written) when the front-end
+ * output falls back to LITERAL (small_compression.c:655-662), when every byte value occurs in
+ * M (the pack marks a pair's start with a byte value that has no code), or when a 32 KiB block
+ * codes to more bits than the pack's stage holds beside its sync list; the caller then runs
+ * the two stages. dc_small_huff_symbols reads the symbol count of M (synchronising). */
+int dc_small_huff_plan(dc_ctx *ctx, const uint8_t *d_in, uint64_t n, int max_symbol_value, int n_ary,
+                       uint64_t *d_hist, dc_dtable *d_table, uint64_t *d_total_bits);
+int dc_small_huff_pack_async(dc_ctx *ctx, const uint8_t *d_in, uint64_t n, const dc_dtable *d_table,
+                             uint64_t bit_base, uint32_t *d_words, uint64_t words_cap,
+                             uint64_t *d_sync_base, uint16_t *d_sync_len, uint32_t sync_syms);
+int dc_small_huff_symbols(dc_ctx *ctx, uint64_t *h_symbols);
+/* C5 decode: the Huffman decode of the m-symbol front-end stream M into d_m (16-B aligned,
+ * >= m bytes), counting the symbols >= 0x80 of every group of 64 chunks on the way (S = 64), then
+ * the front-end inverse (small_compression.c's decompress_bytestring, dc_small_decompress) into
+ * d_out (>= 2 m bytes) from those counts, without the inverse's own counting pass over M. *h_len =
+ * the decoded length (synchronising). Other sync sizes, a LITERAL stream or an unaligned d_m
+ * take the two stages unchanged. */
+int dc_small_huff_decode(dc_ctx *ctx, const uint32_t *d_words, uint64_t bit_base, uint64_t words,
+                         const uint64_t *d_sync_base, const uint16_t *d_sync_len, uint32_t sync_syms, uint64_t m,
+                         const dc_dtable *d_table, uint8_t *d_m, uint8_t *d_out, uint64_t *h_len);
 /* Status word written by the table / plan kernels (host-synchronising read). */
 int dc_huff_table_status(dc_ctx *ctx, const dc_dtable *d_table, int32_t *max_bits);
 /* (5) decode n symbols. d_words/bit_base and the sync index as written by pack. The
