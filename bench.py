@@ -48,6 +48,9 @@ def parse():
     ap.add_argument("--cfg", default="C2")
     ap.add_argument("--frontend", action="store_true",
                     help="C5 pipeline: small_compression.c front-end, then n-ary Huffman (dist.ShardedSmall)")
+    ap.add_argument("--two-stage", action="store_true",
+                    help="C5 at one GPU: the front-end and the Huffman code as two passes (default: the fused "
+                         "one-pass encode and the counted decode, dc_small_huff_*)")
     ap.add_argument("--nary", type=int, default=2)
     ap.add_argument("--size", type=int, default=1 << 30, help="bytes per GPU")
     ap.add_argument("--sync", type=int, default=0, help="sync-index granularity (0 = default)")
@@ -125,7 +128,7 @@ def main():
 
     if a.frontend:   # C5: front-end bodies + halo/LITERAL/re-cut exchanges, then sharded Huffman
         from data_compression_amd.dist import ShardedSmall
-        ss = ShardedSmall(c, table_mode=a.table_mode)
+        ss = ShardedSmall(c, table_mode=a.table_mode, fused=not a.two_stage)
 
         def encode():   # noqa: F811
             state["s"] = ss.encode(x, a.nary, S)
@@ -274,7 +277,7 @@ def main():
                                + ("small front-end + " if a.frontend else "")
                                + f"n={a.nary} Huffman encode+decode"
                                + (" (configs[1] generator at the metric's 1 GiB)" if a.cfg == "C2" else ""),
-                   "frontend": bool(a.frontend),
+                   "frontend": bool(a.frontend), "fused": bool(a.frontend and world == 1 and not a.two_stage),
                    "bytes_per_gpu": n, "n_ary": a.nary, "sync_syms": S,
                    "parallelism": f"shard{world}" if world > 1 else "single"},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK / 1e9,
@@ -430,7 +433,11 @@ def main_nybble(a, dev, rank, world):
     dom_bytes = alg.get(dom, n)
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
     wl = f"C1-nyb-{a.mode}"
-    traffic, traffic_src = pmc_traffic("k_" + dom, argparse.Namespace(cfg=wl, nary=0), n)
+    # the timed stage's kernel as the PMC summary names it (template argument = the transducer mode)
+    kname = {"nyb_enc_tiles": "k_fsm_tiles<0>", "nyb_enca_tiles": "k_fsm_tiles<0>", "nyb_enc_write": "k_fsm_write<0>",
+             "nyb_dec_tiles": "k_fsm_tiles<1>", "nyb_dec_write": "k_fsm_write<1>", "mtf_tiles": "k_mtf_walk<0>",
+             "mtf_ranks": "k_mtf_walk<1>"}.get(dom, "k_" + dom)
+    traffic, traffic_src = pmc_traffic(kname, argparse.Namespace(cfg=wl, nary=0), n)
     kern_sum = sum(float(np.sum(v)) for v in per.values()) / a.profile_steps
     enc_frac = (n + m) / (enc_ms * 1e-3) / HBM_PEAK
     res = {

@@ -109,9 +109,10 @@ static __device__ __forceinline__ uint32_t swar_lower(uint32_t x)   // 'a' <= by
 // is < 0x80) and the start position carries no symbol (in the pack: a byte value z with no
 // code, 0 bits). The M order is unchanged: nothing lies between a pair's two positions.
 // ------------------------------------------------------------------------------------
-// The shifts run with every lane active: a DPP read of a lane that EXEC disables returns 0,
-// and a select such as `lane == 0 ? a : dpp(x)` was compiled as a branch that ran the DPP
-// with lane 0 off, so lane 1 read 0 (the opaque asm keeps the shift out of any branch).
+// The shifts must run with every lane active: a DPP read of a lane that EXEC disables returns
+// 0. `lane == 0 ? a : dpp_wave_shr1(x)` is lowered as a branch (the call has a side effect),
+// which ran the DPP with lane 0 off, so lane 1 read 0: call them as statements of their own
+// (the opaque asm then keeps them from being sunk into a branch).
 static __device__ __forceinline__ uint32_t dpp_wave_shr1(uint32_t x)   // lane l <- lane l - 1 (lane 0: 0)
 {
     uint32_t r = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x138, 0xf, 0xf, false);
@@ -244,8 +245,10 @@ __global__ __launch_bounds__(256) void k_hist_blocks(const uint8_t *__restrict__
                 uint32_t w4[4] = {cur[k].x, cur[k].y, cur[k].z, cur[k].w};
                 if (FE) {   // pair seconds -> letter | 0x80; count the starts
                     const uint64_t p = b * (uint64_t)DC_BLOCK_BYTES + (uint64_t)k * 4096 + (uint64_t)t * 16;
-                    const uint32_t pb = lane == 0 ? ce[k] >> 24 : dpp_wave_shr1(w4[3]) >> 24;
-                    const uint32_t qb = lane == 63 ? (p + 16 < n ? ce[k] & 255u : 0u) : dpp_wave_shl1(w4[0]) & 255u;
+                    // (the shifts as statements of their own: inside `?:` they ran in a branch, lane 0 off)
+                    const uint32_t pd = dpp_wave_shr1(w4[3]), qd = dpp_wave_shl1(w4[0]);
+                    const uint32_t pb = lane == 0 ? ce[k] >> 24 : pd >> 24;
+                    const uint32_t qb = lane == 63 ? (p + 16 < n ? ce[k] & 255u : 0u) : qd & 255u;
                     uint32_t st[4];
                     fe_pair_starts(w4, qb, st);
                     if (p == 0) st[0] &= ~0x80u;   // position 0 never starts a pair
@@ -1782,8 +1785,9 @@ __global__ __launch_bounds__(256) void k_fe_pack(const uint8_t *__restrict__ in,
         for (int k = 0; k < PACK_PIECES; ++k) {
             const uint64_t p = blk_start + (uint64_t)k * PACK_TILE + (uint64_t)t * 16;
             uint32_t w4[4] = {blkv[k].x, blkv[k].y, blkv[k].z, blkv[k].w};
-            const uint32_t pb = lane == 0 ? ve[k] >> 24 : dpp_wave_shr1(w4[3]) >> 24;
-            const uint32_t qb = lane == 63 ? (p + 16 < n ? ve[k] & 255u : 0u) : dpp_wave_shl1(w4[0]) & 255u;
+            const uint32_t pd = dpp_wave_shr1(w4[3]), qd = dpp_wave_shl1(w4[0]);   // (statements of their own)
+            const uint32_t pb = lane == 0 ? ve[k] >> 24 : pd >> 24;
+            const uint32_t qb = lane == 63 ? (p + 16 < n ? ve[k] & 255u : 0u) : qd & 255u;
             uint32_t st[4];
             fe_pair_starts(w4, qb, st);
             if (p == 0) st[0] &= ~0x80u;   // position 0 never starts a pair

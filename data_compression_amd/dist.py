@@ -254,11 +254,14 @@ class ShardedSmall:
     stateless); the ranks' decoded segments concatenate to the input.
     """
 
-    def __init__(self, engine, group=None, table_mode: str = "replicate", table_src: int = 0):
+    def __init__(self, engine, group=None, table_mode: str = "replicate", table_src: int = 0, fused: bool = True):
+        """fused: at world size 1, the one-pass encode and the counted decode (dc_small_huff_*)
+        when the engine has them; False keeps the two stages (front-end, then Huffman)."""
         self.e = engine
         self.h = ShardedHuffman(engine, group, table_mode=table_mode, table_src=table_src)
         self.group = group
         self.world, self.rank = self.h.world, self.h.rank
+        self.fused = fused
 
     def _gather_i64(self, vals):
         t = torch.tensor(vals, dtype=torch.int64, device=self._dev)
@@ -358,7 +361,7 @@ class ShardedSmall:
             w.wait()
 
     def encode(self, x, n_ary: int = 16, sync_syms: int = 64):
-        if self.world == 1 and hasattr(self.e, "small_huff_plan") and x.numel() >= 2:
+        if self.fused and self.world == 1 and hasattr(self.e, "small_huff_plan") and x.numel() >= 2:
             s = self._encode_fused(x, n_ary, sync_syms)
             if s is not None:
                 return s
@@ -406,7 +409,8 @@ class ShardedSmall:
         """out: optional buffer of >= 2 * s.n bytes for the front-end inverse (the result is a
         view of it, or of the Huffman output when a later rank's segment is LITERAL)."""
         kw = {} if out is None else {"out": out}
-        if self.world == 1 and not s.literal and hasattr(self.e, "small_huff_decode") and isinstance(s.bit_base, int):
+        if (self.fused and self.world == 1 and not s.literal and hasattr(self.e, "small_huff_decode")
+                and isinstance(s.bit_base, int)):
             # world 1: the decoder counts the pair symbols per group, and the front-end inverse
             # takes those counts (dc_small_huff_decode: no counting pass over the decoded stream)
             enc = {"words": s.words, "bit_base": s.bit_base, "sync": s.sync, "S": s.sync_syms, "n": s.n,

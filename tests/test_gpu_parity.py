@@ -690,14 +690,16 @@ def _small_body_decode_ref(b):
     return bytes(out)
 
 
-def test_sharded_small_single_rank_on_device(torch_cuda, codec):
+@pytest.mark.parametrize("fused", [True, False])
+def test_sharded_small_single_rank_on_device(torch_cuda, codec, fused):
     """dist.ShardedSmall with the device engine (world size 1): C5 front-end + n=16
-    Huffman equals the oracle's encoding of the reference front-end output; round trip."""
+    Huffman equals the oracle's encoding of the reference front-end output; round trip. Both
+    the one-pass encode + counted decode (dc_small_huff_*) and the two stages."""
     from data_compression_amd import synth
     from data_compression_amd.dist import ShardedSmall
     torch = torch_cuda
     x = synth.log_like(1 << 20, seed=13)
-    sm = ShardedSmall(codec)
+    sm = ShardedSmall(codec, fused=fused)
     s = sm.encode(torch.from_numpy(x).cuda(), n_ary=16, sync_syms=64)
     fe = np.frombuffer(orc.small_compress(x.tobytes()), np.uint8)
     L, el, ev, code, nb, mx = _oracle_encode(fe, 16)

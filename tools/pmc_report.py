@@ -12,7 +12,9 @@ vals = defaultdict(lambda: defaultdict(list))
 for f in sorted(glob.glob(os.path.join(root, "p*", "run_counter_collection.csv"))):
     per = defaultdict(float)
     for r in csv.DictReader(open(f)):
-        k = r["Kernel_Name"].split("(")[0].replace("void ", "").split("<")[0].strip()
+        k = r["Kernel_Name"].split("(")[0].replace("void ", "").strip()
+        if not os.environ.get("PMC_KEEP_TEMPLATE"):   # (nybble: k_fsm_write<0> and <1> are two kernels)
+            k = k.split("<")[0]
         if k == "k_huff_decode8_fix":       # the exact redo of flagged chunks
             k = "k_huff_decode_fix"
         elif k.startswith("k_huff_decode"):   # k_huff_decode8<NW, NC> is the decode launch
@@ -35,7 +37,7 @@ for k in (list(want) + sorted(set(vals) - set(want))):
 if len(sys.argv) > 2:
     import json
     out = {}
-    for k in want:
+    for k in (sorted(vals) if os.environ.get("PMC_ALL") else want):
         if k in vals and "FETCH_SIZE" in vals[k] and "WRITE_SIZE" in vals[k]:
             f = sum(vals[k]["FETCH_SIZE"]) / len(vals[k]["FETCH_SIZE"]) * 1024 * 2
             w = sum(vals[k]["WRITE_SIZE"]) / len(vals[k]["WRITE_SIZE"]) * 1024
