@@ -492,8 +492,10 @@ class Codec:
         if st == -8:
             return self._small_huff_two_stage(x, n_ary, sync_syms, bit_base)
         check("dc_small_huff_pack_async", st)
-        return {"hist": hist, "table": tab, "bits": bits, "words": words, "sync": sync, "S": sync_syms,
-                "bit_base": bit_base, "n": self.small_huff_symbols(), "fused": True}
+        m = self.small_huff_symbols()
+        ng, nch = self.sync_sizes(m, sync_syms)   # the index of m symbols (the buffers hold n + 1)
+        return {"hist": hist, "table": tab, "bits": bits, "words": words, "S": sync_syms, "bit_base": bit_base,
+                "sync": (sync[0][: max(ng, 1)], sync[1][: max(nch, 1)]), "n": m, "fused": True}
 
     def _small_huff_two_stage(self, x, n_ary, sync_syms, bit_base):
         fe = self._t(x.numel() + 64)

@@ -401,7 +401,10 @@ class ShardedSmall:
             return None
         if st != 0:
             raise RuntimeError(f"dc_small_huff_pack_async failed with status {st}")
-        s = ShardStream(buf["words"], 0, bits, buf["sync"], S, self.e.small_huff_symbols(), tab, None, tot, gen)
+        m = self.e.small_huff_symbols()
+        ng, nch = self.e.sync_sizes(m, S)   # the index of m symbols (the buffers hold n + 1)
+        sync = (buf["sync"][0][: max(ng, 1)], buf["sync"][1][: max(nch, 1)])
+        s = ShardStream(buf["words"], 0, bits, sync, S, m, tab, None, tot, gen)
         s.literal = False
         return s
 
