@@ -4145,8 +4145,24 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
     __shared__ __attribute__((aligned(16))) uint8_t s_out[2 * FSM_TILE + 32];
     __shared__ __attribute__((aligned(4))) uint8_t s_rank[256];
     __shared__ __attribute__((aligned(4))) uint8_t s_dump[4 * 256];   // a lane's unused byte stores
+    __shared__ uint2 s_esel[M == M_NYB_ENC ? 256 : 1];   // encode: v_perm selectors per 4-element pattern
     const int t = threadIdx.x;
     if (M == M_NYB_ENC && !aux.rk) fsm_rank_table(s_rank);
+    if (M == M_NYB_ENC) {
+        // pattern t = c1 | c2 << 4 (bit i: element i writes its first / its second byte): the
+        // output bytes in order, first byte i = selector i (S1 = the first bytes), second byte
+        // i = selector 4 + i (S0 = the elements' own bytes); 0x0c = a zero byte
+        uint32_t sel[2] = {0x0c0c0c0cu, 0x0c0c0c0cu};
+        int o = 0;
+        for (int i = 0; i < 4; ++i) {
+            if ((t >> i) & 1) { sel[o >> 2] = (sel[o >> 2] & ~(255u << (8 * (o & 3)))) | ((uint32_t)i << (8 * (o & 3))); ++o; }
+            if ((t >> (4 + i)) & 1) {
+                sel[o >> 2] = (sel[o >> 2] & ~(255u << (8 * (o & 3)))) | ((uint32_t)(4 + i) << (8 * (o & 3)));
+                ++o;
+            }
+        }
+        s_esel[t] = make_uint2(sel[0], sel[1]);
+    }
     const bool nyb_whole = M == M_NYB_ENC && aux.whole;
     const bool enc = FsmMode<M>::enc || nyb_whole;
     const uint64_t body = (M == M_NYB_ENC) ? meta[0] + (aux.is_last ? meta[1] : 0) : meta[0];
@@ -4271,32 +4287,50 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
                     out[o0 + before] = (uint8_t)(w >> (8 * ((kt + 1) & 3)));
                 }
             }
-            // Each element's 0-2 bytes go straight into the stage at their own offset (the count
-            // of bytes before them: a running sum, no serial shift-accumulate): 1 - h + s bytes,
-            // the first = s ? (h ? pair : prev) : x, the second (a miss after a pending hit) = x.
-            // Every byte of the tile's output is written exactly once (no zeroed stage, no ORs).
-            // (r3's 64-bit accumulator with a dword flush every 2 elements: ~26 VALU per element,
-            // the kernel VALU-issue bound at 1.28 ms per GiB)
-            // (no branches: a byte an element does not write goes to this lane's dump slot, so
-            // both stores issue unconditionally, with no exec-mask juggling per element)
-            uint8_t *const so = s_out + P;
-            uint8_t *const dump = s_dump + 4 * t;
+            // Each element writes 0-2 bytes: its first byte (a miss, or any element after a
+            // pending hit) = s ? (h ? pair : prev) : x, its second (a miss after a pending hit) = x.
+            // Four elements at a time in SWAR: the dword of their first bytes B1 and of their own
+            // bytes X, then two v_perm place their 0-8 output bytes in order (selectors by the
+            // 8-bit pattern of who writes what, s_esel), and the lane's run advances by whole
+            // dwords OR-ed into the zeroed stage at its bit offset (the partial last dword too:
+            // ORs are idempotent, so the pending bits are OR-ed again with the next ones).
+            // ~9 VALU per element. (r4's per-element byte stores at a running offset: ~25 VALU and
+            // 2 LDS byte stores per element; r3's 64-bit accumulator flushed every 2 elements ~26.)
             const uint32_t C1 = ~Hx | Sx, C2 = ~Hx & Sx;   // element writes its first / second byte
-            uint32_t pos = 0;
+            uint32_t RK[4];                                 // ranks, 4 bytes per dword (element order)
 #pragma unroll
-            for (int k = 0; k < 16; ++k) {
-                const uint32_t x = W.b(k + 1), prev = W.b(k);
-                const uint32_t hm = 0u - ((Hx >> k) & 1u), sm = 0u - ((Sx >> k) & 1u);   // all-ones masks
-                const uint32_t rq = (k ? rk[k - 1] : rp0) & 7u;
-                const uint32_t pair = 0x88u | (rq << 4) | (rk[k] & 7u);   // the pending hit, then this one
-                // s ? (h ? pair : prev) : x, as bit selects (a ternary became a branch)
-                const uint32_t b1 = (x & ~sm) | (sm & ((pair & hm) | (prev & ~hm)));
-                const uint32_t c1 = (C1 >> k) & 1u, c2 = (C2 >> k) & 1u;
-                *(c1 ? so + pos : dump) = (uint8_t)b1;
-                *(c2 ? so + pos + 1 : dump + 1) = (uint8_t)x;
-                pos += c1 + c2;
+            for (int q = 0; q < 4; ++q)
+                RK[q] = (rk[4 * q] & 255u) | ((rk[4 * q + 1] & 255u) << 8) | ((rk[4 * q + 2] & 255u) << 16) |
+                        ((rk[4 * q + 3] & 255u) << 24);
+            uint32_t pend = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t X = __builtin_amdgcn_alignbyte(W.w[q + 1], W.w[q], 1u);   // elements 4q..4q+3
+                const uint32_t PV = W.w[q];                                                 // the bytes before them
+                const uint32_t RQ = __builtin_amdgcn_alignbyte(RK[q], q ? RK[q - 1] : rp0 << 24, 3u);
+                const uint32_t PR = 0x88888888u | ((RQ & 0x07070707u) << 4) | (RK[q] & 0x07070707u);
+                // bits 4q..4q+3 of a mask -> 0xFF per byte
+                auto bytes = [](uint32_t m4) {
+                    const uint32_t u = (m4 * 0x204081u) & 0x01010101u;
+                    return (u << 8) - u;
+                };
+                const uint32_t HM = bytes((Hx >> (4 * q)) & 15u), SM = bytes((Sx >> (4 * q)) & 15u);
+                const uint32_t B1 = (X & ~SM) | (SM & ((PR & HM) | (PV & ~HM)));
+                const uint32_t c1 = (C1 >> (4 * q)) & 15u, c2 = (C2 >> (4 * q)) & 15u;
+                const uint2 sl = s_esel[c1 | (c2 << 4)];
+                const uint32_t lo = __builtin_amdgcn_perm(X, B1, sl.x), hi = __builtin_amdgcn_perm(X, B1, sl.y);
+                const uint32_t L = 8u * (uint32_t)(__popc(c1) + __popc(c2));   // bits out (0..64)
+                const uint64_t l64 = (uint64_t)lo << nb, h64 = (uint64_t)hi << nb;
+                atomicOr(&s_out32[di], pend | (uint32_t)l64);
+                const uint32_t d1 = (uint32_t)(l64 >> 32) | (uint32_t)h64, d2 = (uint32_t)(h64 >> 32);
+                const uint32_t nt = nb + L;   // 0..88
+                if (nt > 32u) atomicOr(&s_out32[di + 1], d1);
+                if (nt > 64u) atomicOr(&s_out32[di + 2], d2);
+                pend = nt >= 64u ? d2 : nt >= 32u ? d1 : (pend | (uint32_t)l64);
+                di += nt >> 5;
+                nb = nt & 31u;
             }
-            nb = 0;   // (nothing left in the accumulator)
+            nb = 0;   // (every bit is in the stage)
         } else {   // M_NYB_DEC / M_NYB_DBODY: compressed byte x, state s = "at the low nybble"
             // (r2's element loop: per element branches measured 1-3% faster here than the
             // encoder's branch-free form, same-box A/B tools/gpu_r3n.sh)
@@ -4552,8 +4586,22 @@ __global__ __launch_bounds__(SmMode<M>::wthreads) void k_small_write(const uint8
     __shared__ uint32_t s_w[NW];
     __shared__ uint8_t s_first[NW], s_last[NW], s_before, s_after;
     __shared__ __attribute__((aligned(16))) uint32_t s_out[SW];
+    __shared__ uint2 s_sel[16];   // decode: v_perm selectors of the 4-8 output bytes of a dword, per pair pattern
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const bool enc = M == M_SMALL_ENC;
+    if (dec && t < 16) {   // pattern t (bit i: byte i >= 0x80): byte i -> ' ' (S1) then byte i & 0x7F (S0),
+        uint32_t sel[2] = {0x0c0c0c0cu, 0x0c0c0c0cu};   // else byte i (S0); 0x0c = a zero byte
+        int o = 0;
+        for (int i = 0; i < 4; ++i) {
+            if ((t >> i) & 1) {
+                sel[o >> 2] = (sel[o >> 2] & ~(255u << (8 * (o & 3)))) | (0u << (8 * (o & 3)));
+                ++o;
+            }
+            sel[o >> 2] = (sel[o >> 2] & ~(255u << (8 * (o & 3)))) | ((uint32_t)(4 + i) << (8 * (o & 3)));
+            ++o;
+        }
+        s_sel[t] = make_uint2(sel[0], sel[1]);
+    }
     const uint64_t total = enc ? 2 + meta[0] : 1 + meta[0];
     if (enc && total >= len) {   // LITERAL: ' ' + raw input (:655-662), one grid-stride pass
         for (uint64_t i = (uint64_t)blockIdx.x * NT + t; i < len; i += (uint64_t)gridDim.x * NT) out[1 + i] = in[i];
@@ -4616,7 +4664,37 @@ __global__ __launch_bounds__(SmMode<M>::wthreads) void k_small_write(const uint8
     const uint64_t o_tile = (e >> 1) + loc[blockIdx.x].x + (headed ? (enc ? 2 : 1) : 0);   // first output byte
     const int64_t o_al = (int64_t)((((uintptr_t)(out + o_tile)) & ~(uintptr_t)15) - (uintptr_t)out);
     const uint32_t lead = (uint32_t)((int64_t)o_tile - o_al);   // stage offset of the tile's first byte
-    {   // the lane's run: from stage byte P, packed 4 bytes to a dword
+    if (dec && interior) {
+        // Decode, a tile with every byte an element (all but the stream's first and last
+        // tiles): per input dword, its 4 bytes expand to 4-8 by two v_perm (selectors by the
+        // pattern of its bytes >= 0x80, from s_sel), and the lane's run advances by whole
+        // dwords: OR-ed into the stage at the run's bit offset, the partial last dword too (ORs
+        // are idempotent, so the pending bits are OR-ed again with the next ones: no flush
+        // branch). ~20 VALU per input dword where the per-byte loop below takes ~60.
+        const uint32_t P = lead + pre + incl - cnt;
+        uint32_t di = P >> 2, nb = 8u * (P & 3u), pend = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < LD; ++k) {
+            const uint32_t x = vals[k], h = x & 0x80808080u;
+            uint32_t m = h >> 7;                  // bits 0, 8, 16, 24
+            m |= m >> 7;                          // + 1, 9, 17
+            m = (m | (m >> 14)) & 15u;            // the pattern
+            const uint2 sl = s_sel[m];
+            const uint32_t lo = __builtin_amdgcn_perm(x ^ h, 0x20202020u, sl.x);
+            const uint32_t hi = __builtin_amdgcn_perm(x ^ h, 0x20202020u, sl.y);
+            const uint32_t hb = 8u * (uint32_t)__popc(h);   // bits of hi (0..32)
+            const uint64_t l64 = (uint64_t)lo << nb, h64 = (uint64_t)hi << nb;
+            atomicOr(&s_out[di], pend | (uint32_t)l64);                      // always whole
+            const uint32_t d1 = (uint32_t)(l64 >> 32) | (uint32_t)h64;       // nb + hb bits
+            atomicOr(&s_out[di + 1], d1);
+            const uint32_t nt = nb + hb;                                      // 0..56
+            const bool full = nt >= 32u;
+            if (nt > 32u) atomicOr(&s_out[di + 2], (uint32_t)(h64 >> 32));   // (rare: many pairs)
+            pend = full ? (uint32_t)(h64 >> 32) : d1;
+            di += full ? 2u : 1u;
+            nb = nt & 31u;
+        }
+    } else {   // the lane's run: from stage byte P, packed 4 bytes to a dword
         const uint32_t P = lead + pre + incl - cnt;
         uint32_t di = P >> 2, nb = 8u * (P & 3u);
         uint64_t acc = 0;
