@@ -4144,14 +4144,13 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
     __shared__ uint4 s_f[FSM_SUB][4];   // wave totals per chunk
     __shared__ __attribute__((aligned(16))) uint8_t s_out[2 * FSM_TILE + 32];
     __shared__ __attribute__((aligned(4))) uint8_t s_rank[256];
-    __shared__ __attribute__((aligned(4))) uint8_t s_dump[4 * 256];   // a lane's unused byte stores
-    __shared__ uint2 s_esel[M == M_NYB_ENC ? 256 : 1];   // encode: v_perm selectors per 4-element pattern
+    __shared__ uint2 s_esel[256];   // v_perm selectors per 4-element pattern
     const int t = threadIdx.x;
     if (M == M_NYB_ENC && !aux.rk) fsm_rank_table(s_rank);
-    if (M == M_NYB_ENC) {
+    {
         // pattern t = c1 | c2 << 4 (bit i: element i writes its first / its second byte): the
         // output bytes in order, first byte i = selector i (S1 = the first bytes), second byte
-        // i = selector 4 + i (S0 = the elements' own bytes); 0x0c = a zero byte
+        // i = selector 4 + i (S0 = the second bytes); 0x0c = a zero byte
         uint32_t sel[2] = {0x0c0c0c0cu, 0x0c0c0c0cu};
         int o = 0;
         for (int i = 0; i < 4; ++i) {
@@ -4332,28 +4331,51 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
             }
             nb = 0;   // (every bit is in the stage)
         } else {   // M_NYB_DEC / M_NYB_DBODY: compressed byte x, state s = "at the low nybble"
-            // (r2's element loop: per element branches measured 1-3% faster here than the
-            // encoder's branch-free form, same-box A/B tools/gpu_r3n.sh)
-            // each element's 1-2 bytes straight into the stage at their running offset (as the
-            // encoder above: no shift-accumulate chain, every output byte written once)
-            uint8_t *const so = s_out + P;
-            uint8_t *const dump = s_dump + 4 * t;
-            uint32_t pos = 0;
+            // Per element (k < kend): its first byte s ? lo : (two ? hi : x), and with two = !s
+            // and a hit in the high nybble, a second byte lo; lo = the low nybble's dictionary
+            // byte (a hit) or (l & 7) << 4 | the next byte's high nybble, hi = the high nybble's
+            // dictionary byte. Four elements at a time in SWAR, the two dictionary lookups as
+            // v_perm into the 8-byte table, the output placed as in the encoder above (r4's
+            // per-element byte stores: ~26 VALU and 2 LDS byte stores per element).
+            const uint32_t T0 = (uint32_t)tblv, T1 = (uint32_t)(tblv >> 32);
+            const uint64_t kk0 = M == M_NYB_DBODY ? j0 : j0 + 2;   // stream index of element 0
+            const int64_t nvc = (int64_t)len - (int64_t)kk0 - 1;   // elements whose next byte exists
+            const uint32_t NV = nvc >= 16 ? 0xFFFFu : nvc <= 0 ? 0u : (1u << (uint32_t)nvc) - 1u;
+            const uint32_t IN = kend >= 16 ? 0xFFFFu : (1u << kend) - 1u;
+            const uint32_t TW = IN & ~S & fa[c];   // elements writing two bytes (fa: bit 7 of the byte)
+            auto bytes = [](uint32_t m4) {       // 4 mask bits -> 0xFF per byte
+                const uint32_t u = (m4 * 0x204081u) & 0x01010101u;
+                return (u << 8) - u;
+            };
+            uint32_t pend = 0;
 #pragma unroll
-            for (int k = 0; k < 16; ++k) {
-                const uint32_t x = W.b(k + 1);
-                const uint32_t s = (S >> k) & 1u;
-                const uint64_t kk = M == M_NYB_DBODY ? j0 + k : j0 + k + 2;
-                const uint32_t h = x >> 4, l = x & 15u;
-                const uint32_t nxt = (kk + 1 < len) ? (W.b(k + 2) >> 4) : 0u;
-                const uint32_t lm = 0u - ((l >> 3) & 1u);   // a hit in the low nybble (bit selects, no branch)
-                const uint32_t lo_b = ((uint32_t)(tblv >> (8u * (l & 7u))) & 255u & lm) | ((((l & 7u) << 4) + nxt) & ~lm);
-                const uint32_t hi_b = (uint32_t)(tblv >> (8u * (h & 7u))) & 255u;
-                const bool in = (uint32_t)k < kend, two = in && !s && (h & 8u);
-                *(in ? so + pos : dump) = (uint8_t)(s ? lo_b : (two ? hi_b : x));
-                *(two ? so + pos + 1 : dump + 1) = (uint8_t)lo_b;
-                pos += (in ? 1u : 0u) + (two ? 1u : 0u);
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t X = __builtin_amdgcn_alignbyte(W.w[q + 1], W.w[q], 1u);    // elements 4q..4q+3
+                const uint32_t NB = __builtin_amdgcn_alignbyte(W.w[q + 1], W.w[q], 2u);   // the bytes after them
+                const uint32_t NX = (NB >> 4) & 0x0F0F0F0Fu & bytes((NV >> (4 * q)) & 15u);
+                const uint32_t Lb = X & 0x07070707u;
+                const uint32_t TL = __builtin_amdgcn_perm(T1, T0, Lb);                     // tbl[l & 7]
+                const uint32_t TH = __builtin_amdgcn_perm(T1, T0, (X >> 4) & 0x07070707u);  // tbl[h & 7]
+                const uint32_t u3 = (X >> 3) & 0x01010101u, LM = (u3 << 8) - u3;           // low nybble a hit
+                const uint32_t LO = (TL & LM) | (((Lb << 4) | NX) & ~LM);
+                const uint32_t SM = bytes((S >> (4 * q)) & 15u);
+                const uint32_t t4 = (TW >> (4 * q)) & 15u, TM = bytes(t4);
+                const uint32_t F = (SM & LO) | (~SM & ((TM & TH) | (~TM & X)));
+                const uint32_t c1 = (IN >> (4 * q)) & 15u;
+                const uint2 sl = s_esel[c1 | (t4 << 4)];
+                const uint32_t lo = __builtin_amdgcn_perm(LO, F, sl.x), hi = __builtin_amdgcn_perm(LO, F, sl.y);
+                const uint32_t L = 8u * (uint32_t)(__popc(c1) + __popc(t4));
+                const uint64_t l64 = (uint64_t)lo << nb, h64 = (uint64_t)hi << nb;
+                atomicOr(&s_out32[di], pend | (uint32_t)l64);
+                const uint32_t d1 = (uint32_t)(l64 >> 32) | (uint32_t)h64, d2 = (uint32_t)(h64 >> 32);
+                const uint32_t nt = nb + L;
+                if (nt > 32u) atomicOr(&s_out32[di + 1], d1);
+                if (nt > 64u) atomicOr(&s_out32[di + 2], d2);
+                pend = nt >= 64u ? d2 : nt >= 32u ? d1 : (pend | (uint32_t)l64);
+                di += nt >> 5;
+                nb = nt & 31u;
             }
+            nb = 0;
         }
         if (nb) atomicOr(&s_out32[di], (uint32_t)acc);
     }
