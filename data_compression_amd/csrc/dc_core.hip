@@ -4193,16 +4193,22 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
     const int lane = t & 63, wid = t >> 6;
     Fsm ex[FSM_SUB];   // lanes before this one in the wave, per chunk
     uint32_t fa[FSM_SUB], fb[FSM_SUB], fvalid[FSM_SUB];   // the lane's element flags (nyb_lane_flags)
+    uint32_t RKp[FSM_SUB][4];   // encode: the lane's 16 ranks, 4 per dword (kept for the writer)
 #pragma unroll
     for (int c = 0; c < FSM_SUB; ++c) {
         const uint64_t j0 = (uint64_t)blockIdx.x * FSM_TILE + (uint64_t)c * 4096 + (uint64_t)t * 16;
         fa[c] = fb[c] = 0u;
         fvalid[c] = j0 >= nelem ? 0u : nelem - j0 >= 16 ? 0xFFFFu : (1u << (uint32_t)(nelem - j0)) - 1u;
+        RKp[c][0] = RKp[c][1] = RKp[c][2] = RKp[c][3] = ~0u;
         Fsm f = fsm_id();
         if (j0 < nelem) {
             uint32_t rk[16];
             fsm_ranks<M>(W_[c], aux, j0, nelem, rk, s_rank);
             nyb_lane_flags<M>(W_[c], rk, fa[c], fb[c]);
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                RKp[c][q] = (rk[4 * q] & 255u) | ((rk[4 * q + 1] & 255u) << 8) | ((rk[4 * q + 2] & 255u) << 16) |
+                            ((rk[4 * q + 3] & 255u) << 24);
             f = nyb_lane_fsm<M>(fa[c], fb[c], fvalid[c]);
         }
         const Fsm inc = fsm_wave_scan_incl(f, lane);
@@ -4256,8 +4262,6 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
         // every element's state at once, from the lane's entry state
         const uint32_t S = M == M_NYB_ENC ? nyb_enc_states(fa[c], fvalid[c], st_c[c])
                                           : nyb_dec_states(fa[c], fb[c], fvalid[c], st_c[c]);
-        uint32_t rk[16];
-        fsm_ranks<M>(W, aux, j0, nelem, rk, s_rank);
         const uint32_t P = (uint32_t)((int64_t)o0 - o_al);   // stage byte of the lane's first output
         uint32_t di = P >> 2, nb = 8u * (P & 3u);
         uint64_t acc = 0;
@@ -4296,11 +4300,7 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
             // ~9 VALU per element. (r4's per-element byte stores at a running offset: ~25 VALU and
             // 2 LDS byte stores per element; r3's 64-bit accumulator flushed every 2 elements ~26.)
             const uint32_t C1 = ~Hx | Sx, C2 = ~Hx & Sx;   // element writes its first / second byte
-            uint32_t RK[4];                                 // ranks, 4 bytes per dword (element order)
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                RK[q] = (rk[4 * q] & 255u) | ((rk[4 * q + 1] & 255u) << 8) | ((rk[4 * q + 2] & 255u) << 16) |
-                        ((rk[4 * q + 3] & 255u) << 24);
+            const uint32_t *const RK = RKp[c];             // ranks, 4 bytes per dword (element order)
             uint32_t pend = 0;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
