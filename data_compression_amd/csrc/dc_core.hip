@@ -243,21 +243,29 @@ __global__ __launch_bounds__(256) void k_hist_blocks(const uint8_t *__restrict__
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
                 uint32_t w4[4] = {cur[k].x, cur[k].y, cur[k].z, cur[k].w};
-                if (FE) {   // pair seconds -> letter | 0x80; count the starts
+                if (FE) {   // pair seconds -> letter | 0x80, found from the byte before each (SWAR)
                     const uint64_t p = b * (uint64_t)DC_BLOCK_BYTES + (uint64_t)k * 4096 + (uint64_t)t * 16;
-                    // (the shifts as statements of their own: inside `?:` they ran in a branch, lane 0 off)
-                    const uint32_t pd = dpp_wave_shr1(w4[3]), qd = dpp_wave_shl1(w4[0]);
-                    const uint32_t pb = lane == 0 ? ce[k] >> 24 : pd >> 24;
-                    const uint32_t qb = lane == 63 ? (p + 16 < n ? ce[k] & 255u : 0u) : qd & 255u;
-                    uint32_t st[4];
-                    fe_pair_starts(w4, qb, st);
-                    if (p == 0) st[0] &= ~0x80u;   // position 0 never starts a pair
-                    const uint32_t s0 = fe_start_before(pb, w4[0], p);
-                    w4[0] |= (st[0] << 8) | s0;
+                    // (the shift as a statement of its own: inside `?:` it ran in a branch, lane 0 off)
+                    const uint32_t pd = dpp_wave_shr1(w4[3]);
+                    const uint32_t pb = lane == 0 ? ce[k] >> 24 : pd >> 24;   // x[p - 1]
+                    const uint32_t raw3 = w4[3];
+                    uint32_t sc = 0;
 #pragma unroll
-                    for (int q = 1; q < 4; ++q) w4[q] |= (st[q] << 8) | (st[q - 1] >> 24);
-                    pc += (uint32_t)__popc(st[0]) + (uint32_t)__popc(st[1]) + (uint32_t)__popc(st[2]) +
-                          (uint32_t)__popc(st[3]);
+                    for (int q = 0; q < 4; ++q) {
+                        const uint32_t pv = __builtin_amdgcn_alignbyte(w4[q], q ? w4[q - 1] : pb << 24, 3u);   // the bytes before
+                        uint32_t sec = swar_eq(pv, 0x20202020u) & swar_lower(w4[q]);
+                        if (q == 0 && p == 0) sec &= ~0x8080u;   // positions 0, 1: no pair starts at 0
+                        w4[q] |= sec;
+                        sc += (uint32_t)__popc(sec);
+                        if (q == 0 && t == 0 && k == 0) sc -= sec & 0x80u ? 1u : 0u;   // (its start: the previous block's)
+                    }
+                    // the block's starts = its seconds, less the one on its first byte, plus a
+                    // start on its last byte (its second: the next block's first byte)
+                    if (t == 255 && k == 7) {
+                        const uint32_t nx = p + 16 < n ? ce[k] & 255u : 0u;
+                        sc += ((raw3 >> 24) == 0x20u && nx >= 'a' && nx <= 'z') ? 1u : 0u;
+                    }
+                    pc += sc;
                 }
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
