@@ -4820,8 +4820,32 @@ static __device__ __forceinline__ void mtf_apply(uint64_t &L, uint32_t &cnt, uin
     for (int k = (int)n - 1; k >= 0; --k) (void)mtf_touch64(L, cnt, (uint32_t)(S >> (8 * k)) & 255u);
 }
 
+// move v to the front of a full list (8 entries): mtf_touch64 with cnt = 8. On a list of cnt < 8
+// entries padded with zero bytes it leaves the same entries as mtf_touch64 with that cnt (a miss
+// drops the last byte, a pad; a zero v finds the first pad, the byte a miss would drop).
+// pb = 8 pos + 7 for a match at pos (63 for a miss too); hit = a match.
+static __device__ __forceinline__ uint64_t mtf_touch8(uint64_t L, uint32_t v, uint32_t &pb, bool &hit)
+{
+    const uint32_t vb = __builtin_amdgcn_perm(0u, v, 0u);   // v in every byte (no 32-bit multiply)
+    const uint32_t tl = (uint32_t)L ^ vb, th = (uint32_t)(L >> 32) ^ vb;
+    const uint64_t d = (((uint64_t)th << 32) | tl) - 0x0101010101010101ull;
+    const uint32_t zl = (uint32_t)d & ~tl & 0x80808080u, zh = (uint32_t)(d >> 32) & ~th & 0x80808080u;
+    hit = (zl | zh) != 0u;   // the lowest flag is the first match
+    pb = (uint32_t)__builtin_ctzll(((uint64_t)(zh | 0x80000000u) << 32) | zl);
+    const uint64_t m = ~0ull >> (63u - pb);   // bytes [0, pos]: up by one, v in at 0
+    return (((L << 8) | v) & m) | (L & ~m);
+}
+
 // MODE 0: tile summaries from empty lists -> summ[tile]; MODE 1: ranks from entry[tile].
 // Elements are bytes 1..len-1 of `in` (element e = byte e+1; its context is byte e).
+// A lane walks its tile with the 16 lists in LDS (column t). Per element: the next element's
+// list is read before this one's is written back (its context is this element's byte; the same
+// context takes the list just computed), so the LDS round trip overlaps the touch; the input
+// comes in 16-B granules loaded a 64-element group ahead. Lists are full (the initial lists and
+// their compositions) or, in MODE 0, padded with zero bytes (mtf_touch8): a list's count is
+// recovered at the end from its zero bytes and whether a zero was touched in its context.
+// (r4: one lane-local loop that waited on every list read and on the granule just loaded,
+// counts kept per element: 1.64 ms per GiB for MODE 0, 2.03 for MODE 1.)
 template <int MODE>
 __global__ __launch_bounds__(256) void k_mtf_walk(const uint8_t *__restrict__ in, uint64_t len, uint64_t ntiles,
                                                   const MtfSum *__restrict__ entry, MtfSum *__restrict__ summ,
@@ -4838,18 +4862,42 @@ __global__ __launch_bounds__(256) void k_mtf_walk(const uint8_t *__restrict__ in
         s_L[c][t] = MODE ? entry[tile].L[c] : 0ull;
         if (MODE) cnts |= (uint64_t)entry[tile].cnt[c] << (4 * c);
     }
-    // 16 elements per step: their bytes in[e + 1 .. e + 16] cut from two aligned granules by one
-    // uniform byte shift (the next step's first granule is this step's second), ranks leave as
-    // one 16-B store per step (r2 stored 4 ranks at a time at 4-KiB-strided lanes: 3.9 ms per
-    // GiB for this pass against 1.6 for the summary pass)
     uint32_t prev = in[e0];
-    const uintptr_t p0 = (uintptr_t)(in + e0 + 1), end = (uintptr_t)(in + len);
-    const uint32_t sh = (uint32_t)(p0 & 15u), dq = sh >> 2, db = sh & 3u;   // uniform over the lanes
-    uintptr_t g = p0 & ~(uintptr_t)15;
-    uint4 ga = g < end ? *(const uint4 *)g : make_uint4(0u, 0u, 0u, 0u);
-    for (uint64_t e = e0; e < e1; e += 16) {
-        const uint4 gb = g + 16 < end ? *(const uint4 *)(g + 16) : make_uint4(0u, 0u, 0u, 0u);
-        const uint32_t d8[8] = {ga.x, ga.y, ga.z, ga.w, gb.x, gb.y, gb.z, gb.w};
+    if (MODE && !__all(cnts == 0x8888888888888888ull)) {
+        // entry lists of fewer than 8 entries (not produced by this pipeline): counted walk
+        for (uint64_t e = e0; e < e1; e += 16) {
+            const uint32_t cnt16 = e1 - e < 16 ? (uint32_t)(e1 - e) : 16u;
+            uint32_t R[4] = {0u, 0u, 0u, 0u};
+            for (uint32_t k = 0; k < cnt16; ++k) {
+                const uint32_t x = in[e + 1 + k];
+                const uint32_t c = (prev >> 3) & 15u;
+                uint64_t L = s_L[c][t];
+                uint32_t n = (uint32_t)(cnts >> (4 * c)) & 15u;
+                const int r = mtf_touch64(L, n, x);
+                s_L[c][t] = L;
+                cnts = (cnts & ~(15ull << (4 * c))) | ((uint64_t)n << (4 * c));
+                prev = x;
+                R[k >> 2] |= (uint32_t)(r < 0 ? 0xFF : r) << (8 * (k & 3));
+            }
+            if (cnt16 == 16) *reinterpret_cast<uint4 *>(rk + e) = make_uint4(R[0], R[1], R[2], R[3]);
+            else for (uint32_t k = 0; k < cnt16; ++k) rk[e + k] = (uint8_t)(R[k >> 2] >> (8 * (k & 3)));
+        }
+        return;
+    }
+    uint32_t zt = 0;   // MODE 0: bit c = a zero byte was touched in context c
+    uint32_t cc = (prev >> 3) & 15u;
+    uint64_t Lc = s_L[cc][t];
+    // granule i = bytes [gb + 16 i, +16) of `in`, gb = element e0's byte rounded down to 16 B;
+    // element e0 + 16 s + k is byte sh + 16 s + k of granules s, s + 1 (sh uniform: in + 1's
+    // alignment, e0 a multiple of 16)
+    const uint64_t a = (uintptr_t)in & 15u, gb = ((e0 + 1 + a) & ~15ull) - a;
+    const uint32_t sh = (uint32_t)((e0 + 1 + a) & 15u), dq = sh >> 2, db = sh & 3u;
+    auto ld = [&](uint64_t i) {
+        const int64_t o = (int64_t)(gb + 16 * i);   // (-a .. : granule 0 may begin before in)
+        return o < (int64_t)len ? *reinterpret_cast<const uint4 *>(in + o) : make_uint4(0u, 0u, 0u, 0u);
+    };
+    auto step = [&](const uint4 &A, const uint4 &B, uint64_t e) {
+        const uint32_t d8[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
         uint32_t X[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {   // dwords dq + j, dq + j + 1 (dq uniform: selects)
@@ -4858,32 +4906,52 @@ __global__ __launch_bounds__(256) void k_mtf_walk(const uint8_t *__restrict__ in
             for (int k = 1; k < 4; ++k) { lo = dq == (uint32_t)k ? d8[j + k] : lo; hi = dq == (uint32_t)k ? d8[j + k + 1] : hi; }
             X[j] = __builtin_amdgcn_alignbyte(hi, lo, db);
         }
-        const uint32_t cnt16 = e1 - e < 16 ? (uint32_t)(e1 - e) : 16u;
-        uint32_t R[4] = {0u, 0u, 0u, 0u};   // MODE 1: the step's ranks (0..7, 0xFF a miss)
+        uint32_t R[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
-            if ((uint32_t)k >= cnt16) break;
             const uint32_t x = (X[k >> 2] >> (8 * (k & 3))) & 255u;
-            const uint32_t c = (prev >> 3) & 15u;
-            uint64_t L = s_L[c][t];
-            uint32_t n = (uint32_t)(cnts >> (4 * c)) & 15u;
-            const int r = mtf_touch64(L, n, x);
-            s_L[c][t] = L;
-            cnts = (cnts & ~(15ull << (4 * c))) | ((uint64_t)n << (4 * c));
-            prev = x;
-            if (MODE) R[k >> 2] |= (uint32_t)(r < 0 ? 0xFF : r) << (8 * (k & 3));
+            const uint32_t cn = (x >> 3) & 15u;
+            const uint64_t Ln = s_L[cn][t];   // the next element's list (before this write)
+            uint32_t pb;
+            bool hit;
+            const uint64_t L2 = mtf_touch8(Lc, x, pb, hit);
+            s_L[cc][t] = L2;
+            if (MODE) R[k >> 2] |= (hit ? pb >> 3 : 0xFFu) << (8 * (k & 3));
+            else zt |= ((x - 1u) >> 31) << cc;
+            Lc = cn == cc ? L2 : Ln;
+            cc = cn;
         }
-        if (MODE) {
-            if (cnt16 == 16) *reinterpret_cast<uint4 *>(rk + e) = make_uint4(R[0], R[1], R[2], R[3]);
-            else for (uint32_t k = 0; k < cnt16; ++k) rk[e + k] = (uint8_t)(R[k >> 2] >> (8 * (k & 3)));   // ragged end
-        }
-        ga = gb;
-        g += 16;
+        if (MODE) *reinterpret_cast<uint4 *>(rk + e) = make_uint4(R[0], R[1], R[2], R[3]);
+    };
+    uint4 G0 = ld(0), G1 = ld(1), G2 = ld(2), G3 = ld(3), G4 = ld(4);
+    uint64_t e = e0, gi = 0;
+    for (; e + 64 <= e1; e += 64, gi += 4) {
+        const uint4 N1 = ld(gi + 5), N2 = ld(gi + 6), N3 = ld(gi + 7), N4 = ld(gi + 8);
+        step(G0, G1, e);
+        step(G1, G2, e + 16);
+        step(G2, G3, e + 32);
+        step(G3, G4, e + 48);
+        G0 = G4; G1 = N1; G2 = N2; G3 = N3; G4 = N4;
+    }
+    for (; e < e1; ++e) {   // the last tile's ragged end
+        const uint32_t x = in[e + 1];
+        uint32_t pb;
+        bool hit;
+        const uint64_t L2 = mtf_touch8(Lc, x, pb, hit);
+        s_L[cc][t] = L2;
+        if (MODE) rk[e] = (uint8_t)(hit ? pb >> 3 : 0xFFu);
+        else zt |= ((x - 1u) >> 31) << cc;
+        cc = (x >> 3) & 15u;
+        Lc = s_L[cc][t];
     }
     if (!MODE) {
         for (int c = 0; c < 16; ++c) {
-            summ[tile].L[c] = s_L[c][t];
-            summ[tile].cnt[c] = (uint8_t)((cnts >> (4 * c)) & 15u);
+            const uint64_t L = s_L[c][t];
+            uint32_t nz = 0;   // zero bytes: the pads, and a touched zero still on the list
+#pragma unroll
+            for (int q = 0; q < 8; ++q) nz += ((L >> (8 * q)) & 255u) == 0u ? 1u : 0u;
+            summ[tile].L[c] = L;
+            summ[tile].cnt[c] = (uint8_t)(nz ? 8u - nz + ((zt >> c) & 1u) : 8u);
         }
     }
 }

@@ -720,6 +720,13 @@ def _nyb_cases(torch):
     for n in (4099, 300_001):
         cases.append(("bytes", rng.integers(1, 256, size=n, dtype=np.uint8)))   # every context, non-ASCII
         cases.append(("skew", rng.choice(np.frombuffer(b"e tax\x80\x81", np.uint8), size=n)))
+    # zero bytes (outside the reference's C-string domain; the restatement is length-based): the
+    # walk pads short lists with zero bytes, so a touched zero must be told from a pad
+    cases.append(("zeros", rng.integers(0, 256, size=300_001, dtype=np.uint8)))
+    cases.append(("zskew", rng.choice(np.frombuffer(b"\x00\x00e t\x01", np.uint8), size=70_001)))
+    z = synth.english_like(200_003, seed=5)
+    z[rng.integers(0, z.size, size=300)] = 0   # rare zeros: pushed off, or still on a list
+    cases.append(("zrare", z))
     cases.append(("log", synth.log_like(5 << 20, seed=9)))   # 1280 tiles: two reduce levels
     return cases
 
