@@ -4846,10 +4846,15 @@ static __device__ __forceinline__ uint64_t mtf_touch8(uint64_t L, uint32_t v, ui
 // recovered at the end from its zero bytes and whether a zero was touched in its context.
 // (r4: one lane-local loop that waited on every list read and on the granule just loaded,
 // counts kept per element: 1.64 ms per GiB for MODE 0, 2.03 for MODE 1.)
+// MODE 1 with fsumm set also writes the nybble encoder's tile summary of its tile (the FSM
+// tiles of k_fsm_tiles<M_NYB_ENC> are these 4096-element tiles): the composition of its steps'
+// hit masks (nyb_lane_fsm), so the encoder's counting pass (k_fsm_tiles, which re-read the
+// ranks) does not run.
+static_assert(FSM_TILE == MTF_TILE, "k_mtf_walk<1> writes the nybble encoder's tile summaries");
 template <int MODE>
 __global__ __launch_bounds__(256) void k_mtf_walk(const uint8_t *__restrict__ in, uint64_t len, uint64_t ntiles,
                                                   const MtfSum *__restrict__ entry, MtfSum *__restrict__ summ,
-                                                  uint8_t *__restrict__ rk)
+                                                  uint8_t *__restrict__ rk, uint4 *__restrict__ fsumm)
 {
     __shared__ uint64_t s_L[16][256];
     const int t = threadIdx.x;
@@ -4863,11 +4868,15 @@ __global__ __launch_bounds__(256) void k_mtf_walk(const uint8_t *__restrict__ in
         if (MODE) cnts |= (uint64_t)entry[tile].cnt[c] << (4 * c);
     }
     uint32_t prev = in[e0];
+    Fsm acc = fsm_id();   // MODE 1: the encoder's composition of the tile
+    auto fold = [&](uint32_t A, uint32_t valid) {
+        if (MODE) acc = fsm_then(acc, nyb_lane_fsm<M_NYB_ENC>(A, 0u, valid));
+    };
     if (MODE && !__all(cnts == 0x8888888888888888ull)) {
         // entry lists of fewer than 8 entries (not produced by this pipeline): counted walk
         for (uint64_t e = e0; e < e1; e += 16) {
             const uint32_t cnt16 = e1 - e < 16 ? (uint32_t)(e1 - e) : 16u;
-            uint32_t R[4] = {0u, 0u, 0u, 0u};
+            uint32_t R[4] = {0u, 0u, 0u, 0u}, A = 0;
             for (uint32_t k = 0; k < cnt16; ++k) {
                 const uint32_t x = in[e + 1 + k];
                 const uint32_t c = (prev >> 3) & 15u;
@@ -4878,10 +4887,13 @@ __global__ __launch_bounds__(256) void k_mtf_walk(const uint8_t *__restrict__ in
                 cnts = (cnts & ~(15ull << (4 * c))) | ((uint64_t)n << (4 * c));
                 prev = x;
                 R[k >> 2] |= (uint32_t)(r < 0 ? 0xFF : r) << (8 * (k & 3));
+                A |= (r < 0 ? 0u : 1u) << k;
             }
             if (cnt16 == 16) *reinterpret_cast<uint4 *>(rk + e) = make_uint4(R[0], R[1], R[2], R[3]);
             else for (uint32_t k = 0; k < cnt16; ++k) rk[e + k] = (uint8_t)(R[k >> 2] >> (8 * (k & 3)));
+            fold(A, (1u << cnt16) - 1u);
         }
+        if (fsumm) fsumm[tile] = fsm_pack(acc);
         return;
     }
     uint32_t zt = 0;   // MODE 0: bit c = a zero byte was touched in context c
@@ -4906,7 +4918,7 @@ __global__ __launch_bounds__(256) void k_mtf_walk(const uint8_t *__restrict__ in
             for (int k = 1; k < 4; ++k) { lo = dq == (uint32_t)k ? d8[j + k] : lo; hi = dq == (uint32_t)k ? d8[j + k + 1] : hi; }
             X[j] = __builtin_amdgcn_alignbyte(hi, lo, db);
         }
-        uint32_t R[4] = {0u, 0u, 0u, 0u};
+        uint32_t R[4] = {0u, 0u, 0u, 0u}, H = 0;
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
             const uint32_t x = (X[k >> 2] >> (8 * (k & 3))) & 255u;
@@ -4916,12 +4928,15 @@ __global__ __launch_bounds__(256) void k_mtf_walk(const uint8_t *__restrict__ in
             bool hit;
             const uint64_t L2 = mtf_touch8(Lc, x, pb, hit);
             s_L[cc][t] = L2;
-            if (MODE) R[k >> 2] |= (hit ? pb >> 3 : 0xFFu) << (8 * (k & 3));
+            if (MODE) { R[k >> 2] |= (hit ? pb >> 3 : 0xFFu) << (8 * (k & 3)); H |= (hit ? 1u : 0u) << k; }
             else zt |= ((x - 1u) >> 31) << cc;
             Lc = cn == cc ? L2 : Ln;
             cc = cn;
         }
-        if (MODE) *reinterpret_cast<uint4 *>(rk + e) = make_uint4(R[0], R[1], R[2], R[3]);
+        if (MODE) {
+            *reinterpret_cast<uint4 *>(rk + e) = make_uint4(R[0], R[1], R[2], R[3]);
+            fold(H, 0xFFFFu);
+        }
     };
     uint4 G0 = ld(0), G1 = ld(1), G2 = ld(2), G3 = ld(3), G4 = ld(4);
     uint64_t e = e0, gi = 0;
@@ -4933,17 +4948,23 @@ __global__ __launch_bounds__(256) void k_mtf_walk(const uint8_t *__restrict__ in
         step(G3, G4, e + 48);
         G0 = G4; G1 = N1; G2 = N2; G3 = N3; G4 = N4;
     }
-    for (; e < e1; ++e) {   // the last tile's ragged end
-        const uint32_t x = in[e + 1];
-        uint32_t pb;
-        bool hit;
-        const uint64_t L2 = mtf_touch8(Lc, x, pb, hit);
-        s_L[cc][t] = L2;
-        if (MODE) rk[e] = (uint8_t)(hit ? pb >> 3 : 0xFFu);
-        else zt |= ((x - 1u) >> 31) << cc;
-        cc = (x >> 3) & 15u;
-        Lc = s_L[cc][t];
+    for (; e < e1; e += 16) {   // the last tile's ragged end
+        const uint32_t cnt16 = e1 - e < 16 ? (uint32_t)(e1 - e) : 16u;
+        uint32_t A = 0;
+        for (uint32_t k = 0; k < cnt16; ++k) {
+            const uint32_t x = in[e + 1 + k];
+            uint32_t pb;
+            bool hit;
+            const uint64_t L2 = mtf_touch8(Lc, x, pb, hit);
+            s_L[cc][t] = L2;
+            if (MODE) { rk[e + k] = (uint8_t)(hit ? pb >> 3 : 0xFFu); A |= (hit ? 1u : 0u) << k; }
+            else zt |= ((x - 1u) >> 31) << cc;
+            cc = (x >> 3) & 15u;
+            Lc = s_L[cc][t];
+        }
+        fold(A, (1u << cnt16) - 1u);
     }
+    if (MODE && fsumm) fsumm[tile] = fsm_pack(acc);
     if (!MODE) {
         for (int c = 0; c < 16; ++c) {
             const uint64_t L = s_L[c][t];
@@ -6591,7 +6612,7 @@ int dc_huff_base64url(dc_ctx *c, const uint32_t *d_words, uint64_t bit_base, uin
 template <int M>
 static int fsm_run(dc_ctx *c, const uint8_t *d_in, uint64_t len, uint64_t nelem, uint8_t *d_out, uint64_t *h_len,
                    const char *name, FsmAux aux = FsmAux{nullptr, 0, 0, 1, 1}, uint64_t *h_plan = nullptr,
-                   bool write = true, const uint32_t *gexp = nullptr, uint64_t ngroups = 0)
+                   bool write = true, const uint32_t *gexp = nullptr, uint64_t ngroups = 0, bool summ_ready = false)
 {
     const uint64_t ntiles = SmMode<M>::fast ? sm_ntiles<M>(d_in, FsmOff<M>::v, nelem) : (nelem + FSM_TILE - 1) / FSM_TILE;
     const uint64_t nt = ntiles ? ntiles : 1;
@@ -6615,7 +6636,7 @@ static int fsm_run(dc_ctx *c, const uint8_t *d_in, uint64_t len, uint64_t nelem,
             LAUNCH(c, "small_dec_summ", k_small_dec_summ, (ntiles + 255) / 256, 256, gexp, ngroups, d_in, len, ntiles,
                    c->d_summ, c->d_meta);
         else if constexpr (SmMode<M>::fast) LAUNCH(c, name, k_small_tiles<M>, ntiles, 256, d_in, len, nelem, c->d_summ);
-        else LAUNCH(c, name, k_fsm_tiles<M>, ntiles, 256, d_in, len, nelem, c->d_summ, aux);
+        else if (!summ_ready) LAUNCH(c, name, k_fsm_tiles<M>, ntiles, 256, d_in, len, nelem, c->d_summ, aux);
         LAUNCH(c, "fsm_scan_up", k_fsm_scan_up, ng, FSM_GROUP, c->d_summ, ntiles, gsum);
         LAUNCH(c, "fsm_scan", k_fsm_scan, 1, 1024, (const uint4 *)gsum, ng, c->d_entry, c->d_meta, aux.s_init);
     }
@@ -6688,7 +6709,7 @@ static int mtf_run(dc_ctx *c, const uint8_t *d_in, uint64_t len, const MtfSum *h
     HIPCHK(hipStreamSynchronize(c->stream));   // h_init is pageable
     if (ranks && ensure((void **)&c->d_rk, &c->rk_cap, ((len + 3) & ~3ull))) return DC_E_HIP;
     LAUNCH(c, "mtf_tiles", k_mtf_walk<0>, (n0 + 255) / 256, 256, d_in, len, n0, (const MtfSum *)nullptr, S,
-           (uint8_t *)nullptr);
+           (uint8_t *)nullptr, (uint4 *)nullptr);
     for (int l = 0; l + 1 < levels; ++l)
         LAUNCH(c, "mtf_reduce", k_mtf_reduce, (nl[l + 1] * 16 + 255) / 256, 256, (const MtfSum *)(S + off[l]), nl[l],
                S + off[l + 1]);
@@ -6698,9 +6719,13 @@ static int mtf_run(dc_ctx *c, const uint8_t *d_in, uint64_t len, const MtfSum *h
         LAUNCH(c, "mtf_down", k_mtf_down, (groups * 16 + 255) / 256, 256, (const MtfSum *)(S + off[l]), nl[l], pe,
                E + off[l], l == levels - 1 ? fin : (MtfSum *)nullptr);
     }
-    if (ranks)
+    if (ranks) {
+        // the nybble encoder's tile summaries too (fsm_run(..., summ_ready)): its tiles are these
+        const uint64_t ng = (n0 + FSM_GROUP - 1) / FSM_GROUP;
+        if (ensure((void **)&c->d_summ, &c->summ_cap, (n0 + ng) * sizeof(uint4))) return DC_E_HIP;
         LAUNCH(c, "mtf_ranks", k_mtf_walk<1>, (n0 + 255) / 256, 256, d_in, len, n0, (const MtfSum *)E,
-               (MtfSum *)nullptr, c->d_rk);
+               (MtfSum *)nullptr, c->d_rk, c->d_summ);
+    }
     if (h_final) HIPCHK(hipMemcpyAsync(h_final, fin, sizeof(MtfSum), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     c->rk_in = ranks ? d_in : nullptr; c->rk_len = len;
@@ -6775,8 +6800,9 @@ int dc_nyb_compress(dc_ctx *c, const uint8_t *d_in, uint64_t n, int modify, uint
     const MtfSum init = mtf_initial();
     int r = mtf_run(c, d_in, n, &init, true, nullptr);
     if (r) return r;
+    // (the tile summaries: k_mtf_walk<1>'s, when there are ranks)
     return fsm_run<M_NYB_ENC>(c, d_in, n, n - 1, d_out, h_len, "nyb_enca_tiles",
-                              FsmAux{n > 1 ? c->d_rk : nullptr, 0, 0, 1, 1});
+                              FsmAux{n > 1 ? c->d_rk : nullptr, 0, 0, 1, 1}, nullptr, true, nullptr, 0, n > 1);
 }
 
 // ---- chunked nybble container (DCNK) ---------------------------------------------------
@@ -6919,7 +6945,8 @@ int dc_nyb_body_plan(dc_ctx *c, const uint8_t *d_in, uint64_t len, int modify, c
         if (r) return r;
         aux.rk = len > 1 ? c->d_rk : nullptr;
     }
-    int r = fsm_run<M_NYB_ENC>(c, d_in, len, len - 1, nullptr, nullptr, "nyb_body_tiles", aux, h_plan, false);
+    int r = fsm_run<M_NYB_ENC>(c, d_in, len, len - 1, nullptr, nullptr, "nyb_body_tiles", aux, h_plan, false,
+                               nullptr, 0, modify && len > 1);
     if (r) return r;
     // rank of the last element (the byte a pending nybble of this shard belongs to)
     uint8_t last = 0xFF;
