@@ -4043,6 +4043,7 @@ static __device__ __forceinline__ uint32_t byte_bits4(uint32_t d, int bit)   // 
     uint32_t b = (d >> bit) & 0x01010101u;
     return (b | (b >> 7) | (b >> 14) | (b >> 21)) & 15u;
 }
+#define NYB_TPW 2   /* tiles per wave: the second tile's granules load while the first is folded */
 template <int M>
 __global__ __launch_bounds__(256) void k_nyb_tiles(const uint8_t *__restrict__ in, uint64_t len, uint64_t nelem,
                                                    uint64_t ntiles, uint4 *__restrict__ summ)
@@ -4054,41 +4055,52 @@ __global__ __launch_bounds__(256) void k_nyb_tiles(const uint8_t *__restrict__ i
         s_hit[t] = static_rank((uint32_t)t) != 0xFFu ? 1u : 0u;
         __syncthreads();
     }
-    const uint64_t T = (uint64_t)blockIdx.x * 4 + (uint64_t)(t >> 6);
-    if (T >= ntiles) return;   // whole waves (no barriers below)
-    const uint64_t j0 = T * FSM_TILE;
-    const uint32_t nv = nelem - j0 < FSM_TILE ? (uint32_t)(nelem - j0) : (uint32_t)FSM_TILE;
-    const uint64_t B0 = j0 + FsmOff<M>::v;                                  // the tile's first byte
-    const uint32_t sh = (uint32_t)((B0 + ((uintptr_t)in & 15u)) & 15u);    // its place in its granule
-    const int64_t g0 = (int64_t)B0 - (int64_t)sh;                           // granule 0 (may begin before in)
-    uint4 v[5];
+    const uint64_t Tw = ((uint64_t)blockIdx.x * 4 + (uint64_t)(t >> 6)) * NYB_TPW;
+    if (Tw >= ntiles) return;   // whole waves (no barriers below)
+    uint4 v[NYB_TPW][5];
+    uint32_t nvs[NYB_TPW], shs[NYB_TPW];
 #pragma unroll
-    for (int i = 0; i < 5; ++i) {
-        const int64_t o = g0 + 16 * (4 * lane + i);
-        const bool want = i < 4 || (lane == 63 && sh != 0);
-        v[i] = (want && o < (int64_t)len) ? *reinterpret_cast<const uint4 *>(in + o) : make_uint4(0u, 0u, 0u, 0u);
-    }
-    Fsm acc = fsm_id();
+    for (int u = 0; u < NYB_TPW; ++u) {
+        const uint64_t T = Tw + u;
+        const uint64_t j0 = T * FSM_TILE;
+        const uint32_t nv = T >= ntiles ? 0u : nelem - j0 < FSM_TILE ? (uint32_t)(nelem - j0) : (uint32_t)FSM_TILE;
+        const uint64_t B0 = j0 + FsmOff<M>::v;                                  // the tile's first byte
+        const uint32_t sh = (uint32_t)((B0 + ((uintptr_t)in & 15u)) & 15u);    // its place in its granule
+        const int64_t g0 = (int64_t)B0 - (int64_t)sh;                           // granule 0 (may begin before in)
+        nvs[u] = nv; shs[u] = sh;
 #pragma unroll
-    for (int i = 0; i < 5; ++i) {
-        // elements of granule gi: its bytes b with 0 <= 16 gi + b - sh < nv
-        const int gi = 4 * lane + i;
-        const int lo = min(max((int)sh - 16 * gi, 0), 16), hi = min(max((int)nv + (int)sh - 16 * gi, 0), 16);
-        uint32_t valid = hi > lo ? (1u << hi) - (1u << lo) : 0u;
-        if (i == 4 && lane != 63) valid = 0u;
-        const uint32_t d[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
-        uint32_t A = 0, B = 0;
-        if (M == M_NYB_ENC) {
-#pragma unroll
-            for (int k = 0; k < 16; ++k) A |= (uint32_t)s_hit[(d[k >> 2] >> (8 * (k & 3))) & 255u] << k;
-        } else {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) { A |= byte_bits4(d[q], 7) << (4 * q); B |= byte_bits4(d[q], 3) << (4 * q); }
+        for (int i = 0; i < 5; ++i) {
+            const int64_t o = g0 + 16 * (4 * lane + i);
+            const bool want = nv && (i < 4 || (lane == 63 && sh != 0));
+            v[u][i] = (want && o < (int64_t)len) ? *reinterpret_cast<const uint4 *>(in + o) : make_uint4(0u, 0u, 0u, 0u);
         }
-        acc = fsm_then(acc, nyb_lane_fsm<M>(A, B, valid));
     }
-    const Fsm inc = fsm_wave_scan_incl(acc, lane);
-    if (lane == 63) summ[T] = fsm_pack(inc);
+#pragma unroll
+    for (int u = 0; u < NYB_TPW; ++u) {
+        if (Tw + u >= ntiles) break;   // (uniform)
+        const uint32_t nv = nvs[u], sh = shs[u];
+        Fsm acc = fsm_id();
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+            // elements of granule gi: its bytes b with 0 <= 16 gi + b - sh < nv
+            const int gi = 4 * lane + i;
+            const int lo = min(max((int)sh - 16 * gi, 0), 16), hi = min(max((int)nv + (int)sh - 16 * gi, 0), 16);
+            uint32_t valid = hi > lo ? (1u << hi) - (1u << lo) : 0u;
+            if (i == 4 && lane != 63) valid = 0u;
+            const uint32_t d[4] = {v[u][i].x, v[u][i].y, v[u][i].z, v[u][i].w};
+            uint32_t A = 0, B = 0;
+            if (M == M_NYB_ENC) {
+#pragma unroll
+                for (int k = 0; k < 16; ++k) A |= (uint32_t)s_hit[(d[k >> 2] >> (8 * (k & 3))) & 255u] << k;
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) { A |= byte_bits4(d[q], 7) << (4 * q); B |= byte_bits4(d[q], 3) << (4 * q); }
+            }
+            acc = fsm_then(acc, nyb_lane_fsm<M>(A, B, valid));
+        }
+        const Fsm inc = fsm_wave_scan_incl(acc, lane);
+        if (lane == 63) summ[Tw + u] = fsm_pack(inc);
+    }
 }
 
 // Scan of the tile summaries in two levels, all accesses coalesced: k_fsm_scan_up turns each
@@ -6698,7 +6710,7 @@ static int fsm_run(dc_ctx *c, const uint8_t *d_in, uint64_t len, uint64_t nelem,
         else if (summ_ready) {}
         else if ((M == M_NYB_ENC && !aux.rk) || M == M_NYB_DEC || M == M_NYB_DBODY)
             LAUNCH(c, name, k_nyb_tiles<M == M_NYB_DEC ? M_NYB_DEC : M == M_NYB_DBODY ? M_NYB_DBODY : M_NYB_ENC>,
-                   (ntiles + 3) / 4, 256, d_in, len, nelem, ntiles, c->d_summ);
+                   (ntiles + 4 * NYB_TPW - 1) / (4 * NYB_TPW), 256, d_in, len, nelem, ntiles, c->d_summ);
         else LAUNCH(c, name, k_fsm_tiles<M>, ntiles, 256, d_in, len, nelem, c->d_summ, aux);
         LAUNCH(c, "fsm_scan_up", k_fsm_scan_up, ng, FSM_GROUP, c->d_summ, ntiles, gsum);
         LAUNCH(c, "fsm_scan", k_fsm_scan, 1, 1024, (const uint4 *)gsum, ng, c->d_entry, c->d_meta, aux.s_init);
