@@ -4243,6 +4243,15 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
     }
     const bool nyb_whole = M == M_NYB_ENC && aux.whole;
     const bool enc = FsmMode<M>::enc || nyb_whole;
+    // every global read the tile needs is issued here, before the first one is waited for (the
+    // LITERAL test on meta, then the window, then entry/loc after the barrier: three round trips)
+    FsmWin W_[FSM_SUB];
+#pragma unroll
+    for (int c = 0; c < FSM_SUB; ++c)
+        W_[c] = fsm_window(in, len, (int64_t)((uint64_t)blockIdx.x * FSM_TILE + (uint64_t)c * 4096 + (uint64_t)t * 16) +
+                                       FsmOff<M>::v);   // every lane (shuffles)
+    const uint64_t e = entry[blockIdx.x / FSM_GROUP];
+    const uint4 lc = loc[blockIdx.x];
     const uint64_t body = (M == M_NYB_ENC) ? meta[0] + (aux.is_last ? meta[1] : 0) : meta[0];
     const uint64_t total = enc ? 2 + body : 1 + body;
     const bool literal = enc && total >= len;
@@ -4262,11 +4271,6 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
     for (uint32_t i = (uint32_t)t; i < (2 * FSM_TILE + 32) / 16; i += 256)   // the stage is OR-merged into
         reinterpret_cast<uint4 *>(s_out)[i] = make_uint4(0u, 0u, 0u, 0u);
     if (M == M_NYB_ENC && !aux.rk) __syncthreads();   // s_rank (the stage: ordered by the scan's barrier)
-    FsmWin W_[FSM_SUB];
-#pragma unroll
-    for (int c = 0; c < FSM_SUB; ++c)
-        W_[c] = fsm_window(in, len, (int64_t)((uint64_t)blockIdx.x * FSM_TILE + (uint64_t)c * 4096 + (uint64_t)t * 16) +
-                                       FsmOff<M>::v);   // every lane (shuffles)
     // per chunk: the lane's composition, scanned across the wave (shuffles); the wave totals of
     // every chunk through LDS (one barrier)
     const int lane = t & 63, wid = t >> 6;
@@ -4299,8 +4303,6 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
     }
     __syncthreads();
     // entry = the group's entry, then the tile's local exclusive composition (k_fsm_scan_up)
-    const uint64_t e = entry[blockIdx.x / FSM_GROUP];
-    const uint4 lc = loc[blockIdx.x];
     const uint32_t s_g = (uint32_t)(e & 1);
     const uint64_t o_tile = (e >> 1) + (s_g ? lc.y : lc.x) + (headed ? (enc ? 2 : 1) : 0);   // first output byte
     const uint32_t s_tile = s_g ? lc.w : lc.z;
