@@ -3876,14 +3876,42 @@ static __device__ __forceinline__ Fsm elem_fsm(const FsmWin &W, int k, uint64_t 
 // random reads of 64 dwords, mostly broadcasts on text (the SWAR search of the dictionary, a
 // 64-bit multiply and zero test per element, made the tile count kernel VALU-bound: 0.68 ->
 // 0.94 ms per GiB)
+// The kernels' small lookup tables, built at compile time (built per workgroup they cost ~90
+// VALU in every wave of the nybble writer: ~12% of its instructions)
+struct NybTables {
+    uint32_t rank4[64];              // static ranks, 4 bytes per dword
+    uint32_t esel_lo[256], esel_hi[256];   // k_fsm_write's v_perm selectors, per 8-bit pattern
+    constexpr NybTables() : rank4(), esel_lo(), esel_hi()
+    {
+        const char dict[9] = " etaoins";
+        for (int x = 0; x < 256; ++x) {
+            uint32_t r = 0xFFu;
+            for (int k = 7; k >= 0; --k) if ((uint8_t)dict[k] == x) r = (uint32_t)k;
+            rank4[x >> 2] |= r << (8 * (x & 3));
+        }
+        // pattern t = c1 | c2 << 4 (bit i: element i writes its first / its second byte): the
+        // output bytes in order, first byte i = selector i (S1 = the first bytes), second byte
+        // i = selector 4 + i (S0 = the second bytes); 0x0c = a zero byte
+        for (int t = 0; t < 256; ++t) {
+            uint32_t sel[2] = {0x0c0c0c0cu, 0x0c0c0c0cu};
+            int o = 0;
+            for (int i = 0; i < 4; ++i) {
+                if ((t >> i) & 1) { sel[o >> 2] = (sel[o >> 2] & ~(255u << (8 * (o & 3)))) | ((uint32_t)i << (8 * (o & 3))); ++o; }
+                if ((t >> (4 + i)) & 1) {
+                    sel[o >> 2] = (sel[o >> 2] & ~(255u << (8 * (o & 3)))) | ((uint32_t)(4 + i) << (8 * (o & 3)));
+                    ++o;
+                }
+            }
+            esel_lo[t] = sel[0];
+            esel_hi[t] = sel[1];
+        }
+    }
+};
+__constant__ NybTables c_nyb = NybTables();
+
 static __device__ __forceinline__ void fsm_rank_table(uint8_t *s_rank)
 {
-    if (threadIdx.x < 64) {
-        uint32_t v = 0;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) v |= static_rank(4u * threadIdx.x + q) << (8 * q);
-        reinterpret_cast<uint32_t *>(s_rank)[threadIdx.x] = v;
-    }
+    if (threadIdx.x < 64) reinterpret_cast<uint32_t *>(s_rank)[threadIdx.x] = c_nyb.rank4[threadIdx.x];
 }
 template <int M>
 static __device__ __forceinline__ void fsm_ranks(const FsmWin &W, const FsmAux &aux, uint64_t j0, uint64_t nelem,
@@ -4052,7 +4080,7 @@ __global__ __launch_bounds__(256) void k_nyb_tiles(const uint8_t *__restrict__ i
     __shared__ uint8_t s_hit[256];   // static encode: 1 for the dictionary's bytes
     const int t = threadIdx.x, lane = t & 63;
     if (M == M_NYB_ENC) {
-        s_hit[t] = static_rank((uint32_t)t) != 0xFFu ? 1u : 0u;
+        s_hit[t] = ((c_nyb.rank4[t >> 2] >> (8 * (t & 3))) & 255u) != 0xFFu ? 1u : 0u;
         __syncthreads();
     }
     const uint64_t Tw = ((uint64_t)blockIdx.x * 4 + (uint64_t)(t >> 6)) * NYB_TPW;
@@ -4226,21 +4254,7 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
     __shared__ uint2 s_esel[256];   // v_perm selectors per 4-element pattern
     const int t = threadIdx.x;
     if (M == M_NYB_ENC && !aux.rk) fsm_rank_table(s_rank);
-    {
-        // pattern t = c1 | c2 << 4 (bit i: element i writes its first / its second byte): the
-        // output bytes in order, first byte i = selector i (S1 = the first bytes), second byte
-        // i = selector 4 + i (S0 = the second bytes); 0x0c = a zero byte
-        uint32_t sel[2] = {0x0c0c0c0cu, 0x0c0c0c0cu};
-        int o = 0;
-        for (int i = 0; i < 4; ++i) {
-            if ((t >> i) & 1) { sel[o >> 2] = (sel[o >> 2] & ~(255u << (8 * (o & 3)))) | ((uint32_t)i << (8 * (o & 3))); ++o; }
-            if ((t >> (4 + i)) & 1) {
-                sel[o >> 2] = (sel[o >> 2] & ~(255u << (8 * (o & 3)))) | ((uint32_t)(4 + i) << (8 * (o & 3)));
-                ++o;
-            }
-        }
-        s_esel[t] = make_uint2(sel[0], sel[1]);
-    }
+    s_esel[t] = make_uint2(c_nyb.esel_lo[t], c_nyb.esel_hi[t]);   // (NybTables)
     const bool nyb_whole = M == M_NYB_ENC && aux.whole;
     const bool enc = FsmMode<M>::enc || nyb_whole;
     // every global read the tile needs is issued here, before the first one is waited for (the
