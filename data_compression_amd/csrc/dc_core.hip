@@ -1870,8 +1870,10 @@ __global__ __launch_bounds__(256) void k_fe_pack(const uint8_t *__restrict__ in,
             const uint32_t jj = has ? j0 : 0xFFFFu;
             uint32_t ec = 0, cap = 0;   // symbols seen, bits before the chunk start
             auto tally = [&](uint32_t l) {
+#ifndef DC_DIAG_FE_NOTALLY   // (timing ablation only: wrong sync lengths)
                 ec += l != 0u ? 1u : 0u;
                 cap += ec <= jj ? l : 0u;
+#endif
             };
             uint32_t w4[4] = {blkv[k].x, blkv[k].y, blkv[k].z, blkv[k].w};
             asm volatile("" : "+v"(w4[0]), "+v"(w4[1]), "+v"(w4[2]), "+v"(w4[3]));
@@ -3769,6 +3771,46 @@ static __device__ __forceinline__ Fsm fsm_wave_scan_incl(Fsm f, int lane)
     return f;
 }
 static __device__ __forceinline__ uint4 fsm_pack(const Fsm &f) { return make_uint4(f.c0, f.c1, f.s0, f.s1); }
+
+// A composition in 32 bits (counts < 2^15: a 4096-element tile emits <= 8192 bytes): half h =
+// bytes emitted entering in state h | the exit state << 15. Composition: each half of a picks
+// b's half by its exit state (one v_perm) and adds its count (no carry between the halves).
+#define FSMP_ID 0x80000000u
+static __device__ __forceinline__ uint32_t fsmp(const Fsm &f) { return f.c0 | (f.s0 << 15) | (f.c1 << 16) | (f.s1 << 31); }
+static __device__ __forceinline__ Fsm fsmp_unpack(uint32_t x)
+{
+    Fsm f;
+    f.c0 = x & 0x7FFFu; f.s0 = (x >> 15) & 1u; f.c1 = (x >> 16) & 0x7FFFu; f.s1 = x >> 31;
+    return f;
+}
+static __device__ __forceinline__ uint32_t fsmp_then(uint32_t a, uint32_t b)
+{
+    const uint32_t sel = 0x01000100u + ((a >> 15) & 0x00010001u) * 0x0202u;
+    return (a & 0x7FFF7FFFu) + __builtin_amdgcn_perm(b, b, sel);
+}
+// DPP source of a scan step (a lane with no source, or a row outside row_mask, reads FSMP_ID);
+// a statement of its own (inside `?:` it ran in a branch with lanes off)
+template <int CTRL, int ROWS>
+static __device__ __forceinline__ uint32_t fsmp_dpp(uint32_t x)
+{
+    uint32_t r = (uint32_t)__builtin_amdgcn_update_dpp((int)FSMP_ID, (int)x, CTRL, ROWS, 0xf, false);
+    asm volatile("" : "+v"(r));
+    return r;
+}
+// inclusive scan across the wave (every lane active): row_shr 1, 2, 4, 8 within rows of 16,
+// then row_bcast 15 and 31 (register-only: the ds_bpermute scan of fsm_wave_scan_incl issues
+// 18 LDS shuffles); *ex = the exclusive value (wave_shr 1)
+static __device__ __forceinline__ uint32_t fsmp_wave_scan(uint32_t f, uint32_t *ex)
+{
+    f = fsmp_then(fsmp_dpp<0x111, 0xf>(f), f);
+    f = fsmp_then(fsmp_dpp<0x112, 0xf>(f), f);
+    f = fsmp_then(fsmp_dpp<0x114, 0xf>(f), f);
+    f = fsmp_then(fsmp_dpp<0x118, 0xf>(f), f);
+    f = fsmp_then(fsmp_dpp<0x142, 0xa>(f), f);
+    f = fsmp_then(fsmp_dpp<0x143, 0xc>(f), f);
+    *ex = fsmp_dpp<0x138, 0xf>(f);
+    return f;
+}
 static __device__ __forceinline__ Fsm fsm_unpack(const uint4 &v) { Fsm f; f.c0 = v.x; f.c1 = v.y; f.s0 = v.z; f.s1 = v.w; return f; }
 
 __constant__ uint8_t c_static_rank[256];   // " etaoins" -> 0..7, else 0xFF (initialize_dictionary)
@@ -3807,10 +3849,10 @@ static __device__ __forceinline__ uint4 fsm_granule(uintptr_t ad, uintptr_t lo, 
 {
     return (ad + 16 > lo && ad < hi) ? ld_nt(reinterpret_cast<const uint4 *>(ad)) : make_uint4(0u, 0u, 0u, 0u);
 }
-static __device__ __forceinline__ uint4 fsm_shfl_down(const uint4 &v, int d)
+static __device__ __forceinline__ uint4 fsm_shfl_down1(const uint4 &v)   // lane l <- lane l + 1 (DPP; lane 63: 0)
 {
-    return make_uint4((uint32_t)__shfl_down((int)v.x, d, 64), (uint32_t)__shfl_down((int)v.y, d, 64),
-                      (uint32_t)__shfl_down((int)v.z, d, 64), (uint32_t)__shfl_down((int)v.w, d, 64));
+    const uint32_t x = dpp_wave_shl1(v.x), y = dpp_wave_shl1(v.y), z = dpp_wave_shl1(v.z), w = dpp_wave_shl1(v.w);
+    return make_uint4(x, y, z, w);
 }
 // every lane of the wave must call this (shuffles), also lanes without elements
 static __device__ __forceinline__ FsmWin fsm_window(const uint8_t *__restrict__ in, uint64_t len, int64_t g0)
@@ -3821,10 +3863,11 @@ static __device__ __forceinline__ FsmWin fsm_window(const uint8_t *__restrict__ 
     const uint32_t m = (uint32_t)(s & 3), dq = (uint32_t)((s >> 2) & 3);   // byte and dword shift (uniform)
     const int lane = (int)(threadIdx.x & 63);
     const uint4 v0 = fsm_granule(a, lo, hi);
-    uint4 v1 = fsm_shfl_down(v0, 1), v2 = make_uint4(0u, 0u, 0u, 0u);
+    const uint4 s1 = fsm_shfl_down1(v0);
+    uint4 v1 = s1, v2 = make_uint4(0u, 0u, 0u, 0u);
     if (lane == 63) v1 = fsm_granule(a + 16, lo, hi);
     if (4 * dq + m > 14) {   // the window's 18 used bytes reach a third granule (uniform branch)
-        v2 = fsm_shfl_down(v0, 2);
+        v2 = fsm_shfl_down1(s1);   // (lane 62's is lane 63's v0 via a 0: reloaded below)
         if (lane >= 62) v2 = fsm_granule(a + 32, lo, hi);
     }
     const uint32_t d12[12] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w, v2.x, v2.y, v2.z, v2.w};
@@ -3881,7 +3924,8 @@ static __device__ __forceinline__ Fsm elem_fsm(const FsmWin &W, int k, uint64_t 
 struct NybTables {
     uint32_t rank4[64];              // static ranks, 4 bytes per dword
     uint32_t esel_lo[256], esel_hi[256];   // k_fsm_write's v_perm selectors, per 8-bit pattern
-    constexpr NybTables() : rank4(), esel_lo(), esel_hi()
+    uint32_t dsel_lo[16], dsel_hi[16];     // k_small_write's (decode), per 4-bit pair pattern
+    constexpr NybTables() : rank4(), esel_lo(), esel_hi(), dsel_lo(), dsel_hi()
     {
         const char dict[9] = " etaoins";
         for (int x = 0; x < 256; ++x) {
@@ -3904,6 +3948,19 @@ struct NybTables {
             }
             esel_lo[t] = sel[0];
             esel_hi[t] = sel[1];
+        }
+        // pattern t (bit i: byte i >= 0x80): byte i -> ' ' (S1) then byte i & 0x7F (S0), else
+        // byte i (S0); 0x0c = a zero byte
+        for (int t = 0; t < 16; ++t) {
+            uint32_t sel[2] = {0x0c0c0c0cu, 0x0c0c0c0cu};
+            int o = 0;
+            for (int i = 0; i < 4; ++i) {
+                if ((t >> i) & 1) { sel[o >> 2] = (sel[o >> 2] & ~(255u << (8 * (o & 3)))); ++o; }
+                sel[o >> 2] = (sel[o >> 2] & ~(255u << (8 * (o & 3)))) | ((uint32_t)(4 + i) << (8 * (o & 3)));
+                ++o;
+            }
+            dsel_lo[t] = sel[0];
+            dsel_hi[t] = sel[1];
         }
     }
 };
@@ -4126,8 +4183,9 @@ __global__ __launch_bounds__(256) void k_nyb_tiles(const uint8_t *__restrict__ i
             }
             acc = fsm_then(acc, nyb_lane_fsm<M>(A, B, valid));
         }
-        const Fsm inc = fsm_wave_scan_incl(acc, lane);
-        if (lane == 63) summ[Tw + u] = fsm_pack(inc);
+        uint32_t xp;
+        const uint32_t inc = fsmp_wave_scan(fsmp(acc), &xp);
+        if (lane == 63) summ[Tw + u] = fsm_pack(fsmp_unpack(inc));
     }
 }
 
@@ -4308,12 +4366,10 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
                             ((rk[4 * q + 3] & 255u) << 24);
             f = nyb_lane_fsm<M>(fa[c], fb[c], fvalid[c]);
         }
-        const Fsm inc = fsm_wave_scan_incl(f, lane);
-        if (lane == 63) s_f[c][wid] = fsm_pack(inc);
-        const uint32_t c0 = (uint32_t)__shfl_up((int)inc.c0, 1, 64), c1 = (uint32_t)__shfl_up((int)inc.c1, 1, 64);
-        const uint32_t ss = (uint32_t)__shfl_up((int)(inc.s0 | (inc.s1 << 1)), 1, 64);
-        ex[c].c0 = c0; ex[c].c1 = c1; ex[c].s0 = ss & 1u; ex[c].s1 = ss >> 1;
-        if (lane == 0) ex[c] = fsm_id();
+        uint32_t xp;
+        const uint32_t inc = fsmp_wave_scan(fsmp(f), &xp);
+        if (lane == 63) s_f[c][wid] = fsm_pack(fsmp_unpack(inc));
+        ex[c] = fsmp_unpack(xp);
     }
     __syncthreads();
     // entry = the group's entry, then the tile's local exclusive composition (k_fsm_scan_up)
@@ -4706,19 +4762,7 @@ __global__ __launch_bounds__(SmMode<M>::wthreads) void k_small_write(const uint8
     __shared__ uint2 s_sel[16];   // decode: v_perm selectors of the 4-8 output bytes of a dword, per pair pattern
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const bool enc = M == M_SMALL_ENC;
-    if (dec && t < 16) {   // pattern t (bit i: byte i >= 0x80): byte i -> ' ' (S1) then byte i & 0x7F (S0),
-        uint32_t sel[2] = {0x0c0c0c0cu, 0x0c0c0c0cu};   // else byte i (S0); 0x0c = a zero byte
-        int o = 0;
-        for (int i = 0; i < 4; ++i) {
-            if ((t >> i) & 1) {
-                sel[o >> 2] = (sel[o >> 2] & ~(255u << (8 * (o & 3)))) | (0u << (8 * (o & 3)));
-                ++o;
-            }
-            sel[o >> 2] = (sel[o >> 2] & ~(255u << (8 * (o & 3)))) | ((uint32_t)(4 + i) << (8 * (o & 3)));
-            ++o;
-        }
-        s_sel[t] = make_uint2(sel[0], sel[1]);
-    }
+    if (dec && t < 16) s_sel[t] = make_uint2(c_nyb.dsel_lo[t], c_nyb.dsel_hi[t]);   // (NybTables)
     const uint64_t total = enc ? 2 + meta[0] : 1 + meta[0];
     if (enc && total >= len) {   // LITERAL: ' ' + raw input (:655-662), one grid-stride pass
         for (uint64_t i = (uint64_t)blockIdx.x * NT + t; i < len; i += (uint64_t)gridDim.x * NT) out[1 + i] = in[i];
