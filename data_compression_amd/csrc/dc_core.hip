@@ -3735,6 +3735,10 @@ struct FsmAux {
     uint32_t is_last;     // M_NYB_ENC: the shard ends the stream (odd-tail byte, :1000-1009)
     uint32_t whole;       // M_NYB_ENC: whole stream (header 0xAF x[0], LITERAL fallback)
     uint32_t tokens;      // M_NYB_DEC: a hit writes 0x80 | rank, not its static byte (k_nyb_resolve)
+    // M_NYB_ENC with rk: the first touches of each tile (k_mtf_walk<2>), their ranks settled by
+    // k_mtf_resolve in bits 24..31 (rk holds 0xFE there but for a tile's last element)
+    const uint2 *frec;    // MTF_REC per tile: tile offset | byte << 12 | context << 20 | rank << 24
+    const uint2 *fhead;   // per tile: the count of first touches
 };
 #define FSM_SUB 1                          /* 4096-element chunks per tile */
 #define FSM_TILE (4096 * FSM_SUB)
@@ -3972,7 +3976,8 @@ static __device__ __forceinline__ void fsm_rank_table(uint8_t *s_rank)
 }
 template <int M>
 static __device__ __forceinline__ void fsm_ranks(const FsmWin &W, const FsmAux &aux, uint64_t j0, uint64_t nelem,
-                                                 uint32_t (&rk)[16], const uint8_t *s_rank)
+                                                 uint32_t (&rk)[16], const uint8_t *s_rank,
+                                                 const uint8_t *s_patch = nullptr)
 {
     if (M != M_NYB_ENC) return;
     if (aux.rk) {
@@ -3987,6 +3992,16 @@ static __device__ __forceinline__ void fsm_ranks(const FsmWin &W, const FsmAux &
         const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
         for (int k = 0; k < 16; ++k) rk[k] = (w4[k >> 2] >> (8 * (k & 3))) & 255u;
+        if (s_patch) {   // first touches (0xFE): their settled ranks, from the tile's list in LDS
+            uint32_t fe = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) fe |= swar_eq(w4[q], 0xFEFEFEFEu);
+            if (fe & 0x80808080u) {
+#pragma unroll
+                for (int k = 0; k < 16; ++k)
+                    if (rk[k] == 0xFEu) rk[k] = s_patch[(uint32_t)(j0 & (FSM_TILE - 1)) + k];
+            }
+        }
     } else {
 #pragma unroll
         for (int k = 0; k < 16; ++k) rk[k] = s_rank[W.b(k + 1)];
@@ -4085,8 +4100,15 @@ __global__ __launch_bounds__(256) void k_fsm_tiles(const uint8_t *__restrict__ i
 {
     __shared__ uint4 s_f[FSM_SUB][4];   // wave totals per chunk
     __shared__ __attribute__((aligned(4))) uint8_t s_rank[256];
+    __shared__ uint8_t s_patch[M == M_NYB_ENC ? FSM_TILE : 1];   // settled first-touch ranks (k_fsm_write)
     const int t = threadIdx.x;
-    if (M == M_NYB_ENC && !aux.rk) { fsm_rank_table(s_rank); __syncthreads(); }
+    const bool patch = M == M_NYB_ENC && aux.rk && aux.frec;
+    if (patch && (uint32_t)t < aux.fhead[blockIdx.x].x) {
+        const uint32_t r = aux.frec[(uint64_t)blockIdx.x * 128 + t].x;
+        s_patch[r & (FSM_TILE - 1)] = (uint8_t)(r >> 24);
+    }
+    if (M == M_NYB_ENC && !aux.rk) fsm_rank_table(s_rank);
+    if (M == M_NYB_ENC) __syncthreads();
     // chunk c of the tile: elements [c * 4096 + 16 t, +16) for lane t (coalesced per chunk);
     // all chunks' windows are loaded before any is walked
     FsmWin W[FSM_SUB];
@@ -4100,7 +4122,7 @@ __global__ __launch_bounds__(256) void k_fsm_tiles(const uint8_t *__restrict__ i
         Fsm f = fsm_id();
         if (j0 < nelem) {
             uint32_t rk[16], A, B;
-            fsm_ranks<M>(W[c], aux, j0, nelem, rk, s_rank);
+            fsm_ranks<M>(W[c], aux, j0, nelem, rk, s_rank, patch ? s_patch : nullptr);
             nyb_lane_flags<M>(W[c], rk, A, B);
             const uint32_t valid = nelem - j0 >= 16 ? 0xFFFFu : (1u << (uint32_t)(nelem - j0)) - 1u;
             f = nyb_lane_fsm<M>(A, B, valid);
@@ -4310,8 +4332,16 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
     __shared__ __attribute__((aligned(16))) uint8_t s_out[2 * FSM_TILE + 32];
     __shared__ __attribute__((aligned(4))) uint8_t s_rank[256];
     __shared__ uint2 s_esel[256];   // v_perm selectors per 4-element pattern
+    __shared__ uint8_t s_patch[M == M_NYB_ENC ? FSM_TILE : 1];   // settled first-touch ranks, by tile offset
     const int t = threadIdx.x;
     if (M == M_NYB_ENC && !aux.rk) fsm_rank_table(s_rank);
+    const bool patch = M == M_NYB_ENC && aux.rk && aux.frec;
+    if (patch) {   // (a tile holds <= MTF_REC = 128 first touches: one per thread)
+        if ((uint32_t)t < aux.fhead[blockIdx.x].x) {
+            const uint32_t r = aux.frec[(uint64_t)blockIdx.x * 128 + t].x;
+            s_patch[r & (FSM_TILE - 1)] = (uint8_t)(r >> 24);
+        }
+    }
     s_esel[t] = make_uint2(c_nyb.esel_lo[t], c_nyb.esel_hi[t]);   // (NybTables)
     const bool nyb_whole = M == M_NYB_ENC && aux.whole;
     const bool enc = FsmMode<M>::enc || nyb_whole;
@@ -4342,7 +4372,7 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
     }
     for (uint32_t i = (uint32_t)t; i < (2 * FSM_TILE + 32) / 16; i += 256)   // the stage is OR-merged into
         reinterpret_cast<uint4 *>(s_out)[i] = make_uint4(0u, 0u, 0u, 0u);
-    if (M == M_NYB_ENC && !aux.rk) __syncthreads();   // s_rank (the stage: ordered by the scan's barrier)
+    if (M == M_NYB_ENC && (!aux.rk || patch)) __syncthreads();   // s_rank, s_patch (the stage: ordered by the scan's barrier)
     // per chunk: the lane's composition, scanned across the wave (shuffles); the wave totals of
     // every chunk through LDS (one barrier)
     const int lane = t & 63, wid = t >> 6;
@@ -4358,7 +4388,7 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
         Fsm f = fsm_id();
         if (j0 < nelem) {
             uint32_t rk[16];
-            fsm_ranks<M>(W_[c], aux, j0, nelem, rk, s_rank);
+            fsm_ranks<M>(W_[c], aux, j0, nelem, rk, s_rank, patch ? s_patch : nullptr);
             nyb_lane_flags<M>(W_[c], rk, fa[c], fb[c]);
 #pragma unroll
             for (int q = 0; q < 4; ++q)
@@ -4427,7 +4457,8 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
             const uint32_t Hx = (fa[c] & valid) | (~valid & 0xFFFFu), Sx = S & valid;
             // the rank of the pending hit before element 0: the previous window byte's, or the
             // shard's carried one
-            const uint32_t rp0 = j0 ? (aux.rk ? (uint32_t)aux.rk[j0 - 1] : (uint32_t)s_rank[W.b(0)]) : aux.pend_rank;
+            uint32_t rp0 = j0 ? (aux.rk ? (uint32_t)aux.rk[j0 - 1] : (uint32_t)s_rank[W.b(0)]) : aux.pend_rank;
+            if (patch && rp0 == 0xFEu) rp0 = s_patch[(uint32_t)((j0 - 1) & (FSM_TILE - 1))];   // (same tile: a tile's last is settled in rk)
             if (aux.is_last && len >= 2 && len - 2 >= j0 && len - 2 < j0 + kend) {
                 // odd tail (:1000-1009): the stream's last element a hit left pending: its byte,
                 // raw, after the bytes of the elements before it
@@ -4967,69 +4998,93 @@ static __device__ __forceinline__ uint64_t mtf_touch8(uint64_t L, uint32_t v, ui
     return (((L << 8) | v) & m) | (L & ~m);
 }
 
-// MODE 0: tile summaries from empty lists -> summ[tile]; MODE 1: ranks from entry[tile].
-// Elements are bytes 1..len-1 of `in` (element e = byte e+1; its context is byte e).
+// k_mtf_walk: one pass over each 4096-element tile from EMPTY lists (elements are bytes 1..len-1
+// of `in`: element e = byte e+1, its context byte e). MODE 0: the tile summaries -> summ[tile].
+// MODE 2: also the ranks into rk, but for the FIRST TOUCHES. A hit's rank is final already (an
+// entry touched in the tile sits above every entry-list byte, in the same order whatever the
+// entry lists were); a miss on a full list is a miss (0xFF); a miss while the list holds fewer
+// than 8 entries is a first touch, whose rank depends on the entry lists: it is written 0xFE and
+// listed in rec (tile offset | byte << 12 | context << 20, and the nybble encoder's composition
+// of the known elements since the previous first touch), for k_mtf_resolve. head[tile] = (the
+// count, the composition after the last one). (The encoder's FSM tiles are these tiles.)
 // A lane walks its tile with the 16 lists in LDS (column t). Per element: the next element's
 // list is read before this one's is written back (its context is this element's byte; the same
 // context takes the list just computed), so the LDS round trip overlaps the touch; the input
-// comes in 16-B granules loaded a 64-element group ahead. Lists are full (the initial lists and
-// their compositions) or, in MODE 0, padded with zero bytes (mtf_touch8): a list's count is
-// recovered at the end from its zero bytes and whether a zero was touched in its context.
-// (r4: one lane-local loop that waited on every list read and on the granule just loaded,
-// counts kept per element: 1.64 ms per GiB for MODE 0, 2.03 for MODE 1.)
-// MODE 1 with fsumm set also writes the nybble encoder's tile summary of its tile (the FSM
-// tiles of k_fsm_tiles<M_NYB_ENC> are these 4096-element tiles): the composition of its steps'
-// hit masks (nyb_lane_fsm), so the encoder's counting pass (k_fsm_tiles, which re-read the
-// ranks) does not run.
-static_assert(FSM_TILE == MTF_TILE, "k_mtf_walk<1> writes the nybble encoder's tile summaries");
-template <int MODE>
-__global__ __launch_bounds__(256) void k_mtf_walk(const uint8_t *__restrict__ in, uint64_t len, uint64_t ntiles,
-                                                  const MtfSum *__restrict__ entry, MtfSum *__restrict__ summ,
-                                                  uint8_t *__restrict__ rk, uint4 *__restrict__ fsumm)
+// comes in 16-B granules loaded a 64-element group ahead. Lists are padded with zero bytes
+// (mtf_touch8), so a list is short while its last byte is 0 and its count is 8 - its zero bytes,
+// both exact while no element is a zero byte; a tile that has one is walked again with counts
+// (mtf_touch64). (r4 before: a summary pass, then a second walk of every tile from its entry
+// lists for the ranks, 0.90 + 1.24 ms per GiB; first: one lane-local loop that waited on every
+// list read and on the granule just loaded, 1.64 + 2.03 ms.)
+#define MTF_REC 128   /* first touches per tile: <= 8 per context */
+
+// k_mtf_walk<2>'s 16 elements with first touches F (hits H, valid nv; element bytes X, the
+// context byte of element 0 pv, tile offset o): the segments between them fold into accp, each
+// is listed. Out of line: rare after a tile's first few hundred elements, and inlined into the
+// walk's steps it took the walk from 71 to 155 VGPRs (5 -> 3 waves per SIMD).
+struct MtfRecState { uint32_t accp, nrec; };
+static __device__ __noinline__ MtfRecState mtf_records(uint32_t H, uint32_t F, uint32_t nv, uint32_t X0, uint32_t X1,
+                                                       uint32_t X2, uint32_t X3, uint32_t pv, uint32_t o,
+                                                       MtfRecState st, uint2 *__restrict__ trec)
 {
+    const uint32_t X[4] = {X0, X1, X2, X3};
+    uint32_t from = nv;   // elements not folded yet
+    while (F) {
+        const uint32_t k = (uint32_t)__builtin_ctz(F);
+        F &= F - 1u;
+        const uint32_t below = (1u << k) - 1u;
+        st.accp = fsmp_then(st.accp, fsmp(nyb_lane_fsm<M_NYB_ENC>(H, 0u, from & below)));
+        const uint32_t x = (X[k >> 2] >> (8 * (k & 3))) & 255u;
+        const uint32_t p = k ? (X[(k - 1) >> 2] >> (8 * ((k - 1) & 3))) & 255u : pv;
+        // (<= 8 per context, but for a walk with a zero byte, whose pads are ambiguous: its
+        // list is rebuilt by the counted walk; the bound keeps it off the next tile's)
+        if (st.nrec < MTF_REC) trec[st.nrec] = make_uint2((o + k) | (x << 12) | (((p >> 3) & 15u) << 20), st.accp);
+        ++st.nrec;
+        st.accp = FSMP_ID;
+        from &= ~(below | (1u << k));
+    }
+    st.accp = fsmp_then(st.accp, fsmp(nyb_lane_fsm<M_NYB_ENC>(H, 0u, from)));
+    return st;
+}
+static_assert(FSM_TILE == MTF_TILE, "k_mtf_walk<2> composes the nybble encoder's tile summaries");
+template <int MODE>
+__global__ __launch_bounds__(256) void k_mtf_walk(
+    const uint8_t *__restrict__ in, uint64_t len, uint64_t ntiles, MtfSum *__restrict__ summ, uint8_t *__restrict__ rk,
+    uint2 *__restrict__ rec, uint2 *__restrict__ head)
+{
+    static_assert(MODE == 0 || MODE == 2, "summaries, or summaries and ranks");
     __shared__ uint64_t s_L[16][256];
     const int t = threadIdx.x;
     const uint64_t tile = (uint64_t)blockIdx.x * 256 + t;
     if (tile >= ntiles) return;   // no barriers below
     const uint64_t e0 = tile * MTF_TILE;
     const uint64_t e1 = (e0 + MTF_TILE < len - 1) ? e0 + MTF_TILE : len - 1;   // elements [e0, e1)
-    uint64_t cnts = 0;   // nibble c = valid entries of list c
-    for (int c = 0; c < 16; ++c) {
-        s_L[c][t] = MODE ? entry[tile].L[c] : 0ull;
-        if (MODE) cnts |= (uint64_t)entry[tile].cnt[c] << (4 * c);
-    }
-    uint32_t prev = in[e0];
-    Fsm acc = fsm_id();   // MODE 1: the encoder's composition of the tile
-    auto fold = [&](uint32_t A, uint32_t valid) {
-        if (MODE) acc = fsm_then(acc, nyb_lane_fsm<M_NYB_ENC>(A, 0u, valid));
-    };
-    if (MODE && !__all(cnts == 0x8888888888888888ull)) {
-        // entry lists of fewer than 8 entries (not produced by this pipeline): counted walk
-        for (uint64_t e = e0; e < e1; e += 16) {
-            const uint32_t cnt16 = e1 - e < 16 ? (uint32_t)(e1 - e) : 16u;
-            uint32_t R[4] = {0u, 0u, 0u, 0u}, A = 0;
-            for (uint32_t k = 0; k < cnt16; ++k) {
-                const uint32_t x = in[e + 1 + k];
-                const uint32_t c = (prev >> 3) & 15u;
-                uint64_t L = s_L[c][t];
-                uint32_t n = (uint32_t)(cnts >> (4 * c)) & 15u;
-                const int r = mtf_touch64(L, n, x);
-                s_L[c][t] = L;
-                cnts = (cnts & ~(15ull << (4 * c))) | ((uint64_t)n << (4 * c));
-                prev = x;
-                R[k >> 2] |= (uint32_t)(r < 0 ? 0xFF : r) << (8 * (k & 3));
-                A |= (r < 0 ? 0u : 1u) << k;
-            }
-            if (cnt16 == 16) *reinterpret_cast<uint4 *>(rk + e) = make_uint4(R[0], R[1], R[2], R[3]);
-            else for (uint32_t k = 0; k < cnt16; ++k) rk[e + k] = (uint8_t)(R[k >> 2] >> (8 * (k & 3)));
-            fold(A, (1u << cnt16) - 1u);
+    for (int c = 0; c < 16; ++c) s_L[c][t] = 0ull;
+    const uint32_t prev0 = in[e0];
+    uint32_t cc = (prev0 >> 3) & 15u;
+    uint64_t Lc = 0ull;
+    uint32_t anyz = 0;   // 0x80 bits: a zero byte among the tile's elements
+    uint32_t accp = FSMP_ID, nrec = 0;
+    uint2 *const trec = rec + (MODE == 2 ? tile * MTF_REC : 0);
+    // MODE 2, after 16 elements (element k: rank byte k of R, byte k of X, valid bits nv): the
+    // known elements fold into accp, each first touch closes a segment and is listed
+    auto post = [&](const uint32_t (&R)[4], const uint32_t (&X)[4], uint32_t pv, uint64_t e, uint32_t nv) {
+        uint32_t H = 0, F = 0;   // hits (a byte <= 7); first touches (0xFE)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            H |= byte_bits4(~R[q], 7) << (4 * q);
+            F |= byte_bits4(R[q] & ~(R[q] << 7), 7) << (4 * q);
         }
-        if (fsumm) fsumm[tile] = fsm_pack(acc);
-        return;
-    }
-    uint32_t zt = 0;   // MODE 0: bit c = a zero byte was touched in context c
-    uint32_t cc = (prev >> 3) & 15u;
-    uint64_t Lc = s_L[cc][t];
+        F &= nv;
+        if (F) {
+            const MtfRecState st = mtf_records(H, F, nv, X[0], X[1], X[2], X[3], pv, (uint32_t)(e - e0),
+                                               MtfRecState{accp, nrec}, trec);
+            accp = st.accp;
+            nrec = st.nrec;
+        } else {
+            accp = fsmp_then(accp, fsmp(nyb_lane_fsm<M_NYB_ENC>(H, 0u, nv)));
+        }
+    };
     // granule i = bytes [gb + 16 i, +16) of `in`, gb = element e0's byte rounded down to 16 B;
     // element e0 + 16 s + k is byte sh + 16 s + k of granules s, s + 1 (sh uniform: in + 1's
     // alignment, e0 a multiple of 16)
@@ -5048,8 +5103,10 @@ __global__ __launch_bounds__(256) void k_mtf_walk(const uint8_t *__restrict__ in
 #pragma unroll
             for (int k = 1; k < 4; ++k) { lo = dq == (uint32_t)k ? d8[j + k] : lo; hi = dq == (uint32_t)k ? d8[j + k + 1] : hi; }
             X[j] = __builtin_amdgcn_alignbyte(hi, lo, db);
+            anyz |= (X[j] - 0x01010101u) & ~X[j] & 0x80808080u;
         }
-        uint32_t R[4] = {0u, 0u, 0u, 0u}, H = 0;
+        const uint32_t pv = (cc << 3);   // (context of element 0: only its bits 3..6 are used)
+        uint32_t R[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
             const uint32_t x = (X[k >> 2] >> (8 * (k & 3))) & 255u;
@@ -5059,53 +5116,151 @@ __global__ __launch_bounds__(256) void k_mtf_walk(const uint8_t *__restrict__ in
             bool hit;
             const uint64_t L2 = mtf_touch8(Lc, x, pb, hit);
             s_L[cc][t] = L2;
-            if (MODE) { R[k >> 2] |= (hit ? pb >> 3 : 0xFFu) << (8 * (k & 3)); H |= (hit ? 1u : 0u) << k; }
-            else zt |= ((x - 1u) >> 31) << cc;
+            if (MODE == 2) {
+                R[k >> 2] |= (hit ? pb >> 3 : (Lc >> 56) == 0ull ? 0xFEu : 0xFFu) << (8 * (k & 3));
+                asm volatile("" : "+v"(R[k >> 2]));   // (sunk to the step's end, 16 ranks' inputs stayed live: +56 VGPRs)
+            }
             Lc = cn == cc ? L2 : Ln;
             cc = cn;
         }
-        if (MODE) {
+        if (MODE == 2) {
             *reinterpret_cast<uint4 *>(rk + e) = make_uint4(R[0], R[1], R[2], R[3]);
-            fold(H, 0xFFFFu);
+            post(R, X, pv, e, 0xFFFFu);
         }
     };
     uint4 G0 = ld(0), G1 = ld(1), G2 = ld(2), G3 = ld(3), G4 = ld(4);
     uint64_t e = e0, gi = 0;
     for (; e + 64 <= e1; e += 64, gi += 4) {
         const uint4 N1 = ld(gi + 5), N2 = ld(gi + 6), N3 = ld(gi + 7), N4 = ld(gi + 8);
+        // (the steps kept apart: interleaved by the scheduler they held 155 VGPRs, 3 waves per SIMD)
         step(G0, G1, e);
+        __builtin_amdgcn_sched_barrier(0);
         step(G1, G2, e + 16);
+        __builtin_amdgcn_sched_barrier(0);
         step(G2, G3, e + 32);
+        __builtin_amdgcn_sched_barrier(0);
         step(G3, G4, e + 48);
+        __builtin_amdgcn_sched_barrier(0);
         G0 = G4; G1 = N1; G2 = N2; G3 = N3; G4 = N4;
     }
-    for (; e < e1; e += 16) {   // the last tile's ragged end
-        const uint32_t cnt16 = e1 - e < 16 ? (uint32_t)(e1 - e) : 16u;
-        uint32_t A = 0;
-        for (uint32_t k = 0; k < cnt16; ++k) {
+    for (; e < e1; e += 16) {   // the last tile's ragged end, 16 elements at a time
+        const uint32_t nk = e1 - e < 16 ? (uint32_t)(e1 - e) : 16u;
+        const uint32_t pv = (cc << 3);
+        uint32_t R[4] = {~0u, ~0u, ~0u, ~0u}, X[4] = {0u, 0u, 0u, 0u};
+        for (uint32_t k = 0; k < nk; ++k) {
             const uint32_t x = in[e + 1 + k];
             uint32_t pb;
             bool hit;
             const uint64_t L2 = mtf_touch8(Lc, x, pb, hit);
             s_L[cc][t] = L2;
-            if (MODE) { rk[e + k] = (uint8_t)(hit ? pb >> 3 : 0xFFu); A |= (hit ? 1u : 0u) << k; }
-            else zt |= ((x - 1u) >> 31) << cc;
+            const uint32_t r = hit ? pb >> 3 : (Lc >> 56) == 0ull ? 0xFEu : 0xFFu;
+            if (MODE == 2) rk[e + k] = (uint8_t)r;
+            R[k >> 2] = (R[k >> 2] & ~(255u << (8 * (k & 3)))) | (r << (8 * (k & 3)));
+            X[k >> 2] |= x << (8 * (k & 3));
+            anyz |= x == 0u ? 0x80u : 0u;
             cc = (x >> 3) & 15u;
             Lc = s_L[cc][t];
         }
-        fold(A, (1u << cnt16) - 1u);
+        if (MODE == 2) post(R, X, pv, e, (1u << nk) - 1u);
     }
-    if (MODE && fsumm) fsumm[tile] = fsm_pack(acc);
-    if (!MODE) {
-        for (int c = 0; c < 16; ++c) {
-            const uint64_t L = s_L[c][t];
-            uint32_t nz = 0;   // zero bytes: the pads, and a touched zero still on the list
-#pragma unroll
-            for (int q = 0; q < 8; ++q) nz += ((L >> (8 * q)) & 255u) == 0u ? 1u : 0u;
-            summ[tile].L[c] = L;
-            summ[tile].cnt[c] = (uint8_t)(nz ? 8u - nz + ((zt >> c) & 1u) : 8u);
+    uint64_t cnts = 0;   // nibble c = entries of list c
+    if (anyz) {
+        // a zero byte makes the pads ambiguous: the tile again, with counts (rare on text)
+        for (int c = 0; c < 16; ++c) s_L[c][t] = 0ull;
+        accp = FSMP_ID;
+        nrec = 0;
+        uint32_t pvb = prev0;
+        for (uint64_t f = e0; f < e1; f += 16) {
+            const uint32_t nk = e1 - f < 16 ? (uint32_t)(e1 - f) : 16u;
+            const uint32_t pv = pvb;
+            uint32_t R[4] = {~0u, ~0u, ~0u, ~0u}, X[4] = {0u, 0u, 0u, 0u};
+            for (uint32_t k = 0; k < nk; ++k) {
+                const uint32_t x = in[f + 1 + k], c = (pvb >> 3) & 15u;
+                uint64_t L = s_L[c][t];
+                uint32_t n = (uint32_t)(cnts >> (4 * c)) & 15u;
+                const uint32_t nb = n;
+                const int r0 = mtf_touch64(L, n, x);
+                s_L[c][t] = L;
+                cnts = (cnts & ~(15ull << (4 * c))) | ((uint64_t)n << (4 * c));
+                const uint32_t r = r0 >= 0 ? (uint32_t)r0 : nb < 8 ? 0xFEu : 0xFFu;
+                if (MODE == 2) rk[f + k] = (uint8_t)r;
+                R[k >> 2] = (R[k >> 2] & ~(255u << (8 * (k & 3)))) | (r << (8 * (k & 3)));
+                X[k >> 2] |= x << (8 * (k & 3));
+                pvb = x;
+            }
+            if (MODE == 2) post(R, X, pv, f, (1u << nk) - 1u);
         }
     }
+    if (MODE == 2) head[tile] = make_uint2(nrec, accp);
+    for (int c = 0; c < 16; ++c) {
+        const uint64_t L = s_L[c][t];
+        uint32_t nz = 0;   // zero bytes: the pads
+#pragma unroll
+        for (int q = 0; q < 8; ++q) nz += ((L >> (8 * q)) & 255u) == 0u ? 1u : 0u;
+        summ[tile].L[c] = L;
+        summ[tile].cnt[c] = (uint8_t)(anyz ? (uint32_t)(cnts >> (4 * c)) & 15u : 8u - nz);
+    }
+}
+
+// k_mtf_resolve: the first touches k_mtf_walk<2> listed, from each tile's entry lists, and the
+// nybble encoder's tile summaries. The j-th first touch of context c in a tile (j < 8: the list
+// held the j bytes touched in the tile above the entry list) has rank j + its position among
+// the entry list's bytes not touched in the tile yet (a miss past 7, or when absent): G_c = the
+// entry list less those bytes (LDS column t); each first touch takes its byte out. The rank
+// goes into its record (bits 24..31; the encoder's writer reads the tile's list into LDS: rank
+// bytes scattered into rk cost 0.37 ms per GiB in partial-line writes), and into rk only for the
+// tile's last element (read across the tile boundary); the tile's composition is the listed
+// segments with each first touch (a hit or a miss) between them. One lane per tile, its records
+// read 16 at a time.
+__global__ __launch_bounds__(256) void k_mtf_resolve(uint64_t len, uint64_t ntiles, const MtfSum *__restrict__ entry,
+                                                     uint2 *__restrict__ rec, const uint2 *__restrict__ head,
+                                                     uint8_t *__restrict__ rk, uint4 *__restrict__ fsumm)
+{
+    __shared__ uint64_t s_G[16][256];
+    const int t = threadIdx.x;
+    const uint64_t tile = (uint64_t)blockIdx.x * 256 + t;
+    if (tile >= ntiles) return;   // no barriers below
+    const uint2 hd = head[tile];
+    uint64_t jn = 0, gv = 0;   // nibble c: first touches so far / bytes left in G_c
+    for (int c = 0; c < 16; ++c) {
+        s_G[c][t] = entry[tile].L[c];
+        gv |= (uint64_t)min((uint32_t)entry[tile].cnt[c], 8u) << (4 * c);
+    }
+    uint2 *const trec = rec + tile * MTF_REC;
+    const uint64_t e0 = tile * MTF_TILE;
+    const uint32_t last = (uint32_t)(((e0 + MTF_TILE < len - 1) ? e0 + MTF_TILE : len - 1) - e0 - 1);   // the tile's last element
+    uint32_t accp = FSMP_ID;
+    for (uint32_t i0 = 0; i0 < hd.x; i0 += 16) {
+        uint2 r[16];
+#pragma unroll
+        for (uint32_t q = 0; q < 16; ++q) r[q] = i0 + q < hd.x ? trec[i0 + q] : make_uint2(0u, 0u);
+#pragma unroll
+        for (uint32_t q = 0; q < 16; ++q) {
+            if (i0 + q >= hd.x) break;
+            const uint32_t off = r[q].x & 4095u, x = (r[q].x >> 12) & 255u, c = (r[q].x >> 20) & 15u;
+            const uint32_t j = (uint32_t)(jn >> (4 * c)) & 15u, v = (uint32_t)(gv >> (4 * c)) & 15u;
+            uint32_t rank = 0xFFu;
+            if (j < 8u) {
+                const uint64_t G = s_G[c][t];
+                const uint64_t tt = G ^ (0x0101010101010101ull * x);
+                const uint64_t z = (tt - 0x0101010101010101ull) & ~tt & 0x8080808080808080ull;
+                const uint32_t pos = z ? (uint32_t)__builtin_ctzll(z) >> 3 : 8u;
+                if (pos < v) {
+                    rank = j + pos <= 7u ? j + pos : 0xFFu;
+                    const uint64_t lowm = (1ull << (8 * pos)) - 1ull;   // out: the bytes above come down
+                    s_G[c][t] = (G & lowm) | ((G >> 8) & ~lowm);
+                    gv -= 1ull << (4 * c);
+                }
+                jn += 1ull << (4 * c);
+            }
+            trec[i0 + q].x = r[q].x | (rank << 24);
+            if (off == last) rk[e0 + off] = (uint8_t)rank;
+            // the segment before it, then the element: a hit (0 / 1 bytes, to state 1 / 0) or a
+            // miss (1 / 2 bytes, to state 0), as elem_fsm<M_NYB_ENC>
+            accp = fsmp_then(fsmp_then(accp, r[q].y), rank != 0xFFu ? 0x00018000u : 0x00020001u);
+        }
+    }
+    fsumm[tile] = fsm_pack(fsmp_unpack(fsmp_then(accp, hd.y)));
 }
 
 // parent[g] = composition of child summaries [64 g, 64 g + 64); one lane per (group, context)
@@ -5915,6 +6070,8 @@ struct dc_ctx {
     uint64_t *d_entry;      size_t entry_cap;
     MtfSum *d_mtf;          size_t mtf_cap;       // adaptive nybble: tile summaries + entries, all levels
     uint8_t *d_rk;          size_t rk_cap;        // adaptive nybble: rank per element
+    uint2 *d_mrec;          size_t mrec_cap;      // adaptive nybble: first touches per tile + heads
+    MtfSum *h_mtf;                                // adaptive nybble: pinned entry lists (mtf_run)
     uint32_t *d_actl;       size_t actl_cap;      // adaptive nybble decode: control words of a segment
     uint32_t *d_astate;                           // adaptive nybble decode: lists + byte between segments
     const uint8_t *rk_in; uint64_t rk_len;        // identity of the input the ranks belong to
@@ -6089,6 +6246,8 @@ void dc_ctx_destroy(dc_ctx *c)
     if (c->d_entry) (void)hipFree(c->d_entry);
     if (c->d_mtf) (void)hipFree(c->d_mtf);
     if (c->d_rk) (void)hipFree(c->d_rk);
+    if (c->d_mrec) (void)hipFree(c->d_mrec);
+    if (c->h_mtf) (void)hipHostFree(c->h_mtf);
     if (c->d_actl) (void)hipFree(c->d_actl);
     if (c->d_astate) (void)hipFree(c->d_astate);
     if (c->d_kscr) (void)hipFree(c->d_kscr);
@@ -6819,6 +6978,13 @@ static int fsm_write_planned(dc_ctx *c, const uint8_t *d_in, uint64_t len, uint6
     return DC_OK;
 }
 
+// the per-tile first-touch counts of the last mtf_run(ranks) over len bytes (after the records)
+static const uint2 *mtf_heads(const dc_ctx *c, uint64_t len)
+{
+    const uint64_t n0 = len > 1 ? (len - 2) / MTF_TILE + 1 : 0;
+    return c->d_mrec ? c->d_mrec + n0 * MTF_REC : nullptr;
+}
+
 // Adaptive nybble ranks (k_mtf_* pipeline) of elements 1..len-1 of d_in into c->d_rk, from the
 // entry lists h_init. ranks = false: only the composition of the whole input from h_init
 // into *h_final (a shard summary when h_init is empty).
@@ -6840,11 +7006,19 @@ static int mtf_run(dc_ctx *c, const uint8_t *d_in, uint64_t len, const MtfSum *h
     // layout: [summaries, all levels][entries, all levels][init][final]
     if (ensure((void **)&c->d_mtf, &c->mtf_cap, (2 * tot + 2) * sizeof(MtfSum))) return DC_E_HIP;
     MtfSum *S = c->d_mtf, *E = c->d_mtf + tot, *init = c->d_mtf + 2 * tot, *fin = init + 1;
-    HIPCHK(hipMemcpyAsync(init, h_init, sizeof(MtfSum), hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));   // h_init is pageable
+    // the entry lists through a pinned copy: no wait here (the stream is idle at every call: the
+    // calls that follow an mtf_run end by reading back on it)
+    if (!c->h_mtf && hipHostMalloc((void **)&c->h_mtf, sizeof(MtfSum), 0) != hipSuccess) return DC_E_HIP;
+    memcpy(c->h_mtf, h_init, sizeof(MtfSum));
+    HIPCHK(hipMemcpyAsync(init, c->h_mtf, sizeof(MtfSum), hipMemcpyHostToDevice, c->stream));
     if (ranks && ensure((void **)&c->d_rk, &c->rk_cap, ((len + 3) & ~3ull))) return DC_E_HIP;
-    LAUNCH(c, "mtf_tiles", k_mtf_walk<0>, (n0 + 255) / 256, 256, d_in, len, n0, (const MtfSum *)nullptr, S,
-           (uint8_t *)nullptr, (uint4 *)nullptr);
+    if (ranks && ensure((void **)&c->d_mrec, &c->mrec_cap, n0 * (MTF_REC + 1) * sizeof(uint2))) return DC_E_HIP;
+    uint2 *const mrec = c->d_mrec, *const mhead = c->d_mrec + (ranks ? n0 * MTF_REC : 0);
+    if (ranks)   // the summaries, the ranks but for the first touches, and their list: one walk
+        LAUNCH(c, "mtf_tiles", k_mtf_walk<2>, (n0 + 255) / 256, 256, d_in, len, n0, S, c->d_rk, mrec, mhead);
+    else
+        LAUNCH(c, "mtf_tiles", k_mtf_walk<0>, (n0 + 255) / 256, 256, d_in, len, n0, S, (uint8_t *)nullptr,
+               (uint2 *)nullptr, (uint2 *)nullptr);
     for (int l = 0; l + 1 < levels; ++l)
         LAUNCH(c, "mtf_reduce", k_mtf_reduce, (nl[l + 1] * 16 + 255) / 256, 256, (const MtfSum *)(S + off[l]), nl[l],
                S + off[l + 1]);
@@ -6858,11 +7032,13 @@ static int mtf_run(dc_ctx *c, const uint8_t *d_in, uint64_t len, const MtfSum *h
         // the nybble encoder's tile summaries too (fsm_run(..., summ_ready)): its tiles are these
         const uint64_t ng = (n0 + FSM_GROUP - 1) / FSM_GROUP;
         if (ensure((void **)&c->d_summ, &c->summ_cap, (n0 + ng) * sizeof(uint4))) return DC_E_HIP;
-        LAUNCH(c, "mtf_ranks", k_mtf_walk<1>, (n0 + 255) / 256, 256, d_in, len, n0, (const MtfSum *)E,
-               (MtfSum *)nullptr, c->d_rk, c->d_summ);
+        LAUNCH(c, "mtf_ranks", k_mtf_resolve, (n0 + 255) / 256, 256, len, n0, (const MtfSum *)E, mrec,
+               (const uint2 *)mhead, c->d_rk, c->d_summ);
     }
-    if (h_final) HIPCHK(hipMemcpyAsync(h_final, fin, sizeof(MtfSum), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    if (h_final) {
+        HIPCHK(hipMemcpyAsync(h_final, fin, sizeof(MtfSum), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+    }
     c->rk_in = ranks ? d_in : nullptr; c->rk_len = len;
     return DC_OK;
 }
@@ -6937,7 +7113,8 @@ int dc_nyb_compress(dc_ctx *c, const uint8_t *d_in, uint64_t n, int modify, uint
     if (r) return r;
     // (the tile summaries: k_mtf_walk<1>'s, when there are ranks)
     return fsm_run<M_NYB_ENC>(c, d_in, n, n - 1, d_out, h_len, "nyb_enca_tiles",
-                              FsmAux{n > 1 ? c->d_rk : nullptr, 0, 0, 1, 1}, nullptr, true, nullptr, 0, n > 1);
+                              FsmAux{n > 1 ? c->d_rk : nullptr, 0, 0, 1, 1, 0, c->d_mrec, mtf_heads(c, n)}, nullptr, true,
+                              nullptr, 0, n > 1);
 }
 
 // ---- chunked nybble container (DCNK) ---------------------------------------------------
@@ -7079,6 +7256,8 @@ int dc_nyb_body_plan(dc_ctx *c, const uint8_t *d_in, uint64_t len, int modify, c
         int r = mtf_run(c, d_in, len, &init, true, nullptr);
         if (r) return r;
         aux.rk = len > 1 ? c->d_rk : nullptr;
+        aux.frec = c->d_mrec;
+        aux.fhead = mtf_heads(c, len);
     }
     int r = fsm_run<M_NYB_ENC>(c, d_in, len, len - 1, nullptr, nullptr, "nyb_body_tiles", aux, h_plan, false,
                                nullptr, 0, modify && len > 1);
@@ -7107,7 +7286,7 @@ int dc_nyb_body_write(dc_ctx *c, const uint8_t *d_in, uint64_t len, int modify, 
     if (!c || !d_out || !h_len || !d_in || len < 1 || pend_rank > 7) return DC_E_ARG;
     if (modify && len > 1 && (c->rk_in != d_in || c->rk_len != len)) return DC_E_ARG;   // plan this input first
     FsmAux aux{modify && len > 1 ? c->d_rk : nullptr, pend_rank < 0 ? 0u : (uint32_t)pend_rank,
-               pend_rank < 0 ? 0u : 1u, is_last ? 1u : 0u, 0};
+               pend_rank < 0 ? 0u : 1u, is_last ? 1u : 0u, 0, 0, c->d_mrec, mtf_heads(c, len)};
     int r = fsm_run<M_NYB_ENC>(c, d_in, len, len - 1, d_out, h_len, "nyb_body_tiles", aux);
     if (r) return r;
     if (h_state_out) *h_state_out = (int)c->h_pinned[1];
