@@ -3735,10 +3735,11 @@ struct FsmAux {
     uint32_t is_last;     // M_NYB_ENC: the shard ends the stream (odd-tail byte, :1000-1009)
     uint32_t whole;       // M_NYB_ENC: whole stream (header 0xAF x[0], LITERAL fallback)
     uint32_t tokens;      // M_NYB_DEC: a hit writes 0x80 | rank, not its static byte (k_nyb_resolve)
-    // M_NYB_ENC with rk: the first touches of each tile (k_mtf_walk<2>), their ranks settled by
-    // k_mtf_resolve in bits 24..31 (rk holds 0xFE there but for a tile's last element)
-    const uint2 *frec;    // MTF_REC per tile: tile offset | byte << 12 | context << 20 | rank << 24
-    const uint2 *fhead;   // per tile: the count of first touches
+    // M_NYB_ENC with rk: each tile's step records (k_mtf_walk<2>, 2 uint4 each, 128 per tile),
+    // whose second uint4 k_mtf_resolve made the settled ranks of the step's first touches (rk
+    // holds 0xFE there, but for a tile's last element)
+    const uint4 *frec;
+    const uint2 *fhead;   // per tile: x = its records
 };
 #define FSM_SUB 1                          /* 4096-element chunks per tile */
 #define FSM_TILE (4096 * FSM_SUB)
@@ -3977,7 +3978,7 @@ static __device__ __forceinline__ void fsm_rank_table(uint8_t *s_rank)
 template <int M>
 static __device__ __forceinline__ void fsm_ranks(const FsmWin &W, const FsmAux &aux, uint64_t j0, uint64_t nelem,
                                                  uint32_t (&rk)[16], const uint8_t *s_rank,
-                                                 const uint8_t *s_patch = nullptr)
+                                                 const uint4 *pP = nullptr)
 {
     if (M != M_NYB_ENC) return;
     if (aux.rk) {
@@ -3992,15 +3993,12 @@ static __device__ __forceinline__ void fsm_ranks(const FsmWin &W, const FsmAux &
         const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
         for (int k = 0; k < 16; ++k) rk[k] = (w4[k >> 2] >> (8 * (k & 3))) & 255u;
-        if (s_patch) {   // first touches (0xFE): their settled ranks, from the tile's list in LDS
-            uint32_t fe = 0;
+        if (pP) {   // first touches (0xFE): the settled ranks of the lane's step record (LDS)
+            const uint4 P = *pP;
+            const uint32_t p4[4] = {P.x, P.y, P.z, P.w};
 #pragma unroll
-            for (int q = 0; q < 4; ++q) fe |= swar_eq(w4[q], 0xFEFEFEFEu);
-            if (fe & 0x80808080u) {
-#pragma unroll
-                for (int k = 0; k < 16; ++k)
-                    if (rk[k] == 0xFEu) rk[k] = s_patch[(uint32_t)(j0 & (FSM_TILE - 1)) + k];
-            }
+            for (int k = 0; k < 16; ++k)
+                if (rk[k] == 0xFEu) rk[k] = (p4[k >> 2] >> (8 * (k & 3))) & 255u;
         }
     } else {
 #pragma unroll
@@ -4100,15 +4098,8 @@ __global__ __launch_bounds__(256) void k_fsm_tiles(const uint8_t *__restrict__ i
 {
     __shared__ uint4 s_f[FSM_SUB][4];   // wave totals per chunk
     __shared__ __attribute__((aligned(4))) uint8_t s_rank[256];
-    __shared__ uint8_t s_patch[M == M_NYB_ENC ? FSM_TILE : 1];   // settled first-touch ranks (k_fsm_write)
     const int t = threadIdx.x;
-    const bool patch = M == M_NYB_ENC && aux.rk && aux.frec;
-    if (patch && (uint32_t)t < aux.fhead[blockIdx.x].x) {
-        const uint32_t r = aux.frec[(uint64_t)blockIdx.x * 128 + t].x;
-        s_patch[r & (FSM_TILE - 1)] = (uint8_t)(r >> 24);
-    }
-    if (M == M_NYB_ENC && !aux.rk) fsm_rank_table(s_rank);
-    if (M == M_NYB_ENC) __syncthreads();
+    if (M == M_NYB_ENC && !aux.rk) { fsm_rank_table(s_rank); __syncthreads(); }
     // chunk c of the tile: elements [c * 4096 + 16 t, +16) for lane t (coalesced per chunk);
     // all chunks' windows are loaded before any is walked
     FsmWin W[FSM_SUB];
@@ -4122,7 +4113,7 @@ __global__ __launch_bounds__(256) void k_fsm_tiles(const uint8_t *__restrict__ i
         Fsm f = fsm_id();
         if (j0 < nelem) {
             uint32_t rk[16], A, B;
-            fsm_ranks<M>(W[c], aux, j0, nelem, rk, s_rank, patch ? s_patch : nullptr);
+            fsm_ranks<M>(W[c], aux, j0, nelem, rk, s_rank);
             nyb_lane_flags<M>(W[c], rk, A, B);
             const uint32_t valid = nelem - j0 >= 16 ? 0xFFFFu : (1u << (uint32_t)(nelem - j0)) - 1u;
             f = nyb_lane_fsm<M>(A, B, valid);
@@ -4332,14 +4323,25 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
     __shared__ __attribute__((aligned(16))) uint8_t s_out[2 * FSM_TILE + 32];
     __shared__ __attribute__((aligned(4))) uint8_t s_rank[256];
     __shared__ uint2 s_esel[256];   // v_perm selectors per 4-element pattern
-    __shared__ uint8_t s_patch[M == M_NYB_ENC ? FSM_TILE : 1];   // settled first-touch ranks, by tile offset
+    // adaptive encode: the tile's step records (<= 128: one per thread), by step = lane
+    __shared__ uint8_t s_map[M == M_NYB_ENC ? 256 : 1];   // step -> record + 1 (0: none)
+    __shared__ uint4 s_P[M == M_NYB_ENC ? 128 : 1];       // a record's settled first-touch ranks
     const int t = threadIdx.x;
     if (M == M_NYB_ENC && !aux.rk) fsm_rank_table(s_rank);
     const bool patch = M == M_NYB_ENC && aux.rk && aux.frec;
-    if (patch) {   // (a tile holds <= MTF_REC = 128 first touches: one per thread)
-        if ((uint32_t)t < aux.fhead[blockIdx.x].x) {
-            const uint32_t r = aux.frec[(uint64_t)blockIdx.x * 128 + t].x;
-            s_patch[r & (FSM_TILE - 1)] = (uint8_t)(r >> 24);
+    if (patch) {
+        s_map[t] = 0;
+        const uint32_t nrec = aux.fhead[blockIdx.x].x;
+        uint4 q0 = make_uint4(0u, 0u, 0u, 0u), q1 = q0;
+        if ((uint32_t)t < nrec) {
+            const uint4 *const r = aux.frec + 2 * ((uint64_t)blockIdx.x * 128 + t);
+            q0 = r[0];
+            q1 = r[1];
+        }
+        __syncthreads();
+        if ((uint32_t)t < nrec) {
+            s_map[q0.z & 255u] = (uint8_t)(t + 1);
+            s_P[t] = q1;
         }
     }
     s_esel[t] = make_uint2(c_nyb.esel_lo[t], c_nyb.esel_hi[t]);   // (NybTables)
@@ -4388,7 +4390,8 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
         Fsm f = fsm_id();
         if (j0 < nelem) {
             uint32_t rk[16];
-            fsm_ranks<M>(W_[c], aux, j0, nelem, rk, s_rank, patch ? s_patch : nullptr);
+            const uint32_t mr = patch ? s_map[t] : 0u;   // (FSM_SUB = 1: the lane's step is t)
+            fsm_ranks<M>(W_[c], aux, j0, nelem, rk, s_rank, mr ? &s_P[M == M_NYB_ENC ? mr - 1 : 0] : nullptr);
             nyb_lane_flags<M>(W_[c], rk, fa[c], fb[c]);
 #pragma unroll
             for (int q = 0; q < 4; ++q)
@@ -4458,7 +4461,10 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
             // the rank of the pending hit before element 0: the previous window byte's, or the
             // shard's carried one
             uint32_t rp0 = j0 ? (aux.rk ? (uint32_t)aux.rk[j0 - 1] : (uint32_t)s_rank[W.b(0)]) : aux.pend_rank;
-            if (patch && rp0 == 0xFEu) rp0 = s_patch[(uint32_t)((j0 - 1) & (FSM_TILE - 1))];   // (same tile: a tile's last is settled in rk)
+            if (patch && rp0 == 0xFEu && t > 0) {   // (lane 0: the tile's last element is settled in rk)
+                const uint32_t mp = s_map[t - 1];
+                if (mp) rp0 = s_P[mp - 1].w >> 24;
+            }
             if (aux.is_last && len >= 2 && len - 2 >= j0 && len - 2 < j0 + kend) {
                 // odd tail (:1000-1009): the stream's last element a hit left pending: its byte,
                 // raw, after the bytes of the elements before it
@@ -5003,10 +5009,12 @@ static __device__ __forceinline__ uint64_t mtf_touch8(uint64_t L, uint32_t v, ui
 // MODE 2: also the ranks into rk, but for the FIRST TOUCHES. A hit's rank is final already (an
 // entry touched in the tile sits above every entry-list byte, in the same order whatever the
 // entry lists were); a miss on a full list is a miss (0xFF); a miss while the list holds fewer
-// than 8 entries is a first touch, whose rank depends on the entry lists: it is written 0xFE and
-// listed in rec (tile offset | byte << 12 | context << 20, and the nybble encoder's composition
-// of the known elements since the previous first touch), for k_mtf_resolve. head[tile] = (the
-// count, the composition after the last one). (The encoder's FSM tiles are these tiles.)
+// than 8 entries is a first touch, whose rank depends on the entry lists: it is written 0xFE, and
+// each 16-element step that holds one is listed for k_mtf_resolve as a STEP RECORD of two uint4:
+// (the nybble encoder's composition of the steps since the previous record, hits | first
+// touches << 16, step | context byte of its element 0 << 8 | elements << 16, 0), and the step's
+// 16 element bytes. head[tile] = (records, the composition after the last one). (The encoder's
+// FSM tiles are these tiles; a step is a lane of its writer.)
 // A lane walks its tile with the 16 lists in LDS (column t). Per element: the next element's
 // list is read before this one's is written back (its context is this element's byte; the same
 // context takes the list just computed), so the LDS round trip overlaps the touch; the input
@@ -5016,41 +5024,13 @@ static __device__ __forceinline__ uint64_t mtf_touch8(uint64_t L, uint32_t v, ui
 // (mtf_touch64). (r4 before: a summary pass, then a second walk of every tile from its entry
 // lists for the ranks, 0.90 + 1.24 ms per GiB; first: one lane-local loop that waited on every
 // list read and on the granule just loaded, 1.64 + 2.03 ms.)
-#define MTF_REC 128   /* first touches per tile: <= 8 per context */
+#define MTF_REC 128   /* step records per tile: <= its first touches, <= 8 per context */
 
-// k_mtf_walk<2>'s 16 elements with first touches F (hits H, valid nv; element bytes X, the
-// context byte of element 0 pv, tile offset o): the segments between them fold into accp, each
-// is listed. Out of line: rare after a tile's first few hundred elements, and inlined into the
-// walk's steps it took the walk from 71 to 155 VGPRs (5 -> 3 waves per SIMD).
-struct MtfRecState { uint32_t accp, nrec; };
-static __device__ __noinline__ MtfRecState mtf_records(uint32_t H, uint32_t F, uint32_t nv, uint32_t X0, uint32_t X1,
-                                                       uint32_t X2, uint32_t X3, uint32_t pv, uint32_t o,
-                                                       MtfRecState st, uint2 *__restrict__ trec)
-{
-    const uint32_t X[4] = {X0, X1, X2, X3};
-    uint32_t from = nv;   // elements not folded yet
-    while (F) {
-        const uint32_t k = (uint32_t)__builtin_ctz(F);
-        F &= F - 1u;
-        const uint32_t below = (1u << k) - 1u;
-        st.accp = fsmp_then(st.accp, fsmp(nyb_lane_fsm<M_NYB_ENC>(H, 0u, from & below)));
-        const uint32_t x = (X[k >> 2] >> (8 * (k & 3))) & 255u;
-        const uint32_t p = k ? (X[(k - 1) >> 2] >> (8 * ((k - 1) & 3))) & 255u : pv;
-        // (<= 8 per context, but for a walk with a zero byte, whose pads are ambiguous: its
-        // list is rebuilt by the counted walk; the bound keeps it off the next tile's)
-        if (st.nrec < MTF_REC) trec[st.nrec] = make_uint2((o + k) | (x << 12) | (((p >> 3) & 15u) << 20), st.accp);
-        ++st.nrec;
-        st.accp = FSMP_ID;
-        from &= ~(below | (1u << k));
-    }
-    st.accp = fsmp_then(st.accp, fsmp(nyb_lane_fsm<M_NYB_ENC>(H, 0u, from)));
-    return st;
-}
 static_assert(FSM_TILE == MTF_TILE, "k_mtf_walk<2> composes the nybble encoder's tile summaries");
 template <int MODE>
 __global__ __launch_bounds__(256) void k_mtf_walk(
     const uint8_t *__restrict__ in, uint64_t len, uint64_t ntiles, MtfSum *__restrict__ summ, uint8_t *__restrict__ rk,
-    uint2 *__restrict__ rec, uint2 *__restrict__ head)
+    uint4 *__restrict__ rec, uint2 *__restrict__ head)
 {
     static_assert(MODE == 0 || MODE == 2, "summaries, or summaries and ranks");
     __shared__ uint64_t s_L[16][256];
@@ -5065,9 +5045,10 @@ __global__ __launch_bounds__(256) void k_mtf_walk(
     uint64_t Lc = 0ull;
     uint32_t anyz = 0;   // 0x80 bits: a zero byte among the tile's elements
     uint32_t accp = FSMP_ID, nrec = 0;
-    uint2 *const trec = rec + (MODE == 2 ? tile * MTF_REC : 0);
-    // MODE 2, after 16 elements (element k: rank byte k of R, byte k of X, valid bits nv): the
-    // known elements fold into accp, each first touch closes a segment and is listed
+    uint4 *const trec = rec + (MODE == 2 ? 2 * tile * MTF_REC : 0);
+    // MODE 2, after 16 elements (element k: rank byte k of R, byte k of X, valid bits nv): a step
+    // without first touches folds into accp, one with them is listed (two 16-B stores: the
+    // per-first-touch list with its segment folds measured 0.38 ms per GiB in divergent branches)
     auto post = [&](const uint32_t (&R)[4], const uint32_t (&X)[4], uint32_t pv, uint64_t e, uint32_t nv) {
         uint32_t H = 0, F = 0;   // hits (a byte <= 7); first touches (0xFE)
 #pragma unroll
@@ -5077,10 +5058,14 @@ __global__ __launch_bounds__(256) void k_mtf_walk(
         }
         F &= nv;
         if (F) {
-            const MtfRecState st = mtf_records(H, F, nv, X[0], X[1], X[2], X[3], pv, (uint32_t)(e - e0),
-                                               MtfRecState{accp, nrec}, trec);
-            accp = st.accp;
-            nrec = st.nrec;
+            // (<= 128 records, but for a walk with a zero byte, whose pads are ambiguous: its list
+            // is rebuilt by the counted walk; the bound keeps it off the next tile's)
+            if (nrec < MTF_REC) {
+                trec[2 * nrec] = make_uint4(accp, H | (F << 16), (uint32_t)((e - e0) >> 4) | (pv << 8) | (__popc(nv) << 16), 0u);
+                trec[2 * nrec + 1] = make_uint4(X[0], X[1], X[2], X[3]);
+            }
+            ++nrec;
+            accp = FSMP_ID;
         } else {
             accp = fsmp_then(accp, fsmp(nyb_lane_fsm<M_NYB_ENC>(H, 0u, nv)));
         }
@@ -5202,19 +5187,18 @@ __global__ __launch_bounds__(256) void k_mtf_walk(
     }
 }
 
-// k_mtf_resolve: the first touches k_mtf_walk<2> listed, from each tile's entry lists, and the
-// nybble encoder's tile summaries. The j-th first touch of context c in a tile (j < 8: the list
-// held the j bytes touched in the tile above the entry list) has rank j + its position among
-// the entry list's bytes not touched in the tile yet (a miss past 7, or when absent): G_c = the
-// entry list less those bytes (LDS column t); each first touch takes its byte out. The rank
-// goes into its record (bits 24..31; the encoder's writer reads the tile's list into LDS: rank
-// bytes scattered into rk cost 0.37 ms per GiB in partial-line writes), and into rk only for the
-// tile's last element (read across the tile boundary); the tile's composition is the listed
-// segments with each first touch (a hit or a miss) between them. One lane per tile, its records
-// read 16 at a time.
+// k_mtf_resolve: the first touches of k_mtf_walk<2>'s step records, from each tile's entry
+// lists, and the nybble encoder's tile summaries (-> fraw). The j-th first touch of context c in a
+// tile (j < 8: the list held the j bytes touched in the tile above the entry list) has rank j +
+// its position among the entry list's bytes not touched in the tile yet (a miss past 7, or when
+// absent): G_c = the entry list less those bytes (LDS column t); each first touch takes its byte
+// out. A record's second uint4 becomes the step's settled ranks at its first touches (the writer
+// reads the tile's records into LDS; rank bytes scattered into rk cost 0.37 ms per GiB in
+// partial-line writes), and rk gets the tile's last element (read across the tile boundary). One
+// lane per tile.
 __global__ __launch_bounds__(256) void k_mtf_resolve(uint64_t len, uint64_t ntiles, const MtfSum *__restrict__ entry,
-                                                     uint2 *__restrict__ rec, const uint2 *__restrict__ head,
-                                                     uint8_t *__restrict__ rk, uint4 *__restrict__ fsumm)
+                                                     uint4 *__restrict__ rec, const uint2 *__restrict__ head,
+                                                     uint8_t *__restrict__ rk, uint4 *__restrict__ fraw)
 {
     __shared__ uint64_t s_G[16][256];
     const int t = threadIdx.x;
@@ -5226,18 +5210,24 @@ __global__ __launch_bounds__(256) void k_mtf_resolve(uint64_t len, uint64_t ntil
         s_G[c][t] = entry[tile].L[c];
         gv |= (uint64_t)min((uint32_t)entry[tile].cnt[c], 8u) << (4 * c);
     }
-    uint2 *const trec = rec + tile * MTF_REC;
+    uint4 *const trec = rec + 2 * tile * MTF_REC;
     const uint64_t e0 = tile * MTF_TILE;
     const uint32_t last = (uint32_t)(((e0 + MTF_TILE < len - 1) ? e0 + MTF_TILE : len - 1) - e0 - 1);   // the tile's last element
     uint32_t accp = FSMP_ID;
-    for (uint32_t i0 = 0; i0 < hd.x; i0 += 16) {
-        uint2 r[16];
-#pragma unroll
-        for (uint32_t q = 0; q < 16; ++q) r[q] = i0 + q < hd.x ? trec[i0 + q] : make_uint2(0u, 0u);
-#pragma unroll
-        for (uint32_t q = 0; q < 16; ++q) {
-            if (i0 + q >= hd.x) break;
-            const uint32_t off = r[q].x & 4095u, x = (r[q].x >> 12) & 255u, c = (r[q].x >> 20) & 15u;
+    uint4 q0 = hd.x ? trec[0] : make_uint4(0u, 0u, 0u, 0u), q1 = hd.x ? trec[1] : make_uint4(0u, 0u, 0u, 0u);
+    for (uint32_t i = 0; i < hd.x; ++i) {
+        uint4 n0 = q0, n1 = q1;   // the next record, in flight
+        if (i + 1 < hd.x) { n0 = trec[2 * i + 2]; n1 = trec[2 * i + 3]; }
+        const uint32_t X[4] = {q1.x, q1.y, q1.z, q1.w};
+        uint32_t P[4] = {0u, 0u, 0u, 0u}, H = q0.y & 0xFFFFu, F = q0.y >> 16;
+        const uint32_t step = q0.z & 255u, pv = (q0.z >> 8) & 255u, nk = q0.z >> 16;
+        accp = fsmp_then(accp, q0.x);
+        while (F) {
+            const uint32_t k = (uint32_t)__builtin_ctz(F);
+            F &= F - 1u;
+            const uint32_t x = (X[k >> 2] >> (8 * (k & 3))) & 255u;
+            const uint32_t p = k ? (X[(k - 1) >> 2] >> (8 * ((k - 1) & 3))) & 255u : pv;
+            const uint32_t c = (p >> 3) & 15u;
             const uint32_t j = (uint32_t)(jn >> (4 * c)) & 15u, v = (uint32_t)(gv >> (4 * c)) & 15u;
             uint32_t rank = 0xFFu;
             if (j < 8u) {
@@ -5253,14 +5243,15 @@ __global__ __launch_bounds__(256) void k_mtf_resolve(uint64_t len, uint64_t ntil
                 }
                 jn += 1ull << (4 * c);
             }
-            trec[i0 + q].x = r[q].x | (rank << 24);
-            if (off == last) rk[e0 + off] = (uint8_t)rank;
-            // the segment before it, then the element: a hit (0 / 1 bytes, to state 1 / 0) or a
-            // miss (1 / 2 bytes, to state 0), as elem_fsm<M_NYB_ENC>
-            accp = fsmp_then(fsmp_then(accp, r[q].y), rank != 0xFFu ? 0x00018000u : 0x00020001u);
+            P[k >> 2] |= rank << (8 * (k & 3));
+            H |= (rank != 0xFFu ? 1u : 0u) << k;
+            if (16 * step + k == last) rk[e0 + last] = (uint8_t)rank;
         }
+        accp = fsmp_then(accp, fsmp(nyb_lane_fsm<M_NYB_ENC>(H, 0u, nk >= 16 ? 0xFFFFu : (1u << nk) - 1u)));
+        trec[2 * i + 1] = make_uint4(P[0], P[1], P[2], P[3]);
+        q0 = n0; q1 = n1;
     }
-    fsumm[tile] = fsm_pack(fsmp_unpack(fsmp_then(accp, hd.y)));
+    fraw[tile] = fsm_pack(fsmp_unpack(fsmp_then(accp, hd.y)));
 }
 
 // parent[g] = composition of child summaries [64 g, 64 g + 64); one lane per (group, context)
@@ -6070,7 +6061,9 @@ struct dc_ctx {
     uint64_t *d_entry;      size_t entry_cap;
     MtfSum *d_mtf;          size_t mtf_cap;       // adaptive nybble: tile summaries + entries, all levels
     uint8_t *d_rk;          size_t rk_cap;        // adaptive nybble: rank per element
-    uint2 *d_mrec;          size_t mrec_cap;      // adaptive nybble: first touches per tile + heads
+    uint4 *d_mrec;          size_t mrec_cap;      // adaptive nybble: step records, MTF_REC per tile
+    uint2 *d_mhead;         size_t mhead_cap;     // adaptive nybble: records per tile
+    uint4 *d_fraw;          size_t fraw_cap;      // adaptive nybble: the encoder's tile summaries (k_mtf_resolve)
     MtfSum *h_mtf;                                // adaptive nybble: pinned entry lists (mtf_run)
     uint32_t *d_actl;       size_t actl_cap;      // adaptive nybble decode: control words of a segment
     uint32_t *d_astate;                           // adaptive nybble decode: lists + byte between segments
@@ -6247,6 +6240,8 @@ void dc_ctx_destroy(dc_ctx *c)
     if (c->d_mtf) (void)hipFree(c->d_mtf);
     if (c->d_rk) (void)hipFree(c->d_rk);
     if (c->d_mrec) (void)hipFree(c->d_mrec);
+    if (c->d_mhead) (void)hipFree(c->d_mhead);
+    if (c->d_fraw) (void)hipFree(c->d_fraw);
     if (c->h_mtf) (void)hipHostFree(c->h_mtf);
     if (c->d_actl) (void)hipFree(c->d_actl);
     if (c->d_astate) (void)hipFree(c->d_astate);
@@ -6926,7 +6921,8 @@ static int fsm_run(dc_ctx *c, const uint8_t *d_in, uint64_t len, uint64_t nelem,
             LAUNCH(c, "small_dec_summ", k_small_dec_summ, (ntiles + 255) / 256, 256, gexp, ngroups, d_in, len, ntiles,
                    c->d_summ, c->d_meta);
         else if constexpr (SmMode<M>::fast) LAUNCH(c, name, k_small_tiles<M>, ntiles, 256, d_in, len, nelem, c->d_summ);
-        else if (summ_ready) {}
+        else if (summ_ready)   // (k_mtf_resolve's: the scan below rewrites d_summ in place)
+            HIPCHK(hipMemcpyAsync(c->d_summ, c->d_fraw, ntiles * sizeof(uint4), hipMemcpyDeviceToDevice, c->stream));
         else if ((M == M_NYB_ENC && !aux.rk) || M == M_NYB_DEC || M == M_NYB_DBODY)
             LAUNCH(c, name, k_nyb_tiles<M == M_NYB_DEC ? M_NYB_DEC : M == M_NYB_DBODY ? M_NYB_DBODY : M_NYB_ENC>,
                    (ntiles + 4 * NYB_TPW - 1) / (4 * NYB_TPW), 256, d_in, len, nelem, ntiles, c->d_summ);
@@ -6978,11 +6974,10 @@ static int fsm_write_planned(dc_ctx *c, const uint8_t *d_in, uint64_t len, uint6
     return DC_OK;
 }
 
-// the per-tile first-touch counts of the last mtf_run(ranks) over len bytes (after the records)
-static const uint2 *mtf_heads(const dc_ctx *c, uint64_t len)
+// the per-tile record counts of the last mtf_run(ranks)
+static const uint2 *mtf_heads(const dc_ctx *c, uint64_t)
 {
-    const uint64_t n0 = len > 1 ? (len - 2) / MTF_TILE + 1 : 0;
-    return c->d_mrec ? c->d_mrec + n0 * MTF_REC : nullptr;
+    return c->d_mhead;
 }
 
 // Adaptive nybble ranks (k_mtf_* pipeline) of elements 1..len-1 of d_in into c->d_rk, from the
@@ -7012,13 +7007,17 @@ static int mtf_run(dc_ctx *c, const uint8_t *d_in, uint64_t len, const MtfSum *h
     memcpy(c->h_mtf, h_init, sizeof(MtfSum));
     HIPCHK(hipMemcpyAsync(init, c->h_mtf, sizeof(MtfSum), hipMemcpyHostToDevice, c->stream));
     if (ranks && ensure((void **)&c->d_rk, &c->rk_cap, ((len + 3) & ~3ull))) return DC_E_HIP;
-    if (ranks && ensure((void **)&c->d_mrec, &c->mrec_cap, n0 * (MTF_REC + 1) * sizeof(uint2))) return DC_E_HIP;
-    uint2 *const mrec = c->d_mrec, *const mhead = c->d_mrec + (ranks ? n0 * MTF_REC : 0);
+    if (ranks && (ensure((void **)&c->d_mrec, &c->mrec_cap, n0 * 2 * MTF_REC * sizeof(uint4)) ||
+                  ensure((void **)&c->d_mhead, &c->mhead_cap, n0 * sizeof(uint2)) ||
+                  ensure((void **)&c->d_fraw, &c->fraw_cap, n0 * sizeof(uint4))))
+        return DC_E_HIP;
+    uint4 *const mrec = c->d_mrec;
+    uint2 *const mhead = c->d_mhead;
     if (ranks)   // the summaries, the ranks but for the first touches, and their list: one walk
         LAUNCH(c, "mtf_tiles", k_mtf_walk<2>, (n0 + 255) / 256, 256, d_in, len, n0, S, c->d_rk, mrec, mhead);
     else
         LAUNCH(c, "mtf_tiles", k_mtf_walk<0>, (n0 + 255) / 256, 256, d_in, len, n0, S, (uint8_t *)nullptr,
-               (uint2 *)nullptr, (uint2 *)nullptr);
+               (uint4 *)nullptr, (uint2 *)nullptr);
     for (int l = 0; l + 1 < levels; ++l)
         LAUNCH(c, "mtf_reduce", k_mtf_reduce, (nl[l + 1] * 16 + 255) / 256, 256, (const MtfSum *)(S + off[l]), nl[l],
                S + off[l + 1]);
@@ -7028,13 +7027,9 @@ static int mtf_run(dc_ctx *c, const uint8_t *d_in, uint64_t len, const MtfSum *h
         LAUNCH(c, "mtf_down", k_mtf_down, (groups * 16 + 255) / 256, 256, (const MtfSum *)(S + off[l]), nl[l], pe,
                E + off[l], l == levels - 1 ? fin : (MtfSum *)nullptr);
     }
-    if (ranks) {
-        // the nybble encoder's tile summaries too (fsm_run(..., summ_ready)): its tiles are these
-        const uint64_t ng = (n0 + FSM_GROUP - 1) / FSM_GROUP;
-        if (ensure((void **)&c->d_summ, &c->summ_cap, (n0 + ng) * sizeof(uint4))) return DC_E_HIP;
+    if (ranks)   // and the nybble encoder's tile summaries (fsm_run(..., summ_ready)): its tiles are these
         LAUNCH(c, "mtf_ranks", k_mtf_resolve, (n0 + 255) / 256, 256, len, n0, (const MtfSum *)E, mrec,
-               (const uint2 *)mhead, c->d_rk, c->d_summ);
-    }
+               (const uint2 *)mhead, c->d_rk, c->d_fraw);
     if (h_final) {
         HIPCHK(hipMemcpyAsync(h_final, fin, sizeof(MtfSum), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
@@ -7287,7 +7282,8 @@ int dc_nyb_body_write(dc_ctx *c, const uint8_t *d_in, uint64_t len, int modify, 
     if (modify && len > 1 && (c->rk_in != d_in || c->rk_len != len)) return DC_E_ARG;   // plan this input first
     FsmAux aux{modify && len > 1 ? c->d_rk : nullptr, pend_rank < 0 ? 0u : (uint32_t)pend_rank,
                pend_rank < 0 ? 0u : 1u, is_last ? 1u : 0u, 0, 0, c->d_mrec, mtf_heads(c, len)};
-    int r = fsm_run<M_NYB_ENC>(c, d_in, len, len - 1, d_out, h_len, "nyb_body_tiles", aux);
+    int r = fsm_run<M_NYB_ENC>(c, d_in, len, len - 1, d_out, h_len, "nyb_body_tiles", aux, nullptr, true, nullptr,
+                               0, modify && len > 1);
     if (r) return r;
     if (h_state_out) *h_state_out = (int)c->h_pinned[1];
     return DC_OK;
