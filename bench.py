@@ -419,8 +419,10 @@ def main_nybble(a, dev, rank, world):
     for name, ms in kt:
         per.setdefault(name, []).append(ms)
     # SURVEY §8(d), nybble: N + N_comp each way; the plan (tiles) passes read one side
+    # (adaptive: the MTF walk reads the input and writes a rank per element; the resolve pass
+    # reads only the first-touch step records, not priced here)
     alg = {"nyb_enc_tiles": n, "nyb_enca_tiles": n, "nyb_enc_write": n + m, "nyb_dec_tiles": m,
-           "nyb_dec_write": m + n, "mtf_tiles": n, "mtf_ranks": 2 * n}
+           "nyb_dec_write": m + n, "mtf_tiles": 2 * n if modify else n}
     kernels = {}
     for name, v in per.items():
         mm = float(np.mean(v))
@@ -434,9 +436,9 @@ def main_nybble(a, dev, rank, world):
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
     wl = f"C1-nyb-{a.mode}"
     # the timed stage's kernel as the PMC summary names it (template argument = the transducer mode)
-    kname = {"nyb_enc_tiles": "k_fsm_tiles<0>", "nyb_enca_tiles": "k_fsm_tiles<0>", "nyb_enc_write": "k_fsm_write<0>",
-             "nyb_dec_tiles": "k_fsm_tiles<1>", "nyb_dec_write": "k_fsm_write<1>", "mtf_tiles": "k_mtf_walk<0>",
-             "mtf_ranks": "k_mtf_walk<1>"}.get(dom, "k_" + dom)
+    kname = {"nyb_enc_tiles": "k_nyb_tiles<0>", "nyb_enca_tiles": "k_fsm_tiles<0>", "nyb_enc_write": "k_fsm_write<0>",
+             "nyb_dec_tiles": "k_nyb_tiles<1>", "nyb_dec_write": "k_fsm_write<1>",
+             "mtf_tiles": "k_mtf_walk<2>" if modify else "k_mtf_walk<0>", "mtf_ranks": "k_mtf_resolve"}.get(dom, "k_" + dom)
     traffic, traffic_src = pmc_traffic(kname, argparse.Namespace(cfg=wl, nary=0), n)
     kern_sum = sum(float(np.sum(v)) for v in per.values()) / a.profile_steps
     enc_frac = (n + m) / (enc_ms * 1e-3) / HBM_PEAK
