@@ -3978,12 +3978,12 @@ static __device__ __forceinline__ void fsm_rank_table(uint8_t *s_rank)
 template <int M>
 static __device__ __forceinline__ void fsm_ranks(const FsmWin &W, const FsmAux &aux, uint64_t j0, uint64_t nelem,
                                                  uint32_t (&rk)[16], const uint8_t *s_rank,
-                                                 const uint4 *pP = nullptr)
+                                                 const uint4 *pP = nullptr, const uint4 *pre = nullptr)
 {
     if (M != M_NYB_ENC) return;
     if (aux.rk) {
         uint4 v = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
-        if (j0 + 16 <= nelem) v = *reinterpret_cast<const uint4 *>(aux.rk + j0);
+        if (j0 + 16 <= nelem) v = pre ? *pre : *reinterpret_cast<const uint4 *>(aux.rk + j0);   // (pre: loaded early)
         else for (uint64_t q = 0; j0 + q < nelem; ++q) {
             const uint32_t r = aux.rk[j0 + q];
             const uint32_t sh = 8 * (q & 3), msk = ~(255u << sh);
@@ -4356,6 +4356,12 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
                                        FsmOff<M>::v);   // every lane (shuffles)
     const uint64_t e = entry[blockIdx.x / FSM_GROUP];
     const uint4 lc = loc[blockIdx.x];
+    static_assert(FSM_SUB == 1, "one chunk per tile: the lane's step is t (rkpre, s_map)");
+    uint4 rkpre = make_uint4(~0u, ~0u, ~0u, ~0u);   // adaptive: the lane's 16 ranks, with the window
+    {
+        const uint64_t j0 = (uint64_t)blockIdx.x * FSM_TILE + (uint64_t)t * 16;   // (FSM_SUB = 1)
+        if (M == M_NYB_ENC && aux.rk && j0 + 16 <= nelem) rkpre = *reinterpret_cast<const uint4 *>(aux.rk + j0);
+    }
     const uint64_t body = (M == M_NYB_ENC) ? meta[0] + (aux.is_last ? meta[1] : 0) : meta[0];
     const uint64_t total = enc ? 2 + body : 1 + body;
     const bool literal = enc && total >= len;
@@ -4391,7 +4397,7 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
         if (j0 < nelem) {
             uint32_t rk[16];
             const uint32_t mr = patch ? s_map[t] : 0u;   // (FSM_SUB = 1: the lane's step is t)
-            fsm_ranks<M>(W_[c], aux, j0, nelem, rk, s_rank, mr ? &s_P[M == M_NYB_ENC ? mr - 1 : 0] : nullptr);
+            fsm_ranks<M>(W_[c], aux, j0, nelem, rk, s_rank, mr ? &s_P[M == M_NYB_ENC ? mr - 1 : 0] : nullptr, &rkpre);
             nyb_lane_flags<M>(W_[c], rk, fa[c], fb[c]);
 #pragma unroll
             for (int q = 0; q < 4; ++q)
