@@ -6927,6 +6927,7 @@ static int fsm_run(dc_ctx *c, const uint8_t *d_in, uint64_t len, uint64_t nelem,
             LAUNCH(c, "small_dec_summ", k_small_dec_summ, (ntiles + 255) / 256, 256, gexp, ngroups, d_in, len, ntiles,
                    c->d_summ, c->d_meta);
         else if constexpr (SmMode<M>::fast) LAUNCH(c, name, k_small_tiles<M>, ntiles, 256, d_in, len, nelem, c->d_summ);
+        else if (M == M_NYB_ENC && aux.frec && !summ_ready) return DC_E_STATE;   // (ranks with unsettled first touches)
         else if (summ_ready)   // (k_mtf_resolve's: the scan below rewrites d_summ in place)
             HIPCHK(hipMemcpyAsync(c->d_summ, c->d_fraw, ntiles * sizeof(uint4), hipMemcpyDeviceToDevice, c->stream));
         else if ((M == M_NYB_ENC && !aux.rk) || M == M_NYB_DEC || M == M_NYB_DBODY)
