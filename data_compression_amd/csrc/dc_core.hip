@@ -4959,11 +4959,13 @@ __global__ __launch_bounds__(SmMode<M>::wthreads) void k_small_write(const uint8
 //     after(A then B)_c = first-8-distinct(B_c ++ A_c)
 // = touching B_c's entries, oldest first, on top of A_c. The encoder's rank of byte i is its
 // position in the list before the touch (compress_byte_index :833-839, update_context
-// :665-687). Pipeline: k_mtf_walk<0> summarises 4096-element tiles (one lane per tile, the
-// 16 lists as u64 words in LDS); k_mtf_reduce composes 64 summaries per group, level by
-// level; k_mtf_down hands each child its entry lists from the top (the initial " etaoins"
-// lists, or a shard's entry lists); k_mtf_walk<1> re-walks every tile from its entry lists
-// and writes the per-element rank (0..7, 0xFF = miss) that drives k_fsm_*<M_NYB_ENC>.
+// :665-687). Pipeline: k_mtf_walk<2> walks each 4096-element tile once from empty lists (one
+// lane per tile, the 16 lists as u64 words in LDS): the tile summary, and every rank (0..7,
+// 0xFF = miss) that does not depend on the entry lists, the others (first touches) listed;
+// k_mtf_reduce composes 64 summaries per group, level by level; k_mtf_down hands each child its
+// entry lists from the top (the initial " etaoins" lists, or a shard's entry lists);
+// k_mtf_resolve settles the first touches and composes the transducer's tile summaries; the
+// ranks drive k_fsm_write<M_NYB_ENC>. (k_mtf_walk<0>: summaries only, for shard plans.)
 // ------------------------------------------------------------------------------------
 #define MTF_TILE 4096
 #define MTF_FAN 64
@@ -7113,7 +7115,7 @@ int dc_nyb_compress(dc_ctx *c, const uint8_t *d_in, uint64_t n, int modify, uint
     const MtfSum init = mtf_initial();
     int r = mtf_run(c, d_in, n, &init, true, nullptr);
     if (r) return r;
-    // (the tile summaries: k_mtf_walk<1>'s, when there are ranks)
+    // (the tile summaries: k_mtf_resolve's, when there are ranks)
     return fsm_run<M_NYB_ENC>(c, d_in, n, n - 1, d_out, h_len, "nyb_enca_tiles",
                               FsmAux{n > 1 ? c->d_rk : nullptr, 0, 0, 1, 1, 0, c->d_mrec, mtf_heads(c, n)}, nullptr, true,
                               nullptr, 0, n > 1);
