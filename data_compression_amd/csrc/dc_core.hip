@@ -5226,7 +5226,8 @@ __global__ __launch_bounds__(256) void k_mtf_walk(
 // lane per tile.
 __global__ __launch_bounds__(256) void k_mtf_resolve(uint64_t len, uint64_t ntiles, const MtfSum *__restrict__ entry,
                                                      uint4 *__restrict__ rec, const uint2 *__restrict__ head,
-                                                     uint8_t *__restrict__ rk, uint4 *__restrict__ fraw)
+                                                     uint8_t *__restrict__ rk, uint4 *__restrict__ fraw,
+                                                     uint4 *__restrict__ fsumm)
 {
     __shared__ uint64_t s_G[16][256];
     const int t = threadIdx.x;
@@ -5279,7 +5280,9 @@ __global__ __launch_bounds__(256) void k_mtf_resolve(uint64_t len, uint64_t ntil
         trec[2 * i + 1] = make_uint4(P[0], P[1], P[2], P[3]);
         q0 = n0; q1 = n1;
     }
-    fraw[tile] = fsm_pack(fsmp_unpack(fsmp_then(accp, hd.y)));
+    const uint4 f = fsm_pack(fsmp_unpack(fsmp_then(accp, hd.y)));
+    fraw[tile] = f;    // kept for a later write pass (a shard body's: its plan's scan rewrites fsumm)
+    fsumm[tile] = f;   // the transducer's tile summaries, ready for its scan
 }
 
 // parent[g] = composition of child summaries [64 g, 64 g + 64); one lane per (group, context)
@@ -6114,6 +6117,7 @@ struct dc_ctx {
     uint4 *d_mrec;          size_t mrec_cap;      // adaptive nybble: step records, MTF_REC per tile
     uint2 *d_mhead;         size_t mhead_cap;     // adaptive nybble: records per tile
     uint4 *d_fraw;          size_t fraw_cap;      // adaptive nybble: the encoder's tile summaries (k_mtf_resolve)
+    bool summ_fresh;                              // d_summ holds them too (no scan since)
     MtfSum *h_mtf;                                // adaptive nybble: pinned entry lists (mtf_run)
     uint32_t *d_actl;       size_t actl_cap;      // adaptive nybble decode: control words of a segment
     uint32_t *d_astate;                           // adaptive nybble decode: lists + byte between segments
@@ -6972,12 +6976,15 @@ static int fsm_run(dc_ctx *c, const uint8_t *d_in, uint64_t len, uint64_t nelem,
                    c->d_summ, c->d_meta);
         else if constexpr (SmMode<M>::fast) LAUNCH(c, name, k_small_tiles<M>, ntiles, 256, d_in, len, nelem, c->d_summ);
         else if (M == M_NYB_ENC && aux.frec && !summ_ready) return DC_E_STATE;   // (ranks with unsettled first touches)
-        else if (summ_ready)   // (k_mtf_resolve's: the scan below rewrites d_summ in place)
-            HIPCHK(hipMemcpyAsync(c->d_summ, c->d_fraw, ntiles * sizeof(uint4), hipMemcpyDeviceToDevice, c->stream));
+        else if (summ_ready) {   // (k_mtf_resolve's: the scan below rewrites d_summ in place)
+            if (!c->summ_fresh)
+                HIPCHK(hipMemcpyAsync(c->d_summ, c->d_fraw, ntiles * sizeof(uint4), hipMemcpyDeviceToDevice, c->stream));
+        }
         else if ((M == M_NYB_ENC && !aux.rk) || M == M_NYB_DEC || M == M_NYB_DBODY)
             LAUNCH(c, name, k_nyb_tiles<M == M_NYB_DEC ? M_NYB_DEC : M == M_NYB_DBODY ? M_NYB_DBODY : M_NYB_ENC>,
                    (ntiles + 4 * NYB_TPW - 1) / (4 * NYB_TPW), 256, d_in, len, nelem, ntiles, c->d_summ);
         else LAUNCH(c, name, k_fsm_tiles<M>, ntiles, 256, d_in, len, nelem, c->d_summ, aux);
+        c->summ_fresh = false;   // (d_summ rewritten in place: no longer the resolver's summaries)
         LAUNCH(c, "fsm_scan_up", k_fsm_scan_up, ng, FSM_GROUP, c->d_summ, ntiles, gsum);
         LAUNCH(c, "fsm_scan", k_fsm_scan, 1, 1024, (const uint4 *)gsum, ng, c->d_entry, c->d_meta, aux.s_init);
     }
@@ -7078,9 +7085,13 @@ static int mtf_run(dc_ctx *c, const uint8_t *d_in, uint64_t len, const MtfSum *h
         LAUNCH(c, "mtf_down", k_mtf_down, (groups * 16 + 255) / 256, 256, (const MtfSum *)(S + off[l]), nl[l], pe,
                E + off[l], l == levels - 1 ? fin : (MtfSum *)nullptr);
     }
-    if (ranks)   // and the nybble encoder's tile summaries (fsm_run(..., summ_ready)): its tiles are these
+    if (ranks) {   // and the nybble encoder's tile summaries (fsm_run(..., summ_ready)): its tiles are these
+        const uint64_t ng = (n0 + FSM_GROUP - 1) / FSM_GROUP;
+        if (ensure((void **)&c->d_summ, &c->summ_cap, (n0 + ng) * sizeof(uint4))) return DC_E_HIP;
         LAUNCH(c, "mtf_ranks", k_mtf_resolve, (n0 + 255) / 256, 256, len, n0, (const MtfSum *)E, mrec,
-               (const uint2 *)mhead, c->d_rk, c->d_fraw);
+               (const uint2 *)mhead, c->d_rk, c->d_fraw, c->d_summ);
+        c->summ_fresh = true;
+    }
     if (h_final) {
         HIPCHK(hipMemcpyAsync(h_final, fin, sizeof(MtfSum), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
