@@ -129,9 +129,10 @@ def main():
     if a.frontend:   # C5: front-end bodies + halo/LITERAL/re-cut exchanges, then sharded Huffman
         from data_compression_amd.dist import ShardedSmall
         ss = ShardedSmall(c, table_mode=a.table_mode, fused=not a.two_stage)
+        sync_fe = c.alloc_sync(n + 1, S)   # the front-end stream holds up to n + 1 symbols
 
         def encode():   # noqa: F811
-            state["s"] = ss.encode(x, a.nary, S)
+            state["s"] = ss.encode(x, a.nary, S, words=words, sync=sync_fe, table=tab, total=total)
 
         fe_out = torch.empty(2 * n + 64, dtype=torch.uint8, device=dev)   # dc_small_decompress: >= 2 * m
 
@@ -286,6 +287,9 @@ def main():
                      "alg_bytes_per_launch": dom_bytes, "mean_ms": round(dom_ms, 4),
                      "frac_rocprof": round(dom_bytes / (rp_ms * 1e-3) / HBM_PEAK, 4) if rp_ms else None,
                      "rocprof_mean_ms": round(rp_ms, 4) if rp_ms else None, "rocprof_source": rp_src,
+                     "frac_headline": "frac: HIP events around each launch in this run (they include the "
+                                      "launch's own dispatch gap, so they read a few % above rocprof); "
+                                      "frac_rocprof: the committed rocprofv3 kernel-trace mean of this command",
                      "copy_probe_GBps": _r(copy_gbps, 1),
                      "frac_vs_copy": _r(copy_gbps and achieved / copy_gbps, 4),
                      "encode_frac": round(enc_frac, 4), "decode_frac": round(dec_frac, 4),
@@ -490,19 +494,22 @@ def cpu_baseline_nybble(x, a, modify):
     old = os.sched_getaffinity(0)
     core = min(old)
     os.sched_setaffinity(0, {core})
+    reps = []
     try:
-        t0 = time.perf_counter()
-        comp = orc.nybble_compress(s, modify)
-        t1 = time.perf_counter()
-        back = orc.nybble_decompress(comp, modify)
-        t2 = time.perf_counter()
+        for _ in range(CPU_REPS):
+            t0 = time.perf_counter()
+            comp = orc.nybble_compress(s, modify)
+            t1 = time.perf_counter()
+            back = orc.nybble_decompress(comp, modify)
+            t2 = time.perf_counter()
+            assert back == s
+            r = _cpu_report(m, t0, t1, t2, core, f"nybble {'adaptive' if modify else 'static'}, ")
+            r["encode_GBps"] = round(m / (t1 - t0) / 1e9, 4)
+            r["decode_GBps"] = round(m / (t2 - t1) / 1e9, 4)
+            reps.append(r)
     finally:
         os.sched_setaffinity(0, old)
-    assert back == s
-    r = _cpu_report(m, t0, t1, t2, core, f"nybble {'adaptive' if modify else 'static'}, ")
-    r["encode_GBps"] = round(m / (t1 - t0) / 1e9, 4)
-    r["decode_GBps"] = round(m / (t2 - t1) / 1e9, 4)
-    return r
+    return _cpu_median(reps)
 
 
 def bench_input(cfg, n, seed, dev):
@@ -577,15 +584,25 @@ CFG_TEXT = {"C2": "enwik-like text", "C3": "uniform random bytes", "C4": "Zipf s
             "C5": "syslog-like text"}
 
 
+def profile_files(kind):
+    """The committed summaries of one kind ("pmc_traffic" or "rocprof"), newest first, in the
+    order profiles/INDEX.json lists them (by when the profile was taken: the file names' round
+    tags are not in time order, r4f was taken after r4q). Files the index does not list are
+    never cited."""
+    try:
+        idx = json.load(open(os.path.join(REPO, "profiles", "INDEX.json")))
+    except (OSError, ValueError):
+        return []
+    return [os.path.join(REPO, "profiles", f) for f in idx.get(kind, [])]
+
+
 def pmc_traffic(kernel, a, n):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary
     (profiles/*_pmc_traffic.json, written by tools/pmc.sh + tools/pmc_report.py from separate
     --pmc passes of this same bench command; FETCH_SIZE x2 per MI355X_MICROARCH.md). PMC
     counters cannot be read inside the timed run, so the figure is the profiled run's,
     reported only when that run's workload matches this one."""
-    import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic.json")))   # rNN_ prefix: newest last
-    for f in reversed(files):
+    for f in profile_files("pmc_traffic"):
         try:
             d = json.load(open(f))
         except (OSError, ValueError):
@@ -603,8 +620,7 @@ def rocprof_mean(kernel, a, n):
     """Mean launch duration (ms) of `kernel` from the newest committed rocprofv3 --stats summary
     of this bench command (profiles/*_rocprof.json, tools/rocprof_report.py), when its workload
     matches: the roofline fraction by rocprof beside the HIP-event one."""
-    import glob
-    for f in reversed(sorted(glob.glob(os.path.join(REPO, "profiles", "*_rocprof.json")))):
+    for f in profile_files("rocprof"):
         try:
             d = json.load(open(f))
         except (OSError, ValueError):
@@ -663,9 +679,13 @@ def copy_probe(c, x, reps):
     return 2 * m / (ms * 1e-3) / 1e9
 
 
+CPU_REPS = 3   # the CPU baseline is the median of this many timings (the spread is reported)
+
+
 def cpu_baseline(x, a):
     """Oracle (single-threaded C restatement, oracle/dc_oracle.c) on a bounded sample, pinned
-    to one host core (taskset -c 0 equivalent) for the timed part."""
+    to one host core (taskset -c 0 equivalent) for the timed part; the median of
+    CPU_REPS timings, with their spread."""
     from oracle import oracle as orc
     m = min(a.cpu_sample, x.numel())
     s = x[:m].cpu().numpy()
@@ -673,9 +693,19 @@ def cpu_baseline(x, a):
     core = min(old)
     os.sched_setaffinity(0, {core})
     try:
-        return _cpu_timed(orc, s, m, a, core)
+        return _cpu_median([_cpu_timed(orc, s, m, a, core) for _ in range(CPU_REPS)])
     finally:
         os.sched_setaffinity(0, old)
+
+
+def _cpu_median(reps):
+    """The median run of the CPU baseline, with every run's value and the spread."""
+    vals = [r["value"] for r in reps]
+    med = dict(sorted(reps, key=lambda r: r["value"])[len(reps) // 2])
+    med["reps"] = vals
+    med["spread"] = round((max(vals) - min(vals)) / med["value"], 4) if med["value"] else None
+    med["sample"] += f"; median of {len(reps)} timings"
+    return med
 
 
 def _cpu_timed(orc, s, m, a, core):

@@ -274,7 +274,11 @@ __global__ __launch_bounds__(256) void k_hist_blocks(const uint8_t *__restrict__
                         // byte address bin*256 + lane*4 in one v_perm_b32: byte 0 = lane*4,
                         // byte 1 = byte q of the input word, bytes 2-3 = 0
                         const uint32_t addr = __builtin_amdgcn_perm(w4[j], lane4, 0x0c0c0000u | ((4u + q) << 8));
+#ifdef DC_ABL_HIST_NOATOM   // timing ablation only: no LDS counting (wrong histogram)
+                        asm volatile("" ::"v"(addr));
+#else
                         atomicAdd(reinterpret_cast<uint32_t *>(cbase + addr), inc);
+#endif
                     }
                 }
             }
@@ -303,6 +307,9 @@ __global__ __launch_bounds__(256) void k_hist_blocks(const uint8_t *__restrict__
         // 32 KiB block.)
         const uint4 *row = reinterpret_cast<const uint4 *>(&cnt[t * 64]);
         uint32_t acc = 0;
+#ifdef DC_ABL_HIST_NORED   // timing ablation only: no per-block reduction (wrong block histograms)
+        acc = t;
+#else
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
             const uint4 d = row[(k + t) & 15];
@@ -317,6 +324,7 @@ __global__ __launch_bounds__(256) void k_hist_blocks(const uint8_t *__restrict__
                 prevc[4 * k + q] = x;
             }
         }
+#endif
         if (FE) {   // the block's pair starts carry no symbol; block 0 holds the type byte 8
             if (t == 0x20) acc -= s_ps[0] + s_ps[1] + s_ps[2] + s_ps[3];
             if (t == 8 && b == 0) acc += 1u;
@@ -1436,10 +1444,14 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
             for (int k = 0; k < PACK_PIECES; ++k) {
                 const uint32_t w4[4] = {blkv[k].x, blkv[k].y, blkv[k].z, blkv[k].w};
                 uint32_t s0 = 0, s1 = 0;
+#ifdef DC_ABL_PACK_NOLUT   // timing ablation only: every code 4 bits, no table reads (garbage stream)
+                s0 = 32u + (w4[0] & 0u); s1 = 32u + (w4[3] & 0u);
+#else
 #pragma unroll
                 for (int i = 0; i < 8; ++i) s0 += s_nb8[(w4[i >> 2] >> (8 * (i & 3))) & 255u];
 #pragma unroll
                 for (int i = 8; i < 16; ++i) s1 += s_nb8[(w4[i >> 2] >> (8 * (i & 3))) & 255u];
+#endif
                 Hk[k] = s0;
                 Tk[k] = s0 + s1;
                 __builtin_amdgcn_sched_barrier(0);
@@ -1489,9 +1501,14 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
                 auto emit = [&](uint64_t acc, uint32_t nb, uint32_t pos) {
                     const uint64_t al = acc << ((64u - nb) & 63u);
                     const uint32_t hi = (uint32_t)(al >> 32), lo = (uint32_t)al, r = pos & 31u, wi = pos >> 5;
+#ifdef DC_ABL_PACK_NOOR   // timing ablation only: no stage ORs (garbage stream)
+                    asm volatile("" ::"v"(hi >> r), "v"(__builtin_amdgcn_alignbit(hi, lo, r)),
+                                 "v"(__builtin_amdgcn_alignbit(lo, 0u, r)), "v"(wi));
+#else
                     atomicOr(&s_stage[wi], hi >> r);
                     atomicOr(&s_stage[wi + 1], __builtin_amdgcn_alignbit(hi, lo, r));
                     atomicOr(&s_stage[wi + 2], __builtin_amdgcn_alignbit(lo, 0u, r));
+#endif
                 };
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
@@ -1503,7 +1520,11 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
                         uint64_t acc = 0;
 #pragma unroll
                         for (int i = 8 * h; i < 8 * h + 8; ++i) {
+#ifdef DC_ABL_PACK_NOLUT
+                            const uint2 e = make_uint2((w4[i >> 2] >> (8 * (i & 3))) & 15u, 4u);
+#else
                             const uint2 e = s_tab[(w4[i >> 2] >> (8 * (i & 3))) & 255u];
+#endif
                             acc = (acc << e.y) | e.x;
                         }
                         emit(acc, Th, pos);
@@ -2466,7 +2487,11 @@ static __device__ __forceinline__ void d8_batch_q(const uint64_t *const *st, D8W
 #pragma unroll
         for (int j = 0; j < NC; ++j) {
             const uint32_t x = (uint32_t)(win[j] >> (off[j] & 63u));
+#ifdef DC_DIAG_LUTMASK   // timing ablation only: lookups confined to the first entries (conflict free)
+            e[j][k] = *reinterpret_cast<const uint16_t *>(lb + (x & (2u * DC_DIAG_LUTMASK)));
+#else
             e[j][k] = *reinterpret_cast<const uint16_t *>(lb + (x & ((2u << D8_LUT_BITS) - 2u)));
+#endif
             o[j] = __builtin_amdgcn_perm(e[j][k], k ? o[j] : 0u, SEL[k]);
             off[j] += e[j][k];
         }
@@ -6822,7 +6847,7 @@ static int decode_impl(dc_ctx *c, const uint32_t *d_words, uint64_t bit_base, co
     // then; a table rebuilt elsewhere since reads dec_ready 0 in the decoder: a stream error)
     if (!dec_tables_fresh(c, d_table)) LAUNCH(c, "dec_tables", k_dec_tables, 1, 256, const_cast<dc_dtable *>(d_table), derr);
     const bool fast8 = S == 64 && n < (1ull << 37) && words < (1ull << 31) && !c->opt_decode_general;
-    if (d_gexp && !fast8) return DC_E_ARG;
+    if (d_gexp && (!fast8 || c->opt_decode_variant != 0)) return DC_E_ARG;   // (k_huff_decode9 writes no counts)
     if (fast8) {
         // 12 waves x 2 chains, one workgroup per CU: the stage and the 14-bit table fill the
         // LDS (the 8 x 4 split measured 0.89 vs 0.70 ms on 1 GiB C2: spills)
@@ -7348,8 +7373,12 @@ int dc_nyb_body_write(dc_ctx *c, const uint8_t *d_in, uint64_t len, int modify, 
 {
     if (!c || !d_out || !h_len || !d_in || len < 1 || pend_rank > 7) return DC_E_ARG;
     if (modify && len > 1 && (c->rk_in != d_in || c->rk_len != len)) return DC_E_ARG;   // plan this input first
-    FsmAux aux{modify && len > 1 ? c->d_rk : nullptr, pend_rank < 0 ? 0u : (uint32_t)pend_rank,
-               pend_rank < 0 ? 0u : 1u, is_last ? 1u : 0u, 0, 0, c->d_mrec, mtf_heads(c, len)};
+    // the first-touch records only with ranks (an earlier adaptive call leaves d_mrec set: a
+    // static body passing it would trip fsm_run's unsettled-ranks guard)
+    const bool adaptive = modify && len > 1;
+    FsmAux aux{adaptive ? c->d_rk : nullptr, pend_rank < 0 ? 0u : (uint32_t)pend_rank,
+               pend_rank < 0 ? 0u : 1u, is_last ? 1u : 0u, 0, 0, adaptive ? c->d_mrec : nullptr,
+               adaptive ? mtf_heads(c, len) : nullptr};
     int r = fsm_run<M_NYB_ENC>(c, d_in, len, len - 1, d_out, h_len, "nyb_body_tiles", aux, nullptr, true, nullptr,
                                0, modify && len > 1);
     if (r) return r;
@@ -7465,7 +7494,11 @@ int dc_small_huff_decode(dc_ctx *c, const uint32_t *d_words, uint64_t bit_base, 
                          const dc_dtable *d_table, uint8_t *d_m, uint8_t *d_out, uint64_t *h_len)
 {
     if (!c || !d_m || !d_out || !h_len) return DC_E_ARG;
-    if (S != 64 || m < 2 || ((uintptr_t)d_m & 15) || c->opt_decode_general) {   // the two stages as they are
+    // the counted path needs k_huff_decode8 (decode_impl's fast8 conditions; the A/B variant 1
+    // decoder never writes the per-group counts): anything else runs the two stages as they are
+    const bool counted = S == 64 && m >= 2 && !((uintptr_t)d_m & 15) && !c->opt_decode_general &&
+                         c->opt_decode_variant == 0 && m < (1ull << 37) && words < (1ull << 31);
+    if (!counted) {
         const int r = decode_impl(c, d_words, bit_base, nullptr, words, d_sync_base, d_sync_len, S, m, d_table, d_m);
         return r ? r : dc_small_decompress(c, d_m, m, d_out, h_len);
     }

@@ -360,9 +360,12 @@ class ShardedSmall:
         for w in dist.batch_isend_irecv(ops) if ops else []:
             w.wait()
 
-    def encode(self, x, n_ary: int = 16, sync_syms: int = 64):
+    def encode(self, x, n_ary: int = 16, sync_syms: int = 64, words=None, sync=None, table=None, total=None):
+        """words/sync/table/total: optional caller-owned buffers for the fused path (the stream
+        points into them, so a caller that keeps several streams passes distinct ones; without
+        them every encode allocates its own)."""
         if self.fused and self.world == 1 and hasattr(self.e, "small_huff_plan") and x.numel() >= 2:
-            s = self._encode_fused(x, n_ary, sync_syms)
+            s = self._encode_fused(x, n_ary, sync_syms, words, sync, table, total)
             if s is not None:
                 return s
         seg, literal = self.frontend(x, sync_syms)
@@ -370,30 +373,33 @@ class ShardedSmall:
         s.literal = literal
         return s
 
-    def _encode_fused(self, x, n_ary, S):
+    def _encode_fused(self, x, n_ary, S, words=None, sync=None, table=None, total=None):
         """World size 1: the front-end and the Huffman code in one pass over x, the front-end
         output never written (dc_small_huff_plan + dc_small_huff_pack_async): the stream equals
         frontend() + ShardedHuffman.encode() bit for bit. None when the fused path does not
         apply (LITERAL output, every byte value present, DC_E_FALLBACK): the caller runs the
-        two stages. Buffers are kept across calls of the same size."""
+        two stages. Only the histogram (scratch the stream does not keep) is reused across
+        calls; the words, sync index, table and total belong to the returned stream."""
         from ._lib import DcError
         n = x.numel()
-        key = (n, S)
-        buf = getattr(self, "_fbuf", None)
-        if buf is None or buf["key"] != key:
-            buf = self._fbuf = {"key": key, "hist": self.e._t(256, torch.int64), "tab": self.e.alloc_table(),
-                                "total": self.e._t(1, torch.int64), "sync": self.e.alloc_sync(n + 1, S),
-                                "words": None}
+        hist = getattr(self, "_fhist", None)
+        if hist is None:
+            hist = self._fhist = self.e._t(256, torch.int64)
+        tab = table if table is not None else self.e.alloc_table()
+        tot = total if total is not None else self.e._t(1, torch.int64)
+        if sync is None:
+            sync = self.e.alloc_sync(n + 1, S)
         try:
-            _, tab, tot = self.e.small_huff_plan(x, n_ary, hist=buf["hist"], table=buf["tab"], total=buf["total"])
+            _, tab, tot = self.e.small_huff_plan(x, n_ary, hist=hist, table=tab, total=tot)
         except DcError as err:
             if err.rc != -8:
                 raise
             return None
         bits = int(tot.item())
         need = self.e.words_needed(0, bits)
-        if buf["words"] is None or buf["words"].numel() < need:
-            buf["words"] = self.e._t(need + need // 16, torch.int32)
+        if words is None or words.numel() < need:
+            words = self.e._t(need + need // 16, torch.int32)
+        buf = {"words": words, "sync": sync}
         gen = self.e.plan_gen()
         self.e.small_huff_pack_async(x, tab, 0, buf["words"], buf["sync"], S)
         st = self.e.pack_status(tab, gen)

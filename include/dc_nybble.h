@@ -54,9 +54,17 @@ int update_context(context_table_type *context_table, const char context_byte, c
 int compress_byte_index(context_table_type *context_table, int nybble_offset, const char *source, char *dest);
 
 void compress_bytestring(const char *source_original, char *dest_original, bool modify);
+/* Adaptive mode (modify true, and nybble_decompress below) is sequential by definition: each
+ * byte's move-to-front list depends on every byte decoded before it, and the next byte's
+ * context on the value a hit names, so ONE adaptive stream has no parallel decode. On the GPU
+ * its token structure is found in parallel, then one wave settles the list touches (~21 MB/s,
+ * slower than one host core running the reference, ~120 MB/s). The throughput
+ * path for adaptive data is many independent streams: the DCNK chunk container
+ * (dc_nyb_compress_chunked / dc_nyb_decompress_chunked) or dc_nyb_decompress_batch (one lane
+ * per stream, dc_gpu.h). Static mode (modify false) decodes every byte independently. */
 void decompress_bytestring(const char *source, char *dest_original, bool modify);
 void nybble_compress(const char *source_original, char *dest_original);
-void nybble_decompress(const char *source, char *dest_original);
+void nybble_decompress(const char *source, char *dest_original);   /* adaptive: see above */
 
 #ifdef __cplusplus
 }

@@ -710,6 +710,43 @@ def test_sharded_small_single_rank_on_device(torch_cuda, codec, fused):
     assert np.array_equal(sm.decode(s).cpu().numpy(), x)
 
 
+def test_sharded_small_streams_own_their_buffers(torch_cuda, codec):
+    """Two fused encodes of same-size inputs, then both decodes: the first stream's payload,
+    sync index and table must survive the second encode (they were cached per size)."""
+    from data_compression_amd import synth
+    from data_compression_amd.dist import ShardedSmall
+    torch = torch_cuda
+    n = (3 << 16) + 11
+    xs = [synth.log_like(n, seed=31), synth.log_like(n, seed=32)]
+    sm = ShardedSmall(codec, fused=True)
+    ss = [sm.encode(torch.from_numpy(x).cuda(), n_ary=16, sync_syms=64) for x in xs]
+    for x, s in zip(xs, ss):
+        assert np.array_equal(sm.decode(s).cpu().numpy(), x)
+
+
+def test_static_body_after_adaptive_work(torch_cuda):
+    """One context: an adaptive encode (it leaves first-touch records behind), then a static
+    shard body on the same context must still encode (the static write passed the
+    records on and tripped the unsettled-ranks guard)."""
+    from data_compression_amd import synth
+    from data_compression_amd.device import Codec
+    from data_compression_amd.dist import ShardedNybble
+    torch = torch_cuda
+    c = Codec(0)
+    x = synth.english_like(50_001, seed=3)
+    xt = torch.from_numpy(x).cuda()
+    assert c.nyb_compress(xt, True).cpu().numpy().tobytes() == orc.nybble_compress(x.tobytes(), True)
+    c.nyb_body_plan(xt, True, dist_initial_lists())   # adaptive plan too
+    seg, lit = ShardedNybble(c).compress(xt, False)
+    assert not lit
+    assert seg.cpu().numpy().tobytes() == orc.nybble_compress(x.tobytes(), False)
+
+
+def dist_initial_lists():
+    from data_compression_amd.dist import INITIAL_LISTS
+    return INITIAL_LISTS.copy()
+
+
 # ---------------------------------------------------------------- nybble: adaptive in parallel, shards
 def _nyb_cases(torch):
     from data_compression_amd import synth

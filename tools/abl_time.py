@@ -1,0 +1,60 @@
+"""Per-kernel HIP-event times of one codec stage on the 1 GiB bench input, for ablation
+libraries (DC_CORE_LIB=tools/_ablX/libdc_core.so) against the in-tree one.
+
+    python tools/abl_time.py [--stage decode|encode|step] [--cfg C2] [--iters 20] [--tag NAME]
+
+Prints one JSON line: {"tag", "stage", "kernels": {name: mean ms}}. Ablation builds produce
+garbage output: nothing is checked.
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from data_compression_amd import synth  # noqa: E402
+from data_compression_amd.device import Codec  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--cfg", default="C2")
+ap.add_argument("--size", type=int, default=1 << 30)
+ap.add_argument("--nary", type=int, default=2)
+ap.add_argument("--stage", default="decode")
+ap.add_argument("--iters", type=int, default=20)
+ap.add_argument("--warm", type=int, default=30)
+ap.add_argument("--tag", default=os.path.basename(os.path.dirname(os.environ.get("DC_CORE_LIB", "base/x"))))
+a = ap.parse_args()
+dev = torch.device("cuda", 0)
+x = synth.device_text(a.cfg, a.size, seed=0xC2, device=dev)
+c = Codec(0)
+enc = c.encode(x, n_ary=a.nary, sync_syms=64)
+out = torch.empty_like(x)
+
+
+def run():
+    if a.stage == "decode":
+        c.decode_into(enc, out)
+    elif a.stage == "hist":
+        c.hist(x)
+    else:
+        e = c.encode(x, n_ary=a.nary, sync_syms=64)
+        if a.stage == "step":
+            c.decode_into(e, out)
+
+
+for _ in range(a.warm):
+    run()
+torch.cuda.synchronize()
+c.timing(True)
+for _ in range(a.iters):
+    run()
+kt = c.timings()
+c.timing(False)
+per = {}
+for name, ms in kt:
+    per.setdefault(name, []).append(ms)
+print(json.dumps({"tag": a.tag, "stage": a.stage, "cfg": a.cfg,
+                  "kernels": {k: round(float(np.mean(v)), 4) for k, v in per.items()}}), flush=True)
