@@ -14,6 +14,7 @@
 #include <stdlib.h>
 
 #include <atomic>
+#include <type_traits>
 
 #include "dc_gpu.h"
 
@@ -399,21 +400,163 @@ extern "C" int dc_diag_tbl_read(void *h)
 #define TBL_NODES 4096
 
 struct TblLds {   // k_huff_table's LDS (also carved from k_hist_blocks' counters by its last workgroup)
-    __attribute__((aligned(16))) uint64_t key[TBL_SORT_MAX];
+    __attribute__((aligned(16))) uint64_t key[TBL_SORT_MAX];   // sort keys; then the per-length symbol bitmaps
     uint64_t q2[TBL_SORT_MAX];
     int16_t parent[TBL_NODES];
     int32_t len[DC_MAX_SYMS];
-    __attribute__((aligned(16))) uint32_t cnt[DC_MAX_DIGITS + 2];   // also the merge's 64-key window
+    __attribute__((aligned(16))) uint32_t cnt[DC_MAX_DIGITS + 2];
     uint32_t startv[DC_MAX_DIGITS + 2];
     uint32_t starti[DC_MAX_DIGITS + 2];
     uint32_t code[256];
     uint32_t nb[256];
     int k, mn, mx, maxbits, bad;
-    uint32_t rbase[DC_MAX_DIGITS + 1];
-    uint32_t wcnt[4][DC_MAX_DIGITS + 1];
     uint64_t red[4];
 };
 static_assert(sizeof(TblLds) <= 256 * 64 * sizeof(uint32_t), "k_hist_blocks' last workgroup builds the table in its counters' LDS");
+
+// The value lane (lane ^ d) holds, d a power of two < 64, by VALU lane moves only (no LDS
+// crossbar): quad_perm for 1 and 2, row shifts for 4, row_ror:8 (xor 8 in a 16-lane row), and
+// the gfx950 permlane swaps for 16 and 32 (x swapped with itself: the first result holds the
+// lower row / half twice, the second the upper one twice).
+static __device__ __forceinline__ uint32_t lane_xor(uint32_t x, int d, int lane)
+{
+    switch (d) {
+    case 1: return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xf, 0xf, false);   // quad_perm [1,0,3,2]
+    case 2: return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xf, 0xf, false);   // quad_perm [2,3,0,1]
+    case 4: {
+        const uint32_t up = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x104, 0xf, 0xf, false);   // row_shl:4
+        const uint32_t dn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);   // row_shr:4
+        return (lane & 4) ? dn : up;
+    }
+    case 8: return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x128, 0xf, 0xf, false);   // row_ror:8
+    case 16: {
+        const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+        return (lane & 16) ? r[0] : r[1];
+    }
+    default: {
+        const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+        return (lane & 32) ? r[0] : r[1];
+    }
+    }
+}
+
+// inclusive wave64 prefix sum of u64 in DPP (wave_scan_incl's steps on both halves; a lane
+// whose source is outside its row, or a row the row mask leaves out, adds 0)
+static __device__ __forceinline__ uint64_t wave_scan_incl_u64(uint64_t x)
+{
+#define DC_SCAN64_STEP(ctrl, rm)                                                                          \
+    {                                                                                                     \
+        const uint32_t lo_ = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)x, ctrl, rm, 0xf, false);  \
+        const uint32_t hi_ = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(x >> 32), ctrl, rm, 0xf, false); \
+        x += ((uint64_t)hi_ << 32) | lo_;                                                                 \
+    }
+    DC_SCAN64_STEP(0x111, 0xf) DC_SCAN64_STEP(0x112, 0xf) DC_SCAN64_STEP(0x114, 0xf) DC_SCAN64_STEP(0x118, 0xf)
+    DC_SCAN64_STEP(0x142, 0xa) DC_SCAN64_STEP(0x143, 0xc)
+#undef DC_SCAN64_STEP
+    return x;
+}
+
+// One wave sorts a bitonic sequence of 64 distinct u64 keys (one per lane) ascending in lane
+// order: 6 compare-exchange stages on VALU lane moves, branch-free (the lower lane of a pair
+// keeps the smaller key: it takes its partner's when that is smaller, the upper lane when it is
+// larger; keys are distinct, or equal INF pads, so one compare decides both)
+static __device__ __forceinline__ uint64_t wave_bitonic_merge(uint64_t k, int lane)
+{
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const uint32_t plo = lane_xor((uint32_t)k, d, lane), phi = lane_xor((uint32_t)(k >> 32), d, lane);
+        const uint64_t p = ((uint64_t)phi << 32) | plo;
+        const bool take = (p < k) != ((lane & d) != 0);
+        k = take ? p : k;
+    }
+    return k;
+}
+
+// (H3) the batched two-queue n-ary merge by one wave (generate_huffman_tree, n_ary_huffman.c:
+// 868-1005, whose stable re-sort :672-731 orders by (count, node index)). Leaves
+// and dummies sit sorted in key[0, items) as count << 11 | index; internal nodes are created
+// with non-decreasing counts into q2 (a FIFO), and on equal counts a leaf precedes an internal
+// node and an older internal node a younger one. Let smin = the sum of the n smallest live
+// counts: every node created from now on has count >= smin, so every live node of count <=
+// smin is picked before any new one, n at a time, in sorted order. A round therefore merges a
+// window of 32 leaves and 32 internal nodes into one sorted wave (a bitonic merge in registers:
+// the internal half is loaded reversed), keeps the prefix of count <= smin (cut at a half's
+// last key when more nodes lie beyond it), and creates floor(prefix / n) nodes at once. Window
+// keys of internal nodes: count << 11 | (1536 + position in the window): after every leaf on
+// equal counts (leaf indices < 1536), in creation order among themselves, distinct.
+// r4 ranked the window by binary searches through LDS (~2.2k cycles a round); this round is
+// one LDS load, VALU lane moves, and the stores.
+static __device__ void huff_merge_wave(const uint64_t *__restrict__ key, uint64_t *__restrict__ q2,
+                                       int16_t *__restrict__ parent, int items, int nary, int first_internal,
+                                       dc_tree *__restrict__ tree, int *bad)
+{
+    const int lane = threadIdx.x & 63;
+    const bool isL = lane < 32;
+    const int j = isL ? lane : 63 - lane;   // the internal half reversed: a bitonic sequence
+    // per lane, fixed for every round: its group (lane / n) and place in it (lane % n), and
+    // the number of whole groups in lanes 0 .. lane ((lane + 1) / n)
+    const int gq = lane / nary, gr = lane - gq * nary, gwhole = (lane + 1) / nary;
+    const uint64_t jtag = 1536u + (uint32_t)j;
+    int h1 = 0, h2 = 0, t2 = 0, active = items, nxt = first_internal;
+    constexpr uint64_t INF = ~0ull;
+    while (active > 1) {
+        // window: leaves h1 .. h1 + 31 in lanes 0-31, internal nodes h2 + 31 .. h2 in lanes
+        // 32-63 (one LDS read per lane, the address chosen by a select)
+        const int pos = isL ? h1 + j : h2 + j;
+        const bool have = pos < (isL ? items : t2);
+        const uint64_t *src = isL ? key : q2;
+        const uint64_t raw = src[have ? pos : 0];
+        const uint64_t k0 = !have ? INF : isL ? raw : ((raw << 11) | jtag);
+        // a half with more nodes beyond the window bounds the prefix at its last window key
+        const uint64_t lastL = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(k0 >> 32), 31) << 32) |
+                               (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)k0, 31);
+        const uint64_t lastQ = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(k0 >> 32), 32) << 32) |
+                               (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)k0, 32);
+        const uint64_t bound = min(h1 + 32 < items ? lastL : INF, t2 - h2 > 32 ? lastQ : INF);
+        const uint64_t k = wave_bitonic_merge(k0, lane);
+        const uint64_t cnt = k != INF ? (k >> 11) : 0ull;
+        // group sums (a node of this round = lanes kn .. kn + n - 1, summed at lane kn + n - 1)
+        // and smin (the n smallest = group 0): n = 2 by one DPP row shift, else a DPP scan less
+        // the scan n lanes down
+        uint64_t gsum;
+        if (nary == 2) {
+            const uint32_t plo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)cnt, 0x111, 0xf, 0xf, false);
+            const uint32_t phi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(cnt >> 32), 0x111, 0xf, 0xf, false);
+            gsum = cnt + (((uint64_t)phi << 32) | plo);   // odd lanes: the pair ending here
+        } else {
+            const uint64_t S = wave_scan_incl_u64(cnt);
+            const int sl = lane >= nary ? lane - nary : lane;
+            const uint64_t Sd = (uint64_t)(uint32_t)__shfl((int)(uint32_t)S, sl, 64) |
+                                ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(S >> 32), sl, 64) << 32);
+            gsum = S - (lane >= nary ? Sd : 0ull);
+        }
+        const uint64_t smin = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(gsum >> 32), nary - 1) << 32) |
+                              (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)gsum, nary - 1);
+        // qualifying nodes: a prefix of the lanes (k ascending, INF last)
+        const int cq = __popcll(__ballot(k != INF && cnt <= smin && k <= bound));
+        int m = cq > 0 ? __builtin_amdgcn_readlane(gwhole, cq - 1) : 0;   // floor(cq / n)
+        if (m == 0) { m = 1; *bad = 1; }   // cannot happen: the n smallest always qualify
+        const int used = m * nary;
+        const bool inB = lane < used;
+        const bool leaf = (k & 2047u) < 1536u;
+        const int na = __popcll(__ballot(inB && leaf));
+        if (inB && gr == nary - 1) q2[t2 + gq] = gsum;
+        if (inB) {
+            const int node = leaf ? (int)(k & 2047u) : first_internal + h2 + (int)((k & 2047u) - 1536u);
+            const int par = nxt + gq;
+            if (node < TBL_NODES) parent[node] = (int16_t)par;
+            if (tree && gr < 2 && par < TBL_NODES)   // first two children (:978-979)
+                (gr ? tree->right : tree->left)[par] = node;
+        }
+        __builtin_amdgcn_wave_barrier();   // the new nodes' counts are read by the next window
+        h1 += na;
+        h2 += used - na;
+        t2 += m;
+        nxt += m;
+        active -= m * (nary - 1);
+    }
+    if (lane == 0 && nxt >= TBL_NODES) *bad = 1;
+}
 
 // The table of k_huff_table, by one 256-thread workgroup on the LDS S. With d_total set it
 // also writes the encode plan of plan_hist (the histogram of the bytes to be packed): the
@@ -435,8 +578,6 @@ static __device__ void huff_table_body(TblLds &S, const uint64_t *__restrict__ f
     uint32_t *const s_code = S.code;
     uint32_t *const s_nb = S.nb;
     int &s_k = S.k, &s_min = S.mn, &s_max = S.mx, &s_maxbits = S.maxbits, &s_bad = S.bad;
-    uint32_t *const s_rbase = S.rbase;
-    uint32_t (*const s_wcnt)[DC_MAX_DIGITS + 1] = S.wcnt;
 
     const int t = threadIdx.x;
     const int leaves = M + 1;
@@ -502,72 +643,7 @@ static __device__ void huff_table_body(TblLds &S, const uint64_t *__restrict__ f
         }
         TBL_STAMP(8);
         if (nary <= 32 && t < 64) {
-            // Batched two-queue merge by wave 0. Leaves (and dummies) sit sorted in s_key as
-            // count << 11 | index; internal nodes are created in non-decreasing count order
-            // (queue s_q2), and on equal counts a leaf precedes an internal node and an older
-            // internal node a younger one, as in the reference's stable re-sort (:672-731).
-            // Let smin = the sum of the n smallest live nodes: every node created from now on
-            // has count >= smin and a larger index, so all live nodes of count <= smin are picked
-            // before any new one, n at a time, in sorted order. A round therefore takes a window
-            // of 32 leaves and 32 internal nodes, ranks the 64 by binary search in the other
-            // side, keeps the prefix of count <= smin (cut at a window's last key when more
-            // nodes lie beyond it), and creates floor(prefix / n) nodes at once: ~15-20 rounds
-            // on text or bytes where the one-pick-at-a-time loop took 512 dependent picks.
-            // Key of an internal node: count << 11 | 2047 (ties: after every leaf).
-            const int lane = t;
-            const int first_internal = leaves + dummies;
-            const bool isL = lane < 32;
-            const int j = isL ? lane : lane - 32;
-            uint64_t *const s_win = reinterpret_cast<uint64_t *>(s_cnt);   // 64 window keys (reused scratch)
-            uint64_t *const s_B = s_q2 + (TBL_SORT_MAX - 64);               // the round's nodes in rank order
-            int h1 = 0, h2 = 0, t2 = 0, active = items, nxt = first_internal;
-            constexpr uint64_t INF = ~0ull;
-            while (active > 1) {
-                const uint64_t key = isL ? (h1 + j < items ? s_key[h1 + j] : INF)
-                                         : (h2 + j < t2 ? ((s_q2[h2 + j] << 11) | 2047ull) : INF);
-                s_win[lane] = key;
-                __builtin_amdgcn_wave_barrier();
-                // rank in the window union: own position + nodes of the other side before it
-                const uint64_t *other = isL ? s_win + 32 : s_win;
-                int lo = 0;
-#pragma unroll
-                for (int st = 32; st >= 1; st >>= 1)
-                    if (lo + st <= 32 && other[lo + st - 1] < key) lo += st;
-                const int rank = j + lo;
-                const bool valid = key != INF;
-                if (valid) s_B[rank] = key;
-                __builtin_amdgcn_wave_barrier();
-                uint64_t smin = 0;   // every lane sums the n smallest (broadcast reads, no shuffles)
-                for (int q = 0; q < nary; ++q) smin += s_B[q] >> 11;
-                const uint64_t boundL = h1 + 32 < items ? s_win[31] : INF;
-                const uint64_t boundQ = t2 - h2 > 32 ? s_win[63] : INF;
-                const bool qual = valid && (key >> 11) <= smin && key <= boundL && key <= boundQ;
-                const int cq = __popcll(__ballot(qual));
-                int m = cq / nary;
-                if (m == 0) { m = 1; if (lane == 0) s_bad = 1; }   // cannot happen: n smallest always qualify
-                const int used = m * nary;
-                const bool inB = valid && rank < used;
-                const int na = __popcll(__ballot(inB && isL));
-                if (lane < m) {
-                    uint64_t sum = 0;
-                    for (int q = 0; q < nary; ++q) sum += s_B[lane * nary + q] >> 11;
-                    s_q2[t2 + lane] = sum;
-                }
-                if (inB) {
-                    const int node = isL ? (int)(key & 2047u) : first_internal + h2 + j;
-                    const int par = nxt + rank / nary;
-                    if (node < TBL_NODES) s_parent[node] = (int16_t)par;
-                    if (tree && rank % nary < 2 && par < TBL_NODES)   // first two children (:978-979)
-                        (rank % nary ? tree->right : tree->left)[par] = node;
-                }
-                __builtin_amdgcn_wave_barrier();
-                h1 += na;
-                h2 += used - na;
-                t2 += m;
-                nxt += m;
-                active -= m * (nary - 1);
-            }
-            if (lane == 0 && nxt >= TBL_NODES) s_bad = 1;
+            huff_merge_wave(s_key, s_q2, s_parent, items, nary, leaves + dummies, tree, &s_bad);
         } else if (t == 0) {
             // two-queue merge; both queues' heads and next elements held in registers, the
             // element after them prefetched from LDS when a head is consumed, so no pick
@@ -642,12 +718,17 @@ static __device__ void huff_table_body(TblLds &S, const uint64_t *__restrict__ f
     } else {
         for (int i = t; i < leaves; i += 256) s_len[i] = lens_in[i];
     }
-    for (int L = t; L < DC_MAX_DIGITS + 2; L += 256) s_cnt[L] = 0;
-    __syncthreads();
-
+    // canonical codes (convert_lengths_to_encode_table, :1382-1612): min/max over i < M (:1336),
+    // assignment over i <= M. Per length a bitmap of its symbols (in the sort keys' LDS, free
+    // now): counts and ranks are popcounts, and the first value per length is one DPP scan of
+    // the affine steps code -> (code + cnt) * n. Two barriers where r4's per-wave ballot loops
+    // took ten (15k cycles on C2).
+    uint32_t *const s_mask = reinterpret_cast<uint32_t *>(s_key);   // [L - 1][32]: symbols of length L
+    constexpr int MW = DC_MAX_SYMS / 32;
+    static_assert(DC_MAX_DIGITS * MW * sizeof(uint32_t) <= sizeof(S.key), "length bitmaps in the key array");
+    for (int q = t; q < DC_MAX_DIGITS * MW / 4; q += 256) reinterpret_cast<uint4 *>(s_mask)[q] = make_uint4(0u, 0u, 0u, 0u);
     TBL_STAMP(3);
-    // canonical codes: min/max over i < M, assignment over i <= M
-    {   // min / max length over i < M: per thread, per wave (shuffles), one atomic per wave
+    {   // min / max length over i < M: per thread, per wave (DPP-free shuffles), one atomic per wave
         int mx = 0, mnl = 300;
         for (int i = t; i < M; i += 256) {
             const int L = s_len[i];
@@ -663,83 +744,68 @@ static __device__ void huff_table_body(TblLds &S, const uint64_t *__restrict__ f
     }
     __syncthreads();
     const int minL = s_min, maxL = s_max;
-    if (maxL > DC_MAX_DIGITS) {
-        if (t == 0) s_bad = 1;
-    }
-    for (int i0 = 0; i0 < leaves; i0 += 256) {   // counts per length: a ballot per distinct length
-        const int i = i0 + t;
-        const int L = i < leaves ? s_len[i] : 0;
-        const int key = (i < leaves && L >= minL && L <= maxL && L <= DC_MAX_DIGITS) ? L : -1;
-        uint64_t todo = __ballot(key >= 0);
-        while (todo) {
-            const int L0 = __builtin_amdgcn_readlane(key, __builtin_ctzll(todo));
-            const uint64_t m = __ballot(key == L0);
-            if ((t & 63) == 0) atomicAdd(&s_cnt[L0], (uint32_t)__popcll(m));
-            todo &= ~m;
-        }
-    }
-    __syncthreads();
-    TBL_STAMP(9);
-    if (t < 64) {
-        // first canonical value and first sorted slot per length (:1540-1568; int arithmetic,
-        // wraps mod 2^32): the lengths' counts held one per lane, the recurrence walked by
-        // readlane over [minL, maxL] only (the one-lane loop over every length read LDS per
-        // step: 16k cycles)
-        uint32_t code = 0, acc = 0;
-        for (int base = minL; base <= min(maxL, DC_MAX_DIGITS); base += 64) {
-            const int L = base + t;
-            const uint32_t cl = (L <= maxL && L <= DC_MAX_DIGITS) ? s_cnt[L] : 0u;
-            uint32_t sv = 0, si = 0;
-            const int span = min(64, min(maxL, DC_MAX_DIGITS) - base + 1);
-            for (int q = 0; q < span; ++q) {
-                const uint32_t cq = (uint32_t)__builtin_amdgcn_readlane((int)cl, q);
-                if (t == q) { sv = code; si = acc; }
-                code = (code + cq) * (uint32_t)nary;
-                acc += cq;
-            }
-            if (t < span) { s_startv[L] = sv; s_starti[L] = si; }
-        }
-        for (int L = t; L < minL && L <= DC_MAX_DIGITS; L += 64) { s_startv[L] = 0; s_starti[L] = 0; }
-        for (int L = maxL + 1 + t; L <= DC_MAX_DIGITS; L += 64) { s_startv[L] = 0; s_starti[L] = acc; }
+    const int topL = min(maxL, DC_MAX_DIGITS);
+    if (maxL > DC_MAX_DIGITS && t == 0) s_bad = 1;
+    for (int i = t; i < leaves; i += 256) {
+        const int L = s_len[i];
+        if (L >= minL && L <= topL) atomicOr(&s_mask[(L - 1) * MW + (i >> 5)], 1u << (i & 31));
     }
     for (int s = t; s < 256; s += 256) { s_code[s] = 0; s_nb[s] = 0; }
     __syncthreads();
-    for (int L = t; L <= DC_MAX_DIGITS; L += 256) s_rbase[L] = 0;
-    for (int q = t; q < 4 * (DC_MAX_DIGITS + 1); q += 256) (&s_wcnt[0][0])[q] = 0;
+    TBL_STAMP(9);
+    const int nw = (leaves + 31) >> 5;
+    if (t < 64) {
+        // per length: cnt = popcount of its bitmap; first slot = exclusive sum of the counts;
+        // first value (:1540-1568, int arithmetic wrapping mod 2^32) = the composition of the
+        // steps f_L(x) = n x + n cnt_L of the lengths below, applied to 0: an exclusive DPP scan
+        // of (A, B) pairs (x -> A x + B), carried across blocks of 64 lengths
+        uint32_t cin = 0, sin = 0;   // first value and first slot at the block's first length
+        for (int base = minL; base <= topL; base += 64) {
+            const int L = base + t;
+            const bool in = L <= topL;
+            uint32_t cl = 0;
+            if (in)
+                for (int q = 0; q < nw; ++q) cl += (uint32_t)__popc(s_mask[(L - 1) * MW + q]);
+            const uint32_t si = wave_scan_incl(cl);
+            uint32_t A = in ? (uint32_t)nary : 1u, B = in ? (uint32_t)nary * cl : 0u;
+#define DC_AFF_STEP(ctrl, rm)                                                                           \
+            {                                                                                           \
+                const uint32_t Ae = (uint32_t)__builtin_amdgcn_update_dpp(1, (int)A, ctrl, rm, 0xf, false); \
+                const uint32_t Be = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)B, ctrl, rm, 0xf, false); \
+                B = A * Be + B;                                                                         \
+                A = A * Ae;                                                                             \
+            }
+            DC_AFF_STEP(0x111, 0xf) DC_AFF_STEP(0x112, 0xf) DC_AFF_STEP(0x114, 0xf) DC_AFF_STEP(0x118, 0xf)
+            DC_AFF_STEP(0x142, 0xa) DC_AFF_STEP(0x143, 0xc)
+#undef DC_AFF_STEP
+            // exclusive: the inclusive pair of the lane below (identity at lane 0)
+            const uint32_t Ax = (uint32_t)__builtin_amdgcn_update_dpp(1, (int)A, 0x138, 0xf, 0xf, false);   // wave_shr:1
+            const uint32_t Bx = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)B, 0x138, 0xf, 0xf, false);
+            if (in) {
+                s_cnt[L] = cl;
+                s_startv[L] = Ax * cin + Bx;
+                s_starti[L] = sin + si - cl;
+            }
+            const uint32_t A63 = (uint32_t)__builtin_amdgcn_readlane((int)A, 63), B63 = (uint32_t)__builtin_amdgcn_readlane((int)B, 63);
+            cin = A63 * cin + B63;
+            sin += (uint32_t)__builtin_amdgcn_readlane((int)si, 63);
+        }
+        for (int L = t; L < minL && L <= DC_MAX_DIGITS; L += 64) { s_cnt[L] = 0; s_startv[L] = 0; s_starti[L] = 0; }
+        for (int L = topL + 1 + t; L <= DC_MAX_DIGITS; L += 64) {
+            if (L >= minL) { s_cnt[L] = 0; s_startv[L] = 0; s_starti[L] = sin; }
+        }
+    }
     __syncthreads();
     TBL_STAMP(10);
-    const int wvt = t >> 6, lnt = t & 63;
-    for (int i0 = 0; i0 < leaves; i0 += 256) {
-        // canonical rank = symbols of the same length before this one (index order):
-        // within the wave by ballot per distinct length, across waves and chunks from counts
-        const int i = i0 + t;
-        const int L = i < leaves ? s_len[i] : 0;
-        const bool coded = i < leaves && L >= minL && L <= maxL && L <= DC_MAX_DIGITS;
-        const int key = coded ? L : -1;
-        uint32_t r_in = 0;
-        uint64_t todo = __ballot(coded);
-        while (todo) {
-            const int L0 = __builtin_amdgcn_readlane(key, __builtin_ctzll(todo));
-            const uint64_t m = __ballot(key == L0);
-            if (key == L0) r_in = (uint32_t)__popcll(m & ((1ull << lnt) - 1));
-            if (lnt == 0) s_wcnt[wvt][L0] = (uint32_t)__popcll(m);
-            todo &= ~m;
-        }
-        __syncthreads();
-        uint32_t rank = r_in;
-        if (coded) {
-            rank += s_rbase[L];
-            for (int q = 0; q < wvt; ++q) rank += s_wcnt[q][L];
-        }
-        __syncthreads();
-        for (int LL = t; LL <= DC_MAX_DIGITS; LL += 256) {
-            s_rbase[LL] += s_wcnt[0][LL] + s_wcnt[1][LL] + s_wcnt[2][LL] + s_wcnt[3][LL];
-            s_wcnt[0][LL] = s_wcnt[1][LL] = s_wcnt[2][LL] = s_wcnt[3][LL] = 0;
-        }
-        __syncthreads();
-        if (i >= leaves) continue;
+    for (int i = t; i < leaves; i += 256) {
+        // canonical rank = symbols of the same length before this one (index order)
+        const int L = s_len[i];
+        const bool coded = L >= minL && L <= topL;
         T->lengths[i] = L;
         if (coded) {
+            const uint32_t *mk = s_mask + (L - 1) * MW;
+            uint32_t rank = (uint32_t)__popc(mk[i >> 5] & ((1u << (i & 31)) - 1u));
+            for (int q = 0; q < (i >> 5); ++q) rank += (uint32_t)__popc(mk[q]);
             const uint32_t val = s_startv[L] + rank;
             T->enc_len[i] = L;
             T->enc_val[i] = val;
@@ -1296,6 +1362,8 @@ static __device__ __forceinline__ void lds_barrier()
 }
 
 #define PACK_TILE 4096
+#define D8_WSCR (2 * 4096 + 66 * 8 + 512)            /* per-wave scratch of the decoders (bytes)  */
+#define D8_SCRATCH_WAVES 4096                        /* waves with a scratch slot (decoders, pack trash rows) */
 #define PACK_STAGE (PACK_TILE + 64)
 #define PACK_BLK_WORDS 9216     /* 36 KiB: a full block of <= 9 bits/symbol is staged whole  */
 #define PACK_PIECES (DC_BLOCK_BYTES / PACK_TILE)
@@ -1409,6 +1477,9 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
 
     // two blocks per workgroup, grid-stride (r1, 1 GiB C2: 16384 workgroups 0.452 ms against
     // 0.481 at 4096, 0.469 at 32768, 0.504 at 1024)
+#ifdef DC_ABL_PACK_NOLOAD
+    uint4 blkv_keep[PACK_PIECES];
+#endif
     for (uint64_t b = bx; b < nblocks; b += gstride) {
         const uint64_t blk_start = b * (uint64_t)DC_BLOCK_BYTES;
         const uint64_t blk_end = (blk_start + DC_BLOCK_BYTES < n) ? blk_start + DC_BLOCK_BYTES : n;
@@ -1419,9 +1490,19 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
             // (loading the next block ahead measured slower every way tried: in extra
             // registers -8% (147 VGPRs), into these registers once pass B is done -4%, into
             // the caches -10%)
+#ifdef DC_ABL_PACK_NOLOAD   // timing ablation only: every block codes the first block's bytes (no loads)
+            if (b == bx) {
+#pragma unroll
+                for (int k = 0; k < (int)(DC_BLOCK_BYTES / PACK_TILE); ++k)
+                    blkv_keep[k] = LD_PACK(reinterpret_cast<const uint4 *>(in + (uint64_t)k * PACK_TILE + (uint64_t)t * 16));
+            }
+#pragma unroll
+            for (int k = 0; k < (int)(DC_BLOCK_BYTES / PACK_TILE); ++k) blkv[k] = blkv_keep[k];
+#else
 #pragma unroll
             for (int k = 0; k < (int)(DC_BLOCK_BYTES / PACK_TILE); ++k)
                 blkv[k] = LD_PACK(reinterpret_cast<const uint4 *>(in + blk_start + (uint64_t)k * PACK_TILE + (uint64_t)t * 16));
+#endif
         }
         const uint64_t s_excl = block_off[b], s_bits = block_off[b + 1] - s_excl;
         const uint64_t blk_abs = bit_base + s_excl;
@@ -1576,6 +1657,10 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
                     // streaming (nt) stores: same-box A/B on 1 GiB C2, pack 0.420 -> 0.382 ms
                     // (the decode after it reads the payload no slower)
                     uint4 *const d4 = reinterpret_cast<uint4 *>(dst + 4 * q);
+#ifdef DC_ABL_PACK_NOSTORE   // timing ablation only: no payload stores (garbage stream)
+                    asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w), "v"(d4));
+                    continue;
+#endif
                     __builtin_nontemporal_store(bswap32(v.x), &d4->x);
                     __builtin_nontemporal_store(bswap32(v.y), &d4->y);
                     __builtin_nontemporal_store(bswap32(v.z), &d4->z);
@@ -1691,6 +1776,301 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
             *reinterpret_cast<uint4 *>(&s_stage[i]) = make_uint4(0u, 0u, 0u, 0u);
         __syncthreads();
     }
+}
+
+// ------------------------------------------------------------------------------------
+// (H7) pack, one wave per contiguous range of blocks: the product path for 16-B aligned
+// output words (k_huff_pack above keeps the byte-map case and unaligned output).
+// Ablations of k_huff_pack on 1 GiB C2 (profiles/r5d_abl.log): without its loads 0.380 ms
+// against 0.381, without its table reads and stage ORs 0.365, with none of loads, stores,
+// table reads or ORs 0.168: it was bound by instruction issue and its per-block phases
+// (a length pass, workgroup scans, three barriers per 32 KiB), not by HBM. Here a wave owns
+// blocks [b0, b1) and streams them 1 KiB at a time (a piece: 16 bytes per lane), with the
+// next 3 pieces' loads in flight:
+//   * every code is looked up ONCE: a lane folds its G codes into a 64-bit accumulator
+//     (acc = acc << len | code) before it knows where they go, so the position scan needs
+//     no separate length pass (a group of > 64 bits is re-coded code by code, rare);
+//   * the piece's bit positions come from one DPP wave scan and a wave-uniform running bit
+//     position: no workgroup barrier anywhere;
+//   * codes are OR-ed into the wave's stage (<= 1024 words per piece + the carried partial
+//     uint4), the complete uint4s leave as nt stores, the partial one moves to the front;
+//   * only the range's first word (shared with the previous range) and its last partial word
+//     (shared with the next) are OR-ed into HBM (k_block_final_wide zeroed both: they hold a
+//     block's first bit, or the stream's last bit).
+// The sync index is written as k_huff_pack writes it. Workgroup 0 builds the decoder tables.
+// ------------------------------------------------------------------------------------
+#define PW_STAGE 1040   /* words per wave: a piece's <= 1024 words + the carried uint4 + OR slack */
+#define PW_WAVES 4096   /* waves of k_huff_pack_w (1 GiB: 8 blocks, 256 KiB each) */
+struct PackWLds {
+    uint2 tab[257];     // code | bits per byte value; [256] = (0, 0): past the stream's end
+    __attribute__((aligned(16))) uint32_t stage[4][PW_STAGE];
+};
+union PackWUnion {
+    PackWLds p;
+    DecBuildLds d;
+};
+
+// the range [x0, x1) of a wave whose codes are all 8 bits (the byte map of k_huff_pack's fixed8
+// path): stream byte bit_base / 8 + i = code(in[i]), bit_base % 128 == 0
+static __device__ __forceinline__ void pack_w_fixed8(const uint8_t *__restrict__ in, uint64_t n, uint64_t x0, uint64_t x1,
+                                                     const uint2 *tab, uint32_t *__restrict__ out,
+                                                     uint64_t *__restrict__ sync_base, uint16_t *__restrict__ sync_len,
+                                                     uint32_t sync_syms, uint64_t bit_base, int lane)
+{
+    uint8_t *const ob = reinterpret_cast<uint8_t *>(out);
+    const uint32_t slog = (uint32_t)__builtin_ctz(sync_syms);
+    for (uint64_t g = x0 + 16u * (uint64_t)lane; g < x1; g += 1024) {
+        if (g + 16 <= x1) {
+            uint4 v = LD_PACK(reinterpret_cast<const uint4 *>(in + g));
+            uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t x = w4[q];
+                w4[q] = tab[x & 255u].x | (tab[(x >> 8) & 255u].x << 8) | (tab[(x >> 16) & 255u].x << 16) |
+                        (tab[x >> 24].x << 24);
+            }
+            st_nt(reinterpret_cast<uint4 *>(ob + g), make_uint4(w4[0], w4[1], w4[2], w4[3]));
+        } else {
+            for (uint64_t i = g; i < x1; ++i) ob[i] = (uint8_t)tab[in[i]].x;
+        }
+    }
+    // the stream's last word: its bytes past the stream are zero (the pad), whatever the buffer held
+    if (x1 == n && lane < 4 && ((n + 3) & ~3ull) > n + (uint64_t)lane) ob[n + lane] = 0;
+    if (sync_len != nullptr) {   // chunks of S symbols: 8 S bits (the last: 8 x its symbols)
+        for (uint64_t c = (x0 >> slog) + (uint64_t)lane; c < ((x1 + sync_syms - 1) >> slog); c += 64) {
+            const uint64_t s0 = c << slog;
+            sync_len[c] = (uint16_t)(8u * (uint32_t)min((uint64_t)sync_syms, n - s0));
+            if ((c & (DC_SYNC_GROUP - 1)) == 0) sync_base[c >> DC_SYNC_GROUP_LOG] = bit_base + 8 * s0;
+        }
+    }
+}
+
+template <int G>   // codes per accumulator: 8, or 4 above 5.5 bits per symbol
+static __device__ __forceinline__ void pack_w_range(const uint8_t *__restrict__ in, uint64_t x0, uint64_t x1,
+                                                    const uint2 *tab, uint32_t *st, uint32_t *__restrict__ out,
+                                                    const uint64_t *__restrict__ block_off, uint64_t b0,
+                                                    uint64_t bit_base, uint64_t *__restrict__ sync_base,
+                                                    uint16_t *__restrict__ sync_len, uint32_t sync_syms, uint64_t n,
+                                                    uint4 *trash, int lane)
+{
+    const uint64_t word_base = bit_base >> 5;
+    const uint32_t slog = sync_syms ? (uint32_t)__builtin_ctz(sync_syms) : 0u;   // S is a power of two
+    const uint32_t cm = sync_syms >> 4;                                           // lanes per sync chunk
+    uint64_t pos = bit_base + block_off[b0];                 // absolute bit of the next code
+    const uint64_t first_w = (pos >> 5) - word_base;         // out-relative: shared with the previous range
+    uint64_t W0 = first_w & ~3ull;                           // out word of stage word 0 (16-B aligned)
+    bool head = true;                                        // stage uint4 0 is the range's first
+
+    // stores of stage words [a, b) to out[W0 + a ..): the range's first word is OR-ed (shared),
+    // words before it are not this range's; everything stored is zeroed in the stage
+    auto store_words = [&](uint32_t a, uint32_t b, bool hd) {
+        for (uint32_t i = a + (uint32_t)lane; i < b; i += 64) {
+            const uint64_t w = W0 + i;
+            const uint32_t v = st[i];
+            st[i] = 0u;
+            if (hd && w < first_w) continue;
+            if (hd && w == first_w) atomicOr(out + w, bswap32(v));
+            else out[w] = bswap32(v);
+        }
+    };
+
+    // Every load and every store below is issued unconditionally, one per piece each (a lane
+    // with nothing to load reads the stream's last full granule, a lane with nothing to store
+    // repeats its wave's last uint4): a wave's vmcnt retires in issue order, and a path with
+    // fewer memory operations makes the compiler's wait for a piece's prefetched granule drain
+    // everything issued since (vmcnt(0)); with one load and one store per piece on every path
+    // that wait is vmcnt(7), and neither the 3 loads behind it nor the stores are waited for.
+    const uint64_t glast = (n - 16) & ~15ull;   // n >= 1024 (the launcher)
+    const uint64_t npf = (x1 - x0) / 1024;      // whole pieces; then at most one partial (the stream's end)
+    auto issue = [&](uint64_t pc) -> uint4 {   // piece pc's granule of this lane
+        const uint64_t g = x0 + pc * 1024 + 16u * (uint64_t)lane;
+        return LD_PACK(reinterpret_cast<const uint4 *>(in + (pc < npf ? g : glast)));
+    };
+    uint4 r0 = issue(0), r1 = issue(1), r2 = issue(2), r3 = issue(3);
+
+    // TAIL: the partial last piece (its bytes loaded one by one, the missing ones coded as the
+    // (0, 0) entry); a separate instance keeps the masking out of the whole pieces
+    auto piece = [&](auto tail_c, uint4 v, uint64_t pc) {
+        constexpr bool tail = decltype(tail_c)::value;
+        const uint64_t xo = x0 + pc * 1024, g = xo + 16u * (uint64_t)lane;
+        uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+        uint32_t cnt = 16;
+        if (tail) {
+            cnt = g >= x1 ? 0u : (uint32_t)min((uint64_t)16, x1 - g);
+            w4[0] = w4[1] = w4[2] = w4[3] = 0u;
+            for (uint32_t i = 0; i < cnt; ++i) w4[i >> 2] |= (uint32_t)in[g + i] << (8 * (i & 3));
+        }
+        // the table index of byte i: past the end, the (0, 0) entry
+        auto idx = [&](int i) -> uint32_t {
+            const uint32_t b = (w4[i >> 2] >> (8 * (i & 3))) & 255u;
+            return (tail && (uint32_t)i >= cnt) ? 256u : b;
+        };
+        constexpr int NG = 16 / G;
+        uint64_t acc[NG];
+        uint32_t tg[NG], tl = 0;
+#pragma unroll
+        for (int q = 0; q < NG; ++q) {
+            uint64_t a = 0;
+            uint32_t s = 0;
+#pragma unroll
+            for (int j = 0; j < G; ++j) {
+                const uint2 e = tab[idx(q * G + j)];
+                a = (a << e.y) | e.x;
+                s += e.y;
+            }
+            acc[q] = a;
+            tg[q] = s;
+            tl += s;
+        }
+        const uint32_t incl = wave_scan_incl(tl), excl = incl - tl;
+        const uint32_t wtot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        if (sync_len != nullptr) {
+            // chunk bits = inclusive scan at the chunk's last lane - exclusive at its first
+            const uint32_t last = (cm == 4) ? (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0xff, 0xf, 0xf, false)
+                                            : (uint32_t)__shfl((int)incl, lane | (int)(cm - 1), 64);
+            if ((g & (uint64_t)(sync_syms - 1)) == 0 && g < x1) {
+                sync_len[g >> slog] = (uint16_t)(last - excl);
+                if ((g & ((uint64_t)sync_syms * DC_SYNC_GROUP - 1)) == 0) sync_base[g >> (slog + DC_SYNC_GROUP_LOG)] = pos + excl;
+            }
+        }
+        // OR a right-justified run of nb <= 64 bits into the stage at bit p (<= 3 words;
+        // branch-free: the words a run does not reach receive 0)
+        auto emit = [&](uint64_t a, uint32_t nb, uint32_t p) {
+            const uint64_t al = a << ((64u - nb) & 63u);
+            const uint32_t hi = (uint32_t)(al >> 32), lo = (uint32_t)al, rr = p & 31u, wi = p >> 5;
+            atomicOr(&st[wi], hi >> rr);
+            atomicOr(&st[wi + 1], __builtin_amdgcn_alignbit(hi, lo, rr));
+            atomicOr(&st[wi + 2], __builtin_amdgcn_alignbit(lo, 0u, rr));
+        };
+        uint32_t rel = (uint32_t)(pos - ((W0 + word_base) << 5)) + excl;   // stage bit of this lane's first code
+#pragma unroll
+        for (int q = 0; q < NG; ++q) {
+            if (tg[q] <= 64u) {
+                emit(acc[q], tg[q], rel);
+            } else {   // more than 64 bits in the group: code by code (each <= 32 bits)
+                uint32_t p = rel;
+#pragma unroll 1
+                for (int j = 0; j < G; ++j) {
+                    const uint2 e = tab[idx(q * G + j)];
+                    emit(e.x, e.y, p);
+                    p += e.y;
+                }
+            }
+            rel += tg[q];
+        }
+        // complete uint4s leave; the partial one moves to the stage front
+        pos += wtot;
+        const uint32_t E = (uint32_t)(((pos >> 5) - word_base) - W0);   // stage words complete: [0, E)
+        const uint32_t nq = E >> 2;
+        const uint32_t q0 = (head && nq > 0) ? 1u : 0u;
+        if (q0) {   // the range's first uint4: word by word (its words before the range are not ours)
+            store_words(0, 4, true);
+            head = false;
+        }
+        {   // uint4s [q0, nq): one store instruction per lane; lanes past nq repeat uint4 nq - 1
+            // (the same bytes to the same address); with none to store, zeros to the trash uint4
+            const uint32_t q = min(q0 + (uint32_t)lane, nq - 1);
+            const bool any = nq > q0;
+            uint4 *const sq = reinterpret_cast<uint4 *>(st) + (any ? q : PW_STAGE / 4 - 1);
+            const uint4 vv = *sq;
+            uint4 *const d4 = any ? reinterpret_cast<uint4 *>(out + W0) + q : trash;
+            __builtin_nontemporal_store(bswap32(vv.x), &d4->x);
+            __builtin_nontemporal_store(bswap32(vv.y), &d4->y);
+            __builtin_nontemporal_store(bswap32(vv.z), &d4->z);
+            __builtin_nontemporal_store(bswap32(vv.w), &d4->w);
+            if (any && q0 + (uint32_t)lane < nq) *sq = make_uint4(0u, 0u, 0u, 0u);
+        }
+        for (uint32_t q = q0 + 64 + (uint32_t)lane; q < nq; q += 64) {   // dense pieces: > 64 uint4
+            uint4 *const sq = reinterpret_cast<uint4 *>(st) + q;
+            const uint4 vv = *sq;
+            *sq = make_uint4(0u, 0u, 0u, 0u);
+            uint4 *const d4 = reinterpret_cast<uint4 *>(out + W0) + q;
+            __builtin_nontemporal_store(bswap32(vv.x), &d4->x);
+            __builtin_nontemporal_store(bswap32(vv.y), &d4->y);
+            __builtin_nontemporal_store(bswap32(vv.z), &d4->z);
+            __builtin_nontemporal_store(bswap32(vv.w), &d4->w);
+        }
+        if (nq > 0) {
+            if (lane < 4) {   // the partial uint4 to the front (LDS ops of a wave complete in order)
+                const uint32_t c = st[4 * nq + lane];
+                st[4 * nq + lane] = 0u;
+                st[lane] = c;
+            }
+            W0 += 4ull * nq;
+        }
+    };
+
+    using whole = std::integral_constant<bool, false>;
+    uint64_t pc = 0;
+    for (; pc + 4 <= npf; pc += 4) {   // 4 pieces per step, each one's granule issued 4 pieces ahead
+        uint4 v = r0; r0 = issue(pc + 4); piece(whole(), v, pc);
+        v = r1; r1 = issue(pc + 5); piece(whole(), v, pc + 1);
+        v = r2; r2 = issue(pc + 6); piece(whole(), v, pc + 2);
+        v = r3; r3 = issue(pc + 7); piece(whole(), v, pc + 3);
+    }
+    if (pc < npf) piece(whole(), r0, pc++);
+    if (pc < npf) piece(whole(), r1, pc++);
+    if (pc < npf) piece(whole(), r2, pc++);
+    if (x1 - x0 > npf * 1024) piece(std::integral_constant<bool, true>(), r3, npf);
+    // the range's last words: complete ones stored, the partial last one OR-ed (shared with
+    // the next range, or the stream's end: zeroed by the plan)
+    const uint32_t E = (uint32_t)(((pos >> 5) - word_base) - W0);
+    store_words(0, E, head);
+    if ((pos & 31) != 0 && lane == 0) {
+        const uint32_t v = st[E];
+        st[E] = 0u;
+        atomicOr(out + W0 + E, bswap32(v));
+    }
+}
+
+__global__ __launch_bounds__(256) void k_huff_pack_w(const uint8_t *__restrict__ in, uint64_t n,
+                                                     const dc_dtable *__restrict__ T,
+                                                     const uint64_t *__restrict__ block_off, uint64_t bit_base,
+                                                     const uint64_t *__restrict__ d_base, uint32_t *__restrict__ out,
+                                                     uint64_t *__restrict__ sync_base, uint16_t *__restrict__ sync_len,
+                                                     uint32_t sync_syms, uint64_t nblocks, uint64_t words_cap,
+                                                     int *__restrict__ err, int build_dec, uint32_t bpw,
+                                                     uint8_t *__restrict__ scratch, int qmode)
+{
+    __shared__ PackWUnion U;
+    const int t = threadIdx.x, lane = t & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
+    if (build_dec && blockIdx.x == 0) {   // workgroup 0: the decoder tables, beside the pack
+        if (T->status == DC_OK) dec_tables_build(const_cast<dc_dtable *>(T), U.d);
+        return;
+    }
+    if (d_base) bit_base += *d_base;   // device-resident shard offset (dist: no host read)
+    // device-side guards (no host round trip), as k_huff_pack: a byte without a code (plan
+    // error) or an output buffer smaller than the planned stream -> write nothing
+    const uint64_t total = block_off[nblocks];
+    if (err[0] != 0) return;
+    if (((bit_base & 31) + total + 31) / 32 > words_cap) {
+        if (t == 0) err[2] = 1;   // (pack status: DC_E_CAPACITY)
+        return;
+    }
+    U.p.tab[t] = make_uint2(T->code[t], T->nbits[t]);
+    if (t == 0) U.p.tab[256] = make_uint2(0u, 0u);
+    uint32_t *const st = U.p.stage[wv];
+    for (int i = lane; i < PW_STAGE / 4; i += 64) reinterpret_cast<uint4 *>(st)[i] = make_uint4(0u, 0u, 0u, 0u);
+    __syncthreads();   // (the only barrier: the table)
+    const uint64_t gw = (uint64_t)(blockIdx.x - build_dec) * 4 + (uint64_t)wv;
+    const uint64_t b0 = gw * bpw;
+    if (b0 >= nblocks) return;
+    const uint64_t b1 = min(b0 + (uint64_t)bpw, nblocks);
+    const uint64_t x0 = b0 * (uint64_t)DC_BLOCK_BYTES, x1 = min(b1 * (uint64_t)DC_BLOCK_BYTES, n);
+    uint4 *const trash = reinterpret_cast<uint4 *>(scratch + (size_t)(gw & (D8_SCRATCH_WAVES - 1)) * D8_WSCR) + lane;
+    if (T->fixed8 && (bit_base & 127) == 0) {
+        pack_w_fixed8(in, n, x0, x1, U.p.tab, out, sync_base, sync_len, sync_syms, bit_base, lane);
+        return;
+    }
+    // quarter mode (uniform), as k_huff_pack: above 5.5 bits per symbol on average groups of 8
+    // codes often exceed 64 bits
+    if (qmode || 2 * total > 11 * n)
+        pack_w_range<4>(in, x0, x1, U.p.tab, st, out, block_off, b0, bit_base, sync_base, sync_len, sync_syms, n, trash,
+                        lane);
+    else
+        pack_w_range<8>(in, x0, x1, U.p.tab, st, out, block_off, b0, bit_base, sync_base, sync_len, sync_syms, n, trash,
+                        lane);
 }
 
 // C5 fused front-end pack: codes the front-end output M of `in` (see the front-end fusion
@@ -2693,8 +3073,6 @@ static __device__ __forceinline__ void d8_issue(uint4 (&v)[NC][5], const D8Geo<N
 #define D8_STATIC_PCT 60
 #define D8_QSTRIDE 1024   /* u32 between heads */
 #define D8_QWORDS (11 * D8_QSTRIDE)
-#define D8_WSCR (2 * 4096 + 66 * 8 + 512)            /* per-wave scratch of the decoders (bytes)  */
-#define D8_SCRATCH_WAVES 4096                        /* waves with a scratch slot (both kernels)  */
 
 struct D8Sched {
     uint32_t Ts, Dh, ntuples;   // static tuples, slice size, all tuples
@@ -6162,7 +6540,8 @@ struct dc_ctx {
     bool plan_ok;
     // tuning options (dc_ctx_set_option; initial values from the environment, read once here)
     uint32_t opt_hist_grid;       // histogram workgroups (0: default 512)
-    uint32_t opt_pack_grid;       // pack workgroups (0: default, two blocks per workgroup)
+    uint32_t opt_pack_grid;       // pack: blocks per wave of k_huff_pack_w (0: default, ~PW_WAVES waves)
+    uint32_t opt_pack_block;      // 2/3: the wave-per-range pack (k_huff_pack_w; 3: 4 codes a lane), A/B
     uint32_t opt_d8_static;       // decoder: static share of the tuples, percent (0..100)
     uint32_t opt_decode_general;  // 1: always the general decoder (k_huff_decode)
     uint32_t opt_hist_pf;         // histogram: blocks of loads in flight ahead (1..2, 0 = default 2)
@@ -6376,8 +6755,12 @@ int dc_ctx_set_option(dc_ctx *c, int option, int64_t value)
         c->opt_adec_v1 = (uint32_t)value;
         return DC_OK;
     case DC_OPT_HIST_PREFETCH:
-        if (value < 0 || value > 2) return DC_E_ARG;
+        if (value < 0 || value > 3) return DC_E_ARG;
         c->opt_hist_pf = (uint32_t)value;
+        return DC_OK;
+    case DC_OPT_PACK_BLOCK:
+        if (value < 0 || value > 3) return DC_E_ARG;
+        c->opt_pack_block = (uint32_t)value;
         return DC_OK;
     default:
         return DC_E_ARG;
@@ -6485,6 +6868,8 @@ static int hist_impl(dc_ctx *c, const uint8_t *d_in, uint64_t n, uint64_t *d_his
     uint32_t *const hdone = c->d_hflag + 512;
     if (c->opt_hist_pf == 1)
         LAUNCH(c, "hist_blocks", k_hist_blocks<1>, grid, 256, d_in, n, nb, c->d_bh, d_hist, hacc, hdone, c->d_hloc, fuse);
+    else if (c->opt_hist_pf == 3)
+        LAUNCH(c, "hist_blocks", k_hist_blocks<3>, grid, 256, d_in, n, nb, c->d_bh, d_hist, hacc, hdone, c->d_hloc, fuse);
     else LAUNCH(c, "hist_blocks", k_hist_blocks<2>, grid, 256, d_in, n, nb, c->d_bh, d_hist, hacc, hdone, c->d_hloc, fuse);
     return DC_OK;
 }
@@ -6694,12 +7079,22 @@ static int pack_impl(dc_ctx *c, const uint8_t *d_in, uint64_t n, const dc_dtable
     // the blocks' offsets, and the boundary words zeroed (the plan's error flags: its slot)
     const int r = plan_offsets(c, plan_err(c), plan_err_next(c), bit_base, d_base, d_words, words_cap);
     if (r != DC_OK) return r;
-    // two blocks per workgroup (grid-stride) + workgroup 0: the decoder tables (k_huff_table
-    // leaves them to the pack's idle CU time)
-    const uint64_t gmax = c->opt_pack_grid ? c->opt_pack_grid : (nb + 1) / 2;
-    const uint64_t grid = nb < gmax ? nb : gmax;
-    LAUNCH(c, "huff_pack", k_huff_pack, grid + 1, 256, d_in, n, d_table, (const uint64_t *)c->d_off, bit_base, d_base,
-           d_words, d_sync_base, d_sync_len, sync_syms, nb, words_cap, plan_err(c), 1);
+    if ((((uintptr_t)d_words) & 15) == 0 && c->opt_pack_block >= 2 && n >= 1024) {   // A/B: 0.386 vs 0.380 ms
+        if (ensure((void **)&c->d_scr, &c->scr_cap, (size_t)D8_SCRATCH_WAVES * D8_WSCR)) return DC_E_HIP;   // trash rows
+        // one wave per range of bpw blocks (k_huff_pack_w): ~PW_WAVES waves, 4 per workgroup,
+        // + workgroup 0: the decoder tables (k_huff_table leaves them to the pack's idle CU time)
+        const uint64_t bpw = c->opt_pack_grid ? c->opt_pack_grid : (nb + PW_WAVES - 1) / PW_WAVES;
+        const uint64_t waves = (nb + bpw - 1) / bpw;
+        LAUNCH(c, "huff_pack", k_huff_pack_w, (waves + 3) / 4 + 1, 256, d_in, n, d_table, (const uint64_t *)c->d_off,
+               bit_base, d_base, d_words, d_sync_base, d_sync_len, sync_syms, nb, words_cap, plan_err(c), 1,
+               (uint32_t)bpw, (uint8_t *)c->d_scr, c->opt_pack_block == 3 ? 1 : 0);
+    } else {
+        // two blocks per workgroup (grid-stride) + workgroup 0: the decoder tables
+        const uint64_t gmax = c->opt_pack_grid ? c->opt_pack_grid : (nb + 1) / 2;
+        const uint64_t grid = nb < gmax ? nb : gmax;
+        LAUNCH(c, "huff_pack", k_huff_pack, grid + 1, 256, d_in, n, d_table, (const uint64_t *)c->d_off, bit_base,
+               d_base, d_words, d_sync_base, d_sync_len, sync_syms, nb, words_cap, plan_err(c), 1);
+    }
     dec_tables_built(c, d_table);   // workgroup 0 built the decoder tables
     return DC_OK;
 }

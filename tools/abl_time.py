@@ -25,11 +25,15 @@ ap.add_argument("--nary", type=int, default=2)
 ap.add_argument("--stage", default="decode")
 ap.add_argument("--iters", type=int, default=20)
 ap.add_argument("--warm", type=int, default=30)
+ap.add_argument("--opt", action="append", default=[], help="context option name=value (repeatable)")
 ap.add_argument("--tag", default=os.path.basename(os.path.dirname(os.environ.get("DC_CORE_LIB", "base/x"))))
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
 x = synth.device_text(a.cfg, a.size, seed=0xC2, device=dev)
 c = Codec(0)
+for o in a.opt:
+    k, v = o.split("=")
+    c.set_option(k, int(v))
 enc = c.encode(x, n_ary=a.nary, sync_syms=64)
 out = torch.empty_like(x)
 
@@ -56,5 +60,5 @@ c.timing(False)
 per = {}
 for name, ms in kt:
     per.setdefault(name, []).append(ms)
-print(json.dumps({"tag": a.tag, "stage": a.stage, "cfg": a.cfg,
+print(json.dumps({"tag": a.tag, "opts": a.opt, "stage": a.stage, "cfg": a.cfg,
                   "kernels": {k: round(float(np.mean(v)), 4) for k, v in per.items()}}), flush=True)
