@@ -275,11 +275,7 @@ __global__ __launch_bounds__(256) void k_hist_blocks(const uint8_t *__restrict__
                         // byte address bin*256 + lane*4 in one v_perm_b32: byte 0 = lane*4,
                         // byte 1 = byte q of the input word, bytes 2-3 = 0
                         const uint32_t addr = __builtin_amdgcn_perm(w4[j], lane4, 0x0c0c0000u | ((4u + q) << 8));
-#ifdef DC_ABL_HIST_NOATOM   // timing ablation only: no LDS counting (wrong histogram)
-                        asm volatile("" ::"v"(addr));
-#else
                         atomicAdd(reinterpret_cast<uint32_t *>(cbase + addr), inc);
-#endif
                     }
                 }
             }
@@ -308,9 +304,6 @@ __global__ __launch_bounds__(256) void k_hist_blocks(const uint8_t *__restrict__
         // 32 KiB block.)
         const uint4 *row = reinterpret_cast<const uint4 *>(&cnt[t * 64]);
         uint32_t acc = 0;
-#ifdef DC_ABL_HIST_NORED   // timing ablation only: no per-block reduction (wrong block histograms)
-        acc = t;
-#else
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
             const uint4 d = row[(k + t) & 15];
@@ -325,7 +318,6 @@ __global__ __launch_bounds__(256) void k_hist_blocks(const uint8_t *__restrict__
                 prevc[4 * k + q] = x;
             }
         }
-#endif
         if (FE) {   // the block's pair starts carry no symbol; block 0 holds the type byte 8
             if (t == 0x20) acc -= s_ps[0] + s_ps[1] + s_ps[2] + s_ps[3];
             if (t == 8 && b == 0) acc += 1u;
@@ -386,16 +378,6 @@ __global__ __launch_bounds__(256) void k_hist_blocks(const uint8_t *__restrict__
 //     leaf for n = 2.
 //   * canonical values (:1540-1568) with the reference's index-M quirks (:1336, :1421).
 // ------------------------------------------------------------------------------------
-#ifdef DC_DIAG
-__device__ unsigned long long g_tbldiag[16];
-extern "C" int dc_diag_tbl_read(void *h)
-{
-    return hipMemcpyFromSymbol(h, HIP_SYMBOL(g_tbldiag), sizeof(g_tbldiag)) == hipSuccess ? 0 : -2;
-}
-#define TBL_STAMP(k) do { __syncthreads(); if (threadIdx.x == 0) g_tbldiag[k] = __builtin_amdgcn_s_memtime(); } while (0)
-#else
-#define TBL_STAMP(k)
-#endif
 #define TBL_SORT_MAX 2048
 #define TBL_NODES 4096
 
@@ -581,7 +563,6 @@ static __device__ void huff_table_body(TblLds &S, const uint64_t *__restrict__ f
 
     const int t = threadIdx.x;
     const int leaves = M + 1;
-    TBL_STAMP(0);
     int w = 0;
     while ((1 << w) < nary) ++w;
 
@@ -607,7 +588,6 @@ static __device__ void huff_table_body(TblLds &S, const uint64_t *__restrict__ f
             s_key[i] = (i < items) ? ((1ull << 11) | (uint64_t)(leaves + (i - k))) : ~0ull;
         for (int i = t; i < TBL_NODES; i += 256) s_parent[i] = 0;
         __syncthreads();
-    TBL_STAMP(1);
         if (items <= 512) {
             // rank sort (keys are distinct: count << 11 | node index): a key's place is the
             // number of keys below it. Every thread reads the same key pair at each step (an
@@ -641,7 +621,6 @@ static __device__ void huff_table_body(TblLds &S, const uint64_t *__restrict__ f
                 }
             }
         }
-        TBL_STAMP(8);
         if (nary <= 32 && t < 64) {
             huff_merge_wave(s_key, s_q2, s_parent, items, nary, leaves + dummies, tree, &s_bad);
         } else if (t == 0) {
@@ -689,7 +668,6 @@ static __device__ void huff_table_body(TblLds &S, const uint64_t *__restrict__ f
             if (t == 0 && next >= TBL_NODES) s_bad = 1;
         }
         __syncthreads();
-    TBL_STAMP(2);
         if (tree) {   // the whole node list (generate_huffman_tree's in-out list, :868-1005)
             const int first_internal = leaves + dummies;
             const int nodes = first_internal + max(items - 1, 0) / max(nary - 1, 1);
@@ -727,7 +705,6 @@ static __device__ void huff_table_body(TblLds &S, const uint64_t *__restrict__ f
     constexpr int MW = DC_MAX_SYMS / 32;
     static_assert(DC_MAX_DIGITS * MW * sizeof(uint32_t) <= sizeof(S.key), "length bitmaps in the key array");
     for (int q = t; q < DC_MAX_DIGITS * MW / 4; q += 256) reinterpret_cast<uint4 *>(s_mask)[q] = make_uint4(0u, 0u, 0u, 0u);
-    TBL_STAMP(3);
     {   // min / max length over i < M: per thread, per wave (DPP-free shuffles), one atomic per wave
         int mx = 0, mnl = 300;
         for (int i = t; i < M; i += 256) {
@@ -752,7 +729,6 @@ static __device__ void huff_table_body(TblLds &S, const uint64_t *__restrict__ f
     }
     for (int s = t; s < 256; s += 256) { s_code[s] = 0; s_nb[s] = 0; }
     __syncthreads();
-    TBL_STAMP(9);
     const int nw = (leaves + 31) >> 5;
     if (t < 64) {
         // per length: cnt = popcount of its bitmap; first slot = exclusive sum of the counts;
@@ -796,7 +772,6 @@ static __device__ void huff_table_body(TblLds &S, const uint64_t *__restrict__ f
         }
     }
     __syncthreads();
-    TBL_STAMP(10);
     for (int i = t; i < leaves; i += 256) {
         // canonical rank = symbols of the same length before this one (index order)
         const int L = s_len[i];
@@ -836,7 +811,6 @@ static __device__ void huff_table_body(TblLds &S, const uint64_t *__restrict__ f
             else { T->last_written = 0; T->enc_len[i] = 0; T->enc_val[i] = 0; }
         }
     }
-    TBL_STAMP(11);
     for (int i = leaves + t; i < DC_MAX_SYMS; i += 256) {
         T->lengths[i] = 0; T->enc_len[i] = 0; T->enc_val[i] = 0;
     }
@@ -865,9 +839,6 @@ static __device__ void huff_table_body(TblLds &S, const uint64_t *__restrict__ f
     const int fixed_any = __syncthreads_or(s_nb[t] == 8u);
     if (t == 0) {
         T->fixed8 = (fixed_ok && fixed_any) ? 1 : 0;
-#ifdef DC_DIAG
-        g_tbldiag[4] = g_tbldiag[7] = __builtin_amdgcn_s_memtime();
-#endif
         T->n_ary = nary;
         T->w = w;
         T->max_symbol_value = M;
@@ -1477,9 +1448,6 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
 
     // two blocks per workgroup, grid-stride (r1, 1 GiB C2: 16384 workgroups 0.452 ms against
     // 0.481 at 4096, 0.469 at 32768, 0.504 at 1024)
-#ifdef DC_ABL_PACK_NOLOAD
-    uint4 blkv_keep[PACK_PIECES];
-#endif
     for (uint64_t b = bx; b < nblocks; b += gstride) {
         const uint64_t blk_start = b * (uint64_t)DC_BLOCK_BYTES;
         const uint64_t blk_end = (blk_start + DC_BLOCK_BYTES < n) ? blk_start + DC_BLOCK_BYTES : n;
@@ -1490,19 +1458,9 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
             // (loading the next block ahead measured slower every way tried: in extra
             // registers -8% (147 VGPRs), into these registers once pass B is done -4%, into
             // the caches -10%)
-#ifdef DC_ABL_PACK_NOLOAD   // timing ablation only: every block codes the first block's bytes (no loads)
-            if (b == bx) {
-#pragma unroll
-                for (int k = 0; k < (int)(DC_BLOCK_BYTES / PACK_TILE); ++k)
-                    blkv_keep[k] = LD_PACK(reinterpret_cast<const uint4 *>(in + (uint64_t)k * PACK_TILE + (uint64_t)t * 16));
-            }
-#pragma unroll
-            for (int k = 0; k < (int)(DC_BLOCK_BYTES / PACK_TILE); ++k) blkv[k] = blkv_keep[k];
-#else
 #pragma unroll
             for (int k = 0; k < (int)(DC_BLOCK_BYTES / PACK_TILE); ++k)
                 blkv[k] = LD_PACK(reinterpret_cast<const uint4 *>(in + blk_start + (uint64_t)k * PACK_TILE + (uint64_t)t * 16));
-#endif
         }
         const uint64_t s_excl = block_off[b], s_bits = block_off[b + 1] - s_excl;
         const uint64_t blk_abs = bit_base + s_excl;
@@ -1525,14 +1483,10 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
             for (int k = 0; k < PACK_PIECES; ++k) {
                 const uint32_t w4[4] = {blkv[k].x, blkv[k].y, blkv[k].z, blkv[k].w};
                 uint32_t s0 = 0, s1 = 0;
-#ifdef DC_ABL_PACK_NOLUT   // timing ablation only: every code 4 bits, no table reads (garbage stream)
-                s0 = 32u + (w4[0] & 0u); s1 = 32u + (w4[3] & 0u);
-#else
 #pragma unroll
                 for (int i = 0; i < 8; ++i) s0 += s_nb8[(w4[i >> 2] >> (8 * (i & 3))) & 255u];
 #pragma unroll
                 for (int i = 8; i < 16; ++i) s1 += s_nb8[(w4[i >> 2] >> (8 * (i & 3))) & 255u];
-#endif
                 Hk[k] = s0;
                 Tk[k] = s0 + s1;
                 __builtin_amdgcn_sched_barrier(0);
@@ -1582,14 +1536,9 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
                 auto emit = [&](uint64_t acc, uint32_t nb, uint32_t pos) {
                     const uint64_t al = acc << ((64u - nb) & 63u);
                     const uint32_t hi = (uint32_t)(al >> 32), lo = (uint32_t)al, r = pos & 31u, wi = pos >> 5;
-#ifdef DC_ABL_PACK_NOOR   // timing ablation only: no stage ORs (garbage stream)
-                    asm volatile("" ::"v"(hi >> r), "v"(__builtin_amdgcn_alignbit(hi, lo, r)),
-                                 "v"(__builtin_amdgcn_alignbit(lo, 0u, r)), "v"(wi));
-#else
                     atomicOr(&s_stage[wi], hi >> r);
                     atomicOr(&s_stage[wi + 1], __builtin_amdgcn_alignbit(hi, lo, r));
                     atomicOr(&s_stage[wi + 2], __builtin_amdgcn_alignbit(lo, 0u, r));
-#endif
                 };
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
@@ -1601,11 +1550,7 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
                         uint64_t acc = 0;
 #pragma unroll
                         for (int i = 8 * h; i < 8 * h + 8; ++i) {
-#ifdef DC_ABL_PACK_NOLUT
-                            const uint2 e = make_uint2((w4[i >> 2] >> (8 * (i & 3))) & 15u, 4u);
-#else
                             const uint2 e = s_tab[(w4[i >> 2] >> (8 * (i & 3))) & 255u];
-#endif
                             acc = (acc << e.y) | e.x;
                         }
                         emit(acc, Th, pos);
@@ -1657,10 +1602,6 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
                     // streaming (nt) stores: same-box A/B on 1 GiB C2, pack 0.420 -> 0.382 ms
                     // (the decode after it reads the payload no slower)
                     uint4 *const d4 = reinterpret_cast<uint4 *>(dst + 4 * q);
-#ifdef DC_ABL_PACK_NOSTORE   // timing ablation only: no payload stores (garbage stream)
-                    asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w), "v"(d4));
-                    continue;
-#endif
                     __builtin_nontemporal_store(bswap32(v.x), &d4->x);
                     __builtin_nontemporal_store(bswap32(v.y), &d4->y);
                     __builtin_nontemporal_store(bswap32(v.z), &d4->z);
@@ -2271,10 +2212,8 @@ __global__ __launch_bounds__(256) void k_fe_pack(const uint8_t *__restrict__ in,
             const uint32_t jj = has ? j0 : 0xFFFFu;
             uint32_t ec = 0, cap = 0;   // symbols seen, bits before the chunk start
             auto tally = [&](uint32_t l) {
-#ifndef DC_DIAG_FE_NOTALLY   // (timing ablation only: wrong sync lengths)
                 ec += l != 0u ? 1u : 0u;
                 cap += ec <= jj ? l : 0u;
-#endif
             };
             uint32_t w4[4] = {blkv[k].x, blkv[k].y, blkv[k].z, blkv[k].w};
             asm volatile("" : "+v"(w4[0]), "+v"(w4[1]), "+v"(w4[2]), "+v"(w4[3]));
@@ -2711,31 +2650,6 @@ static __device__ uint32_t d8_long(uint32_t lo, uint32_t hi, const dc_dtable *__
     return 0u;
 }
 
-#ifdef DC_AB_KERNELS   // multi_entry (k_huff_decode9's table): A/B alternative, diagnostic builds only (tools/diag_build.sh)
-// Multi-symbol lookup table of k_huff_decode9 (built into its LDS by every workgroup): up to
-// 3 whole codes at the start of a DC_MULTI_BITS-bit LSB-first window, by the canonical search
-// of d8_long repeated after each code while the window holds it. Symbols in bytes 0..2 (the
-// first code in byte 0, unused bytes 0), bits 24..27 = their total bit length, bits 28..29 =
-// how many (0: the first code is longer than the window, or invalid).
-#define DC_MULTI_BITS 13
-static __device__ __forceinline__ uint32_t multi_entry(uint32_t x, const dc_dtable *__restrict__ T, int nary, int w,
-                                                       bool pow2)
-{
-    constexpr uint32_t K = DC_MULTI_BITS;
-    uint32_t syms = 0, used = 0, cnt = 0;
-    while (cnt < 3) {
-        int bad = 0;
-        const uint32_t e = d8_long(x >> used, 0u, T, nary, w, pow2, &bad);
-        const uint32_t L = e & 255u;
-        if (bad || L == 0 || used + L > K) break;
-        syms |= ((e >> 8) & 255u) << (8 * cnt);
-        used += L;
-        ++cnt;
-    }
-    return cnt ? syms | (used << 24) | (cnt << 28) : 0u;
-}
-
-#endif  // DC_AB_KERNELS
 
 // any chunk, any count, exact: words read from HBM (MSB-first bytes; reads clamped to the
 // nwords of the buffer), bytes written one by one
@@ -2756,59 +2670,7 @@ static __device__ void d8_chunk_hbm(const uint32_t *__restrict__ in, uint64_t nw
     }
 }
 
-// one batch (4 symbols) of the NC chains of a lane, interleaved symbol by symbol, with no
-// branch: a window whose code is longer than 12 bits reads entry 0 (length 0), so the chain
-// stops advancing and mn[j] records it; such a chunk is decoded again exactly by
-// k_huff_decode8_fix (codes > 12 bits are ~0.13% of the symbols of C2 text, ~8% of chunks).
-// o[j] receives chain j's 4 output bytes.
-template <int NC>
-static __device__ __forceinline__ void d8_batch(const uint32_t *const *st, uint32_t *c, uint32_t *o,
-                                                const uint16_t *__restrict__ lut, uint32_t *mn)
-{
-    // 4 VALU + 1 LDS read per symbol: the window starts one bit early (c is biased by 31
-    // and the words are read from the stage row's base - 1 word: the bit below the chunk's is
-    // a don't-care), so (win >> off) & (2^16 - 2) is the entry's byte address (no index
-    // scaling); the whole
-    // entry (len | sym << 8) is added to off, whose low 6 bits (all v_lshrrev_b64 reads) are
-    // then the bits consumed (the sym bits start at bit 8; the lengths of a batch sum to
-    // < 64, so they never carry into bit 8); an entry of no code is 0 (dlut15 escapes are
-    // zeroed), so min over the entries finds it
-    uint64_t win[NC];
-    uint32_t off[NC];
-#pragma unroll
-    for (int j = 0; j < NC; ++j) {
-        const uint32_t a = c[j] >> 5;
-        const uint32_t *const sm1 = st[j] - 1;
-        const uint32_t w0 = sm1[a], w1 = sm1[a + 1], w2 = sm1[a + 2];
-        win[j] = ((uint64_t)__builtin_amdgcn_alignbit(w2, w1, c[j]) << 32) | __builtin_amdgcn_alignbit(w1, w0, c[j]);
-        off[j] = 0;
-    }
-    const char *const lb = reinterpret_cast<const char *>(lut);
-    // output byte k <- entry byte 1 (v_perm: S0 = entry bytes 4-7, S1 = output bytes 0-3)
-    constexpr uint32_t SEL[4] = {0x0c0c0c05u, 0x0c0c0500u, 0x0c050100u, 0x05020100u};
-    uint32_t e[NC][4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-#pragma unroll
-        for (int j = 0; j < NC; ++j) {
-            const uint32_t x = (uint32_t)(win[j] >> (off[j] & 63u));
-#ifdef DC_DIAG_LUTMASK   // timing ablation only: lookups confined to the first entries
-            e[j][k] = *reinterpret_cast<const uint16_t *>(lb + (x & (2u * DC_DIAG_LUTMASK)));
-#else
-            e[j][k] = *reinterpret_cast<const uint16_t *>(lb + (x & ((2u << D8_LUT_BITS) - 2u)));
-#endif
-            o[j] = __builtin_amdgcn_perm(e[j][k], k ? o[j] : 0u, SEL[k]);
-            off[j] += e[j][k];
-        }
-    }
-#pragma unroll
-    for (int j = 0; j < NC; ++j) {
-        mn[j] = min(mn[j], min(min(e[j][0], e[j][1]), min(e[j][2], e[j][3])));
-        c[j] += off[j] & 255u;
-    }
-}
-
-// Register window of a chain (DC_D8_QWIN, the default): 2 stage qwords q0:q1 in VGPRs and
+// Register window of a chain: 2 stage qwords q0:q1 in VGPRs and
 // the window's bit position qb in them (0..63). A batch's 64-bit window is a funnel shift of
 // q0:q1 (no stage read on the chain); the qword after q1 is read at the batch start, while
 // the 4 lookups run, and when the batch's codes carry qb past 64 it moves in (q0 <- q1 <- it)
@@ -2817,17 +2679,19 @@ static __device__ __forceinline__ void d8_batch(const uint32_t *const *st, uint3
 // about 40% of the kernel's LDS cycles, profiles/r2k_pmc.txt). (An exec-masked read only
 // where a lane needs it measured worse in code: the compiler waited for it inside the branch
 // and the 16 unrolled branches cost 168 VGPRs with spills.)
-#ifndef DC_D8_QWIN
-#define DC_D8_QWIN 1
-#endif
 template <int NC>
 struct D8Win {
     uint64_t q0[NC], q1[NC];
     uint32_t qb[NC], qp[NC];   // bit position in q0:q1, index of the qword after q1
 };
 
-// chain start at stage bit P (a row of 64-bit words, 8-B aligned): the window starts one bit
-// early (d8_batch's bias), i.e. at P' - 64 with P' = P + 63: q0 = qword P'/64 - 1, which for
+// chain start at stage bit P (a row of 64-bit words, 8-B aligned). 4 VALU + 1 LDS read per
+// symbol: the window starts one bit early (the bit below the chunk's is a don't-care), so
+// (win >> off) & (2^16 - 2) is the entry's byte address (no index scaling); the whole entry
+// (len | sym << 8) is added to off, whose low 6 bits (all v_lshrrev_b64 reads) are then the
+// bits consumed (the lengths of a batch sum to < 64, so they never carry into bit 8); an entry
+// of no code is 0 (dlut15 escapes are zeroed), so min over the entries finds it. The window
+// starts at P' - 64 with P' = P + 63: q0 = qword P'/64 - 1, which for
 // P < 1 is the 8 bytes before the row (LDS in bounds: the previous row's tail, or the
 // scheduler word and padding before the first row; a don't-care bit)
 template <int NC>
@@ -2867,11 +2731,7 @@ static __device__ __forceinline__ void d8_batch_q(const uint64_t *const *st, D8W
 #pragma unroll
         for (int j = 0; j < NC; ++j) {
             const uint32_t x = (uint32_t)(win[j] >> (off[j] & 63u));
-#ifdef DC_DIAG_LUTMASK   // timing ablation only: lookups confined to the first entries (conflict free)
-            e[j][k] = *reinterpret_cast<const uint16_t *>(lb + (x & (2u * DC_DIAG_LUTMASK)));
-#else
             e[j][k] = *reinterpret_cast<const uint16_t *>(lb + (x & ((2u << D8_LUT_BITS) - 2u)));
-#endif
             o[j] = __builtin_amdgcn_perm(e[j][k], k ? o[j] : 0u, SEL[k]);
             off[j] += e[j][k];
         }
@@ -2889,6 +2749,8 @@ static __device__ __forceinline__ void d8_batch_q(const uint64_t *const *st, D8W
     }
 }
 
+// The 16 batches of a 64-symbol chunk (4 pieces of 16 B per lane), unrolled by template
+// recursion; the pieces stay in registers until the chunk is done.
 template <int NC, int Q>
 struct D8PiecesQ {
     static __device__ __forceinline__ void run(const uint64_t *const *st, D8Win<NC> &w, uint32_t (*o)[16],
@@ -2904,28 +2766,6 @@ struct D8PiecesQ {
 template <int NC>
 struct D8PiecesQ<NC, 16> {
     static __device__ __forceinline__ void run(const uint64_t *const *, D8Win<NC> &, uint32_t (*)[16],
-                                               const uint16_t *__restrict__, uint32_t *)
-    {
-    }
-};
-
-// The 16 batches of a 64-symbol chunk (4 pieces of 16 B per lane), unrolled by template
-// recursion; the pieces stay in registers until the chunk is done.
-template <int NC, int Q>
-struct D8Pieces {
-    static __device__ __forceinline__ void run(const uint32_t *const *st, uint32_t *c, uint32_t (*o)[16],
-                                               const uint16_t *__restrict__ lut, uint32_t *mn)
-    {
-        uint32_t b[NC];
-        d8_batch<NC>(st, c, b, lut, mn);
-#pragma unroll
-        for (int j = 0; j < NC; ++j) o[j][Q] = b[j];
-        D8Pieces<NC, Q + 1>::run(st, c, o, lut, mn);
-    }
-};
-template <int NC>
-struct D8Pieces<NC, 16> {
-    static __device__ __forceinline__ void run(const uint32_t *const *, uint32_t *, uint32_t (*)[16],
                                                const uint16_t *__restrict__, uint32_t *)
     {
     }
@@ -2957,9 +2797,6 @@ static __device__ __forceinline__ void d8_out(uint32_t *const *stw, const uint32
         for (int s = 0; s < 4; ++s) {
             const uint32_t ch = 16 * s + (lane >> 2), p = lane & 3;
             const uint4 v = rows[ch * 4 + (p ^ ((ch >> 1) & 3))];
-#ifdef DC_DIAG_NOSTORE
-            asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
-#else
             // streaming (nt) stores: the decoded output is not read again here, and written
             // back at once it leaves no dirty lines for the next kernels' reads to evict
             // (1 GiB C2 step, same-box A/B: the next histogram 0.244 -> 0.208 ms, the decode
@@ -2968,21 +2805,10 @@ static __device__ __forceinline__ void d8_out(uint32_t *const *stw, const uint32
             __builtin_nontemporal_store(v.y, &dst[j][s * 64 + lane].y);
             __builtin_nontemporal_store(v.z, &dst[j][s * 64 + lane].z);
             __builtin_nontemporal_store(v.w, &dst[j][s * 64 + lane].w);
-#endif
         }
     }
 }
 
-#ifdef DC_DIAG   // diagnostic build only (tools/diag_build.sh): per-wave s_memtime split
-__device__ unsigned long long g_d8diag[256 * D8_MAX_WAVES * 4];
-extern "C" int dc_diag_read(void *h, size_t bytes)
-{
-    return hipMemcpyFromSymbol(h, HIP_SYMBOL(g_d8diag), bytes) == hipSuccess ? 0 : -2;
-}
-#define D8_STAMP(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
-#else
-#define D8_STAMP(v)
-#endif
 
 typedef __attribute__((address_space(4))) const uint64_t c_u64;   // scalar (s_load) reads
 
@@ -3246,9 +3072,6 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode8(const uint32_t *__rest
     static_assert(D8_LUT_BITS == DC_LUT15_BITS, "table width");
     for (int i = t; i < (1 << D8_LUT_BITS) / 8; i += NT)
         reinterpret_cast<uint4 *>(L.lut)[i] = reinterpret_cast<const uint4 *>(T->dlut15)[i];
-#ifdef DC_DIAG_SYNTH_LUT   // timing ablation only: every window is a 4-bit code (garbage output)
-    for (int i = t; i < (1 << D8_LUT_BITS); i += NT) L.lut[i] = (uint16_t)(4u | ((i & 255u) << 8));
-#endif
     if (t == 0) L.exhausted = 0;
     __syncthreads();
 
@@ -3257,14 +3080,13 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode8(const uint32_t *__rest
     const uint32_t ngroups = (nchunks + DC_SYNC_GROUP - 1) / DC_SYNC_GROUP;
     const uint32_t ntuples = (ngroups + NC - 1) / NC;
     const uint64_t word_base = bit_base >> 5;
-    const uint32_t *st[NC];
     uint32_t *stw[NC];
-#pragma unroll
-    for (int j = 0; j < NC; ++j) { stw[j] = L.stage[wv * NC + j]; st[j] = stw[j]; }
     const uint64_t *st64[NC];
 #pragma unroll
-    for (int j = 0; j < NC; ++j) st64[j] = reinterpret_cast<const uint64_t *>(stw[j]);
-    (void)st64;
+    for (int j = 0; j < NC; ++j) {
+        stw[j] = L.stage[wv * NC + j];
+        st64[j] = reinterpret_cast<const uint64_t *>(stw[j]);
+    }
     const uint32_t stride = gridDim.x * NW;
     // Software pipeline (per wave, one tuple of NC groups per iteration): while tuple i
     // decodes, the spans of tuple i+1 are in flight into registers and the sync index of
@@ -3275,10 +3097,6 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode8(const uint32_t *__rest
     D8Geo<NC> g, cur;
     D8Meta<NC> m1, m2;   // m2: the first tuple's index only
     uint4 v[NC][5];
-#ifdef DC_DIAG
-    unsigned long long d_stage = 0, d_dec = 0, d_slow = 0;
-    D8_STAMP(d_begin);
-#endif
     D8Sched sc;
     sc.ntuples = ntuples;
     sc.P = stride;
@@ -3321,14 +3139,13 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode8(const uint32_t *__rest
     d8_issue<NC>(v, g, in, lane);
     while (tp < ntuples) {
         __builtin_amdgcn_wave_barrier();
-        D8_STAMP(s1);
         uint32_t c[NC];
         uint4 *dst[NC];
 #pragma unroll
         for (int j = 0; j < NC; ++j) {
             // the group's 4 KiB of output (d8_out); a tuple that is not fast (its chunks are
             // all rewritten by the redo) stores into the chain's trash rows instead
-            c[j] = (cur.fast ? cur.lead[j] + cur.off[j] : 0u) + 31u;   // d8_batch's bias
+            c[j] = cur.fast ? cur.lead[j] + cur.off[j] : 0u;   // the chunk's stage bit
             dst[j] = cur.fast ? reinterpret_cast<uint4 *>(out + (uint64_t)(cur.g0 + j) * DC_SYNC_GROUP * S)
                               : trash + j * 256;
         }
@@ -3337,28 +3154,12 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode8(const uint32_t *__rest
         uint32_t o[NC][16], mn[NC];
 #pragma unroll
         for (int j = 0; j < NC; ++j) mn[j] = cur.fast ? 255u : 0u;
-#ifdef DC_DIAG_NODECODE   // timing ablation only: no lookups (the skeleton: spans, stage, output stores)
-#pragma unroll
-        for (int j = 0; j < NC; ++j)
-#pragma unroll
-            for (int q = 0; q < 16; ++q) o[j][q] = c[j] + q;
-#elif DC_D8_QWIN
         {
-            uint32_t P[NC];
-#pragma unroll
-            for (int j = 0; j < NC; ++j) P[j] = c[j] - 31u;   // the chunk's stage bit
             D8Win<NC> wq;
-            d8_win_init<NC>(wq, st64, P);
+            d8_win_init<NC>(wq, st64, c);
             D8PiecesQ<NC, 0>::run(st64, wq, o, L.lut, mn);
         }
-#else
-        D8Pieces<NC, 0>::run(st, c, o, L.lut, mn);
-#endif
         d8_out<NC>(stw, o, dst, lane);
-#ifdef DC_DIAG
-        D8_STAMP(s2);
-        d_dec += s2 - s1;
-#endif
         // chunks with a code of > 12 bits (and every chunk of a tuple that was not fast:
         // partial group, over-long span) are decoded again exactly by k_huff_decode8_fix:
         // a bit per chunk, and for those chunks their bit offset inside the group
@@ -3394,22 +3195,12 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode8(const uint32_t *__rest
         t1 = t2;
         cur = g;
         __builtin_amdgcn_wave_barrier();   // the stage is rewritten
-        D8_STAMP(s4);
         d8_stage<NC>(cur, v, stw, lane);
-#ifdef DC_DIAG
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        D8_STAMP(s5);
-        d_stage += s5 - s4;
-#endif
         d8_geometry<NC>(g, m1, t1, ntuples, n, nchunks, nwords, word_base, lane);
         t2 = d8_resolve(sc, queue, &L.exhausted, lane);
         d8_load_meta<NC>(m1, t2, ngroups, nchunks, lane, sync_len, sync_base);
         d8_fetch(sc, queue, lane);
         d8_issue<NC>(v, g, in, lane);   // after the index loads: waiting for these covers both
-#ifdef DC_DIAG
-        D8_STAMP(s6);
-        d_slow += s6 - s5;   // diag slot 3: geometry + scheduling + issue
-#endif
     }
     if (lane == 0) {
         // a dequeue issued for a tuple past the end may still be in flight: it must land
@@ -3418,223 +3209,8 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode8(const uint32_t *__rest
         if (atomicAdd(queue + 8 * D8_QSTRIDE, 1u) == gridDim.x * NW - 1)
             for (int h = 0; h <= 8; ++h) atomicExch(queue + h * D8_QSTRIDE, 0u);
     }
-#ifdef DC_DIAG
-    D8_STAMP(d_end);
-    if (lane == 0) {
-        unsigned long long *gg = g_d8diag + (blockIdx.x * NW + wv) * 4;
-        unsigned xcc, hwid;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
-        gg[0] = d_end - d_begin; gg[1] = d_stage; gg[2] = d_dec;
-        gg[3] = ((unsigned long long)(xcc & 15) << 56) | ((unsigned long long)(hwid & 0xffff) << 40) | (d_slow & 0xffffffffffull);
-    }
-#endif
 }
 
-#ifdef DC_AB_KERNELS   // k_huff_decode9: A/B alternative, diagnostic builds only (tools/diag_build.sh)
-// ------------------------------------------------------------------------------------
-// (H8) fast decoder, multi-symbol form (S = 64; same schedule, staging, sync index, output
-// layout and redo protocol as k_huff_decode8, one chain per wave). A lookup in the 13-bit
-// multi-symbol table (multi_entry) yields up to 3 whole codes (2.44 per lookup on C2 text, against 1),
-// so a chunk takes ~26 lookups instead of 64: half the LDS table reads, which bound
-// k_huff_decode8 (random 16-bit reads, ~3.5-way bank conflicts). The symbols of a lookup
-// are appended to a 64-bit byte accumulator; its low dword is stored to the lane's LDS
-// output row every lookup (aligned, conflict-free: rows are 17 dwords apart) and the
-// accumulator moves on a dword when one is complete. A code longer than 13 bits (a lookup
-// with no code: ~0.1% of C2 symbols) is taken after the batch through the 12-bit table and
-// its second level (dlut / dlut2, also in LDS); only a code longer than 12 + dlut2_k bits,
-// or a tuple that is not staged, goes to the exact redo (k_huff_decode8_fix).
-// Measured (r2, 1 GiB C2): 0.569 ms + 0.013 redo against k_huff_decode8's 0.454 + 0.099: a
-// wave runs until its slowest lane has its 64 symbols (max ~38 lookups against a mean of 26),
-// and each lookup carries ~20 VALU of output bookkeeping. Kept as DC_OPT_DECODE_VARIANT 1.
-// ------------------------------------------------------------------------------------
-#define D9_ROW 17   /* dwords per output row: 64 bytes + one dword the last lookup may spill into */
-template <int NW>
-struct Dec9Lds {
-    __attribute__((aligned(16))) uint32_t lut[1 << DC_MULTI_BITS];
-    uint16_t dlut[1 << DC_LUT_BITS];
-    uint16_t dlut2[DC_LUT2_CAP];
-    uint32_t exhausted;
-    __attribute__((aligned(16))) uint32_t stage[NW][D8_STAGE_WORDS];
-    uint32_t rows[NW][64 * D9_ROW];
-    uint32_t tail_pad[64];
-};
-
-template <int NW>
-__global__ __launch_bounds__(NW * 64) void k_huff_decode9(const uint32_t *__restrict__ in, uint64_t bit_base, const uint64_t *__restrict__ d_base,
-                                                          const uint64_t *__restrict__ sync_base,
-                                                          const uint16_t *__restrict__ sync_len, uint64_t n,
-                                                          uint64_t nwords, const dc_dtable *__restrict__ T,
-                                                          uint8_t *__restrict__ out, int *__restrict__ err,
-                                                          uint32_t *__restrict__ queue, uint32_t static_pct,
-                                                          uint64_t *__restrict__ fix_mask, uint64_t *__restrict__ fix_pos,
-                                                          uint8_t *__restrict__ scratch)
-{
-    constexpr int NC = 1;
-    constexpr uint32_t S = 64;
-    constexpr int NT = NW * 64;
-    constexpr uint32_t MB = (1u << DC_MULTI_BITS) - 1;
-    __shared__ Dec9Lds<NW> L;
-    if (!__hip_atomic_load(&T->dec_ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {   // tables rebuilt since
-        d8_stale_exit(err, queue, fix_mask, n, NW);
-        return;
-    }
-    if (d_base) bit_base += *d_base;   // device-resident shard offset (dist: no host read)
-    const int t = threadIdx.x, lane = t & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
-    {
-        const int nary = T->n_ary, w = T->w;
-        const bool pow2 = (nary & (nary - 1)) == 0, ok = T->status == DC_OK;
-        for (int x = t; x < (1 << DC_MULTI_BITS); x += NT) L.lut[x] = ok ? multi_entry((uint32_t)x, T, nary, w, pow2) : 0u;
-    }
-    for (int i = t; i < (1 << DC_LUT_BITS) / 8; i += NT)
-        reinterpret_cast<uint4 *>(L.dlut)[i] = reinterpret_cast<const uint4 *>(T->dlut)[i];
-    for (int i = t; i < DC_LUT2_CAP / 4; i += NT)   // dlut2 is 8-B aligned
-        reinterpret_cast<uint2 *>(L.dlut2)[i] = reinterpret_cast<const uint2 *>(T->dlut2)[i];
-    const uint32_t K2 = (uint32_t)T->dlut2_k, kmask = (1u << K2) - 1;
-    if (t == 0) L.exhausted = 0;
-    __syncthreads();
-
-    const uint32_t nchunks = (uint32_t)((n + S - 1) / S);
-    const uint32_t ngroups = (nchunks + DC_SYNC_GROUP - 1) / DC_SYNC_GROUP;
-    const uint32_t ntuples = ngroups;   // one group per tuple
-    const uint64_t word_base = bit_base >> 5;
-    uint32_t *const stw = L.stage[wv];
-    uint32_t *stws[1] = {stw};
-    uint32_t *const row = L.rows[wv] + lane * D9_ROW;   // this lane's output row
-    const uint32_t stride = gridDim.x * NW;
-    D8Geo<NC> g, cur;
-    D8Meta<NC> m1, m2;
-    uint4 v[NC][5];
-    D8Sched sc;
-    sc.ntuples = ntuples;
-    sc.P = stride;
-    sc.wid = blockIdx.x * NW + wv;
-    sc.Ks = (uint32_t)((uint64_t)ntuples * static_pct / 100 / stride);
-    sc.Ts = sc.Ks * stride;
-    sc.Dh = (ntuples - sc.Ts + 7) / 8;
-    sc.k = 0;
-    sc.head = blockIdx.x & 7;
-    sc.tried = 0;
-    sc.pend = 0;
-    d8_fetch(sc, queue, lane);
-    uint32_t tp = d8_resolve(sc, queue, &L.exhausted, lane);
-    d8_fetch(sc, queue, lane);
-    uint32_t t1 = d8_resolve(sc, queue, &L.exhausted, lane);
-    d8_fetch(sc, queue, lane);
-    uint8_t *const wscr = scratch + (size_t)(blockIdx.x * NW + wv) * D8_WSCR;
-    uint4 *const trash = reinterpret_cast<uint4 *>(wscr);
-    uint32_t *const dummy = reinterpret_cast<uint32_t *>(wscr + 2 * 4096);
-    d8_load_meta<NC>(m2, tp, ngroups, nchunks, lane, sync_len, sync_base);
-    d8_geometry<NC>(g, m2, tp, ntuples, n, nchunks, nwords, word_base, lane);
-    d8_issue<NC>(v, g, in, lane);
-    d8_load_meta<NC>(m1, t1, ngroups, nchunks, lane, sync_len, sync_base);
-    cur = g;
-    d8_stage<NC>(cur, v, stws, lane);
-    d8_geometry<NC>(g, m1, t1, ntuples, n, nchunks, nwords, word_base, lane);
-    uint32_t t2 = d8_resolve(sc, queue, &L.exhausted, lane);
-    d8_load_meta<NC>(m1, t2, ngroups, nchunks, lane, sync_len, sync_base);
-    d8_fetch(sc, queue, lane);
-    d8_issue<NC>(v, g, in, lane);
-    while (tp < ntuples) {
-        __builtin_amdgcn_wave_barrier();
-        // ---- decode this lane's chunk of the staged group into its LDS row ----
-        uint32_t c = cur.fast ? cur.lead[0] + cur.off[0] : 0u;   // stage bit of the next code
-        uint32_t wi = 0;                                       // row dword the accumulator starts at
-        uint64_t acc = 0;                                      // pending output bytes (low = next)
-        uint32_t fill = 0;                                     // pending bits in acc (< 32 between lookups)
-        bool redo = !cur.fast;                                 // not staged: every chunk is redone
-        uint32_t wend = redo ? 0u : 16u;                       // dword 16 = the row's spill dword
-        while (__builtin_amdgcn_ballot_w64(wi < wend)) {   // a batch: 4 lookups in one 64-bit window
-            const bool live = wi < wend;
-            const uint32_t a = c >> 5;
-            const uint32_t w0 = stw[a], w1 = stw[a + 1], w2 = stw[a + 2];
-            const uint64_t win = ((uint64_t)__builtin_amdgcn_alignbit(w2, w1, c) << 32) | __builtin_amdgcn_alignbit(w1, w0, c);
-            uint32_t off = 0, e = 0;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {   // 4 x <= 13 bits fit the window
-                e = L.lut[(uint32_t)(win >> off) & MB];
-                acc |= (uint64_t)(e & 0xFFFFFFu) << fill;
-                row[wi] = (uint32_t)acc;
-                fill += (e >> 25) & 0x18u;          // 8 x codes
-                off += (e >> 24) & 15u;             // their bits
-                const uint32_t k32 = fill & 32u;     // a dword is complete
-                acc >>= k32;
-                fill ^= k32;
-                wi = min(wi + (k32 >> 5), wend);
-            }
-            c = live ? c + off : c;
-            // a code longer than 13 bits stops the lane (no code, no bits): take it through the
-            // 12-bit table's escape and its second level (rare: ~0.1% of C2 symbols)
-            const bool esc = live && wi < wend && (e >> 28) == 0u;
-            if (__builtin_amdgcn_ballot_w64(esc)) {
-                if (esc) {
-                    const uint32_t b = c >> 5;
-                    const uint32_t x = __builtin_amdgcn_alignbit(stw[b + 1], stw[b], c);
-                    const uint32_t d = L.dlut[x & ((1u << DC_LUT_BITS) - 1)];
-                    const uint32_t e2 = (K2 && (d & 255u) == 0u)
-                                            ? L.dlut2[min((((d >> 8) & 255u) << K2) | ((x >> DC_LUT_BITS) & kmask),
-                                                          (uint32_t)DC_LUT2_CAP - 1)]
-                                            : 0u;
-                    if ((e2 & 255u) == 0u) {   // longer still, or invalid: the exact redo
-                        redo = true;
-                        wend = wi;
-                    } else {
-                        acc |= (uint64_t)(e2 >> 8) << fill;
-                        row[wi] = (uint32_t)acc;
-                        fill += 8;
-                        c += e2 & 255u;
-                        const uint32_t k32 = fill & 32u;
-                        acc >>= k32;
-                        fill ^= k32;
-                        wi = min(wi + (k32 >> 5), wend);
-                    }
-                }
-            }
-        }
-        // ---- the group's 64 rows -> 4 KiB of contiguous output (16 B per lane per store) ----
-        __builtin_amdgcn_wave_barrier();
-        {
-            uint4 *dst = cur.fast ? reinterpret_cast<uint4 *>(out + (uint64_t)cur.g0 * DC_SYNC_GROUP * S) : trash;
-            const uint32_t *rows = L.rows[wv];
-#pragma unroll
-            for (int s4 = 0; s4 < 4; ++s4) {
-                const uint32_t ch = 16 * s4 + (lane >> 2), p = lane & 3;
-                const uint32_t *r = rows + ch * D9_ROW + 4 * p;
-                dst[s4 * 64 + lane] = make_uint4(r[0], r[1], r[2], r[3]);
-            }
-        }
-        // chunks to redo exactly (as k_huff_decode8: a bit per chunk + its first bit)
-        {
-            const uint32_t gg = cur.g0;
-            const uint64_t m = __ballot(redo);
-            uint64_t *pp = redo ? fix_pos + (uint64_t)gg * DC_SYNC_GROUP + lane : reinterpret_cast<uint64_t *>(dummy) + lane;
-            *pp = (uint64_t)cur.wo[0] * 32 + cur.lead[0] + cur.off[0];
-            uint64_t *mp = gg < ngroups ? fix_mask + gg : reinterpret_cast<uint64_t *>(dummy) + 64;
-            *mp = m;
-            const uint32_t f = (uint32_t)__builtin_ctzll(m | (1ull << 63));   // (as k_huff_decode8)
-            uint64_t *fp = gg < ngroups ? fix_mask + ngroups + gg : reinterpret_cast<uint64_t *>(dummy) + 65;
-            *fp = (uint64_t)cur.wo[0] * 32 + cur.lead[0] + (uint32_t)__builtin_amdgcn_readlane((int)cur.off[0], (int)f);
-        }
-        tp = t1;
-        t1 = t2;
-        cur = g;
-        __builtin_amdgcn_wave_barrier();   // the stage and the rows are rewritten
-        d8_stage<NC>(cur, v, stws, lane);
-        d8_geometry<NC>(g, m1, t1, ntuples, n, nchunks, nwords, word_base, lane);
-        t2 = d8_resolve(sc, queue, &L.exhausted, lane);
-        d8_load_meta<NC>(m1, t2, ngroups, nchunks, lane, sync_len, sync_base);
-        d8_fetch(sc, queue, lane);
-        d8_issue<NC>(v, g, in, lane);
-    }
-    if (lane == 0) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (atomicAdd(queue + 8 * D8_QSTRIDE, 1u) == gridDim.x * NW - 1)
-            for (int h = 0; h <= 8; ++h) atomicExch(queue + h * D8_QSTRIDE, 0u);
-    }
-}
-
-#endif  // DC_AB_KERNELS
 
 // The exact redo's LDS: the 14-bit table, its second level and the canonical tables of longer
 // codes (d8_long's rule), and a span row per lane.
@@ -3708,10 +3284,6 @@ __global__ __launch_bounds__(D8F_WAVES * 64) void k_huff_decode8_fix(const uint3
     __shared__ uint64_t s_pos[D8F_LIST];   // a listed chunk's start when it is its group's first, else ~0
     __shared__ uint32_t s_wsum[D8F_WAVES];
     const int t = threadIdx.x, lane = t & 63, wv = __builtin_amdgcn_readfirstlane(t >> 6);
-    D8_STAMP(f_begin);
-#ifdef DC_DIAG
-    unsigned long long f_list = 0, f_first = 0, f_dec = 0, f_wait = 0, f_rounds = 0;
-#endif
     if (blockIdx.x == 0 && t < 4) err_next[t] = 0;   // the next decode's error slot
     const uint32_t nchunks = (uint32_t)((n + S - 1) / S);
     const uint32_t ngroups = (nchunks + DC_SYNC_GROUP - 1) / DC_SYNC_GROUP;
@@ -3807,9 +3379,6 @@ __global__ __launch_bounds__(D8F_WAVES * 64) void k_huff_decode8_fix(const uint3
                 }
             }
             __syncthreads();
-#ifdef DC_DIAG
-            if (!f_list) f_list = __builtin_amdgcn_s_memtime() - f_begin;
-#endif
             const uint32_t cnt = min(total - part, (uint32_t)D8F_LIST), nrounds = (cnt + 63) / 64;
             auto chunk_of = [&](uint32_t r) -> uint32_t {
                 return r < nrounds && r * 64 + (uint32_t)lane < cnt ? s_list[r * 64 + lane] : ~0u;
@@ -3830,14 +3399,6 @@ __global__ __launch_bounds__(D8F_WAVES * 64) void k_huff_decode8_fix(const uint3
             while (ra < nrounds) {
                 // stage round A's spans, then start round B's spans and round C's positions
                 const uint64_t a0 = row_base(posa);
-#ifdef DC_DIAG
-                D8_STAMP(f_w0);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                D8_STAMP(f_w1);
-                f_wait += f_w1 - f_w0;
-                if (!f_first) f_first = f_w1 - f_begin;
-                ++f_rounds;
-#endif
                 put_row(sv);
                 load_row(sv, row_base(posb));
                 const uint32_t chc = chunk_of(ra + 2 * D8F_WAVES);
@@ -3918,10 +3479,6 @@ __global__ __launch_bounds__(D8F_WAVES * 64) void k_huff_decode8_fix(const uint3
                     }
                 }
                 if (gexp && valid) atomicAdd(gexp + cha / DC_SYNC_GROUP, ex);
-#ifdef DC_DIAG
-                D8_STAMP(f_d1);
-                f_dec += f_d1 - f_w1;
-#endif
                 ra += D8F_WAVES;
                 cha = chb; posa = posb;
                 chb = chc; posb = posc;
@@ -3930,16 +3487,6 @@ __global__ __launch_bounds__(D8F_WAVES * 64) void k_huff_decode8_fix(const uint3
         }
     }
     if (bad) atomicOr(err, 1);
-#ifdef DC_DIAG
-    D8_STAMP(f_end);
-    if (lane == 0 && blockIdx.x < 256) {
-        unsigned long long *gg = g_d8diag + (blockIdx.x * D8F_WAVES + wv) * 4;
-        gg[0] = f_end - f_begin;
-        gg[1] = (f_list & 0xffffffffull) | (f_first << 32);
-        gg[2] = f_dec;
-        gg[3] = (f_rounds & 255) | ((f_wait & ((1ull << 28) - 1)) << 8) | (f_first << 36);
-    }
-#endif
 }
 
 // base64url rendering of a bit range (int2digit alphabet, n_ary_huffman.c:371-378)
@@ -4860,9 +4407,6 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
         uint64_t acc = 0;
         const uint32_t kend = nelem - j0 < 16 ? (uint32_t)(nelem - j0) : 16u;
         const uint32_t valid = fvalid[c];
-#ifdef DC_DIAG_FSMW_NOLOOP   // timing ablation only: no element loop (garbage output)
-        if (M == M_NYB_ENC) { atomicOr(&s_out32[di], (uint32_t)S ^ valid); continue; }
-#endif
         if (M == M_NYB_ENC) {
             // masks of the lane's elements: a hit, and the state before it; an element past the
             // input counts as a hit in state 0 (no bytes)
@@ -5827,198 +5371,7 @@ static __device__ __forceinline__ void adec_flush(uint32_t w, uintptr_t OA, uint
 typedef __attribute__((address_space(4))) const uint32_t c_u32;   // scalar (s_load) reads
 typedef uint32_t u32x32 __attribute__((ext_vector_type(32)));   // the 16 lists as 32 SGPR dwords
 
-#ifdef DC_AB_KERNELS   // k_nyb_resolve: A/B alternative, diagnostic builds only (tools/diag_build.sh)
-// one token -> its byte, with the list touch. The list of context c lives in VGPR lane c
-// (Llo, Hhi); all else is wave-uniform (SGPRs). Move to front (update_context :665-687) of
-// the entry at p (a hit: its rank; a literal: its position, or 7 when absent, so the last
-// entry drops): bytes [0, p] of the new list come from L << 8 (byte 0 then is 0, | v), the
-// rest from L.
-static __device__ __forceinline__ uint32_t adec_step(uint32_t t, uint32_t &Llo, uint32_t &Lhi, uint32_t &ctx,
-                                                     int lane)
-{
-    const uint64_t L = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)Lhi, (int)ctx) << 32) |
-                       (uint32_t)__builtin_amdgcn_readlane((int)Llo, (int)ctx);
-    uint32_t v, p;
-    if (t & 0x80u) {
-        p = t & 7u;
-        v = (uint32_t)(L >> (8u * p)) & 255u;
-    } else {
-        v = t;
-        const uint64_t ones = 0x0101010101010101ull;
-        const uint64_t x = L ^ (ones * v);
-        const uint64_t z = (x - ones) & ~x & (ones << 7);   // the lowest flagged byte is the first match
-        p = z ? (uint32_t)__builtin_ctzll(z) >> 3 : 7u;
-    }
-    const uint64_t keep = 0xFFFFFFFFFFFFFF00ull << (8u * p);   // bytes above p
-    const uint64_t N = (L ^ ((L ^ (L << 8)) & ~keep)) | (uint64_t)v;
-    const bool mine = lane == (int)ctx;
-    Llo = mine ? (uint32_t)N : Llo;
-    Lhi = mine ? (uint32_t)(N >> 32) : Lhi;
-    ctx = (v >> 3) & 15u;
-    return v;
-}
 
-// lane j (an immediate) of dst := val (an SGPR)
-#define ADEC_PUT(dst, val, j) asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(dst) : "s"(val), "i"(j))
-
-// out[0] is the first byte, out[1..n) the tokens of pass 1; all replaced in place
-__global__ __launch_bounds__(64) void k_nyb_resolve(uint8_t *__restrict__ out, uint64_t n)
-{
-    const int lane = (int)threadIdx.x;
-    const uint64_t L0 = mtf_init_word();
-    uint32_t Llo = lane < 16 ? (uint32_t)L0 : 0u, Lhi = lane < 16 ? (uint32_t)(L0 >> 32) : 0u;
-    uint32_t ctx = ((uint32_t)__builtin_amdgcn_readfirstlane((int)out[0]) >> 3) & 15u;
-    // whole 64-byte blocks at 64-B aligned addresses: tokens by scalar loads a block ahead,
-    // bytes assembled at static positions; the bytes before the first and after the last such
-    // block one at a time (a block of tokens in one VGPR, lane = byte)
-    const uint64_t k0 = min((uint64_t)((64 - (((uintptr_t)out + 1) & 63)) & 63) + 1, n);
-    const uint64_t nblk = (n - k0) / 64, k1 = k0 + 64 * nblk;
-    auto edge = [&](uint64_t ka, uint64_t kb) {   // positions [ka, kb), kb - ka < 64
-        if (ka >= kb) return;
-        const uint64_t m = kb - ka;
-        const uint32_t tv = (uint64_t)lane < m ? out[ka + lane] : 0u;
-        uint32_t ov = 0;
-        for (uint32_t i = 0; i < (uint32_t)m; ++i) {
-            const uint32_t v = adec_step((uint32_t)__builtin_amdgcn_readlane((int)tv, (int)i), Llo, Lhi, ctx, lane);
-            ov = lane == (int)i ? v : ov;
-        }
-        if ((uint64_t)lane < m) out[ka + lane] = (uint8_t)ov;
-    };
-    edge(1, k0);
-    if (nblk) {
-        uint32_t T[16], Tn[16];
-        c_u32 *src = (c_u32 *)(out + k0);
-#pragma unroll
-        for (int j = 0; j < 16; ++j) T[j] = src[j];
-        for (uint64_t b = 0; b < nblk; ++b) {
-            c_u32 *nx = (c_u32 *)(out + k0 + 64 * (b + 1 < nblk ? b + 1 : b));
-#pragma unroll
-            for (int j = 0; j < 16; ++j) Tn[j] = nx[j];   // the next block's tokens, in flight
-            uint32_t dw = 0;
-#pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                uint32_t w = 0;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) w |= adec_step((T[j] >> (8 * q)) & 255u, Llo, Lhi, ctx, lane) << (8 * q);
-                ADEC_PUT(dw, w, j);
-            }
-            if (lane < 16) reinterpret_cast<uint32_t *>(out + k0 + 64 * b)[lane] = dw;
-#pragma unroll
-            for (int j = 0; j < 16; ++j) T[j] = Tn[j];
-        }
-    }
-    edge(k1, n);
-}
-
-#endif  // DC_AB_KERNELS
-
-#ifdef DC_AB_KERNELS   // k_nyb_resolve_s: A/B alternative, diagnostic builds only (tools/diag_build.sh)
-// Third form of pass 2 (the product path since r3): the 16 lists stay in SGPRs. They are one
-// wave-uniform vector of 16 u64; the uniform context index selects one by s_movrels_b64 and
-// the touched list goes back by s_movreld_b64 (M0-relative SGPR addressing), so a byte is
-// ~25 scalar instructions with no VALU on its dependency chain. (k_nyb_resolve read the list
-// from VGPR lane c by two v_readlanes and wrote it back by two per-lane selects: ~190 cycles
-// per byte, 12.4 MB/s.) Tokens by scalar loads a 64-B block ahead; the block's 64 bytes are
-// gathered into one VGPR (v_writelane, immediate lane) and leave as 16 dwords.
-typedef uint64_t u64x16 __attribute__((ext_vector_type(16)));
-
-static __device__ __forceinline__ uint32_t adec_step_s(uint32_t t, u64x16 &lists, uint32_t &ctx)
-{
-    const uint64_t L = lists[ctx];
-    const uint64_t ones = 0x0101010101010101ull;
-    const uint32_t ph = t & 7u;
-    const uint32_t vh = (uint32_t)(L >> (8u * ph)) & 255u;       // a hit: the byte at its rank
-    const uint64_t x = L ^ (ones * (uint64_t)t);
-    const uint64_t z = (x - ones) & ~x & (ones << 7);              // a literal: its first match
-    const uint32_t pl = z ? (uint32_t)__builtin_ctzll(z) >> 3 : 7u;   // (absent: the last drops)
-    const bool hit = (t & 0x80u) != 0;
-    const uint32_t v = hit ? vh : t, p = hit ? ph : pl;
-    const uint64_t keep = 0xFFFFFFFFFFFFFF00ull << (8u * p);      // bytes above p stay
-    lists[ctx] = (L ^ ((L ^ (L << 8)) & ~keep)) | (uint64_t)v;    // move to front (:665-687)
-    ctx = (v >> 3) & 15u;
-    return v;
-}
-
-// The exact step (the reference's search for a literal in its list) over the 16 lists as 32
-// dwords. r3's first form pinned them in s[64:95] and touched them M0-relative in inline asm
-// (s_movrels / s_movreld, ~28 SALU per byte, 16.3 MB/s); the fast resolve below keeps that
-// addressing. Two things learnt there: a 64-bit constant handed to the asm as an "s" operand
-// (0xFFFFFFFFFFFFFF00) became s_mov_b64 with a 32-bit literal that the hardware zero-extends,
-// so masks are made from the inline constant -1 (tools/ubench/adec_asm.hip traced it); and
-// fixed scratch pairs must avoid s100-s101, which gfx950 reserves (compiler-chosen operands).
-static __device__ __forceinline__ uint32_t adec_step_asm(uint32_t t, u32x32 &lists, uint32_t &ctx, uint64_t h80)
-{
-    // (the exact step, also the fast resolve's fallback: plain code, the lists indexed by the
-    // uniform context; a hand-scheduled form with fixed scratch pairs clobbered s100-s101,
-    // which gfx950 reserves)
-    const uint64_t L = ((uint64_t)lists[2 * ctx + 1] << 32) | lists[2 * ctx];
-    const uint64_t ones = 0x0101010101010101ull;
-    const uint32_t ph = t & 7u;
-    const uint32_t vh = (uint32_t)(L >> (8u * ph)) & 255u;
-    const uint64_t x = L ^ (ones * (uint64_t)t);
-    const uint64_t z = (x - ones) & ~x & h80;
-    const uint32_t pl = z ? (uint32_t)__builtin_ctzll(z) >> 3 : 7u;
-    const bool hit = (t & 0x80u) != 0;
-    const uint32_t v = hit ? vh : t, p = hit ? ph : pl;
-    const uint64_t keep = (~0ull << (8u * p)) << 8;              // bytes above p stay
-    const uint64_t N = (L ^ ((L ^ (L << 8)) & ~keep)) | (uint64_t)v;   // move to front (:665-687)
-    lists[2 * ctx] = (uint32_t)N;
-    lists[2 * ctx + 1] = (uint32_t)(N >> 32);
-    ctx = (v >> 3) & 15u;
-    return v;
-}
-// out[0] is the first byte, out[1..n) the tokens of pass 1; all replaced in place
-__global__ __launch_bounds__(64) void k_nyb_resolve_s(uint8_t *__restrict__ out, uint64_t n)
-{
-    const int lane = (int)threadIdx.x;
-    const uint64_t h80 = 0x8080808080808080ull;
-    u32x32 lists;
-#pragma unroll
-    for (int c = 0; c < 16; ++c) {
-        lists[2 * c] = (uint32_t)mtf_init_word();
-        lists[2 * c + 1] = (uint32_t)(mtf_init_word() >> 32);
-    }
-    uint32_t ctx = ((uint32_t)__builtin_amdgcn_readfirstlane((int)out[0]) >> 3) & 15u;
-    const uint64_t k0 = min((uint64_t)((64 - (((uintptr_t)out + 1) & 63)) & 63) + 1, n);
-    const uint64_t nblk = (n - k0) / 64, k1 = k0 + 64 * nblk;
-    auto edge = [&](uint64_t ka, uint64_t kb) {   // positions [ka, kb), kb - ka < 64
-        if (ka >= kb) return;
-        const uint64_t m = kb - ka;
-        const uint32_t tv = (uint64_t)lane < m ? out[ka + lane] : 0u;
-        uint32_t ov = 0;
-        for (uint32_t i = 0; i < (uint32_t)m; ++i) {
-            const uint32_t v = adec_step_asm((uint32_t)__builtin_amdgcn_readlane((int)tv, (int)i), lists, ctx, h80);
-            ov = lane == (int)i ? v : ov;
-        }
-        if ((uint64_t)lane < m) out[ka + lane] = (uint8_t)ov;
-    };
-    edge(1, k0);
-    if (nblk) {
-        uint32_t T[16], Tn[16];
-        c_u32 *src = (c_u32 *)(out + k0);
-#pragma unroll
-        for (int j = 0; j < 16; ++j) T[j] = src[j];
-        for (uint64_t b = 0; b < nblk; ++b) {
-            c_u32 *nx = (c_u32 *)(out + k0 + 64 * (b + 1 < nblk ? b + 1 : b));
-#pragma unroll
-            for (int j = 0; j < 16; ++j) Tn[j] = nx[j];   // the next block's tokens, in flight
-            uint32_t dw = 0;
-#pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                uint32_t w = 0;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) w |= adec_step_asm((T[j] >> (8 * q)) & 255u, lists, ctx, h80) << (8 * q);
-                ADEC_PUT(dw, w, j);
-            }
-            if (lane < 16) reinterpret_cast<uint32_t *>(out + k0 + 64 * b)[lane] = dw;
-#pragma unroll
-            for (int j = 0; j < 16; ++j) T[j] = Tn[j];
-        }
-    }
-    edge(k1, n);
-}
-
-#endif  // DC_AB_KERNELS
 
 // Fourth form (the product path since r3b): what a token gives without the lists is
 // computed beforehand, in parallel (k_nyb_adec_ctl, one dword per token), and the sequential
@@ -6203,126 +5556,165 @@ __global__ __launch_bounds__(64) void k_nyb_resolve_c(uint8_t *__restrict__ out,
     }
 }
 
-#ifdef DC_AB_KERNELS   // k_nyb_adec: the one-pass decoder, A/B only
-__global__ __launch_bounds__(64) void k_nyb_adec(const uint8_t *__restrict__ in, uint64_t len,
-                                                 uint8_t *__restrict__ out, uint64_t *__restrict__ meta)
+
+
+// ---- one lane per stream (DCNK chunks, dc_nyb_decompress_batch) ----------------------
+// A lane walks its own stream byte by byte (the lists make every byte depend on the one
+// before), and a launch has one wave per 64 streams: 4 waves per CU on 65536 streams of 4 KiB.
+// r4's loops read in[pos] and wrote out[q] one byte at a time: a dependent global round trip
+// per input byte (~1.4 us: 46.6 GB/s) and byte stores to 64 private lines per wave (22.7x the
+// output in HBM writes). Here a lane's memory traffic moves only at IO points the whole wave
+// reaches together, so no step of the byte loop waits on memory:
+//  * input the lane reads exactly one byte per step of (the encoder, the length pass) is walked
+//    in 16-B granules, 8 per round, the next round's 8 loads in flight (nl_walk);
+//  * input the lane reads at its own rate (the decoder: 0.5-1 byte per output byte) sits in an
+//    LDS ring of NL_RING bytes per lane, topped up 64 B at a time at the IO points, with the
+//    next 64 B always in flight in registers (nyb_wave_decode);
+//  * output gathers in an LDS ring of two 64-B lines per lane and leaves as whole lines (4 x
+//    16 B) at the IO points; the line the stream shares with the bytes before it waits in LDS
+//    and goes byte by byte at the end, with the last partial line (NlOut).
+#define NL_RING 256    /* decoder input ring per lane (bytes) */
+#define NL_RSTR 272    /* its LDS row stride: 16-B aligned, lanes' rows 4 banks apart */
+#define NL_ORING 128   /* output ring per lane: the line being gathered and the next */
+#define NL_OSTR 144
+#define NL_HSTR 80     /* the head line's row */
+#define NL_P 32        /* decoder steps between two IO points (<= 32 bytes in, <= 32 out) */
+__device__ uint4 nl_zero[1];   // the granule lanes without a stream read (never written)
+// (granule pointers are formed as p - (p & 15), never through an integer: a pointer rebuilt from
+// a uintptr_t made the compiler emit flat loads, which also count in lgkmcnt, so every LDS wait
+// of the byte loop waited for the granules in flight)
+static __device__ __forceinline__ uint4 nl_ld(const uint4 *p) { return *p; }
+
+struct NlOut {        // a lane's output [b + sh, ...): b = the start rounded down to 64 B
+    uint8_t *b;
+    uint32_t sh;
+    uint64_t S;       // next line to send (offset from b, a multiple of 64)
+    bool head;        // line 0 holds bytes before the stream: kept in hrow, sent byte by byte
+    uint8_t *ring, *hrow;
+};
+static __device__ __forceinline__ void nl_out_init(NlOut &o, uint8_t *dst, uint8_t *ring, uint8_t *hrow)
 {
-    const int lane = (int)threadIdx.x;
-    const uint64_t L0 = mtf_init_word();
-    uint32_t Llo = lane < 16 ? (uint32_t)L0 : 0u, Lhi = lane < 16 ? (uint32_t)(L0 >> 32) : 0u;
-    const uintptr_t ib = (uintptr_t)in, ie = ib + len, ob = (uintptr_t)out;
-    uintptr_t A = (ib + 2) & ~(uintptr_t)255;   // input window base (pos >= 2)
-    uint32_t win = adec_load(A, ib, ie, lane), winN = adec_load(A + 256, ib, ie, lane);
-    // output: out[0] = in[1]
-    const uint32_t first = (uint32_t)__builtin_amdgcn_readfirstlane((int)in[1]);
-    uintptr_t OA = ob & ~(uintptr_t)255;
-    uint32_t ow = 0;
-    uint64_t o = 0;
-    uint32_t acc = 0;   // output bytes of the current dword (bytes below ob + o's lane offset)
-    auto put = [&](uint32_t v) {
-        const uintptr_t a = ob + o;
-        if (a - OA >= 256) {   // window complete: store it, start the next
-            adec_flush(ow, OA, ob, a, lane);
-            OA += 256;
-            ow = 0;
-        }
-        const uint32_t sh = 8u * (uint32_t)(a & 3);
-        acc = (sh ? acc : 0u) | (v << sh);
-        ow = writelane(ow, (uint32_t)__builtin_amdgcn_readfirstlane((int)acc), (uint32_t)((a - OA) >> 2));
-        ++o;
-    };
-    put(first);
-    uint32_t pv = first;
-    uint64_t pos = 2;
-    uint32_t off = 0;
-    while (pos < len) {
-        const uintptr_t ap = ib + pos;
-        if (ap - A >= 256) {   // next input window; the one after it starts loading
-            A += 256;
-            win = winN;
-            winN = adec_load(A + 256, ib, ie, lane);
-        }
-        const uint32_t rel = (uint32_t)(ap - A);
-        const uint32_t b = ((uint32_t)__builtin_amdgcn_readlane((int)win, (int)(rel >> 2)) >> (8 * (ap & 3))) & 255u;
-        uint32_t nyb, nxt = b & 15u;
-        if (off == 0) {
-            nyb = b >> 4;
-        } else {
-            nyb = b & 15u;
-            nxt = 0;
-            if (pos + 1 < len) {
-                const uintptr_t an = ap + 1;
-                const uint32_t rn = (uint32_t)(an - A);
-                const uint32_t dw = rn < 256 ? (uint32_t)__builtin_amdgcn_readlane((int)win, (int)(rn >> 2))
-                                             : (uint32_t)__builtin_amdgcn_readlane((int)winN, (int)((rn - 256) >> 2));
-                nxt = ((dw >> (8 * (an & 3))) & 255u) >> 4;
-            }
-        }
-        const int c = (int)((pv >> 3) & 15u);
-        uint64_t L = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)Lhi, c) << 32) |
-                     (uint32_t)__builtin_amdgcn_readlane((int)Llo, c);
-        uint32_t v, used;
-        if (nyb & 8u) { v = (uint32_t)(L >> (8 * (nyb & 7u))) & 255u; used = 1; }
-        else { v = ((nyb & 7u) << 4) + nxt; used = 2; }
-        uint32_t cnt = 8;
-        (void)mtf_touch64(L, cnt, v);
-        Llo = writelane(Llo, (uint32_t)L, (uint32_t)c);
-        Lhi = writelane(Lhi, (uint32_t)(L >> 32), (uint32_t)c);
-        put(v);
-        pv = v;
-        off += used;
-        if (off >= 2) { ++pos; off -= 2; }
-    }
-    adec_flush(ow, OA, ob, ob + o, lane);
-    if (lane == 0) meta[0] = o;
+    o.sh = (uint32_t)((uintptr_t)dst & 63);
+    o.b = dst - o.sh;
+    o.S = 0;
+    o.head = false;
+    o.ring = ring;
+    o.hrow = hrow;
 }
-#endif  // DC_AB_KERNELS
+// W = offset from b past the last byte put: send the line it completed (one per point at most)
+static __device__ __forceinline__ void nl_out_point(NlOut &o, uint64_t W)
+{
+    if (W >= o.S + 64) {
+        const uint4 *src = reinterpret_cast<const uint4 *>(o.ring + (o.S & (NL_ORING - 1)));
+        const uint4 v0 = src[0], v1 = src[1], v2 = src[2], v3 = src[3];
+        if (o.S < o.sh) {
+            uint4 *h = reinterpret_cast<uint4 *>(o.hrow);
+            h[0] = v0; h[1] = v1; h[2] = v2; h[3] = v3;
+            o.head = true;
+        } else {
+            uint4 *d = reinterpret_cast<uint4 *>(o.b + o.S);
+            d[0] = v0; d[1] = v1; d[2] = v2; d[3] = v3;
+        }
+        o.S += 64;
+    }
+}
+static __device__ __forceinline__ void nl_out_finish(const NlOut &o, uint64_t W)
+{
+    for (uint64_t a = o.S > o.sh ? o.S : o.sh; a < W; ++a) o.b[a] = o.ring[a & (NL_ORING - 1)];
+    if (o.head)
+        for (uint32_t a = o.sh; a < 64; ++a) o.b[a] = o.hrow[a];
+}
 
+// Lockstep walk of bytes [lo, hi) of a lane's granules g (offsets from g; every lane of the
+// wave calls it, lanes without bytes with g = nl_zero, lo = hi = 0): fn(byte, valid) per byte
+// in order, point() after every granule. 8 granules a round, the next round's in flight.
+template <class Fn, class Pt>
+static __device__ __forceinline__ void nl_walk(const uint4 *g, uint64_t lo, uint64_t hi, Fn fn, Pt point)
+{
+    const uint64_t k0 = lo >> 4, k1 = hi > lo ? (hi - 1) >> 4 : k0;
+    const bool any = hi > lo;
+    uint4 G[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) G[j] = nl_ld(g + min(k0 + (uint64_t)j, k1));
+    for (uint64_t k = k0; __ballot(any && k <= k1); k += 8) {
+        uint4 N[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) N[j] = nl_ld(g + min(k + 8 + (uint64_t)j, k1));
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int64_t base = (int64_t)(16 * (k + j));
+            const int64_t vlo = (int64_t)lo - base, vhi = (any ? (int64_t)hi : 0) - base;   // valid bytes [vlo, vhi)
+            const uint32_t w[4] = {G[j].x, G[j].y, G[j].z, G[j].w};
+#pragma unroll
+            for (int e = 0; e < 16; ++e) fn((w[e >> 2] >> (8 * (e & 3))) & 255u, e >= vlo && e < vhi);
+            point();
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) G[j] = N[j];
+    }
+}
 
+// DCNK encode: one lane per chunk of K bytes, nybble_compress of the chunk
+// (compress_bytestring, nybble_compression.c:887-1038) into its scratch slot of K + 2 bytes
 __global__ __launch_bounds__(64) void k_nyb_chunk_enc(const uint8_t *__restrict__ in, uint64_t n, uint32_t K,
                                                       uint64_t nchunks, int modify, uint8_t *__restrict__ scr,
                                                       uint64_t *__restrict__ lens)
 {
     __shared__ uint64_t s_L[16][64];
+    __shared__ __attribute__((aligned(16))) uint8_t s_out[64 * NL_OSTR];
+    __shared__ __attribute__((aligned(16))) uint8_t s_head[64 * NL_HSTR];
     const int t = threadIdx.x;
     const uint64_t ch = (uint64_t)blockIdx.x * 64 + t;
-    if (ch >= nchunks) return;
-    const uint8_t *x = in + ch * K;
-    const uint64_t len = (n - ch * K < K) ? n - ch * K : K;
-    uint8_t *out = scr + ch * ((uint64_t)K + 2);
+    const bool live = ch < nchunks;
+    const uint8_t *x = in + (live ? ch * K : 0);
+    const uint64_t len = live ? ((n - ch * K < K) ? n - ch * K : K) : 0;
+    uint8_t *const slot = scr + (live ? ch * ((uint64_t)K + 2) : 0);
     for (int c = 0; c < 16; ++c) s_L[c][t] = mtf_init_word();
-    uint64_t o = 0;
-    out[o++] = 0xAF;
-    uint32_t prev = x[0];
-    out[o++] = (uint8_t)prev;
+    NlOut o;
+    nl_out_init(o, slot, s_out + t * NL_OSTR, s_head + t * NL_HSTR);
+    uint64_t q = 0;   // bytes put
+    auto put = [&](uint32_t v) { o.ring[(o.sh + q) & (NL_ORING - 1)] = (uint8_t)v; ++q; };
+    uint32_t prev = len ? x[0] : 0u;
+    if (len) { put(0xAF); put(prev); }
     int half = 0;
     uint32_t hi = 0;   // pending high nybble (with its byte's value, for a later rewrite)
-    for (uint64_t i = 1; i < len; ++i) {
-        const uint32_t v = x[i];
-        const uint32_t c = (prev >> 3) & 15u;
-        uint64_t L = s_L[c][t];
-        uint32_t cnt = 8;
-        const int r = mtf_touch64(L, cnt, v);   // compress_byte_index :833-839 (rank before the touch)
-        if (modify) s_L[c][t] = L;              // update_context :665-687
-        if (r < 0) {
-            if (half) { out[o++] = (uint8_t)prev; half = 0; }   // miss at offset 1 (:855-857)
-            out[o++] = (uint8_t)v;
-        } else if (!half) {
-            hi = (8u | (uint32_t)r) << 4;
-            half = 1;
-        } else {
-            out[o++] = (uint8_t)(hi | 8u | (uint32_t)r);
-            half = 0;
-        }
-        prev = v;
+    const uintptr_t xa = (uintptr_t)x;
+    const uint4 *g = len > 1 ? reinterpret_cast<const uint4 *>(x - (xa & 15)) : nl_zero;
+    const uint64_t sh = len > 1 ? xa & 15 : 0;
+    nl_walk(g, len > 1 ? sh + 1 : 0, len > 1 ? sh + len : 0,
+        [&](uint32_t v, bool valid) {
+            if (valid) {
+                const uint32_t c = (prev >> 3) & 15u;
+                uint32_t pb;
+                bool hit;
+                // compress_byte_index :833-839 (rank before the touch), update_context :665-687
+                const uint64_t L = mtf_touch8(s_L[c][t], v, pb, hit);
+                if (modify) s_L[c][t] = L;
+                const int r = hit ? (int)(pb >> 3) : -1;
+                if (r < 0) {
+                    if (half) { put(prev); half = 0; }   // miss at offset 1 (:855-857)
+                    put(v);
+                } else if (!half) {
+                    hi = (8u | (uint32_t)r) << 4;
+                    half = 1;
+                } else {
+                    put(hi | 8u | (uint32_t)r);
+                    half = 0;
+                }
+                prev = v;
+            }
+        },
+        [&]() { nl_out_point(o, o.sh + q); });
+    if (half) put(prev);   // odd tail (:1000-1009): the last byte raw
+    if (live && q >= len) {   // LITERAL fallback (:1018-1037): the slot rewritten, byte by byte (rare)
+        slot[0] = ' ';
+        for (uint64_t i = 0; i < len; ++i) slot[1 + i] = x[i];
+        q = len + 1;
+    } else if (live) {
+        nl_out_point(o, o.sh + q);
+        nl_out_finish(o, o.sh + q);
     }
-    if (half) out[o++] = x[len - 1];   // odd tail (:1000-1009)
-    if (o >= len) {                    // LITERAL fallback (:1018-1037)
-        out[0] = ' ';
-        for (uint64_t i = 0; i < len; ++i) out[1 + i] = x[i];
-        o = len + 1;
-    }
-    lens[ch] = o;
+    if (live) lens[ch] = q;
 }
 
 // single workgroup: off[0..nchunks] = exclusive scan of lens (off[nchunks] = total)
@@ -6334,7 +5726,15 @@ __global__ __launch_bounds__(1024) void k_scan_u64(const uint64_t *__restrict__ 
     const uint64_t per = (count + 1023) / 1024;
     const uint64_t a0 = (uint64_t)t * per, a1 = (a0 + per < count) ? a0 + per : count;
     uint64_t sum = 0;
-    for (uint64_t k = a0; k < a1; ++k) sum += lens[k];
+    uint64_t k = a0;   // 8 loads in flight per round (one round trip per count made it latency-bound)
+    for (; k + 8 <= a1; k += 8) {
+        uint64_t v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = lens[k + j];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sum += v[j];
+    }
+    for (; k < a1; ++k) sum += lens[k];
     s[t] = sum;
     __syncthreads();
     for (int d = 1; d < 1024; d <<= 1) {
@@ -6344,7 +5744,14 @@ __global__ __launch_bounds__(1024) void k_scan_u64(const uint64_t *__restrict__ 
         __syncthreads();
     }
     uint64_t o = t ? s[t - 1] : 0;
-    for (uint64_t k = a0; k < a1; ++k) { off[k] = o; o += lens[k]; }
+    for (k = a0; k + 8 <= a1; k += 8) {
+        uint64_t v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = lens[k + j];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { off[k + j] = o; o += v[j]; }
+    }
+    for (; k < a1; ++k) { off[k] = o; o += lens[k]; }
     if (t == 1023) off[count] = s[1023];
 }
 
@@ -6358,70 +5765,109 @@ __global__ __launch_bounds__(256) void k_nyb_chunk_copy(const uint8_t *__restric
     for (uint64_t i = threadIdx.x; i < len; i += 256) payload[a + i] = src[i];
 }
 
-// one lane per chunk: decompress_bytestring (nybble_compression.c:734-817) of the chunk's
-// stream into out + ch*K; a stream that is not a nybble/LITERAL stream of exactly the chunk's
-// length sets *err (bytes >= 0x80 do not round-trip through the reference codec, P8)
 // One lane decodes one whole reference stream (decompress_bytestring, nybble_compression.c:
-// 734-817) of m bytes into exactly `expect` bytes at o; its 16 move-to-front lists are its
-// column of sL (LDS, 8 KiB per 64 lanes). Type dispatch (:744, :799, :806): 0xAF nybbles,
-// ' ' the raw bytes after it, any other type byte (any_type; DCNK chunks are never written so)
-// every byte including the type byte. False: the stream does not decode to `expect` bytes.
-static __device__ bool nyb_lane_decode(const uint8_t *__restrict__ src, uint64_t m, uint64_t expect, int modify,
-                                       bool any_type, uint8_t *__restrict__ o, uint64_t (*sL)[64], int t)
+// 734-817) of m bytes at src into exactly `expect` bytes at o (every lane of the wave calls
+// it; lanes without a stream pass live = false). Type dispatch (:744, :799, :806): 0xAF
+// nybbles, ' ' the raw bytes after it, any other type byte (any_type; DCNK chunks are never
+// written so) every byte including the type byte. Returns false when the stream does not
+// decode to `expect` bytes. One output byte per step: the raw byte 1 of a nybble stream, then
+// a token each (a nybble with bit 3 set: a hit, its rank; any other: a literal of 2 nybbles).
+static __device__ __forceinline__ bool nyb_wave_decode(const uint8_t *__restrict__ src, uint64_t m, uint64_t expect, int modify,
+                                       bool any_type, uint8_t *__restrict__ o, bool live, uint64_t (*sL)[64],
+                                       uint8_t *ring, uint8_t *oring, uint8_t *hrow, int t)
 {
-    if (m == 0) return expect == 0;
-    const uint32_t type = src[0];
-    if (type == ' ') {
-        if (m - 1 != expect) return false;
-        for (uint64_t i = 1; i < m; ++i) o[i - 1] = src[i];
-        return true;
+    if (!live) m = 0;
+    // the input ring: ring[F - NL_RING, F) holds the stream's bytes from offset F - NL_RING of g
+    // (16-B granules, the stream's first byte at offset sh), the 64 B at F in flight in r0..r3
+    const uintptr_t sa = (uintptr_t)src;
+    const uint32_t sh = m ? (uint32_t)(sa & 15) : 0u;
+    const uint4 *const g = m ? reinterpret_cast<const uint4 *>(src - (sa & 15)) : nl_zero;
+    const uint64_t gl = m ? (sh + m - 1) >> 4 : 0;
+#pragma unroll
+    for (int j = 0; j < 12; ++j) reinterpret_cast<uint4 *>(ring)[j] = nl_ld(g + min((uint64_t)j, gl));
+    uint64_t F = 192;
+    uint4 r0 = nl_ld(g + min((uint64_t)12, gl)), r1 = nl_ld(g + min((uint64_t)13, gl)),
+          r2 = nl_ld(g + min((uint64_t)14, gl)), r3 = nl_ld(g + min((uint64_t)15, gl));
+    const uint32_t type = m ? ring[sh] : 0u;
+    const bool raw = type != 0xAFu;
+    bool ok = live;
+    if (live) {
+        if (m == 0) ok = expect == 0;
+        else if (raw) ok = (type == ' ' || any_type) && m - (type == ' ' ? 1 : 0) == expect;
+        else ok = m >= 2 ? expect != 0 : expect == 0;
     }
-    if (type != 0xAF) {
-        if (!any_type || m != expect) return false;
-        for (uint64_t i = 0; i < m; ++i) o[i] = src[i];
-        return true;
-    }
-    if (m < 2) return expect == 0;
-    for (int c = 0; c < 16; ++c) sL[c][t] = mtf_init_word();
-    uint32_t prev = src[1];
-    if (expect == 0) return false;
-    o[0] = (uint8_t)prev;
-    uint64_t q = 1, pos = 2;
+    const uint64_t qe = ok && m >= (raw ? 1u : 2u) ? expect : 0;   // bytes to write
+    if (!raw)
+        for (int c = 0; c < 16; ++c) sL[c][t] = mtf_init_word();
+    uint64_t pos = sh + (raw ? (type == ' ' ? 1u : 0u) : 1u);   // offset (from g) of the next byte
+    const uint64_t pe = sh + m;
+    NlOut out;
+    nl_out_init(out, o, oring, hrow);
+    uint64_t q = 0;
+    uint32_t prev = 0;
     int offn = 0;
-    while (pos < m) {
-        const uint32_t bb = src[pos];
-        uint32_t nyb, nxt;
-        if (offn == 0) { nyb = bb >> 4; nxt = bb & 15; }
-        else { nyb = bb & 15; nxt = (pos + 1 < m) ? (uint32_t)(src[pos + 1] >> 4) : 0u; }
-        const uint32_t c = (prev >> 3) & 15u;
-        uint64_t L = sL[c][t];
-        uint32_t v;
-        int used;
-        if (nyb & 8) { v = (uint32_t)(L >> (8 * (nyb & 7))) & 255u; used = 1; }
-        else { v = ((nyb & 7) << 4) + nxt; used = 2; }
-        if (modify) { uint32_t cnt = 8; (void)mtf_touch64(L, cnt, v); sL[c][t] = L; }
-        if (q >= expect) return false;
-        o[q++] = (uint8_t)v;
-        prev = v;
-        offn += used;
-        if (offn >= 2) { ++pos; offn -= 2; }
+    while (__ballot(q < qe)) {
+        for (int i = 0; i < NL_P; ++i) {
+            if (q < qe) {
+                const uint32_t b0 = ring[pos & (NL_RING - 1)], b1 = ring[(pos + 1) & (NL_RING - 1)];
+                uint32_t v = b0, adv = 2;   // raw byte (and a nybble stream's byte 1)
+                if (!raw && q > 0) {
+                    ok = ok && pos < pe;   // (tokens ran out before expect bytes)
+                    const uint32_t nyb = offn ? b0 & 15u : b0 >> 4;
+                    const uint32_t nxt = offn ? (pos + 1 < pe ? b1 >> 4 : 0u) : b0 & 15u;
+                    const uint32_t c = (prev >> 3) & 15u;
+                    const uint64_t L = sL[c][t];
+                    if (nyb & 8u) { v = (uint32_t)(L >> (8 * (nyb & 7u))) & 255u; adv = 1; }
+                    else { v = ((nyb & 7u) << 4) + nxt; adv = 2; }
+                    if (modify) { uint32_t pb; bool hit; sL[c][t] = mtf_touch8(L, v, pb, hit); }
+                }
+                oring[(out.sh + q) & (NL_ORING - 1)] = (uint8_t)v;
+                ++q;
+                prev = v;
+                offn += (int)adv;
+                if (offn >= 2) { ++pos; offn -= 2; }
+            }
+        }
+        // top the ring up while it leaves room (the bytes below pos are done with), and start the
+        // next 64 B (pos moves <= NL_P bytes between points, F - pos stays >= 64 - NL_P)
+        if (F - pos <= NL_RING - 64) {
+            uint4 *d = reinterpret_cast<uint4 *>(ring + (F & (NL_RING - 1)));
+            d[0] = r0; d[1] = r1; d[2] = r2; d[3] = r3;
+            F += 64;
+            const uint64_t k = F >> 4;
+            r0 = nl_ld(g + min(k, gl));
+            r1 = nl_ld(g + min(k + 1, gl));
+            r2 = nl_ld(g + min(k + 2, gl));
+            r3 = nl_ld(g + min(k + 3, gl));
+        }
+        nl_out_point(out, out.sh + q);
     }
-    return q == expect;
+    if (!raw && pos < pe) ok = false;   // tokens past expect bytes
+    nl_out_finish(out, out.sh + q);
+    return ok;
 }
 
+// DCNK decode: one lane per chunk, its stream into out + ch*K; a stream that is not a
+// nybble/LITERAL stream of exactly the chunk's length sets *err (bytes >= 0x80 do not
+// round-trip through the reference codec, P8)
 __global__ __launch_bounds__(64) void k_nyb_chunk_dec(const uint8_t *__restrict__ payload,
                                                       const uint64_t *__restrict__ off, uint64_t total, uint64_t n,
                                                       uint32_t K, uint64_t nchunks, int modify,
                                                       uint8_t *__restrict__ out, uint64_t *__restrict__ err)
 {
     __shared__ uint64_t s_L[16][64];
+    __shared__ __attribute__((aligned(16))) uint8_t s_in[64 * NL_RSTR];
+    __shared__ __attribute__((aligned(16))) uint8_t s_out[64 * NL_OSTR];
+    __shared__ __attribute__((aligned(16))) uint8_t s_head[64 * NL_HSTR];
     const int t = threadIdx.x;
     const uint64_t ch = (uint64_t)blockIdx.x * 64 + t;
-    if (ch >= nchunks) return;
-    const uint64_t a = off[ch], b = off[ch + 1];
-    const uint64_t expect = (n - ch * K < K) ? n - ch * K : K;
-    if (b < a || b > total || b - a < 1) { *err = 1; return; }
-    if (!nyb_lane_decode(payload + a, b - a, expect, modify, false, out + ch * K, s_L, t)) *err = 1;
+    bool live = ch < nchunks;
+    const uint64_t a = live ? off[ch] : 0, b = live ? off[ch + 1] : 0;
+    const uint64_t expect = live ? ((n - ch * K < K) ? n - ch * K : K) : 0;
+    if (live && (b < a || b > total || b - a < 1)) { *err = 1; live = false; }
+    const bool ok = nyb_wave_decode(payload + a, live ? b - a : 0, expect, modify, false, out + (live ? ch * K : 0),
+                                    live, s_L, s_in + t * NL_RSTR, s_out + t * NL_OSTR, s_head + t * NL_HSTR, t);
+    if (live && !ok) *err = 1;
 }
 
 // dc_nyb_decompress_batch: the output length of each stream (one lane per stream): the token
@@ -6432,32 +5878,30 @@ __global__ __launch_bounds__(64) void k_nyb_batch_len(const uint8_t *__restrict_
                                                       uint64_t count, uint64_t *__restrict__ len, uint64_t *__restrict__ err)
 {
     const uint64_t i = (uint64_t)blockIdx.x * 64 + threadIdx.x;
-    if (i >= count) return;
-    const uint64_t a = in_off[i], b = in_off[i + 1];
-    if (b < a) { len[i] = 0; *err = 1; return; }
-    const uint64_t m = b - a;
-    const uint8_t *src = in + a;
+    const bool live = i < count;
+    const uint64_t a = live ? in_off[i] : 0, b = live ? in_off[i + 1] : 0;
+    if (live && b < a) *err = 1;
+    const uint64_t m = live && b >= a ? b - a : 0;
+    const uint32_t type = m ? in[a] : 0u;
+    const bool nyb = m >= 3 && type == 0xAFu;   // tokens after byte 1
+    // the token structure, 2 states per nybble (s = 1: the second nybble of a literal is next):
+    // per byte, with h / l its nybbles' bit 3: tokens += s ? 1 : 1 + h, s' = s ? !l : h & !l
+    uint64_t tok = 0;
+    uint32_t st = 0;
+    const uintptr_t sa = (uintptr_t)(in + a);
+    const uint4 *g = nyb ? reinterpret_cast<const uint4 *>(in + a - (sa & 15)) : nl_zero;
+    const uint64_t sh = nyb ? sa & 15 : 0;
+    nl_walk(g, nyb ? sh + 2 : 0, nyb ? sh + m : 0,
+        [&](uint32_t v, bool valid) {
+            const uint32_t h = (v >> 7) & 1u, l = (v >> 3) & 1u;
+            const uint32_t add = st ? 1u : 1u + h, ns = st ? l ^ 1u : h & (l ^ 1u);
+            tok += valid ? add : 0u;
+            st = valid ? ns : st;
+        },
+        []() {});
     uint64_t q = 0;
-    if (m > 0) {
-        const uint32_t type = src[0];
-        if (type == 0xAF) {
-            if (m >= 2) {
-                q = 1;
-                uint64_t pos = 2;
-                int offn = 0;
-                while (pos < m) {
-                    const uint32_t bb = src[pos];
-                    const uint32_t nyb = offn == 0 ? bb >> 4 : bb & 15;
-                    offn += (nyb & 8) ? 1 : 2;
-                    ++q;
-                    if (offn >= 2) { ++pos; offn -= 2; }
-                }
-            }
-        } else {
-            q = type == ' ' ? m - 1 : m;
-        }
-    }
-    len[i] = q;
+    if (m > 0) q = type == 0xAFu ? (m >= 2 ? 1 + tok : 0) : type == ' ' ? m - 1 : m;
+    if (live) len[i] = q;
 }
 
 __global__ __launch_bounds__(64) void k_nyb_batch_dec(const uint8_t *__restrict__ in, const uint64_t *__restrict__ in_off,
@@ -6465,12 +5909,18 @@ __global__ __launch_bounds__(64) void k_nyb_batch_dec(const uint8_t *__restrict_
                                                       uint8_t *__restrict__ out, uint64_t *__restrict__ err)
 {
     __shared__ uint64_t s_L[16][64];
+    __shared__ __attribute__((aligned(16))) uint8_t s_in[64 * NL_RSTR];
+    __shared__ __attribute__((aligned(16))) uint8_t s_out[64 * NL_OSTR];
+    __shared__ __attribute__((aligned(16))) uint8_t s_head[64 * NL_HSTR];
     const int t = threadIdx.x;
     const uint64_t i = (uint64_t)blockIdx.x * 64 + t;
-    if (i >= count) return;
-    const uint64_t a = in_off[i], b = in_off[i + 1];
-    if (b < a) return;   // (flagged by k_nyb_batch_len)
-    if (!nyb_lane_decode(in + a, b - a, out_off[i + 1] - out_off[i], modify, true, out + out_off[i], s_L, t)) *err = 1;
+    bool live = i < count;
+    const uint64_t a = live ? in_off[i] : 0, b = live ? in_off[i + 1] : 0;
+    live = live && b >= a;   // (flagged by k_nyb_batch_len)
+    const uint64_t o0 = live ? out_off[i] : 0, o1 = live ? out_off[i + 1] : 0;
+    const bool ok = nyb_wave_decode(in + a, live ? b - a : 0, o1 - o0, modify, true, out + o0, live, s_L,
+                                    s_in + t * NL_RSTR, s_out + t * NL_OSTR, s_head + t * NL_HSTR, t);
+    if (live && !ok) *err = 1;
 }
 
 // ------------------------------------------------------------------------------------
@@ -6487,6 +5937,10 @@ __global__ __launch_bounds__(256) void k_copy_probe(const uint4 *__restrict__ sr
     uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     for (; i < n16; i += stride) st_nt(dst + i, ld_nt(src + i));
 }
+
+#ifdef DC_AB_KERNELS
+#include "dc_ab_kernels.inc"
+#endif
 
 // =====================================================================================
 // host side

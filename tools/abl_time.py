@@ -34,13 +34,24 @@ c = Codec(0)
 for o in a.opt:
     k, v = o.split("=")
     c.set_option(k, int(v))
-enc = c.encode(x, n_ary=a.nary, sync_syms=64)
+if a.stage in ("batch", "chunk_enc"):   # the one-lane-per-stream nybble paths on 4 KiB streams
+    x = x[: 256 << 20]
+    cont = c.nyb_compress_chunked(x, True, 4096)
+    nch = (x.numel() + 4095) // 4096
+    offs = cont[32: 32 + 8 * (nch + 1)].view(torch.int64).clone()
+    pay = cont[32 + 8 * (nch + 1):]
+else:
+    enc = c.encode(x, n_ary=a.nary, sync_syms=64)
 out = torch.empty_like(x)
 
 
 def run():
     if a.stage == "decode":
         c.decode_into(enc, out)
+    elif a.stage == "batch":
+        c.nyb_decompress_batch(pay, offs, True, out_cap=x.numel())
+    elif a.stage == "chunk_enc":
+        c.nyb_compress_chunked(x, True, 4096)
     elif a.stage == "hist":
         c.hist(x)
     else:
