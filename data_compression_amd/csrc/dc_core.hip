@@ -5088,25 +5088,41 @@ __global__ __launch_bounds__(256) void k_mtf_walk(
             post(R, X, pv, e, 0xFFFFu);
         }
     };
-    uint4 G0 = ld(0), G1 = ld(1), G2 = ld(2), G3 = ld(3), G4 = ld(4);
-    uint64_t e = e0, gi = 0;
-    for (; e + 64 <= e1; e += 64, gi += 4) {
-        const uint4 N1 = ld(gi + 5), N2 = ld(gi + 6), N3 = ld(gi + 7), N4 = ld(gi + 8);
+    // 64 elements (granules A..E: their bytes start sh into A): 4 steps, then the 64 ranks as one
+    // 64-B burst (16-B pieces of lines, one per step and lane, left the walk at 2.7x its
+    // algorithmic write traffic)
+    auto quad = [&](const uint4 &A, const uint4 &B, const uint4 &C, const uint4 &D, const uint4 &E, uint64_t ee) {
         // (the steps kept apart: interleaved by the scheduler they held 155 VGPRs, 3 waves per SIMD)
         uint4 Ra, Rb, Rc, Rd;
-        step(G0, G1, e, Ra);
+        step(A, B, ee, Ra);
         __builtin_amdgcn_sched_barrier(0);
-        step(G1, G2, e + 16, Rb);
+        step(B, C, ee + 16, Rb);
         __builtin_amdgcn_sched_barrier(0);
-        step(G2, G3, e + 32, Rc);
+        step(C, D, ee + 32, Rc);
         __builtin_amdgcn_sched_barrier(0);
-        step(G3, G4, e + 48, Rd);
+        step(D, E, ee + 48, Rd);
         __builtin_amdgcn_sched_barrier(0);
-        if (MODE == 2) {   // the group's 64 ranks as one 64-B burst (16-B pieces of lines, one per
-                           // step and lane, left the walk at 2.7x its algorithmic write traffic)
-            uint4 *const rq = reinterpret_cast<uint4 *>(rk + e);
+        if (MODE == 2) {
+            uint4 *const rq = reinterpret_cast<uint4 *>(rk + ee);
             rq[0] = Ra; rq[1] = Rb; rq[2] = Rc; rq[3] = Rd;
         }
+    };
+    uint4 G0 = ld(0), G1 = ld(1), G2 = ld(2), G3 = ld(3), G4 = ld(4);
+    uint64_t e = e0, gi = 0;
+    // 128 elements a round, their 8 granules (128 B of the tile) loaded together a round ahead:
+    // a lane's loads are 4 KiB from its neighbours', so with 4 granules a round each line was
+    // loaded in two halves a round apart, and the wave's 64 lines were gone from L2 in between
+    // (the walk read 2.7x its input from HBM, profiles/r4f_nyb_adaptive_pmc.txt)
+    for (; e + 128 <= e1; e += 128, gi += 8) {
+        const uint4 N1 = ld(gi + 5), N2 = ld(gi + 6), N3 = ld(gi + 7), N4 = ld(gi + 8);
+        const uint4 N5 = ld(gi + 9), N6 = ld(gi + 10), N7 = ld(gi + 11), N8 = ld(gi + 12);
+        quad(G0, G1, G2, G3, G4, e);
+        quad(G4, N1, N2, N3, N4, e + 64);
+        G0 = N4; G1 = N5; G2 = N6; G3 = N7; G4 = N8;
+    }
+    for (; e + 64 <= e1; e += 64, gi += 4) {
+        const uint4 N1 = ld(gi + 5), N2 = ld(gi + 6), N3 = ld(gi + 7), N4 = ld(gi + 8);
+        quad(G0, G1, G2, G3, G4, e);
         G0 = G4; G1 = N1; G2 = N2; G3 = N3; G4 = N4;
     }
     for (; e < e1; e += 16) {   // the last tile's ragged end, 16 elements at a time

@@ -34,7 +34,9 @@ c = Codec(0)
 for o in a.opt:
     k, v = o.split("=")
     c.set_option(k, int(v))
-if a.stage in ("batch", "chunk_enc"):   # the one-lane-per-stream nybble paths on 4 KiB streams
+if a.stage in ("nyb_adaptive", "nyb_static"):   # the whole-stream nybble encoders on 1 GiB
+    pass
+elif a.stage in ("batch", "chunk_enc"):   # the one-lane-per-stream nybble paths on 4 KiB streams
     x = x[: 256 << 20]
     cont = c.nyb_compress_chunked(x, True, 4096)
     nch = (x.numel() + 4095) // 4096
@@ -48,6 +50,8 @@ out = torch.empty_like(x)
 def run():
     if a.stage == "decode":
         c.decode_into(enc, out)
+    elif a.stage in ("nyb_adaptive", "nyb_static"):
+        c.nyb_compress(x, a.stage == "nyb_adaptive")
     elif a.stage == "batch":
         c.nyb_decompress_batch(pay, offs, True, out_cap=x.numel())
     elif a.stage == "chunk_enc":
