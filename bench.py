@@ -130,9 +130,10 @@ def main():
         from data_compression_amd.dist import ShardedSmall
         ss = ShardedSmall(c, table_mode=a.table_mode, fused=not a.two_stage)
         sync_fe = c.alloc_sync(n + 1, S)   # the front-end stream holds up to n + 1 symbols
+        gsync_fe = c.alloc_sync(n + 1 + 2 * S, S) if world > 1 else None   # (a shard's part of the stream's index)
 
         def encode():   # noqa: F811
-            state["s"] = ss.encode(x, a.nary, S, words=words, sync=sync_fe, table=tab, total=total)
+            state["s"] = ss.encode(x, a.nary, S, words=words, sync=sync_fe, table=tab, total=total, gsync=gsync_fe)
 
         fe_out = torch.empty(2 * n + 64, dtype=torch.uint8, device=dev)   # dc_small_decompress: >= 2 * m
 

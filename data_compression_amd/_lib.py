@@ -95,6 +95,8 @@ def _declare_core(L):
         "dc_small_huff_plan": ([vp, P, u64, i32, i32, P, P, P], i32),
         "dc_small_huff_pack_async": ([vp, P, u64, P, u64, P, u64, P, P, u32], i32),
         "dc_small_huff_symbols": ([vp, C.POINTER(u64)], i32),
+        "dc_small_huff_shard_hist": ([vp, P, u64, P, P], i32),
+        "dc_small_huff_shard_pack_async": ([vp, P, u64, P, P, P, u64, P, P, P, P, u32], i32),
         "dc_small_huff_decode": ([vp, P, u64, u64, P, P, u32, u64, P, P, P, C.POINTER(u64)], i32),
         "dc_copy_probe": ([vp, P, P, u64], i32),
         "dc_huff_pack": ([vp, P, u64, P, u64, P, u64, P, P, u32], i32),

@@ -181,13 +181,36 @@ struct HistFuse {
 // front-end): the histogram is that of the front-end output M, per 32 KiB block of the INPUT:
 // a pair's symbol 0x80 + letter counts at its second position (letter | 0x80), each block's
 // ' ' count loses its pair starts, and block 0 gains the type byte 8 (M[0]).
+// FE shard context (dist.ShardedSmall's fused encode at world > 1: FeShard[4] int64 on the
+// device, nullptr for a whole stream): the shard's global bit offset and first symbol index,
+// and the input bytes either side of it, -1 past the stream's ends. A shard whose left byte is
+// -1 starts the stream (the type byte 8, raw x[0]); any other has no header, its x[0] may be a
+// pair's second (after the left byte) or start, and its last byte may start a pair with the
+// right byte.
+struct FeCtx {
+    bool first;
+    uint32_t lb, rb;   // the bytes either side (0 past the stream's ends: never ' ', never a letter)
+};
+static __device__ __forceinline__ FeCtx fe_ctx(const int64_t *shard)
+{
+    FeCtx f{true, 0u, 0u};
+    if (shard) {
+        const int64_t l = shard[2], r = shard[3];
+        f.first = l < 0;
+        f.lb = l < 0 ? 0u : (uint32_t)l & 255u;
+        f.rb = r < 0 ? 0u : (uint32_t)r & 255u;
+    }
+    return f;
+}
+
 template <int PF, bool FE = false>
 __global__ __launch_bounds__(256) void k_hist_blocks(const uint8_t *__restrict__ in, uint64_t n,
                                                      uint64_t nblocks, uint16_t *__restrict__ bh,
                                                      uint64_t *__restrict__ hist, uint64_t *__restrict__ hacc,
                                                      uint32_t *__restrict__ hdone, uint64_t *__restrict__ hloc,
-                                                     HistFuse fuse)
+                                                     HistFuse fuse, const int64_t *__restrict__ shard = nullptr)
 {
+    const FeCtx fc = fe_ctx(FE ? shard : nullptr);
     __shared__ __attribute__((aligned(16))) uint32_t cnt[256 * 64];
     __shared__ uint32_t s_last;
     __shared__ uint32_t s_ps[4];
@@ -248,14 +271,14 @@ __global__ __launch_bounds__(256) void k_hist_blocks(const uint8_t *__restrict__
                     const uint64_t p = b * (uint64_t)DC_BLOCK_BYTES + (uint64_t)k * 4096 + (uint64_t)t * 16;
                     // (the shift as a statement of its own: inside `?:` it ran in a branch, lane 0 off)
                     const uint32_t pd = dpp_wave_shr1(w4[3]);
-                    const uint32_t pb = lane == 0 ? ce[k] >> 24 : pd >> 24;   // x[p - 1]
+                    const uint32_t pb = lane == 0 ? (p == 0 ? fc.lb : ce[k] >> 24) : pd >> 24;   // x[p - 1]
                     const uint32_t raw3 = w4[3];
                     uint32_t sc = 0;
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
                         const uint32_t pv = __builtin_amdgcn_alignbyte(w4[q], q ? w4[q - 1] : pb << 24, 3u);   // the bytes before
                         uint32_t sec = swar_eq(pv, 0x20202020u) & swar_lower(w4[q]);
-                        if (q == 0 && p == 0) sec &= ~0x8080u;   // positions 0, 1: no pair starts at 0
+                        if (q == 0 && p == 0 && fc.first) sec &= ~0x8080u;   // positions 0, 1: no pair starts at 0
                         w4[q] |= sec;
                         sc += (uint32_t)__popc(sec);
                         if (q == 0 && t == 0 && k == 0) sc -= sec & 0x80u ? 1u : 0u;   // (its start: the previous block's)
@@ -263,7 +286,7 @@ __global__ __launch_bounds__(256) void k_hist_blocks(const uint8_t *__restrict__
                     // the block's starts = its seconds, less the one on its first byte, plus a
                     // start on its last byte (its second: the next block's first byte)
                     if (t == 255 && k == 7) {
-                        const uint32_t nx = p + 16 < n ? ce[k] & 255u : 0u;
+                        const uint32_t nx = p + 16 < n ? ce[k] & 255u : fc.rb;
                         sc += ((raw3 >> 24) == 0x20u && nx >= 'a' && nx <= 'z') ? 1u : 0u;
                     }
                     pc += sc;
@@ -284,9 +307,10 @@ __global__ __launch_bounds__(256) void k_hist_blocks(const uint8_t *__restrict__
             for (uint64_t i = base + t; i < n; i += 256) {
                 uint32_t x = in[i];
                 if (FE) {
-                    const bool sec = i >= 2 && in[i - 1] == 0x20 && x >= 'a' && x <= 'z';
-                    const uint32_t nx = i + 1 < n ? in[i + 1] : 0u;
-                    pc += (i >= 1 && x == 0x20u && nx >= 'a' && nx <= 'z') ? 1u : 0u;
+                    const uint32_t pv = i >= 1 ? in[i - 1] : fc.lb;
+                    const bool sec = (i >= 2 || !fc.first) && pv == 0x20 && x >= 'a' && x <= 'z';
+                    const uint32_t nx = i + 1 < n ? in[i + 1] : fc.rb;
+                    pc += ((i >= 1 || !fc.first) && x == 0x20u && nx >= 'a' && nx <= 'z') ? 1u : 0u;
                     x |= sec ? 0x80u : 0u;
                 }
                 atomicAdd(&cnt[x * 64 + lane], inc);
@@ -320,7 +344,7 @@ __global__ __launch_bounds__(256) void k_hist_blocks(const uint8_t *__restrict__
         }
         if (FE) {   // the block's pair starts carry no symbol; block 0 holds the type byte 8
             if (t == 0x20) acc -= s_ps[0] + s_ps[1] + s_ps[2] + s_ps[3];
-            if (t == 8 && b == 0) acc += 1u;
+            if (t == 8 && b == 0 && fc.first) acc += 1u;
         }
         bh[b * 256 + t] = (uint16_t)acc;
         total += acc;
@@ -1238,7 +1262,9 @@ __global__ __launch_bounds__(256) void k_block_final_wide(const uint32_t *__rest
                                                           uint32_t *__restrict__ words, uint64_t words_cap,
                                                           const uint32_t *__restrict__ lcnt,
                                                           const uint32_t *__restrict__ wgcnt, uint64_t *__restrict__ msym,
-                                                          uint32_t *__restrict__ sl32, uint32_t slog)
+                                                          uint32_t *__restrict__ sl32, uint32_t slog,
+                                                          const int64_t *__restrict__ shard = nullptr,
+                                                          uint32_t *__restrict__ gl32 = nullptr)
 {
     // With lcnt set (C5 fused front-end): msym[b] = the index of block b's first symbol
     // (msym[nblocks] = all symbols), and the sync-length dword holding the chunk that spans each
@@ -1279,16 +1305,24 @@ __global__ __launch_bounds__(256) void k_block_final_wide(const uint32_t *__rest
         if (lane == 0) s_c[wv] = call;
         __syncthreads();
         const uint64_t ctot = s_c[0] + s_c[1] + s_c[2] + s_c[3];
+        // (a shard, gl32 set: the same dwords of its global sync index, whose first chunk is also
+        // shared, with the previous shard; k_fe_pack<true>)
+        const uint64_t M = gl32 ? (uint64_t)shard[1] : 0, c0e = (M >> slog) & ~1ull;
+        auto zero_g = [&](uint64_t m) {
+            if (gl32 && M + m > 0 && ((M + m - 1) >> slog) >= c0e) gl32[(((M + m - 1) >> slog) - c0e) >> 1] = 0u;
+        };
         if (t < PLAN_WG_BLOCKS) {
             const uint64_t b = (uint64_t)g * PLAN_WG_BLOCKS + t;
             if (b < nblocks) {
                 const uint64_t m = cbase + lcnt[b];
                 msym[b] = m;
                 if (b > 0) sl32[((m - 1) >> slog) >> 1] = 0u;
+                zero_g(m);
             }
         } else if (t == PLAN_WG_BLOCKS && last) {
             msym[nblocks] = ctot;
             sl32[((ctot - 1) >> slog) >> 1] = 0u;
+            zero_g(ctot);
         }
     }
     if (last) {
@@ -2028,6 +2062,14 @@ __global__ __launch_bounds__(256) void k_huff_pack_w(const uint8_t *__restrict__
 // by atomic adds into the u32 holding their u16 (zeroed by the plan), and so does the other
 // u16 of that u32. Fallbacks (reported in the plan slot's err[1], nothing written): LITERAL
 // output (M >= n bytes), no free byte value for z, a block whose bits exceed the stage.
+// SH (a shard of the stream, dist.ShardedSmall at world > 1; shard = FeShard): the shard's
+// context bytes (fe_ctx), its codes at the global bit shard[0] (the words start at global word
+// shard[0] / 32), its local sync index (chunks from its own first symbol: its own decode), and
+// the stream's GLOBAL sync index over its symbols, chunks at multiples of S of the global symbol
+// index shard[1]: gsync_len (u16, entry c - (c0 & ~1) for global chunk c, c0 = the shard's first;
+// the first and last chunks hold this shard's part only, the gather adds the neighbours') and
+// gsync_base (group g at entry g - ceil(shard[1] / 64 S): the groups that start in this shard).
+template <bool SH>
 __global__ __launch_bounds__(256) void k_fe_pack(const uint8_t *__restrict__ in, uint64_t n,
                                                  const dc_dtable *__restrict__ T,
                                                  const uint64_t *__restrict__ block_off,
@@ -2035,7 +2077,9 @@ __global__ __launch_bounds__(256) void k_fe_pack(const uint8_t *__restrict__ in,
                                                  uint32_t *__restrict__ out, uint64_t *__restrict__ sync_base,
                                                  uint16_t *__restrict__ sync_len, uint32_t sync_syms,
                                                  uint64_t nblocks, uint64_t words_cap, int *__restrict__ err,
-                                                 int build_dec)
+                                                 int build_dec, const int64_t *__restrict__ shard = nullptr,
+                                                 uint64_t *__restrict__ gsync_base = nullptr,
+                                                 uint16_t *__restrict__ gsync_len = nullptr)
 {
     __shared__ uint2 s_tab[256];
     __shared__ uint8_t s_nb8[256];
@@ -2051,6 +2095,9 @@ __global__ __launch_bounds__(256) void k_fe_pack(const uint8_t *__restrict__ in,
     }
     const uint64_t bx = blockIdx.x - (uint64_t)build_dec, gstride = gridDim.x - (uint64_t)build_dec;
     const uint64_t total = block_off[nblocks];
+    const FeCtx fc = fe_ctx(SH ? shard : nullptr);
+    const uint64_t M = SH ? (uint64_t)shard[1] : 0;   // the shard's first symbol, global index
+    if (SH) bit_base += (uint64_t)shard[0];
     if (err[0] != 0) return;
     if (((bit_base & 31) + total + 31) / 32 > words_cap) {
         if (t == 0) err[2] = 1;
@@ -2068,7 +2115,7 @@ __global__ __launch_bounds__(256) void k_fe_pack(const uint8_t *__restrict__ in,
     __syncthreads();
     const uint32_t z = s_z;
     const uint64_t mtot = msym[nblocks];   // symbols of M (the type byte included)
-    if (z > 255u || mtot >= n) {
+    if (z > 255u || (!SH && mtot >= n)) {   // (a shard: the LITERAL test is the whole stream's)
         if (t == 0) err[1] = 1;
         return;
     }
@@ -2077,7 +2124,11 @@ __global__ __launch_bounds__(256) void k_fe_pack(const uint8_t *__restrict__ in,
     const uint32_t slog = (uint32_t)__builtin_ctz(sync_syms), S = sync_syms;
     const uint32_t cbw = (DC_BLOCK_BYTES >> slog) + 2;             // chunk starts a block can hold
     uint32_t *const s_cb = s_stage + (PACK_BLK_WORDS + 4 - cbw);   // the list sits past the payload
-    const uint32_t lim = PACK_BLK_WORDS - cbw - 4;
+    uint32_t *const s_cbg = s_cb - (SH ? cbw : 0u);                 // SH: the global chunks' starts
+    const uint32_t lim = PACK_BLK_WORDS - (SH ? 2 : 1) * cbw - 4;
+    const uint64_t c0e = SH ? (M >> slog) & ~1ull : 0;                  // global chunk of gsync_len[0]
+    const uint64_t g0 = SH ? (M + ((uint64_t)S << DC_SYNC_GROUP_LOG) - 1) >> (slog + DC_SYNC_GROUP_LOG) : 0;
+    uint32_t *const gl32 = reinterpret_cast<uint32_t *>(gsync_len);
     const bool qmode = 2 * total > 11 * mtot;
     const uint32_t Z4 = z * 0x01010101u;
     uint32_t *const sl32 = reinterpret_cast<uint32_t *>(sync_len);
@@ -2109,6 +2160,13 @@ __global__ __launch_bounds__(256) void k_fe_pack(const uint8_t *__restrict__ in,
                     }
                     v = make_uint4(w[0], w[1], w[2], w[3]);
                 }
+                if (SH && n >= p && n < p + 16) {   // the byte after the shard (pair starts at n - 1)
+                    uint32_t w[4] = {v.x, v.y, v.z, v.w};
+                    const uint32_t o = (uint32_t)(n - p);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) w[q] |= (uint32_t)q == (o >> 2) ? fc.rb << (8 * (o & 3)) : 0u;
+                    v = make_uint4(w[0], w[1], w[2], w[3]);
+                }
                 blkv[k] = v;
                 const uint64_t ea = fe_edge_addr(p, lane, n);
                 ve[k] = ea < n ? *reinterpret_cast<const uint32_t *>(in + ea) : 0u;
@@ -2127,6 +2185,8 @@ __global__ __launch_bounds__(256) void k_fe_pack(const uint8_t *__restrict__ in,
         const uint64_t cf = (m0 + S - 1) >> slog;   // the first chunk that starts in this block
         const uint64_t ct = (m1 - 1) >> slog;       // the last one (this block's tail chunk)
         const uint32_t nc = ct >= cf ? (uint32_t)(ct - cf + 1) : 0u;
+        const uint64_t cfg = (M + m0 + S - 1) >> slog, ctg = (M + m1 - 1) >> slog;   // (SH: global chunks)
+        const uint32_t ncg = SH && ctg >= cfg ? (uint32_t)(ctg - cfg + 1) : 0u;
         const uint32_t nwa = sh + nw_blk;
         // ---- the symbols y, pass A: bit and symbol counts per piece ----
         // Pk = bits (<= 512) | symbols << 18 (<= 16) | bits of the first half << 23 (<= 256)
@@ -2136,15 +2196,15 @@ __global__ __launch_bounds__(256) void k_fe_pack(const uint8_t *__restrict__ in,
             const uint64_t p = blk_start + (uint64_t)k * PACK_TILE + (uint64_t)t * 16;
             uint32_t w4[4] = {blkv[k].x, blkv[k].y, blkv[k].z, blkv[k].w};
             const uint32_t pd = dpp_wave_shr1(w4[3]), qd = dpp_wave_shl1(w4[0]);   // (statements of their own)
-            const uint32_t pb = lane == 0 ? ve[k] >> 24 : pd >> 24;
-            const uint32_t qb = lane == 63 ? (p + 16 < n ? ve[k] & 255u : 0u) : qd & 255u;
+            const uint32_t pb = lane == 0 ? (p == 0 ? fc.lb : ve[k] >> 24) : pd >> 24;
+            const uint32_t qb = lane == 63 ? (p + 16 < n ? ve[k] & 255u : fc.rb) : qd & 255u;
             uint32_t st[4];
             fe_pair_starts(w4, qb, st);
-            if (p == 0) st[0] &= ~0x80u;   // position 0 never starts a pair
+            if (p == 0 && fc.first) st[0] &= ~0x80u;   // the stream's position 0 never starts a pair
             uint32_t nul = 0;               // positions without a symbol
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const uint32_t sec = (st[q] << 8) | (q ? st[q - 1] >> 24 : fe_start_before(pb, w4[0], p));
+                const uint32_t sec = (st[q] << 8) | (q ? st[q - 1] >> 24 : fe_start_before(pb, w4[0], fc.first ? p : 16));
                 uint32_t m8 = st[q];
                 if (!full) {   // past the input: no symbol
                     const int64_t v = (int64_t)n - (int64_t)(p + 4 * q);
@@ -2182,11 +2242,12 @@ __global__ __launch_bounds__(256) void k_fe_pack(const uint8_t *__restrict__ in,
             atomicOr(&s_stage[wi + 2], __builtin_amdgcn_alignbit(lo, 0u, r));
         };
         uint64_t run = blk_abs, mrun = m0;
-        if (b == 0) {   // M[0] = the type byte 8 (EIGHT_BIT_PRUNED, small_compression.c:39), chunk 0's start
+        if (b == 0 && fc.first) {   // M[0] = the type byte 8 (EIGHT_BIT_PRUNED, small_compression.c:39), chunk 0's start
             const uint2 h = s_tab[8];
             if (t == 0) {
                 emit(h.x, h.y, (uint32_t)(blk_abs - org));
                 s_cb[0] = 0u;
+                if (SH) s_cbg[0] = 0u;   // (the first shard: global = local)
             }
             run += h.y;
             mrun += 1;
@@ -2210,10 +2271,14 @@ __global__ __launch_bounds__(256) void k_fe_pack(const uint8_t *__restrict__ in,
             const uint32_t j0 = (uint32_t)(0ull - mi) & (S - 1);     // symbols before the chunk start
             const bool has = j0 < Ck;
             const uint32_t jj = has ? j0 : 0xFFFFu;
-            uint32_t ec = 0, cap = 0;   // symbols seen, bits before the chunk start
+            const uint32_t j0g = (uint32_t)(0ull - (mi + M)) & (S - 1);   // (SH: the global chunk start)
+            const bool hasg = SH && j0g < Ck;
+            const uint32_t jjg = hasg ? j0g : 0xFFFFu;
+            uint32_t ec = 0, cap = 0, capg = 0;   // symbols seen, bits before the chunk starts
             auto tally = [&](uint32_t l) {
                 ec += l != 0u ? 1u : 0u;
                 cap += ec <= jj ? l : 0u;
+                if (SH) capg += ec <= jjg ? l : 0u;
             };
             uint32_t w4[4] = {blkv[k].x, blkv[k].y, blkv[k].z, blkv[k].w};
             asm volatile("" : "+v"(w4[0]), "+v"(w4[1]), "+v"(w4[2]), "+v"(w4[3]));
@@ -2259,6 +2324,7 @@ __global__ __launch_bounds__(256) void k_fe_pack(const uint8_t *__restrict__ in,
                 }
             }
             if (has) s_cb[(uint32_t)(((mi + j0) >> slog) - cf)] = (uint32_t)(As - blk_abs) + cap;
+            if (hasg) s_cbg[(uint32_t)(((mi + M + j0g) >> slog) - cfg)] = (uint32_t)(As - blk_abs) + capg;
             __builtin_amdgcn_sched_barrier(0);
         }
         lds_barrier();
@@ -2308,6 +2374,20 @@ __global__ __launch_bounds__(256) void k_fe_pack(const uint8_t *__restrict__ in,
             if (t == 255 && (m0 & (S - 1)) != 0) {   // the previous block's tail chunk: the part in this block
                 const uint64_t c = cf - 1;
                 atomicAdd(&sl32[c >> 1], (nc ? s_cb[0] : (uint32_t)s_bits) << (16u * (uint32_t)(c & 1)));
+            }
+            if (SH) {   // the same over the global chunks (the shard's first and last chunks are partial)
+                const uint64_t hdg = M + m0 > 0 ? ((M + m0 - 1) >> slog) >> 1 : ~0ull, tdg = ctg >> 1;
+                for (uint32_t i = t; i < ncg; i += 256) {
+                    const uint32_t a = s_cbg[i], e = i + 1 < ncg ? s_cbg[i + 1] : (uint32_t)s_bits;
+                    const uint64_t c = cfg + i, ix = c - c0e;
+                    if ((c & (DC_SYNC_GROUP - 1)) == 0) gsync_base[(c >> DC_SYNC_GROUP_LOG) - g0] = blk_abs + a;
+                    if ((c >> 1) == hdg || (c >> 1) == tdg) atomicAdd(&gl32[ix >> 1], (e - a) << (16u * (uint32_t)(ix & 1)));
+                    else gsync_len[ix] = (uint16_t)(e - a);
+                }
+                if (t == 254 && ((M + m0) & (S - 1)) != 0) {
+                    const uint64_t c = cfg - 1, ix = c - c0e;
+                    atomicAdd(&gl32[ix >> 1], (ncg ? s_cbg[0] : (uint32_t)s_bits) << (16u * (uint32_t)(ix & 1)));
+                }
             }
         }
         lds_barrier();
@@ -6306,7 +6386,8 @@ int dc_copy_probe(dc_ctx *c, const void *d_src, void *d_dst, uint64_t bytes)
 // ---- Huffman -----------------------------------------------------------------------
 static uint64_t nblocks_of(uint64_t n) { return (n + DC_BLOCK_BYTES - 1) / DC_BLOCK_BYTES; }
 
-static int hist_impl(dc_ctx *c, const uint8_t *d_in, uint64_t n, uint64_t *d_hist, HistFuse fuse, bool fe = false)
+static int hist_impl(dc_ctx *c, const uint8_t *d_in, uint64_t n, uint64_t *d_hist, HistFuse fuse, bool fe = false,
+                     const int64_t *shard = nullptr)
 {
     if (!c || !d_hist || (n && !d_in)) return DC_E_ARG;
     if (((uintptr_t)d_in) & 15) return DC_E_ARG;
@@ -6319,7 +6400,7 @@ static int hist_impl(dc_ctx *c, const uint8_t *d_in, uint64_t n, uint64_t *d_his
     if (fe) {   // n >= 2 (dc_small_huff_plan)
         const uint64_t grid = nb < 512u ? nb : 512u;
         LAUNCH(c, "fe_hist_blocks", (k_hist_blocks<1, true>), grid, 256, d_in, n, nb, c->d_bh, d_hist,
-               reinterpret_cast<uint64_t *>(c->d_hflag), c->d_hflag + 512, c->d_hloc, fuse);
+               reinterpret_cast<uint64_t *>(c->d_hflag), c->d_hflag + 512, c->d_hloc, fuse, shard);
         return DC_OK;
     }
     if (nb == 0) {
@@ -6461,7 +6542,8 @@ int dc_huff_encode_plan(dc_ctx *c, const uint8_t *d_in, uint64_t n, int M, int n
 // symbol into c->d_msym, and the sync-length dwords of the chunks spanning block boundaries
 // zeroed (S = 1 << slog); one plan launch pair as well, at most PLAN_MAX_WG workgroups.
 static int plan_offsets(dc_ctx *c, int *err, int *err_next, uint64_t bit_base, const uint64_t *d_base,
-                        uint32_t *d_words, uint64_t words_cap, uint32_t *sl32 = nullptr, uint32_t slog = 0)
+                        uint32_t *d_words, uint64_t words_cap, uint32_t *sl32 = nullptr, uint32_t slog = 0,
+                        const int64_t *shard = nullptr, uint32_t *gl32 = nullptr)
 {
     const uint64_t nb = nblocks_of(c->hist_n);
     if (ensure((void **)&c->d_off, &c->off_cap, (nb + 1) * sizeof(uint64_t))) return DC_E_HIP;
@@ -6484,7 +6566,7 @@ static int plan_offsets(dc_ctx *c, int *err, int *err_next, uint64_t bit_base, c
                lcnt, wgcnt);
         LAUNCH(c, "block_scan", k_block_final_wide, nwg, 256, (const uint32_t *)loc, (const uint32_t *)tot, nb,
                (uint32_t)nwg, c->d_off, c->d_meta + 15, err_next, bit_base, d_base, d_words, words_cap,
-               (const uint32_t *)lcnt, (const uint32_t *)wgcnt, c->d_msym, sl32, slog);
+               (const uint32_t *)lcnt, (const uint32_t *)wgcnt, c->d_msym, sl32, slog, shard, gl32);
     } else if (sl32) {
         return DC_E_ARG;
     } else {
@@ -6614,9 +6696,48 @@ int dc_small_huff_pack_async(dc_ctx *c, const uint8_t *d_in, uint64_t n, const d
     if (r != DC_OK) return r;
     const uint64_t gmax = c->opt_pack_grid ? c->opt_pack_grid : (nb + 1) / 2;
     const uint64_t grid = nb < gmax ? nb : gmax;
-    LAUNCH(c, "fe_pack", k_fe_pack, grid + 1, 256, d_in, n, d_table, (const uint64_t *)c->d_off,
+    LAUNCH(c, "fe_pack", k_fe_pack<false>, grid + 1, 256, d_in, n, d_table, (const uint64_t *)c->d_off,
            (const uint64_t *)c->d_msym, bit_base, d_words, d_sync_base, d_sync_len, sync_syms, nb, words_cap,
-           plan_err(c), 1);
+           plan_err(c), 1, (const int64_t *)nullptr, (uint64_t *)nullptr, (uint16_t *)nullptr);
+    dec_tables_built(c, d_table);
+    return DC_OK;
+}
+
+// ---- C5 fused front-end encode of a shard (dist.ShardedSmall at world > 1) ---------------
+// The shard's front-end histogram (the bytes either side from d_shard: FeShard), no table: the
+// caller all-reduces the histograms, then dc_huff_table_plan builds the stream's table and this
+// shard's payload bits under it.
+int dc_small_huff_shard_hist(dc_ctx *c, const uint8_t *d_in, uint64_t n, const int64_t *d_shard, uint64_t *d_hist)
+{
+    if (!c || !d_shard || !d_hist) return DC_E_ARG;
+    if (n < 2) return DC_E_FALLBACK;
+    return hist_impl(c, d_in, n, d_hist, HistFuse{nullptr, 0, 0, nullptr, nullptr, nullptr}, true, d_shard);
+}
+
+// The shard's codes at the global bit d_shard[0] (d_words: word 0 = global word d_shard[0] / 32),
+// its local sync index (its own decode) and its part of the stream's global sync index
+// (k_fe_pack<true>). Nothing is read back: the offsets stay on the device.
+int dc_small_huff_shard_pack_async(dc_ctx *c, const uint8_t *d_in, uint64_t n, const dc_dtable *d_table,
+                                   const int64_t *d_shard, uint32_t *d_words, uint64_t words_cap,
+                                   uint64_t *d_sync_base, uint16_t *d_sync_len, uint64_t *d_gsync_base,
+                                   uint16_t *d_gsync_len, uint32_t sync_syms)
+{
+    if (!c || !d_table || !d_shard || !d_words || !d_sync_base || !d_sync_len || !d_gsync_base || !d_gsync_len ||
+        !sync_ok(sync_syms))
+        return DC_E_ARG;
+    if ((((uintptr_t)d_sync_len) & 3) || (((uintptr_t)d_gsync_len) & 3)) return DC_E_ARG;
+    if (d_in != c->hist_in || n != c->hist_n || !c->hist_fe || !c->plan_ok || !c->plan_total) return DC_E_STATE;
+    const uint64_t nb = nblocks_of(n);
+    const uint32_t slog = (uint32_t)__builtin_ctz(sync_syms);
+    const int r = plan_offsets(c, plan_err(c), plan_err_next(c), 0, reinterpret_cast<const uint64_t *>(d_shard),
+                               d_words, words_cap, reinterpret_cast<uint32_t *>(d_sync_len), slog, d_shard,
+                               reinterpret_cast<uint32_t *>(d_gsync_len));
+    if (r != DC_OK) return r;
+    const uint64_t gmax = c->opt_pack_grid ? c->opt_pack_grid : (nb + 1) / 2;
+    const uint64_t grid = nb < gmax ? nb : gmax;
+    LAUNCH(c, "fe_pack", k_fe_pack<true>, grid + 1, 256, d_in, n, d_table, (const uint64_t *)c->d_off,
+           (const uint64_t *)c->d_msym, (uint64_t)0, d_words, d_sync_base, d_sync_len, sync_syms, nb, words_cap,
+           plan_err(c), 1, d_shard, d_gsync_base, d_gsync_len);
     dec_tables_built(c, d_table);
     return DC_OK;
 }

@@ -168,8 +168,8 @@ class Codec:
         return (int(self.L.dc_huff_sync_groups(n, sync_syms)), int(self.L.dc_huff_sync_chunks(n, sync_syms)))
 
     def alloc_sync(self, n: int, sync_syms: int):
-        g, c = self.sync_sizes(n, sync_syms)
-        return (self._t(max(g, 1), torch.int64), self._t(max(c, 1), torch.int16))
+        g, c = self.sync_sizes(n, sync_syms)   # (2 lengths of slack past the view: the kernels add into whole dwords)
+        return (self._t(max(g, 1), torch.int64), self._t(max(c, 1) + 2, torch.int16)[: max(c, 1)])
 
     def pack(self, x, tab, bit_base, words, sync, sync_syms):
         base, lens = sync if sync is not None else (None, None)
@@ -462,6 +462,25 @@ class Codec:
         check("dc_small_huff_pack_async",
               self.L.dc_small_huff_pack_async(self.ctx, _ptr(x), x.numel(), _ptr(tab), bit_base, _ptr(words),
                                               words.numel(), _ptr(base), _ptr(lens), sync_syms))
+
+    # ---- the same for one shard of the stream (dist.ShardedSmall at world > 1) -------------
+    def small_shard_hist(self, x, shard, hist=None):
+        """dc_small_huff_shard_hist: the histogram of the shard's front-end output; shard = the
+        4 int64 of FeShard on the device (global bit, first symbol, byte before, byte after)."""
+        hist = hist if hist is not None else self._t(256, torch.int64)
+        check("dc_small_huff_shard_hist", self.L.dc_small_huff_shard_hist(self.ctx, _ptr(x), x.numel(), _ptr(shard),
+                                                                          _ptr(hist)))
+        return hist
+
+    def small_shard_pack_async(self, x, tab, shard, words, sync, gsync, sync_syms):
+        """dc_small_huff_shard_pack_async: codes at the global bit shard[0], the local sync index
+        into sync, this shard's part of the stream's sync index into gsync."""
+        base, lens = sync
+        gbase, glens = gsync
+        check("dc_small_huff_shard_pack_async",
+              self.L.dc_small_huff_shard_pack_async(self.ctx, _ptr(x), x.numel(), _ptr(tab), _ptr(shard), _ptr(words),
+                                                    words.numel(), _ptr(base), _ptr(lens), _ptr(gbase), _ptr(glens),
+                                                    sync_syms))
 
     def small_huff_symbols(self) -> int:
         v = C.c_uint64(0)

@@ -252,6 +252,21 @@ class ShardedSmall:
          encoding of the whole front-end output
     Decode: Huffman decode of the rank's segment, then the front-end inverse (per byte,
     stateless); the ranks' decoded segments concatenate to the input.
+
+    Fused (the default where the engine has dc_small_huff_*): at world size 1 the front-end and
+    the Huffman code in one pass over x (_encode_fused). At world size > 1 the same one pass per
+    shard, with no re-cut and no host read in the encode (_encode_fused_shards):
+      1. all_gather of every rank's (first byte, last byte, n): the 1-byte halos, on the device
+      2. the shard's histogram of M (dc_small_huff_shard_hist: the halo bytes are read by the
+         kernel) -> all_reduce -> the stream's table and this shard's bits (dc_huff_table_plan)
+      3. all_gather of every rank's (bits, symbols) -> this shard's global bit offset and first
+         symbol index, on the device
+      4. dc_small_huff_shard_pack_async: the shard's codes at that global bit, its local sync
+         index (its own decode) and its part of the stream's sync index (chunks at multiples of
+         S of the global symbol index; the gather adds the parts of the chunks two shards share)
+    finalize() (before the decode or the gather) reads the offsets back once per step and
+    agrees the fallbacks over the ranks (LITERAL output of the whole stream, a shard whose pack
+    cannot run fused): then every rank re-encodes with the two stages.
     """
 
     def __init__(self, engine, group=None, table_mode: str = "replicate", table_src: int = 0, fused: bool = True):
@@ -360,14 +375,20 @@ class ShardedSmall:
         for w in dist.batch_isend_irecv(ops) if ops else []:
             w.wait()
 
-    def encode(self, x, n_ary: int = 16, sync_syms: int = 64, words=None, sync=None, table=None, total=None):
-        """words/sync/table/total: optional caller-owned buffers for the fused path (the stream
-        points into them, so a caller that keeps several streams passes distinct ones; without
-        them every encode allocates its own)."""
+    def encode(self, x, n_ary: int = 16, sync_syms: int = 64, words=None, sync=None, table=None, total=None,
+               gsync=None):
+        """words/sync/table/total (gsync: world > 1): optional caller-owned buffers for the fused
+        path (the stream points into them, so a caller that keeps several streams passes
+        distinct ones; without them every encode allocates its own)."""
         if self.fused and self.world == 1 and hasattr(self.e, "small_huff_plan") and x.numel() >= 2:
             s = self._encode_fused(x, n_ary, sync_syms, words, sync, table, total)
             if s is not None:
                 return s
+        if self.fused and self.world > 1 and hasattr(self.e, "small_shard_hist"):
+            return self._encode_fused_shards(x, n_ary, sync_syms, words, sync, gsync, table, total)
+        return self._encode_two_stage(x, n_ary, sync_syms)
+
+    def _encode_two_stage(self, x, n_ary, sync_syms):
         seg, literal = self.frontend(x, sync_syms)
         s = self.h.encode(seg, n_ary=n_ary, sync_syms=sync_syms)
         s.literal = literal
@@ -414,9 +435,144 @@ class ShardedSmall:
         s.literal = False
         return s
 
+    # ---- fused encode of a shard (world > 1) -----------------------------------------------
+    def _all_gather_dev(self, t):   # every rank's t, stacked (device, no host read)
+        out = torch.empty(self.world * t.numel(), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, t.reshape(-1).contiguous(), group=self.group)
+        return out.view((self.world,) + tuple(t.shape))
+
+    def _all_reduce_dev(self, t, op=dist.ReduceOp.SUM):
+        dist.all_reduce(t, op=op, group=self.group)
+
+    def _encode_fused_shards(self, x, n_ary, S, words=None, sync=None, gsync=None, table=None, total=None):
+        n = x.numel()
+        if n < 2:
+            raise ValueError("each shard needs >= 2 bytes")
+        dev, r, e = x.device, self.rank, self.e
+        # 1. halos: every rank's first and last byte and size, gathered on the device
+        ends = self._all_gather_dev(torch.stack([x[0].to(torch.int64), x[n - 1].to(torch.int64),
+                                                 torch.tensor(n, dtype=torch.int64, device=dev)]))
+        neg = torch.full((), -1, dtype=torch.int64, device=dev)
+        shard = torch.stack([neg, neg, ends[r - 1, 1] if r > 0 else neg,
+                             ends[r + 1, 0] if r < self.world - 1 else neg]).contiguous()
+        # 2. the shard's histogram of M, the stream's table, this shard's bits under it
+        hist = e.small_shard_hist(x, shard)
+        hg = hist.clone()
+        self._all_reduce_dev(hg)
+        if self.h.table_mode == "broadcast":
+            tab = table if table is not None else e.alloc_table()
+            if r == self.h.table_src:
+                tab = e.table(hg, n_ary, out=tab) if table is not None else e.table(hg, n_ary)
+            self.h._broadcast_table(tab)
+            tot = e.plan(tab, total=total) if total is not None else e.plan(tab)
+        else:
+            tab, tot = e.table_plan(hg, n_ary, out=table, total=total)
+        # 3. every shard's (bits, symbols): this shard's global bit and first symbol
+        m = hist.sum()
+        bm = self._all_gather_dev(torch.stack([tot.reshape(()).to(torch.int64), m]))
+        shard[0] = bm[:r, 0].sum()
+        shard[1] = bm[:r, 1].sum()
+        literal = bm[:, 1].sum() >= ends[:, 2].sum()   # the whole stream's LITERAL test
+        # 4. the pack; buffers: the words sized here need the bits (one host read)
+        if words is None:
+            words = e.alloc_words(0, int(tot.item()) + 32)
+        if sync is None:
+            sync = e.alloc_sync(n + 1, S)
+        if gsync is None:
+            gsync = e.alloc_sync(n + 1 + 2 * S, S)
+        gen = e.plan_gen()
+        e.small_shard_pack_async(x, tab, shard, words, sync, gsync, S)
+        s = ShardStream(words, shard[0:1], -1, sync, S, -1, tab, None, tot, gen)
+        s.literal = False
+        s.shard_fused = {"x": x, "n_ary": n_ary, "shard": shard, "m": m, "gsync": gsync, "literal": literal}
+        return s
+
+    def finalize(self, s):
+        """The host values of a fused shard stream (one read of 4 device scalars) and the
+        fallbacks agreed over the ranks: a LITERAL stream or a shard whose fused pack did not
+        run (DC_E_FALLBACK) makes every rank re-encode with the two stages."""
+        fs = getattr(s, "shard_fused", None)
+        if fs is None or fs.get("done"):
+            return s
+        st = self.e.pack_status(s.table, s.plan_gen)
+        v = torch.stack([fs["shard"][0], fs["shard"][1], s.total.reshape(()).to(torch.int64), fs["m"],
+                         fs["literal"].to(torch.int64)]).cpu().tolist()
+        flags = torch.tensor([1 if (st == -8 or v[4]) else 0, 1 if st not in (0, -8) else 0], dtype=torch.int64,
+                             device=fs["shard"].device)
+        self._all_reduce_dev(flags, dist.ReduceOp.MAX)
+        fb, bad = flags.tolist()
+        if bad:
+            raise RuntimeError(f"rank {self.rank}: fused shard pack failed with status {st} (a rank's plan/pack)")
+        if fb:   # every rank: the two stages
+            t = self._encode_two_stage(fs["x"], fs["n_ary"], s.sync_syms)
+            self.h.finalize(t)
+            s.__dict__.update(t.__dict__)
+            s.shard_fused = None
+            return s
+        s.bit_base, s.bits, s.n, s.totals = int(v[0]), int(v[2]), int(v[3]), None
+        ng, nch = self.e.sync_sizes(s.n, s.sync_syms)
+        s.sync = (s.sync[0][: max(ng, 1)], s.sync[1][: max(nch, 1)])
+        fs["M"] = int(v[1])
+        fs["done"] = True
+        return s
+
+    def gather(self, s, dst: int = 0):
+        """The whole stream on rank dst (ShardedHuffman.gather's words), with, for a fused shard
+        stream, the stream's sync index assembled from the shards' parts: the chunks two shards
+        share are the sums of their parts, each group base comes from the shard it starts in."""
+        self.finalize(s)
+        fs = getattr(s, "shard_fused", None)
+        if fs is None:
+            return self.h.gather(s, dst)
+        dev = s.words.device
+        empty = ShardStream(s.words, s.bit_base, s.bits, (torch.empty(0, dtype=torch.int64, device=dev),
+                                                          torch.empty(0, dtype=torch.int16, device=dev)),
+                            s.sync_syms, s.n, s.table)
+        g = self.h.gather(empty, dst)
+        S = s.sync_syms
+        M, mm = fs["M"], s.n
+        c0 = M // S
+        c0e = c0 & ~1
+        nl = (M + mm - 1) // S - c0 + 1 if mm else 0
+        g0, g1 = -(-M // (64 * S)), -(-(M + mm) // (64 * S))
+        gl = fs["gsync"][1][c0 - c0e: c0 - c0e + nl]
+        gb = fs["gsync"][0][: g1 - g0]
+        meta = self._all_gather_dev(torch.tensor([c0, nl, g0, g1 - g0], dtype=torch.int64, device=dev))
+        metas = meta.cpu().tolist()
+        dst_g = dst if self.group is None else dist.get_global_rank(self.group, dst)
+        if self.rank != dst:
+            ops = [dist.P2POp(dist.isend, t.contiguous(), dst_g, group=self.group)
+                   for t in (gl.view(torch.uint8), gb) if t.numel()]
+            for w in dist.batch_isend_irecv(ops) if ops else []:
+                w.wait()
+            return None
+        nchunk = max(mt[0] + mt[1] for mt in metas)
+        ngroup = (nchunk + 63) // 64
+        lens32 = torch.zeros(nchunk, dtype=torch.int32, device=dev)
+        bases = torch.empty(ngroup, dtype=torch.int64, device=dev)
+        parts, ops = [], []
+        for q, (qc0, qnl, qg0, qng) in enumerate(metas):
+            if q == self.rank:
+                parts.append((qc0, gl.clone()))
+                bases[qg0: qg0 + qng] = gb
+                continue
+            src = q if self.group is None else dist.get_global_rank(self.group, q)
+            t = torch.empty(qnl, dtype=torch.int16, device=dev)
+            if qnl:
+                ops.append(dist.P2POp(dist.irecv, t.view(torch.uint8), src, group=self.group))
+            if qng:
+                ops.append(dist.P2POp(dist.irecv, bases[qg0: qg0 + qng], src, group=self.group))
+            parts.append((qc0, t))
+        for w in dist.batch_isend_irecv(ops) if ops else []:
+            w.wait()
+        for qc0, t in parts:
+            lens32[qc0: qc0 + t.numel()] += t.to(torch.int32) & 0xFFFF
+        return g[0], g[1], bases, (lens32 - ((lens32 >= 32768).to(torch.int32) << 16)).to(torch.int16)   # u16 bits
+
     def decode(self, s, out=None):
         """out: optional buffer of >= 2 * s.n bytes for the front-end inverse (the result is a
         view of it, or of the Huffman output when a later rank's segment is LITERAL)."""
+        self.finalize(s)
         kw = {} if out is None else {"out": out}
         if (self.fused and self.world == 1 and not s.literal and hasattr(self.e, "small_huff_decode")
                 and isinstance(s.bit_base, int)):

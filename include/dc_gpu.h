@@ -233,6 +233,27 @@ int dc_small_huff_pack_async(dc_ctx *ctx, const uint8_t *d_in, uint64_t n, const
                              uint64_t bit_base, uint32_t *d_words, uint64_t words_cap,
                              uint64_t *d_sync_base, uint16_t *d_sync_len, uint32_t sync_syms);
 int dc_small_huff_symbols(dc_ctx *ctx, uint64_t *h_symbols);
+/* The same fused encode for one contiguous shard of the input (dist.ShardedSmall at world > 1;
+ * the front-end's only halo is one byte each side). d_shard: 4 x int64 on the
+ * device, read by the kernels (no host synchronisation): {global bit of the shard's first code,
+ * global index of its first symbol of M, the input byte before the shard (-1: the shard starts the
+ * stream: type byte 8, raw first byte), the input byte after it (-1: none)}.
+ * dc_small_huff_shard_hist: the shard's histogram of M (no table; the caller all-reduces the
+ * shards' histograms and runs dc_huff_table_plan, which also plans this shard's bits).
+ * dc_small_huff_shard_pack_async: the shard's codes at that global bit (d_words: word 0 = the
+ * stream's word d_shard[0] / 32, the shared first and last words holding only this shard's bits,
+ * OR-merged by the gather), its local sync index (chunks of S symbols from its own first symbol:
+ * its own decode) and its part of the stream's sync index (d_gsync_len: u16 per global chunk c
+ * at entry c - (c0 & ~1), c0 = its first chunk, the first and last entries partial: the gather adds
+ * the neighbours' parts; d_gsync_base: the groups that start in the shard, from group
+ * ceil(first symbol / 64 S)). Fallbacks as dc_small_huff_pack_async, except the LITERAL test,
+ * which belongs to the whole stream (the caller's). */
+int dc_small_huff_shard_hist(dc_ctx *ctx, const uint8_t *d_in, uint64_t n, const int64_t *d_shard,
+                             uint64_t *d_hist);
+int dc_small_huff_shard_pack_async(dc_ctx *ctx, const uint8_t *d_in, uint64_t n, const dc_dtable *d_table,
+                                   const int64_t *d_shard, uint32_t *d_words, uint64_t words_cap,
+                                   uint64_t *d_sync_base, uint16_t *d_sync_len, uint64_t *d_gsync_base,
+                                   uint16_t *d_gsync_len, uint32_t sync_syms);
 /* C5 decode: the Huffman decode of the m-symbol front-end stream M into d_m (16-B aligned,
  * >= m bytes), counting the symbols >= 0x80 of every group of 64 chunks on the way (S = 64), then
  * the front-end inverse (small_compression.c's decompress_bytestring, dc_small_decompress) into

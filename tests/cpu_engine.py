@@ -61,7 +61,11 @@ class CpuEngine:
 
     def alloc_sync(self, n, S):
         c = (n + S - 1) // S
-        return (torch.zeros(max((c + 63) // 64, 1), dtype=torch.int64), torch.zeros(max(c, 1), dtype=torch.int16))
+        return (torch.zeros(max((c + 63) // 64, 1), dtype=torch.int64), torch.zeros(max(c, 1) + 2, dtype=torch.int16)[: max(c, 1)])
+
+    def sync_sizes(self, n, S):
+        c = (n + S - 1) // S
+        return (c + 63) // 64, c
 
     def alloc_bytes(self, n):
         return torch.zeros(max(n, 1), dtype=torch.uint8)
@@ -93,6 +97,48 @@ class CpuEngine:
         total = int(sync[1][: (n + S - 1) // S].numpy().view(np.uint16).astype(np.int64).sum())
         y = orc.huff_unpack(stream, total, n, tab["el"], tab["ev"], tab["n_ary"])
         out[:n] = torch.from_numpy(y)
+
+    # ---- the fused C5 encode of a shard (dist.ShardedSmall at world > 1), restated ----------
+    @staticmethod
+    def _shard_syms(x, shard):
+        """The front-end output M of a shard (small_compression.c:582-665; shard = (global bit,
+        first symbol, byte before or -1, byte after or -1)): a pair ' ' + lowercase letter is
+        the symbol letter | 0x80 at its second byte, nothing at its first; the stream's first
+        shard begins with the type byte 8 and a raw first byte."""
+        a = x.numpy().astype(np.int64)
+        left, right = int(shard[2]), int(shard[3])
+        first = left < 0
+        low = (a >= ord("a")) & (a <= ord("z"))
+        prev = np.concatenate([[max(left, 0)], a[:-1]])
+        nxt = np.concatenate([a[1:], [max(right, 0)]])
+        nlow = (nxt >= ord("a")) & (nxt <= ord("z"))
+        i = np.arange(a.size)
+        sec = (prev == ord(" ")) & low & ((i >= 2) | (not first))
+        start = (a == ord(" ")) & nlow & ((i >= 1) | (not first))
+        sym = np.where(sec, a | 0x80, a)[~start]
+        return np.concatenate([[8] if first else [], sym]).astype(np.uint8)
+
+    def small_shard_hist(self, x, shard, hist=None):
+        y = self._shard_syms(x, shard)
+        self._hist_in = torch.from_numpy(y)
+        return torch.from_numpy(orc.histogram(y).astype(np.int64))
+
+    def small_shard_pack_async(self, x, tab, shard, words, sync, gsync, S):
+        y = self._shard_syms(x, shard)
+        B, M = int(shard[0]), int(shard[1])
+        self.pack_async(torch.from_numpy(y), tab, B, words, sync, S)   # codes + the local index
+        t = self._tab(tab)
+        L = t["nb"][y].astype(np.int64)
+        pos = B + np.concatenate([[0], np.cumsum(L)])   # global bit of each symbol (and the end)
+        m = y.size
+        c = (M + np.arange(m)) // S
+        c0e = (M // S) & ~1
+        gl = np.bincount(c - c0e, weights=L).astype(np.int64)
+        gsync[1][: gl.size] = torch.from_numpy(gl.astype(np.uint16).view(np.int16))
+        G = 64 * S
+        g0, g1 = -(-M // G), -(-(M + m) // G)
+        gb = pos[np.arange(g0, g1) * G - M]
+        gsync[0][: gb.size] = torch.from_numpy(gb.astype(np.int64))
 
     # ---- small front-end shard bodies (dist.ShardedSmall), restated with numpy ------------
     def small_body(self, y, left_halo, nelem, head=b"", out=None):

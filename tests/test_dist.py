@@ -84,7 +84,7 @@ def test_sharded_stream_is_bit_identical(world, n_ary, table_mode):
     assert np.array_equal(lens.view(np.uint16), rlens)
 
 
-def _small_worker(rank, world, port, cuts, kind, n_ary, S, q):
+def _small_worker(rank, world, port, cuts, kind, n_ary, S, q, fused=False):
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     from data_compression_amd.dist import ShardedSmall
@@ -93,14 +93,15 @@ def _small_worker(rank, world, port, cuts, kind, n_ary, S, q):
     try:
         x = _small_input(kind, cuts[-1])
         xs = torch.from_numpy(x[cuts[rank]: cuts[rank + 1]].copy())
-        sm = ShardedSmall(CpuEngine())
+        sm = ShardedSmall(CpuEngine(), fused=fused)
         s = sm.encode(xs, n_ary=n_ary, sync_syms=S)
-        y = sm.decode(s)
-        g = sm.h.gather(s, dst=0)
-        q.put(("dec", rank, y.numpy().copy(), s.literal))
+        y = sm.decode(s)   # (finalize: a LITERAL stream falls back to the two stages here)
+        path = "fused" if getattr(s, "shard_fused", None) is not None else "two-stage"
+        g = sm.gather(s, dst=0)
+        q.put(("dec", rank, y.numpy().copy(), s.literal, path))
         if rank == 0:
             words, bits, bases, lens = g
-            q.put(("merged", words.numpy().copy(), bits))
+            q.put(("merged", words.numpy().copy(), bits, bases.numpy().copy(), lens.numpy().copy()))
     finally:
         dist.destroy_process_group()
 
@@ -113,29 +114,39 @@ def _small_input(kind, n):
     return rng.integers(ord("A"), ord("Z") + 1, size=n, dtype=np.uint8)   # no pairs: LITERAL
 
 
-@pytest.mark.parametrize("world,kind", [(2, "log"), (3, "log"), (2, "upper")])
-def test_sharded_small_frontend_huffman(world, kind):
-    """C5 orchestration (dist.ShardedSmall): halo exchange, body per rank, global LITERAL
-    decision, re-cut at 64*S, sharded Huffman. The gathered stream equals the oracle's
+@pytest.mark.parametrize("world,kind,fused,cut", [(2, "log", False, "pair"), (3, "log", False, "pair"),
+                                                  (2, "upper", False, "pair"), (2, "log", True, "pair"),
+                                                  (3, "log", True, "pair"), (3, "log", True, "space_end"),
+                                                  (3, "log", True, "space_start"), (2, "upper", True, "pair")])
+def test_sharded_small_frontend_huffman(world, kind, fused, cut):
+    """C5 orchestration (dist.ShardedSmall). Two stages: halo exchange, body per rank, global
+    LITERAL decision, re-cut at 64*S, sharded Huffman. Fused (world > 1): each shard's one-pass
+    encode at its global bit and symbol offsets, no re-cut (a LITERAL stream falls back to the
+    two stages). Either way the gathered stream AND its sync index equal the oracle's
     single-stream Huffman encoding of the single-stream front-end output, and the ranks'
-    decoded segments concatenate to the input."""
+    decoded segments concatenate to the input. Cuts: on a pair's halves (' ' | letter), after a
+    ' ' that starts no pair, or on a ' ' that starts one (' ' + letter | ...)."""
     from oracle import oracle as orc
     S, n_ary = 64, 16
     total = 64 * S * 4 * world + 777
     x = _small_input(kind, total)
-    # cuts that land on pair halves (' ' then a letter across the boundary) where possible
+    low = lambda v: ord("a") <= v <= ord("z")   # noqa: E731
     cuts = [0]
     for r in range(1, world):
-        c = r * total // world
+        c = r * total // world + 13 * r
         if kind == "log":
-            while not (x[c - 1] == ord(" ") and ord("a") <= x[c] <= ord("z")):
+            want = {"pair": lambda c: x[c - 1] == ord(" ") and low(x[c]),
+                    "space_end": lambda c: x[c - 1] == ord(" ") and not low(x[c]),
+                    "space_start": lambda c: x[c] == ord(" ") and low(x[c + 1])}[cut]
+            while not want(c):
                 c += 1
         cuts.append(c)
     cuts.append(total)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_small_worker, args=(r, world, port, cuts, kind, n_ary, S, q)) for r in range(world)]
+    procs = [ctx.Process(target=_small_worker, args=(r, world, port, cuts, kind, n_ary, S, q, fused))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=180) for _ in range(world + 1)]
@@ -146,14 +157,18 @@ def test_sharded_small_frontend_huffman(world, kind):
     assert np.array_equal(np.concatenate([d[2] for d in decs]), x)
     fe = np.frombuffer(orc.small_compress(x.tobytes()), np.uint8)
     assert all(d[3] == (fe[0] == ord(" ")) for d in decs)
-    _, words, bits = next(r for r in res if r[0] == "merged")
+    assert all(d[4] == ("fused" if fused and kind == "log" else "two-stage") for d in decs)
+    _, words, bits, bases, lens = next(r for r in res if r[0] == "merged")
     h = orc.histogram(fe)
     L = orc.huffman_lengths(h, n_ary)
     el, ev = orc.canonical(L, n_ary)
     code, nb, _ = orc.bitcodes(el, ev, n_ary)
-    payload, rbits, _ = orc.huff_pack(fe, code, nb, sync_syms=S)
+    payload, rbits, idx = orc.huff_pack(fe, code, nb, sync_syms=S)
     assert bits == rbits
     assert np.array_equal(words.view(np.uint8)[: len(payload)], payload)
+    rbase, rlens = orc.sync_compact(idx, 0, rbits)
+    assert np.array_equal(bases.astype(np.uint64), rbase)
+    assert np.array_equal(lens.view(np.uint16), rlens)
 
 
 def _nyb_worker(rank, world, port, cuts, kind, modify, dcuts, q):

@@ -1060,12 +1060,14 @@ def test_sharded_huffman_on_device(torch_cuda, world, n_ary, table_mode, preallo
     assert np.array_equal(merged, ref)
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_small_on_device(torch_cuda, world):
-    """dist.ShardedSmall on the device engine (thread ranks): the halo elements settled on
-    the host, bodies sized then written in place (dc_small_compress_body_plan/_write) at
-    16-B aligned re-cut segments; the OR-merged Huffman shards equal the oracle's encoding
-    of the reference front-end output, and the decoded segments concatenate to the input."""
+@pytest.mark.parametrize("world,fused", [(2, False), (3, False), (2, True), (3, True), (4, True)])
+def test_sharded_small_on_device(torch_cuda, world, fused):
+    """dist.ShardedSmall on the device engine (thread ranks). Two stages: the halo elements
+    settled on the host, bodies sized then written in place (dc_small_compress_body_plan/_write)
+    at 16-B aligned re-cut segments. Fused: each shard's one-pass encode at its global offsets
+    (dc_small_huff_shard_*), offsets on the device until finalize(). Either way the OR-merged
+    Huffman shards equal the oracle's encoding of the reference front-end output, and the
+    decoded segments concatenate to the input."""
     import threading
 
     from data_compression_amd import synth
@@ -1088,12 +1090,22 @@ def test_sharded_small_on_device(torch_cuda, world):
     def run(r):
         try:
             torch.cuda.set_device(0)
-            sm = ShardedSmall(Codec(0))
+            sm = ShardedSmall(Codec(0), fused=fused)
             sm.world = sm.h.world = world
             sm.rank = sm.h.rank = r
             sm.h.table_src = world - 1
             _thread_collectives(sm.h, tr, r, world, torch)
             sm._gather_i64 = lambda vals: tr.gather(r, vals)
+
+            def ag(t):   # (the fused path's device all_gather and all_reduce)
+                v = tr.gather(r, t.reshape(-1).cpu().tolist())
+                return torch.tensor(v, dtype=t.dtype, device=t.device).view((world,) + tuple(t.shape))
+
+            def ar(t, op=None):
+                v = np.array(tr.gather(r, t.reshape(-1).cpu().tolist()), dtype=np.int64)
+                red = v.max(axis=0) if op is not None and op == torch.distributed.ReduceOp.MAX else v.sum(axis=0)
+                t.copy_(torch.from_numpy(red).to(t.device).view(t.shape))
+            sm._all_gather_dev, sm._all_reduce_dev = ag, ar
 
             def shift(send, recv):   # send to r + 1, receive from r - 1
                 slots[r] = send.clone() if send is not None else None
@@ -1103,7 +1115,8 @@ def test_sharded_small_on_device(torch_cuda, world):
                 tr.bar.wait()
             sm._shift = shift
             s = sm.encode(torch.from_numpy(x[cuts[r]: cuts[r + 1]].copy()).cuda(), n_ary=n_ary, sync_syms=S)
-            sm.h.finalize(s)
+            assert (getattr(s, "shard_fused", None) is not None) == fused
+            sm.finalize(s) if fused else sm.h.finalize(s)
             y = sm.decode(s)
             nw = (s.bit_base % 32 + s.bits + 31) // 32
             res[r] = (s.bit_base, s.bits, s.words[:nw].cpu().numpy().copy(), y.cpu().numpy().copy())
