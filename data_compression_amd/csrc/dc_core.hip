@@ -1593,7 +1593,7 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
                         // bytes), or every half in quarter mode: two quarters of 4 codes, each
                         // <= 64 bits unless codes exceed 16 bits, then code by code
                         uint32_t p = pos;
-#pragma unroll 1
+#pragma unroll
                         for (int qq = 0; qq < 2; ++qq) {
                             uint2 e[4];
                             uint32_t nq = 0;
@@ -2298,7 +2298,7 @@ __global__ __launch_bounds__(256) void k_fe_pack(const uint8_t *__restrict__ in,
                     emit(acc, Th, pos);
                 } else {
                     uint32_t pq = pos;
-#pragma unroll 1
+#pragma unroll
                     for (int qq = 0; qq < 2; ++qq) {
                         uint2 e[4];
                         uint32_t nq = 0;

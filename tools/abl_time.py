@@ -36,6 +36,8 @@ for o in a.opt:
     c.set_option(k, int(v))
 if a.stage in ("nyb_adaptive", "nyb_static"):   # the whole-stream nybble encoders on 1 GiB
     pass
+elif a.stage in ("c5_enc", "c5_step"):   # the fused C5 encode (and the counted decode)
+    enc = c.small_huff_encode(x, a.nary, 64)
 elif a.stage in ("batch", "chunk_enc"):   # the one-lane-per-stream nybble paths on 4 KiB streams
     x = x[: 256 << 20]
     cont = c.nyb_compress_chunked(x, True, 4096)
@@ -45,11 +47,16 @@ elif a.stage in ("batch", "chunk_enc"):   # the one-lane-per-stream nybble paths
 else:
     enc = c.encode(x, n_ary=a.nary, sync_syms=64)
 out = torch.empty_like(x)
+out2 = torch.empty(2 * x.numel() + 64, dtype=torch.uint8, device=dev) if a.stage == "c5_step" else None
 
 
 def run():
     if a.stage == "decode":
         c.decode_into(enc, out)
+    elif a.stage in ("c5_enc", "c5_step"):
+        e = c.small_huff_encode(x, a.nary, 64)
+        if a.stage == "c5_step":
+            c.small_huff_decode(e, out=out2)
     elif a.stage in ("nyb_adaptive", "nyb_static"):
         c.nyb_compress(x, a.stage == "nyb_adaptive")
     elif a.stage == "batch":
