@@ -128,11 +128,13 @@ static __device__ __forceinline__ uint32_t dpp_wave_shl1(uint32_t x)   // lane l
 }
 // The dword a lane of the fused kernels loads beside its 16 bytes at p: lane 0 the one
 // holding x[p - 1], lane 63 the one at p + 16 (the lanes between take the byte from their
-// neighbours by DPP wave shifts); others re-read their own first dword (in cache; one
-// unconditional load keeps the compiler's load waits counted)
+// neighbours by DPP wave shifts); the others all read the wave's first dword (one address: one
+// request; one unconditional load keeps the compiler's load waits counted). (r4: each re-read
+// its own first dword, 64 lines per wave-instruction, and behind the nt granule loads every one
+// went back to HBM: the fused histogram fetched 1.58 GB per GiB, profiles/r5z_C5_pmc_traffic.json)
 static __device__ __forceinline__ uint64_t fe_edge_addr(uint64_t p, int lane, uint64_t n)
 {
-    return lane == 0 ? (p >= 4 ? p - 4 : p) : lane == 63 ? (p + 16 < n ? p + 16 : p) : p;
+    return lane == 0 ? (p >= 4 ? p - 4 : p) : lane == 63 ? (p + 16 < n ? p + 16 : p) : p - 16 * (uint64_t)lane;
 }
 // pair starts among the 16 bytes w4 (q = the byte after them, 0 past the input): 0x80 in
 // byte j of st[k] = a START at byte 4k + j
