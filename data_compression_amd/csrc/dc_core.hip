@@ -5671,11 +5671,11 @@ __global__ __launch_bounds__(64) void k_nyb_resolve_c(uint8_t *__restrict__ out,
 //  * output gathers in an LDS ring of two 64-B lines per lane and leaves as whole lines (4 x
 //    16 B) at the IO points; the line the stream shares with the bytes before it waits in LDS
 //    and goes byte by byte at the end, with the last partial line (NlOut).
-#define NL_RING 256    /* decoder input ring per lane (bytes) */
-#define NL_RSTR 272    /* its LDS row stride: 16-B aligned, lanes' rows 4 banks apart */
-#define NL_ORING 128   /* output ring per lane: the line being gathered and the next */
-#define NL_OSTR 144
-#define NL_HSTR 80     /* the head line's row */
+#define NL_RING 128    /* decoder input ring per lane (bytes): two 64-B blocks behind the one in flight */
+#define NL_RSTR 144    /* its LDS row stride: 16-B aligned, lanes' rows 4 banks apart */
+#define NL_LINE 128    /* output leaves in whole 128-B lines (64-B halves a point apart wrote 1.46x) */
+#define NL_ORING 256   /* output ring per lane: the line being gathered and the next */
+#define NL_OSTR 272
 #define NL_P 32        /* decoder steps between two IO points (<= 32 bytes in, <= 32 out) */
 __device__ uint4 nl_zero[1];   // the granule lanes without a stream read (never written)
 // (granule pointers are formed as p - (p & 15), never through an integer: a pointer rebuilt from
@@ -5683,44 +5683,42 @@ __device__ uint4 nl_zero[1];   // the granule lanes without a stream read (never
 // of the byte loop waited for the granules in flight)
 static __device__ __forceinline__ uint4 nl_ld(const uint4 *p) { return *p; }
 
-struct NlOut {        // a lane's output [b + sh, ...): b = the start rounded down to 64 B
+struct NlOut {        // a lane's output [b + sh, ...): b = the start rounded down to NL_LINE
     uint8_t *b;
     uint32_t sh;
-    uint64_t S;       // next line to send (offset from b, a multiple of 64)
-    bool head;        // line 0 holds bytes before the stream: kept in hrow, sent byte by byte
-    uint8_t *ring, *hrow;
+    uint64_t S;       // next line to send (offset from b, a multiple of NL_LINE)
+    uint8_t *ring;
 };
-static __device__ __forceinline__ void nl_out_init(NlOut &o, uint8_t *dst, uint8_t *ring, uint8_t *hrow)
+static __device__ __forceinline__ void nl_out_init(NlOut &o, uint8_t *dst, uint8_t *ring)
 {
-    o.sh = (uint32_t)((uintptr_t)dst & 63);
+    o.sh = (uint32_t)((uintptr_t)dst & (NL_LINE - 1));
     o.b = dst - o.sh;
     o.S = 0;
-    o.head = false;
     o.ring = ring;
-    o.hrow = hrow;
 }
-// W = offset from b past the last byte put: send the line it completed (one per point at most)
+// W = offset from b past the last byte put: send the line it completed (one per point at most:
+// <= 32 bytes are put between points). The stream's first line, which holds bytes before the
+// stream, goes byte by byte (once per stream).
 static __device__ __forceinline__ void nl_out_point(NlOut &o, uint64_t W)
 {
-    if (W >= o.S + 64) {
+    if (W >= o.S + NL_LINE) {
         const uint4 *src = reinterpret_cast<const uint4 *>(o.ring + (o.S & (NL_ORING - 1)));
-        const uint4 v0 = src[0], v1 = src[1], v2 = src[2], v3 = src[3];
         if (o.S < o.sh) {
-            uint4 *h = reinterpret_cast<uint4 *>(o.hrow);
-            h[0] = v0; h[1] = v1; h[2] = v2; h[3] = v3;
-            o.head = true;
+            for (uint32_t a = o.sh; a < NL_LINE; ++a) o.b[a] = o.ring[a];
         } else {
+            uint4 v[NL_LINE / 16];
+#pragma unroll
+            for (int k = 0; k < NL_LINE / 16; ++k) v[k] = src[k];
             uint4 *d = reinterpret_cast<uint4 *>(o.b + o.S);
-            d[0] = v0; d[1] = v1; d[2] = v2; d[3] = v3;
+#pragma unroll
+            for (int k = 0; k < NL_LINE / 16; ++k) d[k] = v[k];
         }
-        o.S += 64;
+        o.S += NL_LINE;
     }
 }
 static __device__ __forceinline__ void nl_out_finish(const NlOut &o, uint64_t W)
 {
     for (uint64_t a = o.S > o.sh ? o.S : o.sh; a < W; ++a) o.b[a] = o.ring[a & (NL_ORING - 1)];
-    if (o.head)
-        for (uint32_t a = o.sh; a < 64; ++a) o.b[a] = o.hrow[a];
 }
 
 // Lockstep walk of bytes [lo, hi) of a lane's granules g (offsets from g; every lane of the
@@ -5760,7 +5758,6 @@ __global__ __launch_bounds__(64) void k_nyb_chunk_enc(const uint8_t *__restrict_
 {
     __shared__ uint64_t s_L[16][64];
     __shared__ __attribute__((aligned(16))) uint8_t s_out[64 * NL_OSTR];
-    __shared__ __attribute__((aligned(16))) uint8_t s_head[64 * NL_HSTR];
     const int t = threadIdx.x;
     const uint64_t ch = (uint64_t)blockIdx.x * 64 + t;
     const bool live = ch < nchunks;
@@ -5769,7 +5766,7 @@ __global__ __launch_bounds__(64) void k_nyb_chunk_enc(const uint8_t *__restrict_
     uint8_t *const slot = scr + (live ? ch * ((uint64_t)K + 2) : 0);
     for (int c = 0; c < 16; ++c) s_L[c][t] = mtf_init_word();
     NlOut o;
-    nl_out_init(o, slot, s_out + t * NL_OSTR, s_head + t * NL_HSTR);
+    nl_out_init(o, slot, s_out + t * NL_OSTR);
     uint64_t q = 0;   // bytes put
     auto put = [&](uint32_t v) { o.ring[(o.sh + q) & (NL_ORING - 1)] = (uint8_t)v; ++q; };
     uint32_t prev = len ? x[0] : 0u;
@@ -5872,7 +5869,7 @@ __global__ __launch_bounds__(256) void k_nyb_chunk_copy(const uint8_t *__restric
 // a token each (a nybble with bit 3 set: a hit, its rank; any other: a literal of 2 nybbles).
 static __device__ __forceinline__ bool nyb_wave_decode(const uint8_t *__restrict__ src, uint64_t m, uint64_t expect, int modify,
                                        bool any_type, uint8_t *__restrict__ o, bool live, uint64_t (*sL)[64],
-                                       uint8_t *ring, uint8_t *oring, uint8_t *hrow, int t)
+                                       uint8_t *ring, uint8_t *oring, int t)
 {
     if (!live) m = 0;
     // the input ring: ring[F - NL_RING, F) holds the stream's bytes from offset F - NL_RING of g
@@ -5882,10 +5879,11 @@ static __device__ __forceinline__ bool nyb_wave_decode(const uint8_t *__restrict
     const uint4 *const g = m ? reinterpret_cast<const uint4 *>(src - (sa & 15)) : nl_zero;
     const uint64_t gl = m ? (sh + m - 1) >> 4 : 0;
 #pragma unroll
-    for (int j = 0; j < 12; ++j) reinterpret_cast<uint4 *>(ring)[j] = nl_ld(g + min((uint64_t)j, gl));
-    uint64_t F = 192;
-    uint4 r0 = nl_ld(g + min((uint64_t)12, gl)), r1 = nl_ld(g + min((uint64_t)13, gl)),
-          r2 = nl_ld(g + min((uint64_t)14, gl)), r3 = nl_ld(g + min((uint64_t)15, gl));
+    for (int j = 0; j < NL_RING / 16; ++j) reinterpret_cast<uint4 *>(ring)[j] = nl_ld(g + min((uint64_t)j, gl));
+    uint64_t F = NL_RING;
+    constexpr uint64_t f0 = NL_RING / 16;
+    uint4 r0 = nl_ld(g + min(f0, gl)), r1 = nl_ld(g + min(f0 + 1, gl)), r2 = nl_ld(g + min(f0 + 2, gl)),
+          r3 = nl_ld(g + min(f0 + 3, gl));
     const uint32_t type = m ? ring[sh] : 0u;
     const bool raw = type != 0xAFu;
     bool ok = live;
@@ -5900,7 +5898,7 @@ static __device__ __forceinline__ bool nyb_wave_decode(const uint8_t *__restrict
     uint64_t pos = sh + (raw ? (type == ' ' ? 1u : 0u) : 1u);   // offset (from g) of the next byte
     const uint64_t pe = sh + m;
     NlOut out;
-    nl_out_init(out, o, oring, hrow);
+    nl_out_init(out, o, oring);
     uint64_t q = 0;
     uint32_t prev = 0;
     int offn = 0;
@@ -5927,7 +5925,8 @@ static __device__ __forceinline__ bool nyb_wave_decode(const uint8_t *__restrict
             }
         }
         // top the ring up while it leaves room (the bytes below pos are done with), and start the
-        // next 64 B (pos moves <= NL_P bytes between points, F - pos stays >= 64 - NL_P)
+        // next 64 B (pos moves <= NL_P bytes between points: F - pos stays >= 2, and a block is
+        // written over bytes below pos only)
         if (F - pos <= NL_RING - 64) {
             uint4 *d = reinterpret_cast<uint4 *>(ring + (F & (NL_RING - 1)));
             d[0] = r0; d[1] = r1; d[2] = r2; d[3] = r3;
@@ -5956,7 +5955,6 @@ __global__ __launch_bounds__(64) void k_nyb_chunk_dec(const uint8_t *__restrict_
     __shared__ uint64_t s_L[16][64];
     __shared__ __attribute__((aligned(16))) uint8_t s_in[64 * NL_RSTR];
     __shared__ __attribute__((aligned(16))) uint8_t s_out[64 * NL_OSTR];
-    __shared__ __attribute__((aligned(16))) uint8_t s_head[64 * NL_HSTR];
     const int t = threadIdx.x;
     const uint64_t ch = (uint64_t)blockIdx.x * 64 + t;
     bool live = ch < nchunks;
@@ -5964,7 +5962,7 @@ __global__ __launch_bounds__(64) void k_nyb_chunk_dec(const uint8_t *__restrict_
     const uint64_t expect = live ? ((n - ch * K < K) ? n - ch * K : K) : 0;
     if (live && (b < a || b > total || b - a < 1)) { *err = 1; live = false; }
     const bool ok = nyb_wave_decode(payload + a, live ? b - a : 0, expect, modify, false, out + (live ? ch * K : 0),
-                                    live, s_L, s_in + t * NL_RSTR, s_out + t * NL_OSTR, s_head + t * NL_HSTR, t);
+                                    live, s_L, s_in + t * NL_RSTR, s_out + t * NL_OSTR, t);
     if (live && !ok) *err = 1;
 }
 
@@ -6009,7 +6007,6 @@ __global__ __launch_bounds__(64) void k_nyb_batch_dec(const uint8_t *__restrict_
     __shared__ uint64_t s_L[16][64];
     __shared__ __attribute__((aligned(16))) uint8_t s_in[64 * NL_RSTR];
     __shared__ __attribute__((aligned(16))) uint8_t s_out[64 * NL_OSTR];
-    __shared__ __attribute__((aligned(16))) uint8_t s_head[64 * NL_HSTR];
     const int t = threadIdx.x;
     const uint64_t i = (uint64_t)blockIdx.x * 64 + t;
     bool live = i < count;
@@ -6017,7 +6014,7 @@ __global__ __launch_bounds__(64) void k_nyb_batch_dec(const uint8_t *__restrict_
     live = live && b >= a;   // (flagged by k_nyb_batch_len)
     const uint64_t o0 = live ? out_off[i] : 0, o1 = live ? out_off[i + 1] : 0;
     const bool ok = nyb_wave_decode(in + a, live ? b - a : 0, o1 - o0, modify, true, out + o0, live, s_L,
-                                    s_in + t * NL_RSTR, s_out + t * NL_OSTR, s_head + t * NL_HSTR, t);
+                                    s_in + t * NL_RSTR, s_out + t * NL_OSTR, t);
     if (live && !ok) *err = 1;
 }
 
@@ -6213,7 +6210,7 @@ static int ctx_create(dc_ctx **out, int device, void *stream, bool own)
         return DC_E_HIP;
     }
     c->opt_d8_static = D8_STATIC_PCT;
-    {   // A/B knobs of tools/ab_env.sh and tools/dec_ab.py, read once per context and clamped
+    {   // A/B knobs (environment; tools/kern_ab.py sets the same options per context), read once and clamped
         const char *e;
         if ((e = getenv("DC_HIST_GRID"))) (void)dc_ctx_set_option(c, DC_OPT_HIST_GRID, atoll(e));
         if ((e = getenv("DC_PACK_GRID"))) (void)dc_ctx_set_option(c, DC_OPT_PACK_GRID, atoll(e));

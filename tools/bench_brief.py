@@ -1,4 +1,4 @@
-"""One-line summary of a bench.py JSON line on stdin (tools/gpu_r4.sh)."""
+"""One-line summary of a bench.py JSON line on stdin."""
 import json
 import sys
 
