@@ -62,6 +62,11 @@ def parse():
     ap.add_argument("--gather-reps", type=int, default=5,
                     help="N > 1: timed gathers of the whole stream to rank 0 after the timed region")
     ap.add_argument("--profile-steps", type=int, default=20)
+    ap.add_argument("--in-flight", type=int, default=2,
+                    help="steps in flight: L codec contexts, each on its own HIP stream with its own buffers, "
+                         "take steps i = j mod L (at one GPU each from its own host thread), so one step's "
+                         "serial tail (table build, plan, redo, host reads) overlaps the next step's kernels. "
+                         "Every step still codes the whole input; ms_per_step_serial beside it is one context")
     ap.add_argument("--codec", default="huffman", choices=["huffman", "nybble"],
                     help="nybble: nybble_compression.c's codec on 1 GiB of English-like text (--mode)")
     ap.add_argument("--mode", default="static", choices=["static", "adaptive"],
@@ -110,78 +115,40 @@ def main():
         S = int(st.item())
     ngroups, nchunks = c.sync_sizes(n, S)
 
-    from data_compression_amd.dist import ShardedHuffman
-    sh = ShardedHuffman(c, table_mode=a.table_mode)
-    hist = torch.empty(256, dtype=torch.int64, device=dev)
-    tab = torch.empty(c.table_bytes, dtype=torch.uint8, device=dev)
-    total = torch.empty(1, dtype=torch.int64, device=dev)
-    words = torch.empty(c.words_needed(2**40, 32 * n) + 8, dtype=torch.int32, device=dev)
-    sync = c.alloc_sync(n, S)
-    out = torch.empty(n, dtype=torch.uint8, device=dev)
-    state = {}
-
-    def encode():   # hist -> [all_reduce] -> table -> plan -> [all_gather] -> pack
-        state["s"] = sh.encode(x, a.nary, S, words=words, sync=sync, hist=hist, table=tab, total=total)
-
-    def decode():
-        sh.decode(state["s"], out=out)
-
-    if a.frontend:   # C5: front-end bodies + halo/LITERAL/re-cut exchanges, then sharded Huffman
-        from data_compression_amd.dist import ShardedSmall
-        ss = ShardedSmall(c, table_mode=a.table_mode, fused=not a.two_stage)
-        sync_fe = c.alloc_sync(n + 1, S)   # the front-end stream holds up to n + 1 symbols
-        gsync_fe = c.alloc_sync(n + 1 + 2 * S, S) if world > 1 else None   # (a shard's part of the stream's index)
-
-        def encode():   # noqa: F811
-            state["s"] = ss.encode(x, a.nary, S, words=words, sync=sync_fe, table=tab, total=total, gsync=gsync_fe)
-
-        fe_out = torch.empty(2 * n + 64, dtype=torch.uint8, device=dev)   # dc_small_decompress: >= 2 * m
-
-        def decode():   # noqa: F811
-            state["dec"] = ss.decode(state["s"], out=fe_out)
-
-    def step():
-        encode()
-        decode()
-
+    lanes = [Lane(a, dev, local, x, S, n, world) for _ in range(max(1, a.in_flight))]
+    lane0 = lanes[0]
+    c, state = lane0.c, lane0.state
+    threaded = world == 1   # (at N > 1 one host thread keeps every rank's collectives in one order)
     _phase(rank, "buffers ready")
-    for _ in range(a.prewarm + a.warmup):   # the same count on every rank (steps hold collectives)
-        step()
+    run_steps(lanes, a.prewarm + a.warmup, threaded)   # the same count on every rank (steps hold collectives)
     torch.cuda.synchronize()
     _phase(rank, "warmup done")
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    if world > 1:
-        tt = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        el = float(tt.item())
-    ms_step = el / a.steps * 1e3
+    ms_step = timed_steps(lanes, a.steps, threaded, world, dev)
     _phase(rank, "timed steps done")
+    ms_serial = timed_steps(lanes[:1], a.steps, False, world, dev) if len(lanes) > 1 else ms_step
+    _phase(rank, "serial steps done")
+    torch.cuda.set_stream(lane0.stream)   # the rest runs on lane 0 (its codec's stream)
+    encode, decode, step = lane0.encode, lane0.decode, lane0.step
+    sh = lane0.sh
     # encode / decode split: HIP events on the codec's stream (torch's current stream) inside
     # back-to-back steps run right after the timed region (clocks still at their steady
     # state): before the histogram, between the pack and the decode, after the redo, so
-    # encode_ms + decode_ms is the step (split_step_ms beside ms_per_step shows it)
+    # encode_ms + decode_ms is the step (split_step_ms beside ms_per_step shows it). The
+    # per-kernel HIP-event durations follow, then the copy probe: all before the round-trip
+    # checks (the first steps after a 1 GiB torch.equal ran ~2 ms slower in all, which moved
+    # whichever timing came next, tools/bench_split_diag.py)
     enc_ms, dec_ms, split_step_ms = split_timed(encode, decode, a.profile_steps)
+    c.timing(True)
+    for _ in range(a.profile_steps):
+        step()
+    kt = c.timings()
+    c.timing(False)
+    copy_gbps = copy_probe(c, x, a.profile_steps)
 
     # ---- correctness of the measured configuration (outside the timed region) ----------
-    st = c.pack_status(state["s"].table if a.frontend else tab)
-    y = state["dec"] if a.frontend else out
-    if a.frontend and world > 1:
-        # a rank's decoded front-end segment covers a different byte range than its input
-        # shard (the re-cut moves bytes between ranks): compare the concatenations through a
-        # position-weighted checksum over global offsets
-        ok = st == 0 and c.decode_status() == 0 and _concat_equal(y, x, world, dev)
-    else:
-        ok = st == 0 and c.decode_status() == 0 and bool(torch.equal(y, x))
-    bits = state["s"].bits if a.frontend else int(total.item())   # this rank's payload bits
+    st = c.pack_status(state["s"].table)
+    ok = st == 0 and all([ln.roundtrip_ok() for ln in lanes])   # (each lane's last step)
+    bits = state["s"].bits if a.frontend else int(lane0.total.item())   # this rank's payload bits
     if world > 1:
         okt = torch.tensor([1 if ok else 0], device=dev)
         dist.all_reduce(okt, op=dist.ReduceOp.MIN)
@@ -218,15 +185,6 @@ def main():
             gather["bytes_to_rank0"] = int(g[0].numel() * 4 + g[2].numel() * 8 + g[3].numel() * 2)
         _phase(rank, "gather timed")
 
-    # ---- encode / decode split and per-kernel HIP-event durations ------------------------
-    # The split comes from the same back-to-back step loop as the timed region: HIP events on
-    # the codec's stream (torch's current stream) before the histogram, between the pack and
-    # the decode, and after the redo of every step, so encode_ms + decode_ms is the step.
-    c.timing(True)
-    for _ in range(a.profile_steps):
-        step()
-    kt = c.timings()
-    c.timing(False)
     per = {}
     for name, ms in kt:
         per.setdefault(name, []).append(ms)
@@ -253,7 +211,6 @@ def main():
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
     traffic, traffic_src = pmc_traffic("k_" + dom, a, n)
     rp_ms, rp_src = rocprof_mean("k_" + dom, a, n)
-    copy_gbps = copy_probe(c, x, a.profile_steps)
 
     # whole-pipeline rooflines (SURVEY §8(d) bytes over the whole encode / whole decode time:
     # extra passes such as the histogram's read of the input count against them)
@@ -270,6 +227,8 @@ def main():
         "warmup": a.warmup,
         "prewarm": a.prewarm,
         "ms_per_step": round(ms_step, 4),
+        "in_flight": len(lanes),
+        "ms_per_step_serial": round(ms_serial, 4),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -329,45 +288,19 @@ def main_nybble(a, dev, rank, world):
       adaptive nybble_compress (modify=true); its decode is sequential by definition (each
                byte's list depends on every byte before it), timed once on a 16 MiB sample
     N > 1: every rank codes its own 1 GiB stream (independent objects, no collective)."""
-    from data_compression_amd import synth
-    from data_compression_amd.device import Codec
     n = a.size
     modify = a.mode == "adaptive"
     x = bench_input("C1", n, 0xC1 + 7919 * rank, dev)
     torch.cuda.synchronize()
-    c = Codec(dev.index or 0)
-    comp_buf = torch.empty(n + 2, dtype=torch.uint8, device=dev)
-    out = torch.empty(2 * n + 16, dtype=torch.uint8, device=dev)
-    st = {}
-
-    def encode():
-        st["comp"] = c.nyb_compress(x, modify, out=comp_buf)
-
-    def decode():
-        st["y"] = c.nyb_decompress(st["comp"], modify, out=out)
-
-    def step():
-        encode()
-        if not modify:
-            decode()
-
-    for _ in range(a.prewarm + a.warmup):   # the same count on every rank (steps hold collectives)
-        step()
+    lanes = [NybLane(dev, x, modify) for _ in range(max(1, a.in_flight))]
+    lane0 = lanes[0]
+    c, st, encode, decode, step = lane0.c, lane0.st, lane0.encode, lane0.decode, lane0.step
+    # (no collective in a step: every lane has a host thread of its own at any N)
+    run_steps(lanes, a.prewarm + a.warmup, True)
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    if world > 1:
-        tt = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        el = float(tt.item())
-    ms_step = el / a.steps * 1e3
+    ms_step = timed_steps(lanes, a.steps, True, world, dev)
+    ms_serial = timed_steps(lanes[:1], a.steps, False, world, dev) if len(lanes) > 1 else ms_step
+    torch.cuda.set_stream(lane0.stream)   # the rest runs on lane 0 (its codec's stream)
     m = st["comp"].numel()
 
     def timed(fn, k):
@@ -414,12 +347,16 @@ def main_nybble(a, dev, rank, world):
                      "path": "dc_nyb_decompress_batch: one lane per independent stream (lengths, scan, decode)"}
     else:
         dec_ms = timed(decode, a.profile_steps)
-        ok = bool(torch.equal(st["y"], x))
+        ok = True
     c.timing(True)
     for _ in range(a.profile_steps):
         step()
     kt = c.timings()
     c.timing(False)
+    # round trips after the timings (bench.py main: a 1 GiB compare slows the steps after it);
+    # adaptive: every lane's stream equals lane 0's, whose round trip the sample checked
+    ok = ok and all([ln.roundtrip_ok() if not modify else bool(torch.equal(ln.st["comp"], st["comp"]))
+                     for ln in lanes])
     per = {}
     for name, ms in kt:
         per.setdefault(name, []).append(ms)
@@ -451,7 +388,9 @@ def main_nybble(a, dev, rank, world):
         "metric": NYB_METRIC if not modify else NYB_METRIC.replace("encode+decode", "encode"),
         "value": round(world * n / (ms_step * 1e-3) / 1e9, 2),
         "unit": "GB/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup, "prewarm": a.prewarm,
-        "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "ms_per_step": round(ms_step, 4),
+        "in_flight": len(lanes),
+        "ms_per_step_serial": round(ms_serial, 4), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "u8", "data": "synthetic",
         "config": {"workload": f"nybble {'adaptive (nybble_compress)' if modify else 'static (compress_bytestring)'}"
                                f" on {n >> 20} MiB of C1 English-like text per GPU"
@@ -484,6 +423,37 @@ def main_nybble(a, dev, rank, world):
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+class NybLane:
+    """bench.py's nybble step (main_nybble) on a codec context of its own, on its own HIP stream
+    with its own buffers (steps in flight, as Lane)."""
+
+    def __init__(self, dev, x, modify):
+        from data_compression_amd.device import Codec
+        n = x.numel()
+        self.stream = torch.cuda.Stream(dev)
+        self.x, self.modify, self.st = x, modify, {}
+        with torch.cuda.stream(self.stream):
+            self.c = Codec(dev.index or 0, stream=self.stream)
+            self.comp_buf = torch.empty(n + 2, dtype=torch.uint8, device=dev)
+            self.out = torch.empty(2 * n + 16, dtype=torch.uint8, device=dev)
+
+    def encode(self):
+        self.st["comp"] = self.c.nyb_compress(self.x, self.modify, out=self.comp_buf)
+
+    def decode(self):
+        self.st["y"] = self.c.nyb_decompress(self.st["comp"], self.modify, out=self.out)
+
+    def step(self):
+        with torch.cuda.stream(self.stream):
+            self.encode()
+            if not self.modify:
+                self.decode()
+
+    def roundtrip_ok(self):   # (adaptive: main_nybble checks a sample's round trip)
+        with torch.cuda.stream(self.stream):
+            return self.modify or bool(torch.equal(self.st["y"], self.x))
 
 
 def cpu_baseline_nybble(x, a, modify):
@@ -637,6 +607,117 @@ def rocprof_mean(kernel, a, n):
 
 def _r(v, nd):
     return None if v is None else round(v, nd)
+
+
+class Lane:
+    """One codec context on its own HIP stream with its own buffers: the bench step (encode +
+    decode of the whole input x, world ranks) as lane.step(). Steps in flight (--in-flight)
+    are lanes taking alternate steps; a lane's state holds its last step's stream and output."""
+
+    def __init__(self, a, dev, local, x, S, n, world):
+        from data_compression_amd.device import Codec
+        from data_compression_amd.dist import ShardedHuffman, ShardedSmall
+        self.stream = torch.cuda.Stream(dev)
+        self.x, self.n, self.world, self.dev, self.frontend = x, n, world, dev, a.frontend
+        self.state = st = {}
+        with torch.cuda.stream(self.stream):
+            self.c = c = Codec(local, stream=self.stream)
+            self.sh = sh = ShardedHuffman(c, table_mode=a.table_mode)
+            hist = torch.empty(256, dtype=torch.int64, device=dev)
+            self.tab = tab = torch.empty(c.table_bytes, dtype=torch.uint8, device=dev)
+            self.total = total = torch.empty(1, dtype=torch.int64, device=dev)
+            words = torch.empty(c.words_needed(2**40, 32 * n) + 8, dtype=torch.int32, device=dev)
+            if not a.frontend:
+                sync = c.alloc_sync(n, S)
+                self.out = out = torch.empty(n, dtype=torch.uint8, device=dev)
+
+                def encode():   # hist -> [all_reduce] -> table -> plan -> [all_gather] -> pack
+                    st["s"] = sh.encode(x, a.nary, S, words=words, sync=sync, hist=hist, table=tab, total=total)
+
+                def decode():
+                    sh.decode(st["s"], out=out)
+                    st["dec"] = out
+            else:   # C5: front-end bodies + halo/LITERAL/re-cut exchanges, then sharded Huffman
+                ss = ShardedSmall(c, table_mode=a.table_mode, fused=not a.two_stage)
+                sync_fe = c.alloc_sync(n + 1, S)   # the front-end stream holds up to n + 1 symbols
+                gsync_fe = c.alloc_sync(n + 1 + 2 * S, S) if world > 1 else None   # (a shard's part of the stream's index)
+                fe_out = torch.empty(2 * n + 64, dtype=torch.uint8, device=dev)   # dc_small_decompress: >= 2 * m
+
+                def encode():
+                    st["s"] = ss.encode(x, a.nary, S, words=words, sync=sync_fe, table=tab, total=total, gsync=gsync_fe)
+
+                def decode():
+                    st["dec"] = ss.decode(st["s"], out=fe_out)
+        self.encode, self.decode = encode, decode
+
+    def step(self):
+        with torch.cuda.stream(self.stream):
+            self.encode()
+            self.decode()
+
+    def roundtrip_ok(self):
+        with torch.cuda.stream(self.stream):
+            y = self.state["dec"]
+            if self.frontend and self.world > 1:
+                # a rank's decoded front-end segment covers a different byte range than its input
+                # shard (the re-cut moves bytes between ranks): compare the concatenations through
+                # a position-weighted checksum over global offsets
+                ok = _concat_equal(y, self.x, self.world, self.dev)
+            else:
+                ok = bool(torch.equal(y, self.x))
+            return self.c.decode_status() == 0 and ok
+
+
+def run_steps(lanes, k, threaded):
+    """k steps, step i on lane i mod L. threaded: one host thread per lane (a codec call that
+    ends in a host read then blocks only its own lane); otherwise issued in order by this
+    thread (at N > 1: every rank's collectives in the same order)."""
+    nl = len(lanes)
+    if nl == 1 or not threaded:
+        for i in range(k):
+            lanes[i % nl].step()
+        return
+    import threading
+    dev = torch.cuda.current_device() if torch.cuda.is_available() else None
+    errs = []
+
+    def work(j):
+        try:
+            if dev is not None:   # (the current device is per thread)
+                torch.cuda.set_device(dev)
+            for _ in range(j, k, nl):
+                lanes[j].step()
+        except BaseException as e:   # re-raised on the calling thread
+            errs.append(e)
+
+    ts = [threading.Thread(target=work, args=(j,)) for j in range(1, nl)]
+    for t in ts:
+        t.start()
+    work(0)
+    for t in ts:
+        t.join()
+    if errs:
+        raise errs[0]
+
+
+def timed_steps(lanes, k, threaded, world, dev):
+    """ms per step of k steps over the lanes, bracketed by a barrier and a device-wide
+    synchronize on both sides; the max over ranks."""
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run_steps(lanes, k, threaded)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+    return el / k * 1e3
 
 
 def split_timed(encode, decode, k):
