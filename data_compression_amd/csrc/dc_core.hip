@@ -4621,6 +4621,169 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
     }
 }
 
+// Static nybble encode writer, one wave per 4096-element tile (k_nyb_tiles' geometry): lane l
+// owns the 64 contiguous elements [64 l, 64 l + 64) of its wave's tile, read as four aligned
+// 16-B granules plus the next lane's first dword (DPP; lane 63 loads it), so no per-16-element
+// window shuffles; its composition is folded from four 16-element ones (their states from both
+// entry states kept for the writer) and scanned across the wave once: no workgroup barrier and
+// no cross-wave combination per tile. The four waves of a workgroup share the lookup tables
+// only; each stages its tile's output in an LDS row of its own, written as k_fsm_write's SWAR
+// writer does (dwords OR-ed at the run's bit offset), then stored as whole granules. Static
+// dictionary only (no rank array) and a 16-B aligned input: fsm_run takes k_fsm_write otherwise.
+__global__ __launch_bounds__(256) void k_nyb_enc_wtile(const uint8_t *__restrict__ in, uint64_t len, uint64_t nelem,
+                                                       uint64_t ntiles, const uint64_t *__restrict__ entry,
+                                                       const uint4 *__restrict__ loc, const uint64_t *__restrict__ meta,
+                                                       uint8_t *__restrict__ out, FsmAux aux)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t s_out[4][2 * FSM_TILE + 32];
+    __shared__ __attribute__((aligned(4))) uint8_t s_rank[256];
+    __shared__ uint2 s_esel[256];
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    fsm_rank_table(s_rank);
+    s_esel[t] = make_uint2(c_nyb.esel_lo[t], c_nyb.esel_hi[t]);   // (NybTables)
+    const uint64_t T = (uint64_t)blockIdx.x * 4 + (uint64_t)wid;
+    const bool live = T < ntiles;
+    const uint64_t j0 = T * FSM_TILE + 64 * (uint64_t)lane;   // the lane's first element (stream byte j0 + 1)
+    // every global read first: bytes [j0, j0 + 64), the byte after them, the tile's entry
+    uint32_t D[17];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint64_t o = j0 + 16 * (uint64_t)i;
+        const uint4 g = (live && o < len) ? ld_nt(reinterpret_cast<const uint4 *>(in + o)) : make_uint4(0u, 0u, 0u, 0u);
+        D[4 * i] = g.x; D[4 * i + 1] = g.y; D[4 * i + 2] = g.z; D[4 * i + 3] = g.w;
+    }
+    D[16] = dpp_wave_shl1(D[0]);
+    if (lane == 63) D[16] = (live && j0 + 64 < len) ? *reinterpret_cast<const uint32_t *>(in + j0 + 64) : 0u;
+    const uint64_t Tc = live ? T : ntiles - 1;
+    const uint64_t e = entry[Tc / FSM_GROUP];
+    const uint4 lc = loc[Tc];
+    const bool whole = aux.whole != 0;
+    const uint64_t body = meta[0] + (aux.is_last ? meta[1] : 0);
+    if (whole && 2 + body >= len) {   // LITERAL (:1018-1037): ' ' + the raw bytes, one grid-stride pass
+        for (uint64_t i = (uint64_t)blockIdx.x * 256 + t; i < len; i += (uint64_t)gridDim.x * 256) out[1 + i] = in[i];
+        if (blockIdx.x == 0 && t == 0) out[0] = ' ';
+        return;
+    }
+    if (blockIdx.x == 0 && t == 0 && whole) { out[0] = 0xAF; out[1] = in[0]; }
+    __syncthreads();   // s_rank, s_esel
+    if (!live) return;   // (whole waves: no barrier below)
+    // ranks, 4 per dword (element order), and the 16-element blocks' hit masks and states
+    uint32_t RK[16], A[4], V[4], S0[4], S1[4];
+    uint32_t comp = FSMP_ID;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const uint32_t X = __builtin_amdgcn_alignbyte(D[q + 1], D[q], 1u);
+        RK[q] = (uint32_t)s_rank[X & 255u] | ((uint32_t)s_rank[(X >> 8) & 255u] << 8) |
+                ((uint32_t)s_rank[(X >> 16) & 255u] << 16) | ((uint32_t)s_rank[X >> 24] << 24);
+    }
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        const uint64_t kb = j0 + 16 * (uint64_t)b;
+        V[b] = kb >= nelem ? 0u : nelem - kb >= 16 ? 0xFFFFu : (1u << (uint32_t)(nelem - kb)) - 1u;
+        uint32_t h = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {   // a hit: rank byte < 0x80; 4 byte flags -> 4 bits
+            const uint32_t m = (~RK[4 * b + q] >> 7) & 0x01010101u;
+            h |= (((m * 0x204081u) >> 21) & 15u) << (4 * q);
+        }
+        A[b] = h & V[b];
+        S0[b] = nyb_enc_states(A[b], V[b], 0u);
+        S1[b] = nyb_enc_states(A[b], V[b], 1u);
+        const uint32_t miss = ~A[b] & V[b];
+        Fsm f;
+        f.c0 = __popc(A[b] & S0[b] & 0xFFFFu) + __popc(miss) + __popc(miss & S0[b]);
+        f.c1 = __popc(A[b] & S1[b] & 0xFFFFu) + __popc(miss) + __popc(miss & S1[b]);
+        f.s0 = (S0[b] >> 16) & 1u;
+        f.s1 = (S1[b] >> 16) & 1u;
+        comp = fsmp_then(comp, fsmp(f));
+    }
+    uint32_t xp;
+    const uint32_t inc = fsmp_wave_scan(comp, &xp);
+    const uint32_t s_g = (uint32_t)(e & 1);
+    const uint64_t o_tile = (e >> 1) + (s_g ? lc.y : lc.x) + (whole ? 2 : 0);   // the tile's first output byte
+    const uint32_t s_tile = s_g ? lc.w : lc.z;
+    const Fsm x = fsmp_unpack(xp), tot = fsmp_unpack((uint32_t)__builtin_amdgcn_readlane((int)inc, 63));
+    const uint64_t o0 = o_tile + (s_tile ? x.c1 : x.c0);
+    uint32_t st = s_tile ? x.s1 : x.s0;
+    const uint64_t s_end = o_tile + (s_tile ? tot.c1 : tot.c0);
+    const int64_t o_al = (int64_t)((((uintptr_t)(out + o_tile)) & ~(uintptr_t)15) - (uintptr_t)out);
+    uint4 *const so = reinterpret_cast<uint4 *>(s_out[wid]);
+    for (int i = lane; i < (2 * FSM_TILE + 32) / 16; i += 64) so[i] = make_uint4(0u, 0u, 0u, 0u);
+    __builtin_amdgcn_wave_barrier();
+    uint32_t *const s_out32 = reinterpret_cast<uint32_t *>(s_out[wid]);
+    const uint32_t P = (uint32_t)((int64_t)o0 - o_al);   // stage byte of the lane's first output
+    uint32_t di = P >> 2, nb = 8u * (P & 3u), pend = 0;
+    // the rank of a hit pending before element 0: the byte before it, or the shard's carried one
+    const uint32_t rp0 = j0 ? (uint32_t)s_rank[D[0] & 255u] : aux.pend_rank;
+    uint64_t ob = o0;   // the output byte of the block's first element
+    auto bytes = [](uint32_t m4) {   // 4 mask bits -> 0xFF per byte
+        const uint32_t u = (m4 * 0x204081u) & 0x01010101u;
+        return (u << 8) - u;
+    };
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        const uint32_t S = st ? S1[b] : S0[b];
+        const uint32_t Hx = A[b] | (~V[b] & 0xFFFFu), Sx = S & V[b];   // (past the input: a hit in state 0)
+        const uint32_t C1 = ~Hx | Sx, C2 = ~Hx & Sx;   // element writes its first / second byte
+        if (aux.is_last && len >= 2 && len - 2 >= j0 + 16 * (uint64_t)b && len - 2 < j0 + 16 * (uint64_t)b + 16) {
+            // odd tail (:1000-1009): the stream's last element a hit left pending: its byte, raw,
+            // after the bytes of the elements before it
+            const uint32_t kt = (uint32_t)(len - 2 - j0 - 16 * (uint64_t)b);
+            if (((Hx & ~Sx) >> kt) & 1u) {
+                const uint32_t below = (1u << kt) - 1u;
+                const uint32_t k = 16u * (uint32_t)b + kt + 1u;   // its window byte
+                uint32_t w = D[0];
+#pragma unroll
+                for (uint32_t q = 1; q < 17; ++q) w = (k >> 2) == q ? D[q] : w;
+                out[ob + __popc(~Hx & below) + __popc(Sx & below)] = (uint8_t)(w >> (8 * (k & 3)));
+            }
+        }
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+            const int q = 4 * b + qq;
+            const uint32_t X = __builtin_amdgcn_alignbyte(D[q + 1], D[q], 1u);   // elements 4q..4q+3
+            const uint32_t PV = D[q];                                            // the bytes before them
+            const uint32_t RQ = __builtin_amdgcn_alignbyte(RK[q], q ? RK[q - 1] : rp0 << 24, 3u);
+            const uint32_t PR = 0x88888888u | ((RQ & 0x07070707u) << 4) | (RK[q] & 0x07070707u);
+            const uint32_t HM = bytes((Hx >> (4 * qq)) & 15u), SM = bytes((Sx >> (4 * qq)) & 15u);
+            const uint32_t B1 = (X & ~SM) | (SM & ((PR & HM) | (PV & ~HM)));
+            const uint32_t c1 = (C1 >> (4 * qq)) & 15u, c2 = (C2 >> (4 * qq)) & 15u;
+            const uint2 sl = s_esel[c1 | (c2 << 4)];
+            const uint32_t lo = __builtin_amdgcn_perm(X, B1, sl.x), hi = __builtin_amdgcn_perm(X, B1, sl.y);
+            const uint32_t nbytes = (uint32_t)(__popc(c1) + __popc(c2));
+            const uint64_t l64 = (uint64_t)lo << nb, h64 = (uint64_t)hi << nb;
+            atomicOr(&s_out32[di], pend | (uint32_t)l64);
+            const uint32_t d1 = (uint32_t)(l64 >> 32) | (uint32_t)h64, d2 = (uint32_t)(h64 >> 32);
+            const uint32_t nt = nb + 8u * nbytes;   // 0..88
+            if (nt > 32u) atomicOr(&s_out32[di + 1], d1);
+            if (nt > 64u) atomicOr(&s_out32[di + 2], d2);
+            pend = nt >= 64u ? d2 : nt >= 32u ? d1 : (pend | (uint32_t)l64);
+            di += nt >> 5;
+            nb = nt & 31u;
+            ob += nbytes;
+        }
+        st = (S >> 16) & 1u;
+    }
+    __builtin_amdgcn_wave_barrier();
+    // store [o_tile, s_end): whole granules as uint4, the first and last granule bytewise
+    const int64_t end = (int64_t)s_end, beg = (int64_t)o_tile;
+    if (end > beg) {
+        const int64_t ng = (end - o_al + 15) / 16;
+        const uint8_t *const sb = s_out[wid];
+        for (int64_t g = lane; g < ng; g += 64) {
+            const int64_t b0 = o_al + 16 * g;
+            if (b0 >= beg && b0 + 16 <= end) {
+                st_nt(reinterpret_cast<uint4 *>(out + b0), so[g]);
+            } else {
+                for (int q = 0; q < 16; ++q) {
+                    const int64_t bq = b0 + q;
+                    if (bq >= beg && bq < end) out[bq] = sb[16 * g + q];
+                }
+            }
+        }
+    }
+}
+
 // ------------------------------------------------------------------------------------
 // Small front-end (small_compression.c:507-665) and its inverse, stateless: each element's
 // output (0 or 1 byte encoding, 1 or 2 decoding) depends only on its byte and the bytes
@@ -6091,6 +6254,7 @@ struct dc_ctx {
     uint32_t opt_hist_grid;       // histogram workgroups (0: default 512)
     uint32_t opt_pack_grid;       // pack: blocks per wave of k_huff_pack_w (0: default, ~PW_WAVES waves)
     uint32_t opt_pack_block;      // 2/3: the wave-per-range pack (k_huff_pack_w; 3: 4 codes a lane), A/B
+    uint32_t opt_nyb_wtile_off;   // 1: the static nybble encode writes with k_fsm_write (A/B, parity tests)
     uint32_t opt_d8_static;       // decoder: static share of the tuples, percent (0..100)
     uint32_t opt_decode_general;  // 1: always the general decoder (k_huff_decode)
     uint32_t opt_hist_pf;         // histogram: blocks of loads in flight ahead (1..2, 0 = default 2)
@@ -6310,6 +6474,10 @@ int dc_ctx_set_option(dc_ctx *c, int option, int64_t value)
     case DC_OPT_PACK_BLOCK:
         if (value < 0 || value > 3) return DC_E_ARG;
         c->opt_pack_block = (uint32_t)value;
+        return DC_OK;
+    case DC_OPT_NYB_WTILE_OFF:
+        if (value != 0 && value != 1) return DC_E_ARG;
+        c->opt_nyb_wtile_off = (uint32_t)value;
         return DC_OK;
     default:
         return DC_E_ARG;
@@ -7009,6 +7177,9 @@ static int fsm_run(dc_ctx *c, const uint8_t *d_in, uint64_t len, uint64_t nelem,
         if constexpr (SmMode<M>::fast)
             LAUNCH(c, SmMode<M>::dec ? "small_dec_write" : "small_write", k_small_write<M>, wgrid, SmMode<M>::wthreads, d_in, len, nelem, (const uint64_t *)c->d_entry,
                    (const uint4 *)c->d_summ, (const uint64_t *)c->d_meta, d_out);
+        else if (M == M_NYB_ENC && !aux.rk && ntiles && !((uintptr_t)d_in & 15) && !c->opt_nyb_wtile_off)
+            LAUNCH(c, FsmMode<M>::wname, k_nyb_enc_wtile, (ntiles + 3) / 4, 256, d_in, len, nelem, ntiles,
+                   (const uint64_t *)c->d_entry, (const uint4 *)c->d_summ, (const uint64_t *)c->d_meta, d_out, aux);
         else
             LAUNCH(c, FsmMode<M>::wname, k_fsm_write<M>, wgrid, 256, d_in, len, nelem, (const uint64_t *)c->d_entry,
                    (const uint4 *)c->d_summ, (const uint64_t *)c->d_meta, d_out, aux);
@@ -7038,6 +7209,9 @@ static int fsm_write_planned(dc_ctx *c, const uint8_t *d_in, uint64_t len, uint6
     if constexpr (SmMode<M>::fast)
         LAUNCH(c, SmMode<M>::dec ? "small_dec_write" : "small_write", k_small_write<M>, ntiles ? ntiles : 1, SmMode<M>::wthreads, d_in, len, nelem,
                (const uint64_t *)c->d_entry, (const uint4 *)c->d_summ, (const uint64_t *)c->d_meta, d_out);
+    else if (M == M_NYB_ENC && !aux.rk && ntiles && !((uintptr_t)d_in & 15) && !c->opt_nyb_wtile_off)
+        LAUNCH(c, FsmMode<M>::wname, k_nyb_enc_wtile, (ntiles + 3) / 4, 256, d_in, len, nelem, ntiles,
+               (const uint64_t *)c->d_entry, (const uint4 *)c->d_summ, (const uint64_t *)c->d_meta, d_out, aux);
     else
         LAUNCH(c, FsmMode<M>::wname, k_fsm_write<M>, ntiles ? ntiles : 1, 256, d_in, len, nelem, (const uint64_t *)c->d_entry,
                (const uint4 *)c->d_summ, (const uint64_t *)c->d_meta, d_out, aux);

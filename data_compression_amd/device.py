@@ -76,7 +76,7 @@ class Codec:
         check("dc_ctx_set_timing", self.L.dc_ctx_set_timing(self.ctx, int(enable)))
 
     OPTIONS = {"hist_grid": 1, "pack_grid": 2, "decode_static_pct": 3, "decode_general": 4, "hist_prefetch": 5,
-               "decode_variant": 6, "nyb_adec_v1": 7, "pack_block": 8}
+               "decode_variant": 6, "nyb_adec_v1": 7, "pack_block": 8, "nyb_wtile_off": 9}
 
     def set_option(self, name, value: int):
         """dc_ctx_set_option (dc_gpu.h DC_OPT_*): tuning knobs of this context."""

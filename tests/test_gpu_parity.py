@@ -789,6 +789,31 @@ def test_nybble_encode_parallel_vs_oracle(torch_cuda, codec, modify):
                 assert np.array_equal(back.cpu().numpy(), x), (kind, x.size)
 
 
+@pytest.mark.parametrize("wtile_off", [0, 1])
+def test_nybble_static_writers_vs_oracle(torch_cuda, wtile_off):
+    """The static encode's two writers (DC_OPT_NYB_WTILE_OFF: 0 = a wave per 4096-element tile,
+    k_nyb_enc_wtile; 1 = a workgroup per tile, k_fsm_write), byte-exact against the reference
+    restatement (nybble_compression.c compress_bytestring, modify = false) on the ragged, every-
+    context and zero-byte cases, a LITERAL fallback, and odd element counts at tile edges."""
+    from data_compression_amd.device import Codec
+    torch = torch_cuda
+    c = Codec(0)
+    c.set_option("nyb_wtile_off", wtile_off)
+    cases = _nyb_cases(torch)
+    rng = np.random.default_rng(11)
+    cases.append(("literal", rng.integers(128, 256, size=70_001, dtype=np.uint8)))   # no byte a hit
+    for n in (4096 * 4 + 1, 4096 * 4 + 2, 4096 * 5 - 1, 64 * 3 + 2):
+        cases.append(("edge", synth_text(n, seed=n)))
+    for kind, x in cases:
+        got = c.nyb_compress(torch.from_numpy(x).cuda(), False).cpu().numpy().tobytes()
+        assert got == orc.nybble_compress(x.tobytes(), False), (kind, x.size, wtile_off)
+
+
+def synth_text(n, seed):
+    from data_compression_amd import synth
+    return synth.english_like(n, seed=seed)
+
+
 @pytest.mark.parametrize("v1", [0, 1, 3])
 def test_nybble_adaptive_decode_edges(torch_cuda, codec, v1):
     """Adaptive decode (tokens by the static transducer, then the resolve in place: 0 = control
