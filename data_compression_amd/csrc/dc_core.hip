@@ -4784,6 +4784,138 @@ __global__ __launch_bounds__(256) void k_nyb_enc_wtile(const uint8_t *__restrict
     }
 }
 
+// The static nybble decode writer (and the adaptive decode's token pass, aux.tokens) in
+// k_nyb_enc_wtile's geometry: a wave per 4096-element tile, 64 contiguous elements (compressed
+// bytes j + 2) a lane, the lane's composition folded from four 16-element ones and scanned once;
+// the per-element writer is k_fsm_write's decode SWAR form. 16-B aligned input only.
+__global__ __launch_bounds__(256) void k_nyb_dec_wtile(const uint8_t *__restrict__ in, uint64_t len, uint64_t nelem,
+                                                       uint64_t ntiles, const uint64_t *__restrict__ entry,
+                                                       const uint4 *__restrict__ loc, uint8_t *__restrict__ out,
+                                                       FsmAux aux)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t s_out[4][2 * FSM_TILE + 32];
+    __shared__ uint2 s_esel[256];
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    s_esel[t] = make_uint2(c_nyb.esel_lo[t], c_nyb.esel_hi[t]);   // (NybTables)
+    const uint64_t T = (uint64_t)blockIdx.x * 4 + (uint64_t)wid;
+    const bool live = T < ntiles;
+    const uint64_t j0 = T * FSM_TILE + 64 * (uint64_t)lane;   // the lane's first element (stream byte j0 + 2)
+    uint32_t R[17];   // stream bytes [j0, j0 + 68)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint64_t o = j0 + 16 * (uint64_t)i;
+        const uint4 g = (live && o < len) ? ld_nt(reinterpret_cast<const uint4 *>(in + o)) : make_uint4(0u, 0u, 0u, 0u);
+        R[4 * i] = g.x; R[4 * i + 1] = g.y; R[4 * i + 2] = g.z; R[4 * i + 3] = g.w;
+    }
+    R[16] = dpp_wave_shl1(R[0]);
+    if (lane == 63) R[16] = (live && j0 + 64 < len) ? *reinterpret_cast<const uint32_t *>(in + j0 + 64) : 0u;
+    const uint64_t Tc = live ? T : ntiles - 1;
+    const uint64_t e = entry[Tc / FSM_GROUP];
+    const uint4 lc = loc[Tc];
+    if (blockIdx.x == 0 && t == 0) out[0] = in[1];
+    __syncthreads();   // s_esel
+    if (!live) return;   // (whole waves: no barrier below)
+    uint32_t A[4], B[4], V[4], S0[4], S1[4];
+    uint32_t comp = FSMP_ID;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        const uint64_t kb = j0 + 16 * (uint64_t)b;
+        V[b] = kb >= nelem ? 0u : nelem - kb >= 16 ? 0xFFFFu : (1u << (uint32_t)(nelem - kb)) - 1u;
+        uint32_t h = 0, l = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t X = __builtin_amdgcn_alignbyte(R[4 * b + q + 1], R[4 * b + q], 2u);   // elements 4q..4q+3
+            h |= byte_bits4(X, 7) << (4 * q);
+            l |= byte_bits4(X, 3) << (4 * q);
+        }
+        A[b] = h; B[b] = l;
+        S0[b] = nyb_dec_states(h, l, V[b], 0u);
+        S1[b] = nyb_dec_states(h, l, V[b], 1u);
+        Fsm f;
+        f.c0 = __popc(V[b]) + __popc(V[b] & h & ~S0[b]);
+        f.c1 = __popc(V[b]) + __popc(V[b] & h & ~S1[b]);
+        f.s0 = (S0[b] >> 16) & 1u;
+        f.s1 = (S1[b] >> 16) & 1u;
+        comp = fsmp_then(comp, fsmp(f));
+    }
+    uint32_t xp;
+    const uint32_t inc = fsmp_wave_scan(comp, &xp);
+    const uint32_t s_g = (uint32_t)(e & 1);
+    const uint64_t o_tile = (e >> 1) + (s_g ? lc.y : lc.x) + 1;   // the tile's first output byte (after out[0])
+    const uint32_t s_tile = s_g ? lc.w : lc.z;
+    const Fsm x = fsmp_unpack(xp), tot = fsmp_unpack((uint32_t)__builtin_amdgcn_readlane((int)inc, 63));
+    const uint64_t o0 = o_tile + (s_tile ? x.c1 : x.c0);
+    uint32_t st = s_tile ? x.s1 : x.s0;
+    const uint64_t s_end = o_tile + (s_tile ? tot.c1 : tot.c0);
+    const int64_t o_al = (int64_t)((((uintptr_t)(out + o_tile)) & ~(uintptr_t)15) - (uintptr_t)out);
+    uint4 *const so = reinterpret_cast<uint4 *>(s_out[wid]);
+    for (int i = lane; i < (2 * FSM_TILE + 32) / 16; i += 64) so[i] = make_uint4(0u, 0u, 0u, 0u);
+    __builtin_amdgcn_wave_barrier();
+    uint32_t *const s_out32 = reinterpret_cast<uint32_t *>(s_out[wid]);
+    const uint32_t P = (uint32_t)((int64_t)o0 - o_al);
+    uint32_t di = P >> 2, nb = 8u * (P & 3u), pend = 0;
+    const uint64_t tblv = aux.tokens ? 0x8786858483828180ull : NYB_DICT;   // hit bytes (k_fsm_write)
+    const uint32_t T0 = (uint32_t)tblv, T1 = (uint32_t)(tblv >> 32);
+    auto bytes = [](uint32_t m4) {   // 4 mask bits -> 0xFF per byte
+        const uint32_t u = (m4 * 0x204081u) & 0x01010101u;
+        return (u << 8) - u;
+    };
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        const uint32_t S = st ? S1[b] : S0[b];
+        const int64_t nvc = (int64_t)len - (int64_t)(j0 + 16 * (uint64_t)b + 2) - 1;   // elements whose next byte exists
+        const uint32_t NV = nvc >= 16 ? 0xFFFFu : nvc <= 0 ? 0u : (1u << (uint32_t)nvc) - 1u;
+        const uint32_t IN = V[b];
+        const uint32_t TW = IN & ~S & A[b];   // elements writing two bytes
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+            const int q = 4 * b + qq;
+            const uint32_t X = __builtin_amdgcn_alignbyte(R[q + 1], R[q], 2u);    // elements 4q..4q+3
+            const uint32_t NB = __builtin_amdgcn_alignbyte(R[q + 1], R[q], 3u);   // the bytes after them
+            const uint32_t NX = (NB >> 4) & 0x0F0F0F0Fu & bytes((NV >> (4 * qq)) & 15u);
+            const uint32_t Lb = X & 0x07070707u;
+            const uint32_t TL = __builtin_amdgcn_perm(T1, T0, Lb);                     // tbl[l & 7]
+            const uint32_t TH = __builtin_amdgcn_perm(T1, T0, (X >> 4) & 0x07070707u);  // tbl[h & 7]
+            const uint32_t u3 = (X >> 3) & 0x01010101u, LM = (u3 << 8) - u3;           // low nybble a hit
+            const uint32_t LO = (TL & LM) | (((Lb << 4) | NX) & ~LM);
+            const uint32_t SM = bytes((S >> (4 * qq)) & 15u);
+            const uint32_t t4 = (TW >> (4 * qq)) & 15u, TM = bytes(t4);
+            const uint32_t F = (SM & LO) | (~SM & ((TM & TH) | (~TM & X)));
+            const uint32_t c1 = (IN >> (4 * qq)) & 15u;
+            const uint2 sl = s_esel[c1 | (t4 << 4)];
+            const uint32_t lo = __builtin_amdgcn_perm(LO, F, sl.x), hi = __builtin_amdgcn_perm(LO, F, sl.y);
+            const uint32_t L = 8u * (uint32_t)(__popc(c1) + __popc(t4));
+            const uint64_t l64 = (uint64_t)lo << nb, h64 = (uint64_t)hi << nb;
+            atomicOr(&s_out32[di], pend | (uint32_t)l64);
+            const uint32_t d1 = (uint32_t)(l64 >> 32) | (uint32_t)h64, d2 = (uint32_t)(h64 >> 32);
+            const uint32_t nt = nb + L;
+            if (nt > 32u) atomicOr(&s_out32[di + 1], d1);
+            if (nt > 64u) atomicOr(&s_out32[di + 2], d2);
+            pend = nt >= 64u ? d2 : nt >= 32u ? d1 : (pend | (uint32_t)l64);
+            di += nt >> 5;
+            nb = nt & 31u;
+        }
+        st = (S >> 16) & 1u;
+    }
+    __builtin_amdgcn_wave_barrier();
+    const int64_t end = (int64_t)s_end, beg = (int64_t)o_tile;
+    if (end > beg) {
+        const int64_t ng = (end - o_al + 15) / 16;
+        const uint8_t *const sb = s_out[wid];
+        for (int64_t g = lane; g < ng; g += 64) {
+            const int64_t b0 = o_al + 16 * g;
+            if (b0 >= beg && b0 + 16 <= end) {
+                st_nt(reinterpret_cast<uint4 *>(out + b0), so[g]);
+            } else {
+                for (int q = 0; q < 16; ++q) {
+                    const int64_t bq = b0 + q;
+                    if (bq >= beg && bq < end) out[bq] = sb[16 * g + q];
+                }
+            }
+        }
+    }
+}
+
 // ------------------------------------------------------------------------------------
 // Small front-end (small_compression.c:507-665) and its inverse, stateless: each element's
 // output (0 or 1 byte encoding, 1 or 2 decoding) depends only on its byte and the bytes
@@ -6254,7 +6386,7 @@ struct dc_ctx {
     uint32_t opt_hist_grid;       // histogram workgroups (0: default 512)
     uint32_t opt_pack_grid;       // pack: blocks per wave of k_huff_pack_w (0: default, ~PW_WAVES waves)
     uint32_t opt_pack_block;      // 2/3: the wave-per-range pack (k_huff_pack_w; 3: 4 codes a lane), A/B
-    uint32_t opt_nyb_wtile_off;   // 1: the static nybble encode writes with k_fsm_write (A/B, parity tests)
+    uint32_t opt_nyb_wtile_off;   // 1: the nybble encode / decode write with k_fsm_write (A/B, parity tests)
     uint32_t opt_d8_static;       // decoder: static share of the tuples, percent (0..100)
     uint32_t opt_decode_general;  // 1: always the general decoder (k_huff_decode)
     uint32_t opt_hist_pf;         // histogram: blocks of loads in flight ahead (1..2, 0 = default 2)
@@ -7180,6 +7312,9 @@ static int fsm_run(dc_ctx *c, const uint8_t *d_in, uint64_t len, uint64_t nelem,
         else if (M == M_NYB_ENC && !aux.rk && ntiles && !((uintptr_t)d_in & 15) && !c->opt_nyb_wtile_off)
             LAUNCH(c, FsmMode<M>::wname, k_nyb_enc_wtile, (ntiles + 3) / 4, 256, d_in, len, nelem, ntiles,
                    (const uint64_t *)c->d_entry, (const uint4 *)c->d_summ, (const uint64_t *)c->d_meta, d_out, aux);
+        else if (M == M_NYB_DEC && ntiles && !((uintptr_t)d_in & 15) && !c->opt_nyb_wtile_off)
+            LAUNCH(c, FsmMode<M>::wname, k_nyb_dec_wtile, (ntiles + 3) / 4, 256, d_in, len, nelem, ntiles,
+                   (const uint64_t *)c->d_entry, (const uint4 *)c->d_summ, d_out, aux);
         else
             LAUNCH(c, FsmMode<M>::wname, k_fsm_write<M>, wgrid, 256, d_in, len, nelem, (const uint64_t *)c->d_entry,
                    (const uint4 *)c->d_summ, (const uint64_t *)c->d_meta, d_out, aux);

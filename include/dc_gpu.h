@@ -126,8 +126,9 @@ enum {
     DC_OPT_PACK_BLOCK = 8,        /* 2: the wave-per-range pack (k_huff_pack_w) instead of the
                                      workgroup-per-block one (k_huff_pack); 3: the same at 4 codes
                                      a lane; A/B (0.386 vs 0.380 ms on 1 GiB C2) */
-    DC_OPT_NYB_WTILE_OFF = 9      /* 1: the static nybble encode writes each 4096-element tile with
-                                     a workgroup (k_fsm_write) instead of a wave (k_nyb_enc_wtile) */
+    DC_OPT_NYB_WTILE_OFF = 9      /* 1: the static nybble encode and the nybble decode write each
+                                     4096-element tile with a workgroup (k_fsm_write) instead of a
+                                     wave (k_nyb_enc_wtile / k_nyb_dec_wtile) */
 };
 int dc_ctx_set_option(dc_ctx *ctx, int option, int64_t value);
 const char *dc_version(void);

@@ -791,10 +791,11 @@ def test_nybble_encode_parallel_vs_oracle(torch_cuda, codec, modify):
 
 @pytest.mark.parametrize("wtile_off", [0, 1])
 def test_nybble_static_writers_vs_oracle(torch_cuda, wtile_off):
-    """The static encode's two writers (DC_OPT_NYB_WTILE_OFF: 0 = a wave per 4096-element tile,
-    k_nyb_enc_wtile; 1 = a workgroup per tile, k_fsm_write), byte-exact against the reference
-    restatement (nybble_compression.c compress_bytestring, modify = false) on the ragged, every-
-    context and zero-byte cases, a LITERAL fallback, and odd element counts at tile edges."""
+    """The static codec's two writers each way (DC_OPT_NYB_WTILE_OFF: 0 = a wave per 4096-element
+    tile, k_nyb_enc_wtile / k_nyb_dec_wtile; 1 = a workgroup per tile, k_fsm_write), byte-exact
+    against the reference restatement (nybble_compression.c compress_bytestring and
+    decompress_bytestring, modify = false) on the ragged, every-context and zero-byte cases, a
+    LITERAL fallback, and odd element counts at tile edges."""
     from data_compression_amd.device import Codec
     torch = torch_cuda
     c = Codec(0)
@@ -805,8 +806,12 @@ def test_nybble_static_writers_vs_oracle(torch_cuda, wtile_off):
     for n in (4096 * 4 + 1, 4096 * 4 + 2, 4096 * 5 - 1, 64 * 3 + 2):
         cases.append(("edge", synth_text(n, seed=n)))
     for kind, x in cases:
+        ref = orc.nybble_compress(x.tobytes(), False)
         got = c.nyb_compress(torch.from_numpy(x).cuda(), False).cpu().numpy().tobytes()
-        assert got == orc.nybble_compress(x.tobytes(), False), (kind, x.size, wtile_off)
+        assert got == ref, (kind, x.size, wtile_off)
+        # the decode writers (k_nyb_dec_wtile / k_fsm_write<M_NYB_DEC>) on the reference's stream
+        back = c.nyb_decompress(torch.from_numpy(np.frombuffer(ref, np.uint8).copy()).cuda(), False)
+        assert back.cpu().numpy().tobytes() == orc.nybble_decompress(ref, False), (kind, x.size, wtile_off)
 
 
 def synth_text(n, seed):

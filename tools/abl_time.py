@@ -36,6 +36,8 @@ for o in a.opt:
     c.set_option(k, int(v))
 if a.stage in ("nyb_adaptive", "nyb_static"):   # the whole-stream nybble encoders on 1 GiB
     pass
+elif a.stage == "nyb_static_step":   # the static encode and the decode of its output
+    ybuf = torch.empty(2 * x.numel() + 16, dtype=torch.uint8, device=dev)
 elif a.stage in ("c5_enc", "c5_step"):   # the fused C5 encode (and the counted decode)
     enc = c.small_huff_encode(x, a.nary, 64)
 elif a.stage in ("batch", "chunk_enc"):   # the one-lane-per-stream nybble paths on 4 KiB streams
@@ -59,6 +61,8 @@ def run():
             c.small_huff_decode(e, out=out2)
     elif a.stage in ("nyb_adaptive", "nyb_static"):
         c.nyb_compress(x, a.stage == "nyb_adaptive")
+    elif a.stage == "nyb_static_step":
+        c.nyb_decompress(c.nyb_compress(x, False), False, out=ybuf)
     elif a.stage == "batch":
         c.nyb_decompress_batch(pay, offs, True, out_cap=x.numel())
     elif a.stage == "chunk_enc":
