@@ -791,7 +791,7 @@ def test_nybble_encode_parallel_vs_oracle(torch_cuda, codec, modify):
 
 @pytest.mark.parametrize("wtile_off", [0, 1])
 def test_nybble_static_writers_vs_oracle(torch_cuda, wtile_off):
-    """The static codec's two writers each way (DC_OPT_NYB_WTILE_OFF: 0 = a wave per 4096-element
+    """The nybble codec's two writers each way (and the adaptive encode's) (DC_OPT_NYB_WTILE_OFF: 0 = a wave per 4096-element
     tile, k_nyb_enc_wtile / k_nyb_dec_wtile; 1 = a workgroup per tile, k_fsm_write), byte-exact
     against the reference restatement (nybble_compression.c compress_bytestring and
     decompress_bytestring, modify = false) on the ragged, every-context and zero-byte cases, a
@@ -812,6 +812,9 @@ def test_nybble_static_writers_vs_oracle(torch_cuda, wtile_off):
         # the decode writers (k_nyb_dec_wtile / k_fsm_write<M_NYB_DEC>) on the reference's stream
         back = c.nyb_decompress(torch.from_numpy(np.frombuffer(ref, np.uint8).copy()).cuda(), False)
         assert back.cpu().numpy().tobytes() == orc.nybble_decompress(ref, False), (kind, x.size, wtile_off)
+        if x.size < 2_000_000:   # the adaptive encode's writer (k_nyb_enc_wtile<true> / k_fsm_write)
+            got = c.nyb_compress(torch.from_numpy(x).cuda(), True).cpu().numpy().tobytes()
+            assert got == orc.nybble_compress(x.tobytes(), True), (kind, x.size, wtile_off, "adaptive")
 
 
 def synth_text(n, seed):
