@@ -4649,7 +4649,9 @@ __global__ __launch_bounds__(256) void k_nyb_enc_wtile(const uint8_t *__restrict
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const uint64_t o = j0 + 16 * (uint64_t)i;
-        const uint4 g = (live && o < len) ? ld_nt(reinterpret_cast<const uint4 *>(in + o)) : make_uint4(0u, 0u, 0u, 0u);
+        // (plain loads: a wave's four loads each take 16 B of every lane's 64, so a line is read
+        // by four instructions; nt loads fetched the tile 1.23x)
+        const uint4 g = (live && o < len) ? *reinterpret_cast<const uint4 *>(in + o) : make_uint4(0u, 0u, 0u, 0u);
         D[4 * i] = g.x; D[4 * i + 1] = g.y; D[4 * i + 2] = g.z; D[4 * i + 3] = g.w;
     }
     D[16] = dpp_wave_shl1(D[0]);
@@ -4804,7 +4806,7 @@ __global__ __launch_bounds__(256) void k_nyb_dec_wtile(const uint8_t *__restrict
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const uint64_t o = j0 + 16 * (uint64_t)i;
-        const uint4 g = (live && o < len) ? ld_nt(reinterpret_cast<const uint4 *>(in + o)) : make_uint4(0u, 0u, 0u, 0u);
+        const uint4 g = (live && o < len) ? *reinterpret_cast<const uint4 *>(in + o) : make_uint4(0u, 0u, 0u, 0u);   // (as above)
         R[4 * i] = g.x; R[4 * i + 1] = g.y; R[4 * i + 2] = g.z; R[4 * i + 3] = g.w;
     }
     R[16] = dpp_wave_shl1(R[0]);
