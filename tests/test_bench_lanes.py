@@ -28,8 +28,12 @@ def test_run_steps_counts(nl, k, threaded):
     if not threaded or nl == 1:   # in order, on the caller's thread
         assert [j for j, _ in log] == [i % nl for i in range(k)]
         assert {t for _, t in log} == {threading.get_ident()}
-    elif k >= nl:
-        assert len({t for _, t in log}) == nl
+    else:   # lane 0 on the caller's thread, every other lane on one thread of its own
+        main = threading.get_ident()
+        for q in range(nl):
+            ts = {t for j, t in log if j == q}
+            if ts:
+                assert len(ts) == 1 and (main in ts) == (q == 0), (q, ts)
 
 
 def test_run_steps_reraises():
