@@ -1,6 +1,6 @@
 # Multi-rank rehearsal on a one-GPU box (run under gpurun): ranks share the GPU, collectives over
 # gloo (RCCL refuses two ranks on one device). 2-rank C2 (broadcast table default, gather timed),
-# then 4-rank C2 with the input generated on the device (the r2/r3 stall of 4 processes' torch
+# then 4-rank C2 with the input generated on the device, 4-rank fused C5 and 3-rank C4 (the r2/r3 stall of 4 processes' torch
 # generation at once is gone with synth.device_text's flat gather), per-rank phase lines and
 # stack dumps. Prints each line's value, the launches per step of every kernel, round trip.
 # usage: bash tools/gpu_rehearse.sh TAG
@@ -21,3 +21,5 @@ run() {   # N PORT LOG extra-args...
 run 2 29511 gpurun_out/${TAG}_gloo2_C2.log --gather-reps 1 || exit 1
 run 2 29513 gpurun_out/${TAG}_gloo2_C2_replicate.log --gather-reps 0 --table-mode replicate || exit 1
 run 4 29512 gpurun_out/${TAG}_gloo4_C2_devsynth.log --gather-reps 1 || { for f in gpurun_out/trace_rank*.log; do echo "== $f"; tail -12 $f; done; exit 1; }
+run 4 29514 gpurun_out/${TAG}_gloo4_C5_fused.log --cfg C5 --nary 16 --frontend || exit 1
+run 3 29515 gpurun_out/${TAG}_gloo3_C4.log --cfg C4 --nary 2 --gather-reps 1 || exit 1
