@@ -4628,8 +4628,12 @@ __global__ __launch_bounds__(256) void k_fsm_write(const uint8_t *__restrict__ i
 // entry states kept for the writer) and scanned across the wave once: no workgroup barrier and
 // no cross-wave combination per tile. The four waves of a workgroup share the lookup tables
 // only; each stages its tile's output in an LDS row of its own, written as k_fsm_write's SWAR
-// writer does (dwords OR-ed at the run's bit offset), then stored as whole granules. Static
-// dictionary only (no rank array) and a 16-B aligned input: fsm_run takes k_fsm_write otherwise.
+// writer does (dwords OR-ed at the run's bit offset), then stored as whole granules. ADA: the
+// adaptive encode's ranks (aux.rk, element-indexed, 16-B aligned at every 64-element run) with
+// the first touches of each 16-element step (step 4 l + b = the lane's block b) settled from its
+// k_mtf_resolve record; otherwise the static dictionary. A 16-B aligned input: fsm_run takes
+// k_fsm_write otherwise.
+template <bool ADA>
 __global__ __launch_bounds__(256) void k_nyb_enc_wtile(const uint8_t *__restrict__ in, uint64_t len, uint64_t nelem,
                                                        uint64_t ntiles, const uint64_t *__restrict__ entry,
                                                        const uint4 *__restrict__ loc, const uint64_t *__restrict__ meta,
@@ -4639,12 +4643,35 @@ __global__ __launch_bounds__(256) void k_nyb_enc_wtile(const uint8_t *__restrict
     __shared__ __attribute__((aligned(4))) uint8_t s_rank[256];
     __shared__ uint2 s_esel[256];
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-    fsm_rank_table(s_rank);
+    if (!ADA) fsm_rank_table(s_rank);
     s_esel[t] = make_uint2(c_nyb.esel_lo[t], c_nyb.esel_hi[t]);   // (NybTables)
     const uint64_t T = (uint64_t)blockIdx.x * 4 + (uint64_t)wid;
     const bool live = T < ntiles;
     const uint64_t j0 = T * FSM_TILE + 64 * (uint64_t)lane;   // the lane's first element (stream byte j0 + 1)
-    // every global read first: bytes [j0, j0 + 64), the byte after them, the tile's entry
+    // every global read first: bytes [j0, j0 + 64), the byte after them, (ADA) the ranks, the
+    // record count and the first 32 step records (a text tile holds ~24: the records need not
+    // wait for the count), the tile's entry
+    uint32_t RK[16];   // ranks, 4 per dword (element order)
+    uint4 rq0 = make_uint4(0u, 0u, 0u, 0u), rq1 = rq0;
+    uint32_t nrec = 0, rk_prev = 0;
+    if (ADA) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint64_t k = j0 + 16 * (uint64_t)i;
+            const uint4 v = (live && k + 16 <= nelem) ? *reinterpret_cast<const uint4 *>(aux.rk + k)
+                                                      : make_uint4(~0u, ~0u, ~0u, ~0u);
+            RK[4 * i] = v.x; RK[4 * i + 1] = v.y; RK[4 * i + 2] = v.z; RK[4 * i + 3] = v.w;
+        }
+        if (aux.frec && live) {
+            nrec = aux.fhead[T].x;
+            if (lane < 32) {
+                const uint4 *const rp = aux.frec + 2 * (T * 128 + (uint64_t)lane);
+                rq0 = rp[0];
+                rq1 = rp[1];
+            }
+        }
+        if (lane == 0 && live && j0) rk_prev = aux.rk[j0 - 1];   // the tile before's last element, settled in rk
+    }
     uint32_t D[17];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -4669,14 +4696,65 @@ __global__ __launch_bounds__(256) void k_nyb_enc_wtile(const uint8_t *__restrict
     if (blockIdx.x == 0 && t == 0 && whole) { out[0] = 0xAF; out[1] = in[0]; }
     __syncthreads();   // s_rank, s_esel
     if (!live) return;   // (whole waves: no barrier below)
-    // ranks, 4 per dword (element order), and the 16-element blocks' hit masks and states
-    uint32_t RK[16], A[4], V[4], S0[4], S1[4];
+    // ranks, and the 16-element blocks' hit masks and states
+    uint32_t A[4], V[4], S0[4], S1[4];
     uint32_t comp = FSMP_ID;
+    if (!ADA) {
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-        const uint32_t X = __builtin_amdgcn_alignbyte(D[q + 1], D[q], 1u);
-        RK[q] = (uint32_t)s_rank[X & 255u] | ((uint32_t)s_rank[(X >> 8) & 255u] << 8) |
-                ((uint32_t)s_rank[(X >> 16) & 255u] << 16) | ((uint32_t)s_rank[X >> 24] << 24);
+        for (int q = 0; q < 16; ++q) {
+            const uint32_t X = __builtin_amdgcn_alignbyte(D[q + 1], D[q], 1u);
+            RK[q] = (uint32_t)s_rank[X & 255u] | ((uint32_t)s_rank[(X >> 8) & 255u] << 8) |
+                    ((uint32_t)s_rank[(X >> 16) & 255u] << 16) | ((uint32_t)s_rank[X >> 24] << 24);
+        }
+    } else {
+        if (j0 < nelem && j0 + 64 > nelem) {   // the stream's last run: its ranks bytewise
+            for (uint32_t k = (uint32_t)((nelem - j0) & ~15ull); j0 + k < nelem; ++k) {
+                const uint32_t r = aux.rk[j0 + k], sh = 8 * (k & 3), msk = ~(255u << sh);
+#pragma unroll
+                for (uint32_t q = 0; q < 16; ++q)
+                    if ((k >> 2) == q) RK[q] = (RK[q] & msk) | (r << sh);
+            }
+        }
+        if (aux.frec) {   // first touches (0xFE): the settled ranks of the step's record
+            // (in the wave's output row, before the row is zeroed: step -> record + 1 at 2 KiB,
+            // the records' settled ranks below it)
+            uint4 *const s_P = reinterpret_cast<uint4 *>(s_out[wid]);
+            uint8_t *const s_map = s_out[wid] + 2048;
+            reinterpret_cast<uint32_t *>(s_map)[lane] = 0u;
+            __builtin_amdgcn_wave_barrier();
+            if (lane < 32 && (uint32_t)lane < nrec) {
+                s_map[rq0.z & 255u] = (uint8_t)(lane + 1);
+                s_P[lane] = rq1;
+            }
+            if (__builtin_amdgcn_readfirstlane((int)nrec) > 32) {   // (rare: records past the first 32)
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const uint32_t r = 32u + (uint32_t)lane + 64u * h;
+                    if (r < nrec && r < 128u) {   // (MTF_REC)
+                        const uint4 *const rp = aux.frec + 2 * (T * 128 + r);
+                        const uint4 a = rp[0], b = rp[1];
+                        s_map[a.z & 255u] = (uint8_t)(r + 1);
+                        s_P[r] = b;
+                    }
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const uint32_t mr = s_map[4 * lane + b];
+                if (mr) {
+                    const uint4 Pv = s_P[mr - 1];
+                    const uint32_t p4[4] = {Pv.x, Pv.y, Pv.z, Pv.w};
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const uint32_t z = RK[4 * b + q] ^ 0xFEFEFEFEu;   // zero bytes: 0xFE ranks
+                        const uint32_t m = ~(((z & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | z | 0x7F7F7F7Fu);
+                        const uint32_t M = (m >> 7) * 0xFFu;
+                        RK[4 * b + q] = (RK[4 * b + q] & ~M) | (p4[q] & M);
+                    }
+                }
+            }
+        }
     }
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
@@ -4710,13 +4788,21 @@ __global__ __launch_bounds__(256) void k_nyb_enc_wtile(const uint8_t *__restrict
     const uint64_t s_end = o_tile + (s_tile ? tot.c1 : tot.c0);
     const int64_t o_al = (int64_t)((((uintptr_t)(out + o_tile)) & ~(uintptr_t)15) - (uintptr_t)out);
     uint4 *const so = reinterpret_cast<uint4 *>(s_out[wid]);
+    __builtin_amdgcn_wave_barrier();   // (ADA: the records in the row are read)
     for (int i = lane; i < (2 * FSM_TILE + 32) / 16; i += 64) so[i] = make_uint4(0u, 0u, 0u, 0u);
     __builtin_amdgcn_wave_barrier();
     uint32_t *const s_out32 = reinterpret_cast<uint32_t *>(s_out[wid]);
     const uint32_t P = (uint32_t)((int64_t)o0 - o_al);   // stage byte of the lane's first output
     uint32_t di = P >> 2, nb = 8u * (P & 3u), pend = 0;
-    // the rank of a hit pending before element 0: the byte before it, or the shard's carried one
-    const uint32_t rp0 = j0 ? (uint32_t)s_rank[D[0] & 255u] : aux.pend_rank;
+    // the rank of a hit pending before element 0: the byte before it (ADA: the lane before's last
+    // rank; lane 0: the tile before's last element), or the shard's carried one
+    uint32_t rp0;
+    if (ADA) {
+        rp0 = dpp_wave_shr1(RK[15]) >> 24;
+        if (lane == 0) rp0 = j0 ? rk_prev : aux.pend_rank;
+    } else {
+        rp0 = j0 ? (uint32_t)s_rank[D[0] & 255u] : aux.pend_rank;
+    }
     uint64_t ob = o0;   // the output byte of the block's first element
     auto bytes = [](uint32_t m4) {   // 4 mask bits -> 0xFF per byte
         const uint32_t u = (m4 * 0x204081u) & 0x01010101u;
@@ -7312,7 +7398,11 @@ static int fsm_run(dc_ctx *c, const uint8_t *d_in, uint64_t len, uint64_t nelem,
             LAUNCH(c, SmMode<M>::dec ? "small_dec_write" : "small_write", k_small_write<M>, wgrid, SmMode<M>::wthreads, d_in, len, nelem, (const uint64_t *)c->d_entry,
                    (const uint4 *)c->d_summ, (const uint64_t *)c->d_meta, d_out);
         else if (M == M_NYB_ENC && !aux.rk && ntiles && !((uintptr_t)d_in & 15) && !c->opt_nyb_wtile_off)
-            LAUNCH(c, FsmMode<M>::wname, k_nyb_enc_wtile, (ntiles + 3) / 4, 256, d_in, len, nelem, ntiles,
+            LAUNCH(c, FsmMode<M>::wname, k_nyb_enc_wtile<false>, (ntiles + 3) / 4, 256, d_in, len, nelem, ntiles,
+                   (const uint64_t *)c->d_entry, (const uint4 *)c->d_summ, (const uint64_t *)c->d_meta, d_out, aux);
+        else if (M == M_NYB_ENC && aux.rk && ntiles && !((uintptr_t)d_in & 15) && !((uintptr_t)aux.rk & 15) &&
+                 !c->opt_nyb_wtile_off)
+            LAUNCH(c, FsmMode<M>::wname, k_nyb_enc_wtile<true>, (ntiles + 3) / 4, 256, d_in, len, nelem, ntiles,
                    (const uint64_t *)c->d_entry, (const uint4 *)c->d_summ, (const uint64_t *)c->d_meta, d_out, aux);
         else if (M == M_NYB_DEC && ntiles && !((uintptr_t)d_in & 15) && !c->opt_nyb_wtile_off)
             LAUNCH(c, FsmMode<M>::wname, k_nyb_dec_wtile, (ntiles + 3) / 4, 256, d_in, len, nelem, ntiles,
@@ -7347,7 +7437,7 @@ static int fsm_write_planned(dc_ctx *c, const uint8_t *d_in, uint64_t len, uint6
         LAUNCH(c, SmMode<M>::dec ? "small_dec_write" : "small_write", k_small_write<M>, ntiles ? ntiles : 1, SmMode<M>::wthreads, d_in, len, nelem,
                (const uint64_t *)c->d_entry, (const uint4 *)c->d_summ, (const uint64_t *)c->d_meta, d_out);
     else if (M == M_NYB_ENC && !aux.rk && ntiles && !((uintptr_t)d_in & 15) && !c->opt_nyb_wtile_off)
-        LAUNCH(c, FsmMode<M>::wname, k_nyb_enc_wtile, (ntiles + 3) / 4, 256, d_in, len, nelem, ntiles,
+        LAUNCH(c, FsmMode<M>::wname, k_nyb_enc_wtile<false>, (ntiles + 3) / 4, 256, d_in, len, nelem, ntiles,
                (const uint64_t *)c->d_entry, (const uint4 *)c->d_summ, (const uint64_t *)c->d_meta, d_out, aux);
     else
         LAUNCH(c, FsmMode<M>::wname, k_fsm_write<M>, ntiles ? ntiles : 1, 256, d_in, len, nelem, (const uint64_t *)c->d_entry,
