@@ -382,10 +382,12 @@ def main_nybble(a, dev, rank, world):
     # (the writers: a wave per tile for the static encode and the decode, k_fsm_write for the
     # adaptive encode's ranks; DC_OPT_NYB_WTILE_OFF, dc_gpu.h)
     kname = {"nyb_enc_tiles": "k_nyb_tiles<0>", "nyb_enca_tiles": "k_fsm_tiles<0>",
-             "nyb_enc_write": "k_fsm_write<0>" if modify else "k_nyb_enc_wtile",
+             "nyb_enc_write": "k_nyb_enc_wtile<true>" if modify else "k_nyb_enc_wtile<false>",
              "nyb_dec_tiles": "k_nyb_tiles<1>", "nyb_dec_write": "k_nyb_dec_wtile",
              "mtf_tiles": "k_mtf_walk<2>" if modify else "k_mtf_walk<0>", "mtf_ranks": "k_mtf_resolve"}.get(dom, "k_" + dom)
     traffic, traffic_src = pmc_traffic(kname, argparse.Namespace(cfg=wl, nary=0), n)
+    if traffic is None and "<" in kname:   # (a summary from before the kernel was a template)
+        traffic, traffic_src = pmc_traffic(kname.split("<")[0], argparse.Namespace(cfg=wl, nary=0), n)
     kern_sum = sum(float(np.sum(v)) for v in per.values()) / a.profile_steps
     enc_frac = (n + m) / (enc_ms * 1e-3) / HBM_PEAK
     res = {
