@@ -5677,10 +5677,20 @@ __global__ __launch_bounds__(256) void k_mtf_resolve(uint64_t len, uint64_t ntil
     const uint64_t e0 = tile * MTF_TILE;
     const uint32_t last = (uint32_t)(((e0 + MTF_TILE < len - 1) ? e0 + MTF_TILE : len - 1) - e0 - 1);   // the tile's last element
     uint32_t accp = FSMP_ID;
-    uint4 q0 = hd.x ? trec[0] : make_uint4(0u, 0u, 0u, 0u), q1 = hd.x ? trec[1] : make_uint4(0u, 0u, 0u, 0u);
-    for (uint32_t i = 0; i < hd.x; ++i) {
-        uint4 n0 = q0, n1 = q1;   // the next record, in flight
-        if (i + 1 < hd.x) { n0 = trec[2 * i + 2]; n1 = trec[2 * i + 3]; }
+    // records 4 at a time, the next 4 in flight (the first 4 slots read before the count is
+    // known: they exist for every tile; one record at a time made each a dependent round trip)
+    uint4 A[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) A[k] = trec[k];
+    for (uint32_t i0 = 0; i0 < hd.x; i0 += 4) {
+      uint4 B[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) B[k] = (i0 + 4 + (uint32_t)(k >> 1) < hd.x) ? trec[2 * i0 + 8 + k] : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const uint32_t i = i0 + (uint32_t)kk;
+        if (i >= hd.x) break;
+        const uint4 q0 = A[2 * kk], q1 = A[2 * kk + 1];
         const uint32_t X[4] = {q1.x, q1.y, q1.z, q1.w};
         uint32_t P[4] = {0u, 0u, 0u, 0u}, H = q0.y & 0xFFFFu, F = q0.y >> 16;
         const uint32_t step = q0.z & 255u, pv = (q0.z >> 8) & 255u, nk = q0.z >> 16;
@@ -5712,7 +5722,9 @@ __global__ __launch_bounds__(256) void k_mtf_resolve(uint64_t len, uint64_t ntil
         }
         accp = fsmp_then(accp, fsmp(nyb_lane_fsm<M_NYB_ENC>(H, 0u, nk >= 16 ? 0xFFFFu : (1u << nk) - 1u)));
         trec[2 * i + 1] = make_uint4(P[0], P[1], P[2], P[3]);
-        q0 = n0; q1 = n1;
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) A[k] = B[k];
     }
     const uint4 f = fsm_pack(fsmp_unpack(fsmp_then(accp, hd.y)));
     fraw[tile] = f;    // kept for a later write pass (a shard body's: its plan's scan rewrites fsumm)
