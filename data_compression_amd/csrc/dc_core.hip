@@ -5444,9 +5444,30 @@ static __device__ __forceinline__ uint64_t mtf_touch8(uint64_t L, uint32_t v, ui
     return (((L << 8) | v) & m) | (L & ~m);
 }
 
+// mtf_touch8 of byte k of X (k a constant), returning 8 x the match position (56 for a miss) in
+// place of pb: the byte is never extracted (it is broadcast, and shifted in under the list, by
+// byte permutes); the moved bytes [0, pos] are z ^ (z - 1) of the match flags z (all bytes for a
+// miss, z = 0) and pos their popcount / 8 - 1 (12 VALU ops where ctz and a shifted mask took 14)
+static __device__ __forceinline__ uint64_t mtf_touch8x(uint64_t L, uint32_t X, uint32_t k, uint32_t &pos8, bool &hit)
+{
+    const uint32_t vb = __builtin_amdgcn_perm(0u, X, k * 0x01010101u);
+    const uint32_t Ll = (uint32_t)L, Lh = (uint32_t)(L >> 32);
+    const uint32_t tl = Ll ^ vb, th = Lh ^ vb;
+    const uint64_t d = (((uint64_t)th << 32) | tl) - 0x0101010101010101ull;
+    const uint32_t zl = (uint32_t)d & ~tl & 0x80808080u, zh = (uint32_t)(d >> 32) & ~th & 0x80808080u;
+    hit = (zl | zh) != 0u;   // the lowest flag is the first match
+    const uint64_t z = ((uint64_t)zh << 32) | zl, m = z ^ (z - 1ull);
+    // pos8 = 8 pos: popcount(m) - 8 as two accumulating v_bcnt (the compiler adds them with a third op)
+    asm("v_bcnt_u32_b32 %0, %1, -8\n\tv_bcnt_u32_b32 %0, %2, %0" : "=&v"(pos8) : "v"((uint32_t)m), "v"((uint32_t)(m >> 32)));
+    const uint32_t sl = __builtin_amdgcn_perm(Ll, X, 0x06050400u | k);   // (L << 8 | x), low dword
+    const uint32_t sh = __builtin_amdgcn_alignbyte(Lh, Ll, 3u);          // (L << 8), high dword
+    return ((((uint64_t)sh << 32) | sl) & m) | (L & ~m);
+}
+
 // k_mtf_walk: one pass over each 4096-element tile from EMPTY lists (elements are bytes 1..len-1
 // of `in`: element e = byte e+1, its context byte e). MODE 0: the tile summaries -> summ[tile].
-// MODE 2: also the ranks into rk, but for the FIRST TOUCHES. A hit's rank is final already (an
+// MODE 2: also the ranks into rk, but for the FIRST TOUCHES (MODE + 1: the same for an input of any
+// alignment, with the dword selects an unaligned tile start needs). A hit's rank is final already (an
 // entry touched in the tile sits above every entry-list byte, in the same order whatever the
 // entry lists were); a miss on a full list is a miss (0xFF); a miss while the list holds fewer
 // than 8 entries is a first touch, whose rank depends on the entry lists: it is written 0xFE, and
@@ -5472,7 +5493,8 @@ __global__ __launch_bounds__(256) void k_mtf_walk(
     const uint8_t *__restrict__ in, uint64_t len, uint64_t ntiles, MtfSum *__restrict__ summ, uint8_t *__restrict__ rk,
     uint4 *__restrict__ rec, uint2 *__restrict__ head)
 {
-    static_assert(MODE == 0 || MODE == 2, "summaries, or summaries and ranks");
+    static_assert(MODE >= 0 && MODE <= 3, "summaries (0), or summaries and ranks (2); + 1: any input alignment");
+    constexpr bool RANKS = MODE >= 2, GEN = (MODE & 1) != 0;
     __shared__ uint64_t s_L[16][256];
     const int t = threadIdx.x;
     const uint64_t tile = (uint64_t)blockIdx.x * 256 + t;
@@ -5485,7 +5507,7 @@ __global__ __launch_bounds__(256) void k_mtf_walk(
     uint64_t Lc = 0ull;
     uint32_t anyz = 0;   // 0x80 bits: a zero byte among the tile's elements
     uint32_t accp = FSMP_ID, nrec = 0;
-    uint4 *const trec = rec + (MODE == 2 ? 2 * tile * MTF_REC : 0);
+    uint4 *const trec = rec + (RANKS ? 2 * tile * MTF_REC : 0);
     // MODE 2, after 16 elements (element k: rank byte k of R, byte k of X, valid bits nv): a step
     // without first touches folds into accp, one with them is listed (two 16-B stores: the
     // per-first-touch list with its segment folds measured 0.38 ms per GiB in divergent branches)
@@ -5523,10 +5545,12 @@ __global__ __launch_bounds__(256) void k_mtf_walk(
         const uint32_t d8[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
         uint32_t X[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {   // dwords dq + j, dq + j + 1 (dq uniform: selects)
+        for (int j = 0; j < 4; ++j) {   // dwords dq + j, dq + j + 1 (dq uniform: selects, GEN only)
             uint32_t lo = d8[j], hi = d8[j + 1];
+            if (GEN) {
 #pragma unroll
-            for (int k = 1; k < 4; ++k) { lo = dq == (uint32_t)k ? d8[j + k] : lo; hi = dq == (uint32_t)k ? d8[j + k + 1] : hi; }
+                for (int k = 1; k < 4; ++k) { lo = dq == (uint32_t)k ? d8[j + k] : lo; hi = dq == (uint32_t)k ? d8[j + k + 1] : hi; }
+            }
             X[j] = __builtin_amdgcn_alignbyte(hi, lo, db);
             anyz |= (X[j] - 0x01010101u) & ~X[j] & 0x80808080u;
         }
@@ -5534,21 +5558,22 @@ __global__ __launch_bounds__(256) void k_mtf_walk(
         uint32_t R[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
-            const uint32_t x = (X[k >> 2] >> (8 * (k & 3))) & 255u;
-            const uint32_t cn = (x >> 3) & 15u;
+            uint32_t cn;   // (x >> 3) & 15 of byte x: one v_bfe (the compiler splits a ubfe into a shift and a mask)
+            asm("v_bfe_u32 %0, %1, %2, 4" : "=v"(cn) : "v"(X[k >> 2]), "n"(8 * (k & 3) + 3));
             const uint64_t Ln = s_L[cn][t];   // the next element's list (before this write)
-            uint32_t pb;
+            uint32_t p8;   // 8 x the match position
             bool hit;
-            const uint64_t L2 = mtf_touch8(Lc, x, pb, hit);
+            const uint64_t L2 = mtf_touch8x(Lc, X[k >> 2], (uint32_t)(k & 3), p8, hit);
             s_L[cc][t] = L2;
-            if (MODE == 2) {
-                R[k >> 2] |= (hit ? pb >> 3 : (Lc >> 56) == 0ull ? 0xFEu : 0xFFu) << (8 * (k & 3));
+            if (RANKS) {   // the rank, 8 x, into byte k & 3 (a shift by 8 (k & 3) - 3 takes out the 8)
+                const uint32_t r8 = hit ? p8 : (Lc >> 56) == 0ull ? 0xFEu << 3 : 0xFFu << 3;
+                R[k >> 2] |= (k & 3) ? r8 << (8 * (k & 3) - 3) : r8 >> 3;
                 asm volatile("" : "+v"(R[k >> 2]));   // (sunk to the step's end, 16 ranks' inputs stayed live: +56 VGPRs)
             }
             Lc = cn == cc ? L2 : Ln;
             cc = cn;
         }
-        if (MODE == 2) {
+        if (RANKS) {
             Rout = make_uint4(R[0], R[1], R[2], R[3]);   // (stored by the group: 64 B at once)
             post(R, X, pv, e, 0xFFFFu);
         }
@@ -5567,7 +5592,7 @@ __global__ __launch_bounds__(256) void k_mtf_walk(
         __builtin_amdgcn_sched_barrier(0);
         step(D, E, ee + 48, Rd);
         __builtin_amdgcn_sched_barrier(0);
-        if (MODE == 2) {
+        if (RANKS) {
             uint4 *const rq = reinterpret_cast<uint4 *>(rk + ee);
             rq[0] = Ra; rq[1] = Rb; rq[2] = Rc; rq[3] = Rd;
         }
@@ -5601,14 +5626,14 @@ __global__ __launch_bounds__(256) void k_mtf_walk(
             const uint64_t L2 = mtf_touch8(Lc, x, pb, hit);
             s_L[cc][t] = L2;
             const uint32_t r = hit ? pb >> 3 : (Lc >> 56) == 0ull ? 0xFEu : 0xFFu;
-            if (MODE == 2) rk[e + k] = (uint8_t)r;
+            if (RANKS) rk[e + k] = (uint8_t)r;
             R[k >> 2] = (R[k >> 2] & ~(255u << (8 * (k & 3)))) | (r << (8 * (k & 3)));
             X[k >> 2] |= x << (8 * (k & 3));
             anyz |= x == 0u ? 0x80u : 0u;
             cc = (x >> 3) & 15u;
             Lc = s_L[cc][t];
         }
-        if (MODE == 2) post(R, X, pv, e, (1u << nk) - 1u);
+        if (RANKS) post(R, X, pv, e, (1u << nk) - 1u);
     }
     uint64_t cnts = 0;   // nibble c = entries of list c
     if (anyz) {
@@ -5630,15 +5655,15 @@ __global__ __launch_bounds__(256) void k_mtf_walk(
                 s_L[c][t] = L;
                 cnts = (cnts & ~(15ull << (4 * c))) | ((uint64_t)n << (4 * c));
                 const uint32_t r = r0 >= 0 ? (uint32_t)r0 : nb < 8 ? 0xFEu : 0xFFu;
-                if (MODE == 2) rk[f + k] = (uint8_t)r;
+                if (RANKS) rk[f + k] = (uint8_t)r;
                 R[k >> 2] = (R[k >> 2] & ~(255u << (8 * (k & 3)))) | (r << (8 * (k & 3)));
                 X[k >> 2] |= x << (8 * (k & 3));
                 pvb = x;
             }
-            if (MODE == 2) post(R, X, pv, f, (1u << nk) - 1u);
+            if (RANKS) post(R, X, pv, f, (1u << nk) - 1u);
         }
     }
-    if (MODE == 2) head[tile] = make_uint2(nrec, accp);
+    if (RANKS) head[tile] = make_uint2(nrec, accp);
     for (int c = 0; c < 16; ++c) {
         const uint64_t L = s_L[c][t];
         uint32_t nz = 0;   // zero bytes: the pads
@@ -7500,10 +7525,18 @@ static int mtf_run(dc_ctx *c, const uint8_t *d_in, uint64_t len, const MtfSum *h
         return DC_E_HIP;
     uint4 *const mrec = c->d_mrec;
     uint2 *const mhead = c->d_mhead;
-    if (ranks)   // the summaries, the ranks but for the first touches, and their list: one walk
+    // a tile's elements start (1 + d_in % 16) % 16 bytes into its first granule: within its first
+    // dword for the usual 16-B aligned input (k_mtf_walk<0/2>, no dword selects), anywhere (<1/3>)
+    const bool gen = (((uintptr_t)d_in + 1) & 15u) >= 4u;
+    if (ranks && !gen)   // the summaries, the ranks but for the first touches, and their list: one walk
         LAUNCH(c, "mtf_tiles", k_mtf_walk<2>, (n0 + 255) / 256, 256, d_in, len, n0, S, c->d_rk, mrec, mhead);
-    else
+    else if (ranks)
+        LAUNCH(c, "mtf_tiles", k_mtf_walk<3>, (n0 + 255) / 256, 256, d_in, len, n0, S, c->d_rk, mrec, mhead);
+    else if (!gen)
         LAUNCH(c, "mtf_tiles", k_mtf_walk<0>, (n0 + 255) / 256, 256, d_in, len, n0, S, (uint8_t *)nullptr,
+               (uint4 *)nullptr, (uint2 *)nullptr);
+    else
+        LAUNCH(c, "mtf_tiles", k_mtf_walk<1>, (n0 + 255) / 256, 256, d_in, len, n0, S, (uint8_t *)nullptr,
                (uint4 *)nullptr, (uint2 *)nullptr);
     for (int l = 0; l + 1 < levels; ++l)
         LAUNCH(c, "mtf_reduce", k_mtf_reduce, (nl[l + 1] * 16 + 255) / 256, 256, (const MtfSum *)(S + off[l]), nl[l],

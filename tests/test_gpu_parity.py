@@ -771,13 +771,18 @@ def _nyb_cases(torch):
 @pytest.mark.parametrize("modify", [True, False])
 def test_nybble_encode_parallel_vs_oracle(torch_cuda, codec, modify):
     """Adaptive encode by per-tile move-to-front summaries (k_mtf_*), byte-exact against the
-    reference restatement, at ragged sizes, every context, and a misaligned device buffer."""
+    reference restatement, at ragged sizes, every context, and misaligned device buffers (offset
+    1: a tile's elements still start in its first granule dword, k_mtf_walk<2>; offset 5: they
+    start in its second, the any-alignment walk k_mtf_walk<3>)."""
     torch = torch_cuda
     for kind, x in _nyb_cases(torch):
         ref = orc.nybble_compress(x.tobytes(), modify)
-        buf = torch.zeros(x.size + 1, dtype=torch.uint8, device="cuda")
-        buf[1:] = torch.from_numpy(x).cuda()
-        for xt in (torch.from_numpy(x).cuda(), buf[1:]):
+        xd = torch.from_numpy(x).cuda()
+        b1 = torch.zeros(x.size + 1, dtype=torch.uint8, device="cuda")
+        b1[1:] = xd
+        b5 = torch.zeros(x.size + 5, dtype=torch.uint8, device="cuda")
+        b5[5:] = xd
+        for xt in (xd, b1[1:], b5[5:]):
             got = codec.nyb_compress(xt, modify).cpu().numpy().tobytes()
             assert got == ref, (kind, x.size)
         if modify and x.size < 400_000:
