@@ -5455,8 +5455,8 @@ static __device__ __forceinline__ uint64_t mtf_touch8x(uint64_t L, uint32_t X, u
     const uint32_t tl = Ll ^ vb, th = Lh ^ vb;
     const uint64_t d = (((uint64_t)th << 32) | tl) - 0x0101010101010101ull;
     const uint32_t zl = (uint32_t)d & ~tl & 0x80808080u, zh = (uint32_t)(d >> 32) & ~th & 0x80808080u;
-    hit = (zl | zh) != 0u;   // the lowest flag is the first match
-    const uint64_t z = ((uint64_t)zh << 32) | zl, m = z ^ (z - 1ull);
+    const uint64_t z = ((uint64_t)zh << 32) | zl, m = z ^ (z - 1ull);   // the lowest flag is the first match
+    hit = z != 0ull;
     // pos8 = 8 pos: popcount(m) - 8 as two accumulating v_bcnt (the compiler adds them with a third op)
     asm("v_bcnt_u32_b32 %0, %1, -8\n\tv_bcnt_u32_b32 %0, %2, %0" : "=&v"(pos8) : "v"((uint32_t)m), "v"((uint32_t)(m >> 32)));
     const uint32_t sl = __builtin_amdgcn_perm(Ll, X, 0x06050400u | k);   // (L << 8 | x), low dword
