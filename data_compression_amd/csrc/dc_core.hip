@@ -5476,10 +5476,13 @@ static __device__ __forceinline__ uint64_t mtf_touch8x(uint64_t L, uint32_t X, u
 // touches << 16, step | context byte of its element 0 << 8 | elements << 16, 0), and the step's
 // 16 element bytes. head[tile] = (records, the composition after the last one). (The encoder's
 // FSM tiles are these tiles; a step is a lane of its writer.)
-// A lane walks its tile with the 16 lists in LDS (column t). Per element: the next element's
-// list is read before this one's is written back (its context is this element's byte; the same
-// context takes the list just computed), so the LDS round trip overlaps the touch; the input
-// comes in 16-B granules loaded a 64-element group ahead. Lists are padded with zero bytes
+// A lane walks its tile with the 16 lists in LDS (column t). Per element: the touched list is
+// written back, then the next element's list read (its context is this element's byte; the
+// same address returns the list just written: no compare and selects); the other 3 waves of a
+// SIMD cover the round trip (r5: 26 -> 23 VALU per element, 1.128 -> 1.117 ms per GiB, against
+// reading it before the write, profiles/r5walk2_mtf_walk_raw_ab.log); the input
+// comes in 16-B granules loaded a 64-element group ahead. 23 VALU per element in all (r4: 35,
+// 1.311 ms per GiB, profiles/r5walk_mtf_walk_valu_ab.log). Lists are padded with zero bytes
 // (mtf_touch8), so a list is short while its last byte is 0 and its count is 8 - its zero bytes,
 // both exact while no element is a zero byte; a tile that has one is walked again with counts
 // (mtf_touch64). (r4 before: a summary pass, then a second walk of every tile from its entry
@@ -5560,7 +5563,6 @@ __global__ __launch_bounds__(256) void k_mtf_walk(
         for (int k = 0; k < 16; ++k) {
             uint32_t cn;   // (x >> 3) & 15 of byte x: one v_bfe (the compiler splits a ubfe into a shift and a mask)
             asm("v_bfe_u32 %0, %1, %2, 4" : "=v"(cn) : "v"(X[k >> 2]), "n"(8 * (k & 3) + 3));
-            const uint64_t Ln = s_L[cn][t];   // the next element's list (before this write)
             uint32_t p8;   // 8 x the match position
             bool hit;
             const uint64_t L2 = mtf_touch8x(Lc, X[k >> 2], (uint32_t)(k & 3), p8, hit);
@@ -5570,7 +5572,7 @@ __global__ __launch_bounds__(256) void k_mtf_walk(
                 R[k >> 2] |= (k & 3) ? r8 << (8 * (k & 3) - 3) : r8 >> 3;
                 asm volatile("" : "+v"(R[k >> 2]));   // (sunk to the step's end, 16 ranks' inputs stayed live: +56 VGPRs)
             }
-            Lc = cn == cc ? L2 : Ln;
+            Lc = s_L[cn][t];   // the next element's list, after this write (the same context: L2)
             cc = cn;
         }
         if (RANKS) {
