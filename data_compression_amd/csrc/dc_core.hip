@@ -1755,301 +1755,6 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
     }
 }
 
-// ------------------------------------------------------------------------------------
-// (H7) pack, one wave per contiguous range of blocks: the product path for 16-B aligned
-// output words (k_huff_pack above keeps the byte-map case and unaligned output).
-// Ablations of k_huff_pack on 1 GiB C2 (profiles/r5d_abl.log): without its loads 0.380 ms
-// against 0.381, without its table reads and stage ORs 0.365, with none of loads, stores,
-// table reads or ORs 0.168: it was bound by instruction issue and its per-block phases
-// (a length pass, workgroup scans, three barriers per 32 KiB), not by HBM. Here a wave owns
-// blocks [b0, b1) and streams them 1 KiB at a time (a piece: 16 bytes per lane), with the
-// next 3 pieces' loads in flight:
-//   * every code is looked up ONCE: a lane folds its G codes into a 64-bit accumulator
-//     (acc = acc << len | code) before it knows where they go, so the position scan needs
-//     no separate length pass (a group of > 64 bits is re-coded code by code, rare);
-//   * the piece's bit positions come from one DPP wave scan and a wave-uniform running bit
-//     position: no workgroup barrier anywhere;
-//   * codes are OR-ed into the wave's stage (<= 1024 words per piece + the carried partial
-//     uint4), the complete uint4s leave as nt stores, the partial one moves to the front;
-//   * only the range's first word (shared with the previous range) and its last partial word
-//     (shared with the next) are OR-ed into HBM (k_block_final_wide zeroed both: they hold a
-//     block's first bit, or the stream's last bit).
-// The sync index is written as k_huff_pack writes it. Workgroup 0 builds the decoder tables.
-// ------------------------------------------------------------------------------------
-#define PW_STAGE 1040   /* words per wave: a piece's <= 1024 words + the carried uint4 + OR slack */
-#define PW_WAVES 4096   /* waves of k_huff_pack_w (1 GiB: 8 blocks, 256 KiB each) */
-struct PackWLds {
-    uint2 tab[257];     // code | bits per byte value; [256] = (0, 0): past the stream's end
-    __attribute__((aligned(16))) uint32_t stage[4][PW_STAGE];
-};
-union PackWUnion {
-    PackWLds p;
-    DecBuildLds d;
-};
-
-// the range [x0, x1) of a wave whose codes are all 8 bits (the byte map of k_huff_pack's fixed8
-// path): stream byte bit_base / 8 + i = code(in[i]), bit_base % 128 == 0
-static __device__ __forceinline__ void pack_w_fixed8(const uint8_t *__restrict__ in, uint64_t n, uint64_t x0, uint64_t x1,
-                                                     const uint2 *tab, uint32_t *__restrict__ out,
-                                                     uint64_t *__restrict__ sync_base, uint16_t *__restrict__ sync_len,
-                                                     uint32_t sync_syms, uint64_t bit_base, int lane)
-{
-    uint8_t *const ob = reinterpret_cast<uint8_t *>(out);
-    const uint32_t slog = (uint32_t)__builtin_ctz(sync_syms);
-    for (uint64_t g = x0 + 16u * (uint64_t)lane; g < x1; g += 1024) {
-        if (g + 16 <= x1) {
-            uint4 v = LD_PACK(reinterpret_cast<const uint4 *>(in + g));
-            uint32_t w4[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const uint32_t x = w4[q];
-                w4[q] = tab[x & 255u].x | (tab[(x >> 8) & 255u].x << 8) | (tab[(x >> 16) & 255u].x << 16) |
-                        (tab[x >> 24].x << 24);
-            }
-            st_nt(reinterpret_cast<uint4 *>(ob + g), make_uint4(w4[0], w4[1], w4[2], w4[3]));
-        } else {
-            for (uint64_t i = g; i < x1; ++i) ob[i] = (uint8_t)tab[in[i]].x;
-        }
-    }
-    // the stream's last word: its bytes past the stream are zero (the pad), whatever the buffer held
-    if (x1 == n && lane < 4 && ((n + 3) & ~3ull) > n + (uint64_t)lane) ob[n + lane] = 0;
-    if (sync_len != nullptr) {   // chunks of S symbols: 8 S bits (the last: 8 x its symbols)
-        for (uint64_t c = (x0 >> slog) + (uint64_t)lane; c < ((x1 + sync_syms - 1) >> slog); c += 64) {
-            const uint64_t s0 = c << slog;
-            sync_len[c] = (uint16_t)(8u * (uint32_t)min((uint64_t)sync_syms, n - s0));
-            if ((c & (DC_SYNC_GROUP - 1)) == 0) sync_base[c >> DC_SYNC_GROUP_LOG] = bit_base + 8 * s0;
-        }
-    }
-}
-
-template <int G>   // codes per accumulator: 8, or 4 above 5.5 bits per symbol
-static __device__ __forceinline__ void pack_w_range(const uint8_t *__restrict__ in, uint64_t x0, uint64_t x1,
-                                                    const uint2 *tab, uint32_t *st, uint32_t *__restrict__ out,
-                                                    const uint64_t *__restrict__ block_off, uint64_t b0,
-                                                    uint64_t bit_base, uint64_t *__restrict__ sync_base,
-                                                    uint16_t *__restrict__ sync_len, uint32_t sync_syms, uint64_t n,
-                                                    uint4 *trash, int lane)
-{
-    const uint64_t word_base = bit_base >> 5;
-    const uint32_t slog = sync_syms ? (uint32_t)__builtin_ctz(sync_syms) : 0u;   // S is a power of two
-    const uint32_t cm = sync_syms >> 4;                                           // lanes per sync chunk
-    uint64_t pos = bit_base + block_off[b0];                 // absolute bit of the next code
-    const uint64_t first_w = (pos >> 5) - word_base;         // out-relative: shared with the previous range
-    uint64_t W0 = first_w & ~3ull;                           // out word of stage word 0 (16-B aligned)
-    bool head = true;                                        // stage uint4 0 is the range's first
-
-    // stores of stage words [a, b) to out[W0 + a ..): the range's first word is OR-ed (shared),
-    // words before it are not this range's; everything stored is zeroed in the stage
-    auto store_words = [&](uint32_t a, uint32_t b, bool hd) {
-        for (uint32_t i = a + (uint32_t)lane; i < b; i += 64) {
-            const uint64_t w = W0 + i;
-            const uint32_t v = st[i];
-            st[i] = 0u;
-            if (hd && w < first_w) continue;
-            if (hd && w == first_w) atomicOr(out + w, bswap32(v));
-            else out[w] = bswap32(v);
-        }
-    };
-
-    // Every load and every store below is issued unconditionally, one per piece each (a lane
-    // with nothing to load reads the stream's last full granule, a lane with nothing to store
-    // repeats its wave's last uint4): a wave's vmcnt retires in issue order, and a path with
-    // fewer memory operations makes the compiler's wait for a piece's prefetched granule drain
-    // everything issued since (vmcnt(0)); with one load and one store per piece on every path
-    // that wait is vmcnt(7), and neither the 3 loads behind it nor the stores are waited for.
-    const uint64_t glast = (n - 16) & ~15ull;   // n >= 1024 (the launcher)
-    const uint64_t npf = (x1 - x0) / 1024;      // whole pieces; then at most one partial (the stream's end)
-    auto issue = [&](uint64_t pc) -> uint4 {   // piece pc's granule of this lane
-        const uint64_t g = x0 + pc * 1024 + 16u * (uint64_t)lane;
-        return LD_PACK(reinterpret_cast<const uint4 *>(in + (pc < npf ? g : glast)));
-    };
-    uint4 r0 = issue(0), r1 = issue(1), r2 = issue(2), r3 = issue(3);
-
-    // TAIL: the partial last piece (its bytes loaded one by one, the missing ones coded as the
-    // (0, 0) entry); a separate instance keeps the masking out of the whole pieces
-    auto piece = [&](auto tail_c, uint4 v, uint64_t pc) {
-        constexpr bool tail = decltype(tail_c)::value;
-        const uint64_t xo = x0 + pc * 1024, g = xo + 16u * (uint64_t)lane;
-        uint32_t w4[4] = {v.x, v.y, v.z, v.w};
-        uint32_t cnt = 16;
-        if (tail) {
-            cnt = g >= x1 ? 0u : (uint32_t)min((uint64_t)16, x1 - g);
-            w4[0] = w4[1] = w4[2] = w4[3] = 0u;
-            for (uint32_t i = 0; i < cnt; ++i) w4[i >> 2] |= (uint32_t)in[g + i] << (8 * (i & 3));
-        }
-        // the table index of byte i: past the end, the (0, 0) entry
-        auto idx = [&](int i) -> uint32_t {
-            const uint32_t b = (w4[i >> 2] >> (8 * (i & 3))) & 255u;
-            return (tail && (uint32_t)i >= cnt) ? 256u : b;
-        };
-        constexpr int NG = 16 / G;
-        uint64_t acc[NG];
-        uint32_t tg[NG], tl = 0;
-#pragma unroll
-        for (int q = 0; q < NG; ++q) {
-            uint64_t a = 0;
-            uint32_t s = 0;
-#pragma unroll
-            for (int j = 0; j < G; ++j) {
-                const uint2 e = tab[idx(q * G + j)];
-                a = (a << e.y) | e.x;
-                s += e.y;
-            }
-            acc[q] = a;
-            tg[q] = s;
-            tl += s;
-        }
-        const uint32_t incl = wave_scan_incl(tl), excl = incl - tl;
-        const uint32_t wtot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-        if (sync_len != nullptr) {
-            // chunk bits = inclusive scan at the chunk's last lane - exclusive at its first
-            const uint32_t last = (cm == 4) ? (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0xff, 0xf, 0xf, false)
-                                            : (uint32_t)__shfl((int)incl, lane | (int)(cm - 1), 64);
-            if ((g & (uint64_t)(sync_syms - 1)) == 0 && g < x1) {
-                sync_len[g >> slog] = (uint16_t)(last - excl);
-                if ((g & ((uint64_t)sync_syms * DC_SYNC_GROUP - 1)) == 0) sync_base[g >> (slog + DC_SYNC_GROUP_LOG)] = pos + excl;
-            }
-        }
-        // OR a right-justified run of nb <= 64 bits into the stage at bit p (<= 3 words;
-        // branch-free: the words a run does not reach receive 0)
-        auto emit = [&](uint64_t a, uint32_t nb, uint32_t p) {
-            const uint64_t al = a << ((64u - nb) & 63u);
-            const uint32_t hi = (uint32_t)(al >> 32), lo = (uint32_t)al, rr = p & 31u, wi = p >> 5;
-            atomicOr(&st[wi], hi >> rr);
-            atomicOr(&st[wi + 1], __builtin_amdgcn_alignbit(hi, lo, rr));
-            atomicOr(&st[wi + 2], __builtin_amdgcn_alignbit(lo, 0u, rr));
-        };
-        uint32_t rel = (uint32_t)(pos - ((W0 + word_base) << 5)) + excl;   // stage bit of this lane's first code
-#pragma unroll
-        for (int q = 0; q < NG; ++q) {
-            if (tg[q] <= 64u) {
-                emit(acc[q], tg[q], rel);
-            } else {   // more than 64 bits in the group: code by code (each <= 32 bits)
-                uint32_t p = rel;
-#pragma unroll 1
-                for (int j = 0; j < G; ++j) {
-                    const uint2 e = tab[idx(q * G + j)];
-                    emit(e.x, e.y, p);
-                    p += e.y;
-                }
-            }
-            rel += tg[q];
-        }
-        // complete uint4s leave; the partial one moves to the stage front
-        pos += wtot;
-        const uint32_t E = (uint32_t)(((pos >> 5) - word_base) - W0);   // stage words complete: [0, E)
-        const uint32_t nq = E >> 2;
-        const uint32_t q0 = (head && nq > 0) ? 1u : 0u;
-        if (q0) {   // the range's first uint4: word by word (its words before the range are not ours)
-            store_words(0, 4, true);
-            head = false;
-        }
-        {   // uint4s [q0, nq): one store instruction per lane; lanes past nq repeat uint4 nq - 1
-            // (the same bytes to the same address); with none to store, zeros to the trash uint4
-            const uint32_t q = min(q0 + (uint32_t)lane, nq - 1);
-            const bool any = nq > q0;
-            uint4 *const sq = reinterpret_cast<uint4 *>(st) + (any ? q : PW_STAGE / 4 - 1);
-            const uint4 vv = *sq;
-            uint4 *const d4 = any ? reinterpret_cast<uint4 *>(out + W0) + q : trash;
-            __builtin_nontemporal_store(bswap32(vv.x), &d4->x);
-            __builtin_nontemporal_store(bswap32(vv.y), &d4->y);
-            __builtin_nontemporal_store(bswap32(vv.z), &d4->z);
-            __builtin_nontemporal_store(bswap32(vv.w), &d4->w);
-            if (any && q0 + (uint32_t)lane < nq) *sq = make_uint4(0u, 0u, 0u, 0u);
-        }
-        for (uint32_t q = q0 + 64 + (uint32_t)lane; q < nq; q += 64) {   // dense pieces: > 64 uint4
-            uint4 *const sq = reinterpret_cast<uint4 *>(st) + q;
-            const uint4 vv = *sq;
-            *sq = make_uint4(0u, 0u, 0u, 0u);
-            uint4 *const d4 = reinterpret_cast<uint4 *>(out + W0) + q;
-            __builtin_nontemporal_store(bswap32(vv.x), &d4->x);
-            __builtin_nontemporal_store(bswap32(vv.y), &d4->y);
-            __builtin_nontemporal_store(bswap32(vv.z), &d4->z);
-            __builtin_nontemporal_store(bswap32(vv.w), &d4->w);
-        }
-        if (nq > 0) {
-            if (lane < 4) {   // the partial uint4 to the front (LDS ops of a wave complete in order)
-                const uint32_t c = st[4 * nq + lane];
-                st[4 * nq + lane] = 0u;
-                st[lane] = c;
-            }
-            W0 += 4ull * nq;
-        }
-    };
-
-    using whole = std::integral_constant<bool, false>;
-    uint64_t pc = 0;
-    for (; pc + 4 <= npf; pc += 4) {   // 4 pieces per step, each one's granule issued 4 pieces ahead
-        uint4 v = r0; r0 = issue(pc + 4); piece(whole(), v, pc);
-        v = r1; r1 = issue(pc + 5); piece(whole(), v, pc + 1);
-        v = r2; r2 = issue(pc + 6); piece(whole(), v, pc + 2);
-        v = r3; r3 = issue(pc + 7); piece(whole(), v, pc + 3);
-    }
-    if (pc < npf) piece(whole(), r0, pc++);
-    if (pc < npf) piece(whole(), r1, pc++);
-    if (pc < npf) piece(whole(), r2, pc++);
-    if (x1 - x0 > npf * 1024) piece(std::integral_constant<bool, true>(), r3, npf);
-    // the range's last words: complete ones stored, the partial last one OR-ed (shared with
-    // the next range, or the stream's end: zeroed by the plan)
-    const uint32_t E = (uint32_t)(((pos >> 5) - word_base) - W0);
-    store_words(0, E, head);
-    if ((pos & 31) != 0 && lane == 0) {
-        const uint32_t v = st[E];
-        st[E] = 0u;
-        atomicOr(out + W0 + E, bswap32(v));
-    }
-}
-
-__global__ __launch_bounds__(256) void k_huff_pack_w(const uint8_t *__restrict__ in, uint64_t n,
-                                                     const dc_dtable *__restrict__ T,
-                                                     const uint64_t *__restrict__ block_off, uint64_t bit_base,
-                                                     const uint64_t *__restrict__ d_base, uint32_t *__restrict__ out,
-                                                     uint64_t *__restrict__ sync_base, uint16_t *__restrict__ sync_len,
-                                                     uint32_t sync_syms, uint64_t nblocks, uint64_t words_cap,
-                                                     int *__restrict__ err, int build_dec, uint32_t bpw,
-                                                     uint8_t *__restrict__ scratch, int qmode)
-{
-    __shared__ PackWUnion U;
-    const int t = threadIdx.x, lane = t & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
-    if (build_dec && blockIdx.x == 0) {   // workgroup 0: the decoder tables, beside the pack
-        if (T->status == DC_OK) dec_tables_build(const_cast<dc_dtable *>(T), U.d);
-        return;
-    }
-    if (d_base) bit_base += *d_base;   // device-resident shard offset (dist: no host read)
-    // device-side guards (no host round trip), as k_huff_pack: a byte without a code (plan
-    // error) or an output buffer smaller than the planned stream -> write nothing
-    const uint64_t total = block_off[nblocks];
-    if (err[0] != 0) return;
-    if (((bit_base & 31) + total + 31) / 32 > words_cap) {
-        if (t == 0) err[2] = 1;   // (pack status: DC_E_CAPACITY)
-        return;
-    }
-    U.p.tab[t] = make_uint2(T->code[t], T->nbits[t]);
-    if (t == 0) U.p.tab[256] = make_uint2(0u, 0u);
-    uint32_t *const st = U.p.stage[wv];
-    for (int i = lane; i < PW_STAGE / 4; i += 64) reinterpret_cast<uint4 *>(st)[i] = make_uint4(0u, 0u, 0u, 0u);
-    __syncthreads();   // (the only barrier: the table)
-    const uint64_t gw = (uint64_t)(blockIdx.x - build_dec) * 4 + (uint64_t)wv;
-    const uint64_t b0 = gw * bpw;
-    if (b0 >= nblocks) return;
-    const uint64_t b1 = min(b0 + (uint64_t)bpw, nblocks);
-    const uint64_t x0 = b0 * (uint64_t)DC_BLOCK_BYTES, x1 = min(b1 * (uint64_t)DC_BLOCK_BYTES, n);
-    uint4 *const trash = reinterpret_cast<uint4 *>(scratch + (size_t)(gw & (D8_SCRATCH_WAVES - 1)) * D8_WSCR) + lane;
-    if (T->fixed8 && (bit_base & 127) == 0) {
-        pack_w_fixed8(in, n, x0, x1, U.p.tab, out, sync_base, sync_len, sync_syms, bit_base, lane);
-        return;
-    }
-    // quarter mode (uniform), as k_huff_pack: above 5.5 bits per symbol on average groups of 8
-    // codes often exceed 64 bits
-    if (qmode || 2 * total > 11 * n)
-        pack_w_range<4>(in, x0, x1, U.p.tab, st, out, block_off, b0, bit_base, sync_base, sync_len, sync_syms, n, trash,
-                        lane);
-    else
-        pack_w_range<8>(in, x0, x1, U.p.tab, st, out, block_off, b0, bit_base, sync_base, sync_len, sync_syms, n, trash,
-                        lane);
-}
-
 // C5 fused front-end pack: codes the front-end output M of `in` (see the front-end fusion
 // block above k_hist_blocks) without M ever being written. The blocks are k_huff_pack's: 32 KiB
 // of the INPUT, lane t of wave w coding piece k = input bytes [k*4096 + 16t, +16), whose
@@ -6511,7 +6216,7 @@ struct dc_ctx {
     bool plan_ok;
     // tuning options (dc_ctx_set_option; initial values from the environment, read once here)
     uint32_t opt_hist_grid;       // histogram workgroups (0: default 512)
-    uint32_t opt_pack_grid;       // pack: blocks per wave of k_huff_pack_w (0: default, ~PW_WAVES waves)
+    uint32_t opt_pack_grid;       // pack: workgroups of k_huff_pack (0: a block pair each; A/B builds: blocks per wave of k_huff_pack_w)
     uint32_t opt_pack_block;      // 2/3: the wave-per-range pack (k_huff_pack_w; 3: 4 codes a lane), A/B
     uint32_t opt_nyb_wtile_off;   // 1: the nybble encode / decode write with k_fsm_write (A/B, parity tests)
     uint32_t opt_d8_static;       // decoder: static share of the tuples, percent (0..100)
@@ -6730,8 +6435,12 @@ int dc_ctx_set_option(dc_ctx *c, int option, int64_t value)
         if (value < 0 || value > 3) return DC_E_ARG;
         c->opt_hist_pf = (uint32_t)value;
         return DC_OK;
-    case DC_OPT_PACK_BLOCK:
+    case DC_OPT_PACK_BLOCK:   // 2/3: k_huff_pack_w, in DC_AB_KERNELS builds only
+#ifdef DC_AB_KERNELS
         if (value < 0 || value > 3) return DC_E_ARG;
+#else
+        if (value != 0) return DC_E_ARG;
+#endif
         c->opt_pack_block = (uint32_t)value;
         return DC_OK;
     case DC_OPT_NYB_WTILE_OFF:
@@ -7057,6 +6766,7 @@ static int pack_impl(dc_ctx *c, const uint8_t *d_in, uint64_t n, const dc_dtable
     // the blocks' offsets, and the boundary words zeroed (the plan's error flags: its slot)
     const int r = plan_offsets(c, plan_err(c), plan_err_next(c), bit_base, d_base, d_words, words_cap);
     if (r != DC_OK) return r;
+#ifdef DC_AB_KERNELS
     if ((((uintptr_t)d_words) & 15) == 0 && c->opt_pack_block >= 2 && n >= 1024) {   // A/B: 0.386 vs 0.380 ms
         if (ensure((void **)&c->d_scr, &c->scr_cap, (size_t)D8_SCRATCH_WAVES * D8_WSCR)) return DC_E_HIP;   // trash rows
         // one wave per range of bpw blocks (k_huff_pack_w): ~PW_WAVES waves, 4 per workgroup,
@@ -7066,7 +6776,9 @@ static int pack_impl(dc_ctx *c, const uint8_t *d_in, uint64_t n, const dc_dtable
         LAUNCH(c, "huff_pack", k_huff_pack_w, (waves + 3) / 4 + 1, 256, d_in, n, d_table, (const uint64_t *)c->d_off,
                bit_base, d_base, d_words, d_sync_base, d_sync_len, sync_syms, nb, words_cap, plan_err(c), 1,
                (uint32_t)bpw, (uint8_t *)c->d_scr, c->opt_pack_block == 3 ? 1 : 0);
-    } else {
+    } else
+#endif
+    {
         // two blocks per workgroup (grid-stride) + workgroup 0: the decoder tables
         const uint64_t gmax = c->opt_pack_grid ? c->opt_pack_grid : (nb + 1) / 2;
         const uint64_t grid = nb < gmax ? nb : gmax;

@@ -48,6 +48,7 @@ class ShardStream:
     totals: torch.Tensor = None   # the ranks' payload bits (device), when bit_base is a tensor
     total: torch.Tensor = None    # this shard's payload bits (device), as planned
     plan_gen: int = None          # the engine's plan identity (pack_status of THIS encode)
+    status_ok: bool = False       # finalize() has checked this stream's pack status
 
 
 class ShardedHuffman:
@@ -155,9 +156,11 @@ class ShardedHuffman:
             s.bit_base, s.bits, s.totals = int(sum(tv[: self.rank])), int(tv[self.rank]), None
         elif s.bits < 0:
             s.bits = int(s.total.item()) if s.total is not None else int(self.e.plan_total())
-        st = self.e.pack_status(s.table, s.plan_gen)
-        if st != 0:
-            raise RuntimeError(f"rank {self.rank}: pack failed with status {st} (dc_huff_pack_status)")
+        if not s.status_ok:
+            st = self.e.pack_status(s.table, s.plan_gen)
+            if st != 0:
+                raise RuntimeError(f"rank {self.rank}: pack failed with status {st} (dc_huff_pack_status)")
+            s.status_ok = True
         return s
 
     def decode(self, s: ShardStream, out=None):
@@ -433,6 +436,7 @@ class ShardedSmall:
         sync = (buf["sync"][0][: max(ng, 1)], buf["sync"][1][: max(nch, 1)])
         s = ShardStream(buf["words"], 0, bits, sync, S, m, tab, None, tot, gen)
         s.literal = False
+        s.fused = True
         return s
 
     # ---- fused encode of a shard (world > 1) -----------------------------------------------
@@ -448,6 +452,11 @@ class ShardedSmall:
         n = x.numel()
         if n < 2:
             raise ValueError("each shard needs >= 2 bytes")
+        if x.data_ptr() % 16:
+            # the fused kernels read the shard as 16-B granules (dc_small_huff_shard_hist returns
+            # DC_E_ARG otherwise); an aligned copy keeps this rank in step with the others'
+            # collectives below, where a raise here would leave them waiting in the all_reduce
+            x = x.clone()
         dev, r, e = x.device, self.rank, self.e
         # 1. halos: every rank's first and last byte and size, gathered on the device
         ends = self._all_gather_dev(torch.stack([x[0].to(torch.int64), x[n - 1].to(torch.int64),
@@ -484,6 +493,7 @@ class ShardedSmall:
         e.small_shard_pack_async(x, tab, shard, words, sync, gsync, S)
         s = ShardStream(words, shard[0:1], -1, sync, S, -1, tab, None, tot, gen)
         s.literal = False
+        s.fused = True
         s.shard_fused = {"x": x, "n_ary": n_ary, "shard": shard, "m": m, "gsync": gsync, "literal": literal}
         return s
 
@@ -508,6 +518,7 @@ class ShardedSmall:
             self.h.finalize(t)
             s.__dict__.update(t.__dict__)
             s.shard_fused = None
+            s.fused = False
             return s
         s.bit_base, s.bits, s.n, s.totals = int(v[0]), int(v[2]), int(v[3]), None
         ng, nch = self.e.sync_sizes(s.n, s.sync_syms)
@@ -525,9 +536,11 @@ class ShardedSmall:
         if fs is None:
             return self.h.gather(s, dst)
         dev = s.words.device
+        # (this stream's own plan generation and total: finalize() above already checked its
+        # pack status, and the words gather must not read a later plan's on this context)
         empty = ShardStream(s.words, s.bit_base, s.bits, (torch.empty(0, dtype=torch.int64, device=dev),
                                                           torch.empty(0, dtype=torch.int16, device=dev)),
-                            s.sync_syms, s.n, s.table)
+                            s.sync_syms, s.n, s.table, None, s.total, s.plan_gen, True)
         g = self.h.gather(empty, dst)
         S = s.sync_syms
         M, mm = fs["M"], s.n

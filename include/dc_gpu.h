@@ -125,7 +125,8 @@ enum {
                                      3 tokens + the plain-code resolve (k_nyb_resolve_s) (A/B) */
     DC_OPT_PACK_BLOCK = 8,        /* 2: the wave-per-range pack (k_huff_pack_w) instead of the
                                      workgroup-per-block one (k_huff_pack); 3: the same at 4 codes
-                                     a lane; A/B (0.386 vs 0.380 ms on 1 GiB C2) */
+                                     a lane; A/B builds only (-DDC_AB_KERNELS; 0.386 vs 0.380 ms
+                                     on 1 GiB C2): a product build accepts 0 alone */
     DC_OPT_NYB_WTILE_OFF = 9      /* 1: the static nybble encode and the nybble decode write each
                                      4096-element tile with a workgroup (k_fsm_write) instead of a
                                      wave (k_nyb_enc_wtile / k_nyb_dec_wtile) */
@@ -225,6 +226,9 @@ int dc_huff_pack_status_gen(dc_ctx *ctx, const dc_dtable *d_table, uint32_t gen)
  * (4) two plan launches (block bit offsets, each block's first symbol index, the sync-length
  *     words of chunks spanning block boundaries zeroed) and the pack. d_sync_len (4-B aligned)
  *     and d_sync_base are required, sized for dc_small_huff_symbols() symbols: at most n + 1.
+ *     Sizing: the kernels clear and add d_sync_len as whole dwords (two u16 lengths at a time),
+ *     so allocate ceil(chunks / 2) * 2 + 2 u16 entries, chunks = ceil((n + 1) / S): with an odd
+ *     chunk count the last dword reaches one entry past the last chunk.
  * dc_huff_pack_status then returns DC_E_FALLBACK (nothing usable written) when the front-end
  * output falls back to LITERAL (small_compression.c:655-662), when every byte value occurs in
  * M (the pack marks a pair's start with a byte value that has no code), or when a 32 KiB block
@@ -250,7 +254,10 @@ int dc_small_huff_symbols(dc_ctx *ctx, uint64_t *h_symbols);
  * at entry c - (c0 & ~1), c0 = its first chunk, the first and last entries partial: the gather adds
  * the neighbours' parts; d_gsync_base: the groups that start in the shard, from group
  * ceil(first symbol / 64 S)). Fallbacks as dc_small_huff_pack_async, except the LITERAL test,
- * which belongs to the whole stream (the caller's). */
+ * which belongs to the whole stream (the caller's). Sizes: d_sync_len / d_sync_base as for
+ * dc_small_huff_pack_async (n + 1 symbols, u16 lengths rounded up to whole dwords + 2 entries);
+ * d_gsync_len / d_gsync_base for n + 1 + 2 S symbols (the shard's chunks counted from c0 & ~1,
+ * plus the partial chunks it shares at either end), the lengths rounded the same way. */
 int dc_small_huff_shard_hist(dc_ctx *ctx, const uint8_t *d_in, uint64_t n, const int64_t *d_shard,
                              uint64_t *d_hist);
 int dc_small_huff_shard_pack_async(dc_ctx *ctx, const uint8_t *d_in, uint64_t n, const dc_dtable *d_table,
