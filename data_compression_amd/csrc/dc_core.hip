@@ -6437,7 +6437,7 @@ int dc_ctx_set_option(dc_ctx *c, int option, int64_t value)
         return DC_OK;
     case DC_OPT_PACK_BLOCK:   // 2/3: k_huff_pack_w, in DC_AB_KERNELS builds only
 #ifdef DC_AB_KERNELS
-        if (value < 0 || value > 3) return DC_E_ARG;
+        if (value < 0 || value > 5) return DC_E_ARG;
 #else
         if (value != 0) return DC_E_ARG;
 #endif
@@ -6767,7 +6767,17 @@ static int pack_impl(dc_ctx *c, const uint8_t *d_in, uint64_t n, const dc_dtable
     const int r = plan_offsets(c, plan_err(c), plan_err_next(c), bit_base, d_base, d_words, words_cap);
     if (r != DC_OK) return r;
 #ifdef DC_AB_KERNELS
-    if ((((uintptr_t)d_words) & 15) == 0 && c->opt_pack_block >= 2 && n >= 1024) {   // A/B: 0.386 vs 0.380 ms
+    if (c->opt_pack_block == 5) {   // A/B: a half-block stage, more workgroups per CU (k_huff_pack_half)
+        LAUNCH(c, "huff_pack", k_huff_pack_half, (nb + 1) / 2, 256, d_in, n, d_table, (const uint64_t *)c->d_off,
+               bit_base, d_base, d_words, d_sync_base, d_sync_len, sync_syms, nb, words_cap, plan_err(c));
+    } else if (c->opt_pack_block == 4) {   // A/B: the next block in flight by LDS-DMA (k_huff_pack_dma)
+        int ncu = 256;
+        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device);
+        const uint64_t grid = (uint64_t)ncu * PKD_WG_PER_CU;
+        LAUNCH(c, "huff_pack", k_huff_pack_dma, (nb < grid ? nb : grid) + 1, 256, d_in, n, d_table,
+               (const uint64_t *)c->d_off, bit_base, d_base, d_words, d_sync_base, d_sync_len, sync_syms, nb, words_cap,
+               plan_err(c), 1);
+    } else if ((((uintptr_t)d_words) & 15) == 0 && c->opt_pack_block >= 2 && n >= 1024) {   // A/B: 0.386 vs 0.380 ms
         if (ensure((void **)&c->d_scr, &c->scr_cap, (size_t)D8_SCRATCH_WAVES * D8_WSCR)) return DC_E_HIP;   // trash rows
         // one wave per range of bpw blocks (k_huff_pack_w): ~PW_WAVES waves, 4 per workgroup,
         // + workgroup 0: the decoder tables (k_huff_table leaves them to the pack's idle CU time)
