@@ -1,4 +1,4 @@
-# Round-5 profiling call (run under gpurun): every GPU test and smoke(); for the C2 bench line,
+# Round-6 profiling call (gpu_profile5.sh + C3's rocprof and PMC summaries) (run under gpurun): every GPU test and smoke(); for the C2 bench line,
 # C4 and C5 (fused): rocprofv3 --kernel-trace --stats of the bench command and PMC passes
 # (FETCH_SIZE, WRITE_SIZE, an SQ group; one rocprofv3 run each) summarised as the JSON bench.py
 # cites (profiles/INDEX.json, updated here first so the lines after cite these); then the bench
@@ -9,7 +9,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-TAG=${1:-r5z}
+TAG=${1:-r6z}
 OUT=gpurun_out/profiles_${TAG}
 mkdir -p gpurun_out $OUT profiles
 GiB=1073741824
@@ -50,12 +50,14 @@ brief() { python tools/bench_brief.py; }
 # ---- profiles first (so the bench lines below cite them)
 rocprof_stats ${TAG} C2 $GiB 2 || exit 1
 pmc_traffic ${TAG} C2 $GiB 2 || exit 1
+rocprof_stats ${TAG}_C3 C3 $GiB 16 --cfg C3 --nary 16 || exit 1
+pmc_traffic ${TAG}_C3 C3 $GiB 16 --cfg C3 --nary 16 || exit 1
 rocprof_stats ${TAG}_C4 C4 $GiB 2 --cfg C4 --nary 2 || exit 1
 pmc_traffic ${TAG}_C4 C4 $GiB 2 --cfg C4 --nary 2 || exit 1
 rocprof_stats ${TAG}_C5 C5 $GiB 16 --cfg C5 --nary 16 --frontend || exit 1
 pmc_traffic ${TAG}_C5 C5 $GiB 16 --cfg C5 --nary 16 --frontend || exit 1
-index_add rocprof ${TAG}_rocprof.json ${TAG}_C4_rocprof.json ${TAG}_C5_rocprof.json
-index_add pmc_traffic ${TAG}_pmc_traffic.json ${TAG}_C4_pmc_traffic.json ${TAG}_C5_pmc_traffic.json
+index_add rocprof ${TAG}_rocprof.json ${TAG}_C3_rocprof.json ${TAG}_C4_rocprof.json ${TAG}_C5_rocprof.json
+index_add pmc_traffic ${TAG}_pmc_traffic.json ${TAG}_C3_pmc_traffic.json ${TAG}_C4_pmc_traffic.json ${TAG}_C5_pmc_traffic.json
 echo "profiles done"
 # ---- the bench lines
 timeout -k 10 400 python bench.py > $OUT/${TAG}_bench.log 2>&1 || { tail -5 $OUT/${TAG}_bench.log; exit 1; }
@@ -70,7 +72,7 @@ done
 for m in static adaptive; do
   KEEP_TEMPLATE=1 pmc_traffic ${TAG}_nyb_$m C1-nyb-$m $GiB 0 --codec nybble --mode $m || exit 1
 done
-index_add pmc_traffic ${TAG}_pmc_traffic.json ${TAG}_C4_pmc_traffic.json ${TAG}_C5_pmc_traffic.json ${TAG}_nyb_static_pmc_traffic.json ${TAG}_nyb_adaptive_pmc_traffic.json
+index_add pmc_traffic ${TAG}_pmc_traffic.json ${TAG}_C3_pmc_traffic.json ${TAG}_C4_pmc_traffic.json ${TAG}_C5_pmc_traffic.json ${TAG}_nyb_static_pmc_traffic.json ${TAG}_nyb_adaptive_pmc_traffic.json
 for m in static adaptive; do
   timeout -k 10 400 python bench.py --codec nybble --mode $m > $OUT/${TAG}_nyb_$m.log 2>&1 || { tail -5 $OUT/${TAG}_nyb_$m.log; exit 1; }
   tail -1 $OUT/${TAG}_nyb_$m.log | brief
@@ -78,4 +80,4 @@ for m in static adaptive; do
   ST=$(ls gpurun_out/${TAG}_nprof_$m/*/run_kernel_stats.csv gpurun_out/${TAG}_nprof_$m/run_kernel_stats.csv 2>/dev/null | head -1)
   cp $ST $OUT/${TAG}_nyb_${m}_kernel_stats.csv
 done
-echo "profile5 done"
+echo "profile6 done"
