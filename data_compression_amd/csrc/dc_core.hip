@@ -1076,67 +1076,7 @@ static __device__ void dec_tables_build(dc_dtable *__restrict__ T, DecBuildLds &
     };
     wide(T->dlut14, DC_LUT14_BITS, false);
     wide(T->dlut15, DC_LUT15_BITS, true);
-    // 4-bit digits (n = 9..16) with codes of <= 4 digits: a 15-bit first level escapes every
-    // 4-digit (16-bit) code to the exact redo (C5's n = 16 front-end stream: half its chunks hold
-    // one, 0.13 ms per GiB), so dlut16 too: the symbol of the next 16 bits as a byte (4 per u32
-    // store); the fast decoder's N16 form takes the code's length from the canonical limits
-    const bool n16 = w == 4 && maxbits <= 16 && !T->fixed8;
-    if (n16) {
-        // a code of L digits is L 4-bit digits < n, MSB first; its canonical value is the base-n
-        // number they spell (code *= n per length, n_ary_huffman.c:1540-1568), so 16-bit windows
-        // are decoded digit by digit (a digit >= n: no code)
-        uint32_t *const dw = reinterpret_cast<uint32_t *>(T->dlut16);
-#pragma unroll 4
-        for (uint32_t p = t; p < (1u << 16) / 4; p += 256) {
-            uint32_t pr = 0;
-#pragma unroll
-            for (uint32_t q = 0; q < 4; ++q) {
-                const uint32_t x = 4 * p + q, top = __builtin_bitreverse32(x) >> 16;   // the window's 16 bits, MSB first
-                uint32_t sym = 0, v = 0;   // (no code: a corrupt stream, caught by the decoder's chunk-length check)
-                for (int L = 1; L <= maxL && L <= 4; ++L) {
-                    const uint32_t d = (top >> (16 - 4 * L)) & 15u;
-                    if (d >= (uint32_t)nary) break;
-                    v = v * (uint32_t)nary + d;
-                    if (L >= minL && v - S.startv[L] < S.cnt[L]) {
-                        sym = S.syms[(S.starti[L] + v - S.startv[L]) & (DC_MAX_SYMS - 1)] & 255u;
-                        break;
-                    }
-                }
-                pr |= sym << (8 * q);
-            }
-            dw[p] = pr;
-        }
-    }
-    if (t == 0) {
-        T->dlut2_k = l2ok ? (int32_t)K : 0;
-        T->n16 = n16 ? 1 : 0;
-        // dlut16's lengths: codes of > L digits are the windows at or past the digit string of
-        // first[L] + count[L] (the value after the last L-digit code), left-justified: every
-        // window when L < minL, none when L >= maxL. Each limit as 12 bits (its low 20 bits are
-        // zero: L <= 3), 0..4096, and the decoder's test t12 >= limit as the guard bit 0x8000 of
-        // t12 + 0x8000 - limit (16-bit fields: no carry between them)
-        uint32_t lim12[3];
-        for (int L = 1; L <= 3; ++L) {
-            uint32_t v = 4096u;   // never reached
-            if (n16 && L < maxL) {
-                if (L < minL) {
-                    v = 0;
-                } else {
-                    uint32_t B = S.startv[L] + S.cnt[L], bits = 0;
-                    for (int i = 0; i < L; ++i) {   // B's L base-n digits, as 4-bit digits
-                        bits |= (B % (uint32_t)nary) << (4 * i);
-                        B /= (uint32_t)nary;
-                    }
-                    v = bits << (12 - 4 * L);
-                }
-            }
-            lim12[L - 1] = v;
-        }
-        T->n16_th[0] = ((0x8000u - lim12[0]) << 16) | (0x8000u - lim12[1]);
-        T->n16_th[1] = 0x8000u - lim12[2];
-        T->n16_th[2] = 0;
-        T->n16_th[3] = 4;
-    }
+    if (t == 0) T->dlut2_k = l2ok ? (int32_t)K : 0;
     __syncthreads();
     if (t == 0) {   // every table store of the workgroup before the flag (agent scope)
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -2554,18 +2494,9 @@ static __device__ __forceinline__ void d8_win_init(D8Win<NC> &w, const uint64_t 
     }
 }
 
-// N16 (dc_dtable.n16: 4-bit digits, codes of up to 4 digits): the LDS table is dlut16, the next
-// 16 bits' symbol as a byte; the code's bits = 4 + 4 x the canonical limits its first 12 bits
-// (MSB first) reach, three 12-bit compares as guard bits of 16-bit fields (dc_dtable.n16_th), all
-// VALU: the chain's next window does not wait for the LDS read. A batch's 4 codes may then take
-// 64 bits, one more than the window holds past its early bit: a batch whose first three codes
-// took 48 is redone.
-struct D8N16 {
-    uint32_t c1, c2, base;   // dc_dtable.n16_th[0], [1], [3]
-};
-template <int NC, bool N16 = false>
+template <int NC>
 static __device__ __forceinline__ void d8_batch_q(const uint64_t *const *st, D8Win<NC> &w, uint32_t *o,
-                                                  const uint16_t *__restrict__ lut, uint32_t *mn, const D8N16 &th)
+                                                  const uint16_t *__restrict__ lut, uint32_t *mn)
 {
     uint64_t win[NC], nx[NC];
     uint32_t off[NC];
@@ -2580,35 +2511,21 @@ static __device__ __forceinline__ void d8_batch_q(const uint64_t *const *st, D8W
         off[j] = 0;
     }
     const char *const lb = reinterpret_cast<const char *>(lut);
-    const uint8_t *const lb8 = reinterpret_cast<const uint8_t *>(lut);
     constexpr uint32_t SEL[4] = {0x0c0c0c05u, 0x0c0c0500u, 0x0c050100u, 0x05020100u};
-    uint32_t e[NC][4], o3[NC];
+    uint32_t e[NC][4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
 #pragma unroll
         for (int j = 0; j < NC; ++j) {
             const uint32_t x = (uint32_t)(win[j] >> (off[j] & 63u));
-            if (!N16) {
-                e[j][k] = *reinterpret_cast<const uint16_t *>(lb + (x & ((2u << D8_LUT_BITS) - 2u)));
-            } else {
-                const uint32_t sym = lb8[(x >> 1) & 0xFFFFu];   // (bit 0: the early bit)
-                // the window's first 12 bits MSB first, against the three limits at once: two in
-                // the 16-bit fields of one dword, their guard bits set where the window reaches them
-                const uint32_t t12 = (__builtin_bitreverse32(x) >> 19) & 0xFFFu;
-                const uint32_t d1 = ((t12 << 16) | t12) + th.c1, d2 = t12 + th.c2;
-                const uint32_t nb = th.base + 4u * (uint32_t)__popc((d1 & 0x80008000u) | ((d2 >> 15) & 1u));
-                e[j][k] = nb | (sym << 8);
-                off[j] += nb;   // (the length does not wait for the symbol's LDS read)
-            }
+            e[j][k] = *reinterpret_cast<const uint16_t *>(lb + (x & ((2u << D8_LUT_BITS) - 2u)));
             o[j] = __builtin_amdgcn_perm(e[j][k], k ? o[j] : 0u, SEL[k]);
-            if (!N16) off[j] += e[j][k];
-            if (N16 && k == 2) o3[j] = off[j] & 255u;   // the first three codes' bits
+            off[j] += e[j][k];
         }
     }
 #pragma unroll
     for (int j = 0; j < NC; ++j) {
-        if (N16) mn[j] = o3[j] >= 48u ? 0u : mn[j];
-        else mn[j] = min(mn[j], min(min(e[j][0], e[j][1]), min(e[j][2], e[j][3])));
+        mn[j] = min(mn[j], min(min(e[j][0], e[j][1]), min(e[j][2], e[j][3])));
         // a batch takes <= 60 bits (4 codes of <= 15), so qb < 124: one qword at most
         const uint32_t qb = w.qb[j] + (off[j] & 255u);
         const bool r = qb >= 64u;
@@ -2621,22 +2538,22 @@ static __device__ __forceinline__ void d8_batch_q(const uint64_t *const *st, D8W
 
 // The 16 batches of a 64-symbol chunk (4 pieces of 16 B per lane), unrolled by template
 // recursion; the pieces stay in registers until the chunk is done.
-template <int NC, int Q, bool N16 = false>
+template <int NC, int Q>
 struct D8PiecesQ {
     static __device__ __forceinline__ void run(const uint64_t *const *st, D8Win<NC> &w, uint32_t (*o)[16],
-                                               const uint16_t *__restrict__ lut, uint32_t *mn, const D8N16 &th)
+                                               const uint16_t *__restrict__ lut, uint32_t *mn)
     {
         uint32_t b[NC];
-        d8_batch_q<NC, N16>(st, w, b, lut, mn, th);
+        d8_batch_q<NC>(st, w, b, lut, mn);
 #pragma unroll
         for (int j = 0; j < NC; ++j) o[j][Q] = b[j];
-        D8PiecesQ<NC, Q + 1, N16>::run(st, w, o, lut, mn, th);
+        D8PiecesQ<NC, Q + 1>::run(st, w, o, lut, mn);
     }
 };
-template <int NC, bool N16>
-struct D8PiecesQ<NC, 16, N16> {
+template <int NC>
+struct D8PiecesQ<NC, 16> {
     static __device__ __forceinline__ void run(const uint64_t *const *, D8Win<NC> &, uint32_t (*)[16],
-                                               const uint16_t *__restrict__, uint32_t *, const D8N16 &)
+                                               const uint16_t *__restrict__, uint32_t *)
     {
     }
 };
@@ -2691,7 +2608,6 @@ struct D8Geo {            // where a tuple's spans and chunks lie; all uniform e
     uint32_t lead[NC];    // stage bit of the group's first chunk
     uint32_t last[NC];    // last uint4 of the stage
     uint32_t off[NC];     // this lane's chunk: bit offset inside the group span
-    uint32_t len[NC];     // and its bits (N16: the decode's end is checked against it)
     bool fast;
 };
 
@@ -2733,7 +2649,6 @@ static __device__ __forceinline__ void d8_geometry(D8Geo<NC> &g, const D8Meta<NC
     for (int j = 0; j < NC; ++j) {
         const uint32_t span = __builtin_amdgcn_readlane(in[j], 63);
         g.off[j] = in[j] - len[j];
-        g.len[j] = len[j];
         const uint64_t rel = m.base[j] - (word_base << 5);
         g.wo[j] = (uint32_t)(rel >> 5) & ~3u;
         g.lead[j] = (uint32_t)rel & 127u;
@@ -2873,7 +2788,7 @@ static __device__ void d8_stale_exit(int *__restrict__ err, uint32_t *__restrict
 // EXP (the C5 decode, dc_small_huff_decode): also the number of symbols >= 0x80 of every group
 // into gexp[group] (each is a front-end pair: two output bytes), so the front-end inverse needs
 // no counting pass of its own; the redo adds those of the chunks it rewrites.
-template <int NW, int NC, bool EXP = false, bool N16 = false>
+template <int NW, int NC, bool EXP = false>
 __global__ __launch_bounds__(NW * 64) void k_huff_decode8(const uint32_t *__restrict__ in, uint64_t bit_base, const uint64_t *__restrict__ d_base,
                                                           const uint64_t *__restrict__ sync_base,
                                                           const uint16_t *__restrict__ sync_len, uint64_t n,
@@ -2943,7 +2858,7 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode8(const uint32_t *__rest
     // hold a code of > 15 bits (to the exact redo; 2.5% with the 14-bit table of r1)
     static_assert(D8_LUT_BITS == DC_LUT15_BITS, "table width");
     for (int i = t; i < (1 << D8_LUT_BITS) / 8; i += NT)
-        reinterpret_cast<uint4 *>(L.lut)[i] = reinterpret_cast<const uint4 *>(N16 ? (const void *)T->dlut16 : (const void *)T->dlut15)[i];
+        reinterpret_cast<uint4 *>(L.lut)[i] = reinterpret_cast<const uint4 *>(T->dlut15)[i];
     if (t == 0) L.exhausted = 0;
     __syncthreads();
 
@@ -2960,16 +2875,6 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode8(const uint32_t *__rest
         st64[j] = reinterpret_cast<const uint64_t *>(stw[j]);
     }
     const uint32_t stride = gridDim.x * NW;
-    // dlut16 (4-bit digits with 16-bit codes): the canonical limits of 1-3 digit codes as
-    // thresholds of the MSB-first window (D8N16)
-    D8N16 th{0u, 0u, 4u};
-    // (an N16 launch on a table without dlut16, e.g. codes of 5 digits: every chunk to the redo)
-    const bool n16ok = !N16 || T->n16 != 0;
-    if (N16) {
-        th.c1 = T->n16_th[0];
-        th.c2 = T->n16_th[1];
-        th.base = T->n16_th[3];
-    }
     // Software pipeline (per wave, one tuple of NC groups per iteration): while tuple i
     // decodes, the spans of tuple i+1 are in flight into registers and the sync index of
     // tuple i+2 too, so no iteration waits for a global round trip.
@@ -3035,20 +2940,11 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode8(const uint32_t *__rest
         // fast (the fixup skips chunks past the end), reaches 0 on a code of > 12 bits
         uint32_t o[NC][16], mn[NC];
 #pragma unroll
-        for (int j = 0; j < NC; ++j) mn[j] = (cur.fast && (!N16 || n16ok)) ? 255u : 0u;
+        for (int j = 0; j < NC; ++j) mn[j] = cur.fast ? 255u : 0u;
         {
             D8Win<NC> wq;
             d8_win_init<NC>(wq, st64, c);
-            if (!N16) {
-                D8PiecesQ<NC, 0>::run(st64, wq, o, L.lut, mn, th);
-            } else {
-                D8PiecesQ<NC, 0, true>::run(st64, wq, o, L.lut, mn, th);
-                // no escapes to flag a code the table does not hold (a corrupt stream): a chunk
-                // must end where its length says, or it is redone (and reported) exactly
-#pragma unroll
-                for (int j = 0; j < NC; ++j)
-                    mn[j] = ((wq.qp[j] - 1u) * 64u + wq.qb[j] - 63u == c[j] + cur.len[j]) ? mn[j] : 0u;
-            }
+            D8PiecesQ<NC, 0>::run(st64, wq, o, L.lut, mn);
         }
         d8_out<NC>(stw, o, dst, lane);
         // chunks with a code of > 12 bits (and every chunk of a tuple that was not fast:
@@ -3111,8 +3007,7 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode8(const uint32_t *__rest
 #ifndef D8F_ROW
 #define D8F_ROW 20   /* words of a lane's staged span (longer chunks re-stage it further on; r2-r3: 24) */
 #endif
-static_assert(offsetof(dc_dtable, dlut14) % 16 == 0 && offsetof(dc_dtable, dlut15) % 16 == 0 && offsetof(dc_dtable, dlut16) % 16 == 0 &&
-                  offsetof(dc_dtable, dlut2) % 8 == 0,
+static_assert(offsetof(dc_dtable, dlut14) % 16 == 0 && offsetof(dc_dtable, dlut15) % 16 == 0 && offsetof(dc_dtable, dlut2) % 8 == 0,
               "table copies");
 struct FixLds {
     __attribute__((aligned(16))) uint16_t lut[1 << D8F_LUT_BITS];   // the fast decoder's 14-bit first level
@@ -6289,7 +6184,6 @@ struct dc_ctx {
     // takes the next slot, which a kernel of the call before cleared (no memset launch)
     int *d_errp, *d_errd;
     uint32_t gen_p, gen_d;
-    const dc_dtable *w4_tab;                      // the table this context last wrote, if n = 9..16 (N16 decode hint)
     const dc_dtable *dec_fresh;                   // decoder tables current: this context's last pack built them,
     uint64_t dec_fresh_gen;                       // ... while g_table_gen had this value (see table_written)
     uint32_t *d_queue;                            // decode tuple scheduler heads (D8Sched)
@@ -6349,13 +6243,10 @@ struct dc_ctx {
 // recycled buffer filled by another context, is never taken for the packed one. (Keyed on the
 // address alone, such a table skipped the rebuild and its decode reported a stream error.)
 static std::atomic<uint64_t> g_table_gen{1};
-static void table_written(dc_ctx *c, const dc_dtable *t, int nary)
+static void table_written(dc_ctx *c)
 {
     c->dec_fresh = nullptr;
     g_table_gen.fetch_add(1, std::memory_order_relaxed);
-    // a hint only (the N16 decoder checks the table's own n16 flag and sends every chunk to the
-    // exact redo when it is not set): the table this context last wrote with 4-bit digits
-    c->w4_tab = (nary >= 9 && nary <= 16) ? t : nullptr;
 }
 static void dec_tables_built(dc_ctx *c, const dc_dtable *t)
 {
@@ -6678,7 +6569,7 @@ static int table_common(dc_ctx *c, const uint64_t *d_freq, int is_hist, const in
                         int nary, dc_dtable *d_table)
 {
     if (!c || !d_table || M < 0 || M >= DC_MAX_SYMS || nary < 2 || nary > 256) return DC_E_ARG;
-    table_written(c, d_table, nary);
+    table_written(c);
     LAUNCH(c, "huff_table", k_huff_table, 1, 256, d_freq, is_hist, d_len, M, nary, d_table, (dc_tree *)nullptr,
            (const uint64_t *)nullptr, (uint64_t *)nullptr, (int *)nullptr, (int *)nullptr);
     return DC_OK;
@@ -6687,7 +6578,7 @@ static int table_common(dc_ctx *c, const uint64_t *d_freq, int is_hist, const in
 int dc_huff_tree(dc_ctx *c, const uint64_t *d_freq, int M, int nary, dc_dtable *d_table, dc_tree *d_tree)
 {
     if (!c || !d_freq || !d_table || !d_tree || M < 0 || M >= DC_MAX_SYMS || nary < 2 || nary > 256) return DC_E_ARG;
-    table_written(c, d_table, nary);
+    table_written(c);
     LAUNCH(c, "huff_tree", k_huff_table, 1, 256, d_freq, 0, (const int32_t *)nullptr, M, nary, d_table, d_tree,
            (const uint64_t *)nullptr, (uint64_t *)nullptr, (int *)nullptr, (int *)nullptr);
     return DC_OK;
@@ -6753,7 +6644,7 @@ int dc_huff_table_plan(dc_ctx *c, const uint64_t *d_hist, int M, int nary, dc_dt
     if (!c || !d_hist || !d_table || !d_total_bits || M < 0 || M >= DC_MAX_SYMS || nary < 2 || nary > 256) return DC_E_ARG;
     if (!c->hist_in && c->hist_n) return DC_E_STATE;
     ++c->gen_p;   // this plan's error slot (the table kernel clears the next one)
-    table_written(c, d_table, nary);
+    table_written(c);
     // the table of d_hist (e.g. the all-reduced histogram of every shard) and, in the same
     // launch, the payload bits of THIS context's last histogram under it (huff_table_body's plan)
     LAUNCH(c, "huff_table", k_huff_table, 1, 256, d_hist, 1, (const int32_t *)nullptr, M, nary, d_table,
@@ -6769,7 +6660,7 @@ int dc_huff_encode_plan(dc_ctx *c, const uint8_t *d_in, uint64_t n, int M, int n
 {
     if (!c || !d_table || !d_total_bits || M < 0 || M >= DC_MAX_SYMS || nary < 2 || nary > 256) return DC_E_ARG;
     ++c->gen_p;
-    table_written(c, d_table, nary);
+    table_written(c);
     const int r = hist_impl(c, d_in, n, d_hist,
                             HistFuse{d_table, M, nary, d_total_bits, plan_err(c), plan_err_next(c)});
     if (r != DC_OK) { --c->gen_p; return r; }
@@ -6930,7 +6821,7 @@ int dc_small_huff_plan(dc_ctx *c, const uint8_t *d_in, uint64_t n, int M, int na
     if (!c || !d_table || !d_total_bits || !d_hist || M < 255 || M >= DC_MAX_SYMS || nary < 2 || nary > 256) return DC_E_ARG;
     if (n < 2) return DC_E_FALLBACK;   // the front-end output of < 2 bytes is LITERAL
     ++c->gen_p;
-    table_written(c, d_table, nary);
+    table_written(c);
     const int r = hist_impl(c, d_in, n, d_hist, HistFuse{d_table, M, nary, d_total_bits, plan_err(c), plan_err_next(c)},
                             true);
     if (r != DC_OK) { --c->gen_p; return r; }
@@ -7111,20 +7002,13 @@ static int decode_impl(dc_ctx *c, const uint32_t *d_words, uint64_t bit_base, co
                    spct, (uint64_t *)c->d_fix, (uint64_t *)c->d_fixpos, (uint8_t *)c->d_scr);
         } else
 #endif
-        const bool n16 = c->w4_tab == d_table;   // 4-bit digits: dlut16, no redo of 16-bit codes
-#define D8_LAUNCH_EXP(EXP_, N16_)                                                                             \
-        LAUNCH(c, "huff_decode", (k_huff_decode8<11, 2, EXP_, N16_>), (tuples + 10) / 11 < 256 ? (tuples + 10) / 11 : 256, \
-               11 * 64, d_words, bit_base, d_base, d_sync_base, d_sync_len, n, words, d_table, d_out, derr,        \
-               c->d_queue, spct, (uint64_t *)c->d_fix, (uint64_t *)c->d_fixpos, (uint8_t *)c->d_scr, d_gexp)
         if (d_gexp) {   // (C5) with the symbols >= 0x80 per group
-            if (n16) D8_LAUNCH_EXP(true, true);
-            else D8_LAUNCH_EXP(true, false);
-        } else if (n16) {
-            D8_LAUNCH_EXP(false, true);
+            LAUNCH(c, "huff_decode", (k_huff_decode8<11, 2, true>), (tuples + 10) / 11 < 256 ? (tuples + 10) / 11 : 256,
+                   11 * 64, d_words, bit_base, d_base, d_sync_base, d_sync_len, n, words, d_table, d_out, derr,
+                   c->d_queue, spct, (uint64_t *)c->d_fix, (uint64_t *)c->d_fixpos, (uint8_t *)c->d_scr, d_gexp);
         } else {   // one code per lookup, 11 waves x 2 chains (the 15-bit table takes 64 KiB of LDS)
             D8_LAUNCH(11, 2);
         }
-#undef D8_LAUNCH_EXP
 #undef D8_LAUNCH
         c->last_groups = groups;
         LAUNCH(c, "huff_decode_fix", k_huff_decode8_fix, 256, D8F_WAVES * 64, d_words, n, words, d_table, d_out,

@@ -72,21 +72,12 @@ typedef struct dc_dtable {
     uint16_t dlut2[DC_LUT2_CAP];
     int32_t dlut2_k, dec_ready;   /* dec_ready: lut/dlut/dlut2/dlut14/dlut15 are current */
     int32_t fixed8;               /* every byte's code is 8 bits (or absent): pack and decode are byte maps */
-    int32_t n16;                  /* dlut16 is built: w = 4 (n = 9..16), codes of <= 16 bits, not fixed8 */
-    int32_t pad_[2];
-    uint32_t n16_th[4];           /* dlut16's code lengths: bits = n16_th[3] + 4 x #{i < 3: window >
-                                     n16_th[i]} (the MSB-first 32-bit window; canonical limits of
-                                     1-, 2-, 3-digit codes as 4-bit digit strings) */
+    int32_t pad_[3];
     /* dlut14: next 14 bits -> bits | sym << 8 for codes of <= 14 bits; bits 0: longer, sym =
      * the escape id of its 12-bit prefix (as dlut); 16-B aligned for vector copies */
     uint16_t dlut14[1 << DC_LUT14_BITS];
     /* dlut15: the same on the next 15 bits (the fast decoder's table) */
     uint16_t dlut15[1 << DC_LUT15_BITS];
-    /* dlut16 (n16 set: 4-bit digits, codes of up to 4 digits, which a 15-bit table escapes to the
-     * exact redo): the next 16 bits -> the symbol, one byte; the code's length follows from the
-     * canonical limits lim[4], lim[8], lim[12] (the fast decoder's N16 form, which redoes no chunk
-     * of a valid stream) */
-    uint8_t dlut16[1 << 16];
 } dc_dtable;
 
 /* Node list of the n-ary Huffman tree (generate_huffman_tree's in-out list[],
