@@ -6437,7 +6437,7 @@ int dc_ctx_set_option(dc_ctx *c, int option, int64_t value)
         return DC_OK;
     case DC_OPT_PACK_BLOCK:   // 2/3: k_huff_pack_w, in DC_AB_KERNELS builds only
 #ifdef DC_AB_KERNELS
-        if (value < 0 || value > 5) return DC_E_ARG;
+        if (value < 0 || value > 6) return DC_E_ARG;
 #else
         if (value != 0) return DC_E_ARG;
 #endif
@@ -6767,7 +6767,12 @@ static int pack_impl(dc_ctx *c, const uint8_t *d_in, uint64_t n, const dc_dtable
     const int r = plan_offsets(c, plan_err(c), plan_err_next(c), bit_base, d_base, d_words, words_cap);
     if (r != DC_OK) return r;
 #ifdef DC_AB_KERNELS
-    if (c->opt_pack_block == 5) {   // A/B: a half-block stage, more workgroups per CU (k_huff_pack_half)
+    if (c->opt_pack_block == 6) {   // A/B: one code-table read per byte (k_huff_pack_fold)
+        const uint64_t gmax = c->opt_pack_grid ? c->opt_pack_grid : (nb + 1) / 2;
+        const uint64_t grid = nb < gmax ? nb : gmax;
+        LAUNCH(c, "huff_pack", k_huff_pack_fold, grid + 1, 256, d_in, n, d_table, (const uint64_t *)c->d_off, bit_base,
+               d_base, d_words, d_sync_base, d_sync_len, sync_syms, nb, words_cap, plan_err(c), 1);
+    } else if (c->opt_pack_block == 5) {   // A/B: a half-block stage, more workgroups per CU (k_huff_pack_half)
         LAUNCH(c, "huff_pack", k_huff_pack_half, (nb + 1) / 2, 256, d_in, n, d_table, (const uint64_t *)c->d_off,
                bit_base, d_base, d_words, d_sync_base, d_sync_len, sync_syms, nb, words_cap, plan_err(c));
     } else if (c->opt_pack_block == 4) {   // A/B: the next block in flight by LDS-DMA (k_huff_pack_dma)
