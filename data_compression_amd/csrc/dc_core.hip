@@ -1393,6 +1393,7 @@ __global__ void k_zero_bounds(const uint64_t *__restrict__ off, uint64_t nblocks
 // and over ranges of 4-16 blocks per workgroup, 0.45-0.50 ms, against 0.373 for this pack after
 // the plan launches: a look-back costs ~2 us per agent-scope round trip, and ranges of blocks
 // long enough to hide it leave the last dispatch round unbalanced.)
+template <bool PF = false>   // PF (A/B): the next block loaded piece by piece as pass B frees each
 __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ in, uint64_t n,
                                                    const dc_dtable *__restrict__ T,
                                                    const uint64_t *__restrict__ block_off, uint64_t bit_base,
@@ -1484,12 +1485,20 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
 
     // two blocks per workgroup, grid-stride (r1, 1 GiB C2: 16384 workgroups 0.452 ms against
     // 0.481 at 4096, 0.469 at 32768, 0.504 at 1024)
+    uint4 blkv[PACK_PIECES];
+    auto load_block = [&](uint64_t bb) {
+#pragma unroll
+        for (int k = 0; k < (int)(DC_BLOCK_BYTES / PACK_TILE); ++k)
+            blkv[k] = LD_PACK(reinterpret_cast<const uint4 *>(in + bb * (uint64_t)DC_BLOCK_BYTES + (uint64_t)k * PACK_TILE + (uint64_t)t * 16));
+    };
+    const uint64_t nfull = n / DC_BLOCK_BYTES;
+    if (PF && bx < nfull) load_block(bx);
     for (uint64_t b = bx; b < nblocks; b += gstride) {
         const uint64_t blk_start = b * (uint64_t)DC_BLOCK_BYTES;
         const uint64_t blk_end = (blk_start + DC_BLOCK_BYTES < n) ? blk_start + DC_BLOCK_BYTES : n;
-        uint4 blkv[PACK_PIECES];
         const bool full = (blk_start + DC_BLOCK_BYTES <= n);
-        if (full) {
+        const uint64_t bnext = b + gstride;   // (PF: its loads go out as pass B frees each piece)
+        if (!PF && full) {
             // the whole 32 KiB block: 8 independent 16-B loads per lane in flight at once
             // (loading the next block ahead measured slower every way tried: in extra
             // registers -8% (147 VGPRs), into these registers once pass B is done -4%, into
@@ -1619,6 +1628,8 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
                         }
                     }
                 }
+                if (PF && bnext < nfull)   // piece k of the next block, in flight through the rest
+                    blkv[k] = LD_PACK(reinterpret_cast<const uint4 *>(in + bnext * (uint64_t)DC_BLOCK_BYTES + (uint64_t)k * PACK_TILE + (uint64_t)t * 16));
                 __builtin_amdgcn_sched_barrier(0);   // keep the pieces' lookups from being hoisted
             }
             lds_barrier();
@@ -1752,6 +1763,7 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
         for (uint32_t i = 4u * t; i < PACK_BLK_WORDS + 4; i += 1024u)
             *reinterpret_cast<uint4 *>(&s_stage[i]) = make_uint4(0u, 0u, 0u, 0u);
         __syncthreads();
+        if (PF && bnext < nfull) load_block(bnext);
     }
 }
 
@@ -6437,7 +6449,7 @@ int dc_ctx_set_option(dc_ctx *c, int option, int64_t value)
         return DC_OK;
     case DC_OPT_PACK_BLOCK:   // 2/3: k_huff_pack_w, in DC_AB_KERNELS builds only
 #ifdef DC_AB_KERNELS
-        if (value < 0 || value > 6) return DC_E_ARG;
+        if (value < 0 || value > 7) return DC_E_ARG;
 #else
         if (value != 0) return DC_E_ARG;
 #endif
@@ -6767,7 +6779,14 @@ static int pack_impl(dc_ctx *c, const uint8_t *d_in, uint64_t n, const dc_dtable
     const int r = plan_offsets(c, plan_err(c), plan_err_next(c), bit_base, d_base, d_words, words_cap);
     if (r != DC_OK) return r;
 #ifdef DC_AB_KERNELS
-    if (c->opt_pack_block == 6) {   // A/B: one code-table read per byte (k_huff_pack_fold)
+    if (c->opt_pack_block == 7) {   // A/B: the next block's pieces loaded as pass B frees them, persistent grid
+        int ncu = 256;
+        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device);
+        const uint64_t gmax = c->opt_pack_grid ? c->opt_pack_grid : (uint64_t)ncu * 4;
+        const uint64_t grid = nb < gmax ? nb : gmax;
+        LAUNCH(c, "huff_pack", k_huff_pack<true>, grid + 1, 256, d_in, n, d_table, (const uint64_t *)c->d_off, bit_base,
+               d_base, d_words, d_sync_base, d_sync_len, sync_syms, nb, words_cap, plan_err(c), 1);
+    } else if (c->opt_pack_block == 6) {   // A/B: one code-table read per byte (k_huff_pack_fold)
         const uint64_t gmax = c->opt_pack_grid ? c->opt_pack_grid : (nb + 1) / 2;
         const uint64_t grid = nb < gmax ? nb : gmax;
         LAUNCH(c, "huff_pack", k_huff_pack_fold, grid + 1, 256, d_in, n, d_table, (const uint64_t *)c->d_off, bit_base,
@@ -6797,7 +6816,7 @@ static int pack_impl(dc_ctx *c, const uint8_t *d_in, uint64_t n, const dc_dtable
         // two blocks per workgroup (grid-stride) + workgroup 0: the decoder tables
         const uint64_t gmax = c->opt_pack_grid ? c->opt_pack_grid : (nb + 1) / 2;
         const uint64_t grid = nb < gmax ? nb : gmax;
-        LAUNCH(c, "huff_pack", k_huff_pack, grid + 1, 256, d_in, n, d_table, (const uint64_t *)c->d_off, bit_base,
+        LAUNCH(c, "huff_pack", k_huff_pack<>, grid + 1, 256, d_in, n, d_table, (const uint64_t *)c->d_off, bit_base,
                d_base, d_words, d_sync_base, d_sync_len, sync_syms, nb, words_cap, plan_err(c), 1);
     }
     dec_tables_built(c, d_table);   // workgroup 0 built the decoder tables
