@@ -1788,6 +1788,28 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
 // index shard[1]: gsync_len (u16, entry c - (c0 & ~1) for global chunk c, c0 = the shard's first;
 // the first and last chunks hold this shard's part only, the gather adds the neighbours') and
 // gsync_base (group g at entry g - ceil(shard[1] / 64 S): the groups that start in this shard).
+// Bits of a piece before its symbol number jj (and jjg): the sum of the lengths L (a byte per
+// position, 0 = no symbol) of the positions whose inclusive symbol count is <= jj. Counts by
+// SWAR prefix sums per dword, the sums by v_dot4 against the 0/1 bytes of the compare.
+template <bool SH>
+static __device__ __forceinline__ void fe_chunk_bits(const uint32_t (&L)[4], uint32_t jj, uint32_t jjg, uint32_t &cap,
+                                                     uint32_t &capg)
+{
+    const uint32_t J = 0x80808080u + min(jj, 16u) * 0x01010101u, Jg = 0x80808080u + min(jjg, 16u) * 0x01010101u;
+    uint32_t prev = 0;   // the symbol count before the dword, in every byte
+    cap = 0;
+    capg = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t nz = ((L[q] + 0x7F7F7F7Fu) >> 7) & 0x01010101u;   // 1 per position with a symbol
+        const uint32_t y = nz + (nz << 8);
+        const uint32_t C = y + (y << 16) + prev;                          // inclusive counts (<= 16)
+        prev = __builtin_amdgcn_perm(0u, C, 0x03030303u);
+        cap = __builtin_amdgcn_udot4(L[q], ((J - C) >> 7) & 0x01010101u, cap, false);
+        if (SH) capg = __builtin_amdgcn_udot4(L[q], ((Jg - C) >> 7) & 0x01010101u, capg, false);
+    }
+}
+
 template <bool SH>
 __global__ __launch_bounds__(256) void k_fe_pack(const uint8_t *__restrict__ in, uint64_t n,
                                                  const dc_dtable *__restrict__ T,
@@ -1993,11 +2015,13 @@ __global__ __launch_bounds__(256) void k_fe_pack(const uint8_t *__restrict__ in,
             const uint32_t j0g = (uint32_t)(0ull - (mi + M)) & (S - 1);   // (SH: the global chunk start)
             const bool hasg = SH && j0g < Ck;
             const uint32_t jjg = hasg ? j0g : 0xFFFFu;
-            uint32_t ec = 0, cap = 0, capg = 0;   // symbols seen, bits before the chunk starts
-            auto tally = [&](uint32_t l) {
-                ec += l != 0u ? 1u : 0u;
-                cap += ec <= jj ? l : 0u;
-                if (SH) capg += ec <= jjg ? l : 0u;
+            // the piece's code lengths, a byte each (<= 32), for the chunk start's bit offset
+            // after pass B (fe_chunk_bits: SWAR, ~3.75 VALU per symbol with the packing; the
+            // per-symbol count and compare it replaced cost ~5: fe_pack 0.671 -> 0.641 ms per GiB
+            // of C5, profiles/r6k_fe_tally_nyb_ranks_ab.log)
+            uint32_t L4[4] = {0u, 0u, 0u, 0u};
+            auto tally = [&](int i, uint32_t l) {
+                L4[i >> 2] = (i & 3) ? L4[i >> 2] | (l << (8 * (i & 3))) : l;
             };
             uint32_t w4[4] = {blkv[k].x, blkv[k].y, blkv[k].z, blkv[k].w};
             asm volatile("" : "+v"(w4[0]), "+v"(w4[1]), "+v"(w4[2]), "+v"(w4[3]));
@@ -2012,7 +2036,7 @@ __global__ __launch_bounds__(256) void k_fe_pack(const uint8_t *__restrict__ in,
                     for (int i = 8 * h; i < 8 * h + 8; ++i) {
                         const uint2 e = s_tab[(w4[i >> 2] >> (8 * (i & 3))) & 255u];
                         acc = (acc << e.y) | e.x;
-                        tally(e.y);
+                        tally(i, e.y);
                     }
                     emit(acc, Th, pos);
                 } else {
@@ -2027,7 +2051,7 @@ __global__ __launch_bounds__(256) void k_fe_pack(const uint8_t *__restrict__ in,
                             const uint32_t wv = qq ? w4[2 * h + 1] : w4[2 * h];
                             e[i] = s_tab[(wv >> (8 * (bi & 3))) & 255u];
                             nq += e[i].y;
-                            tally(e[i].y);
+                            tally(bi, e[i].y);
                         }
                         if (nq <= 64u) {
                             uint64_t acc = 0;
@@ -2042,6 +2066,8 @@ __global__ __launch_bounds__(256) void k_fe_pack(const uint8_t *__restrict__ in,
                     }
                 }
             }
+            uint32_t cap, capg = 0;   // bits before the chunk starts
+            fe_chunk_bits<SH>(L4, jj, jjg, cap, capg);
             if (has) s_cb[(uint32_t)(((mi + j0) >> slog) - cf)] = (uint32_t)(As - blk_abs) + cap;
             if (hasg) s_cbg[(uint32_t)(((mi + M + j0g) >> slog) - cfg)] = (uint32_t)(As - blk_abs) + capg;
             __builtin_amdgcn_sched_barrier(0);
