@@ -118,12 +118,21 @@ class CpuEngine:
         sym = np.where(sec, a | 0x80, a)[~start]
         return np.concatenate([[8] if first else [], sym]).astype(np.uint8)
 
+    @staticmethod
+    def _check_granules(x):
+        # the HIP kernels read a shard as 16-B granules: dc_small_huff_shard_hist returns
+        # DC_E_ARG for a misaligned one (device.Codec raises), and so does this restatement
+        if x.data_ptr() % 16:
+            raise RuntimeError("dc_small_huff_shard_hist: status -1 (shard not 16-B aligned)")
+
     def small_shard_hist(self, x, shard, hist=None):
+        self._check_granules(x)
         y = self._shard_syms(x, shard)
         self._hist_in = torch.from_numpy(y)
         return torch.from_numpy(orc.histogram(y).astype(np.int64))
 
     def small_shard_pack_async(self, x, tab, shard, words, sync, gsync, S):
+        self._check_granules(x)
         y = self._shard_syms(x, shard)
         B, M = int(shard[0]), int(shard[1])
         self.pack_async(torch.from_numpy(y), tab, B, words, sync, S)   # codes + the local index

@@ -84,7 +84,7 @@ def test_sharded_stream_is_bit_identical(world, n_ary, table_mode):
     assert np.array_equal(lens.view(np.uint16), rlens)
 
 
-def _small_worker(rank, world, port, cuts, kind, n_ary, S, q, fused=False):
+def _small_worker(rank, world, port, cuts, kind, n_ary, S, q, fused=False, misalign=-1):
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     from data_compression_amd.dist import ShardedSmall
@@ -93,6 +93,11 @@ def _small_worker(rank, world, port, cuts, kind, n_ary, S, q, fused=False):
     try:
         x = _small_input(kind, cuts[-1])
         xs = torch.from_numpy(x[cuts[rank]: cuts[rank + 1]].copy())
+        if rank == misalign:   # a slice one byte into a buffer: not 16-B aligned
+            buf = torch.empty(xs.numel() + 1, dtype=torch.uint8)
+            buf[1:] = xs
+            xs = buf[1:]
+            assert xs.data_ptr() % 16
         sm = ShardedSmall(CpuEngine(), fused=fused)
         s = sm.encode(xs, n_ary=n_ary, sync_syms=S)
         y = sm.decode(s)   # (finalize: a LITERAL stream falls back to the two stages here)
@@ -114,18 +119,21 @@ def _small_input(kind, n):
     return rng.integers(ord("A"), ord("Z") + 1, size=n, dtype=np.uint8)   # no pairs: LITERAL
 
 
-@pytest.mark.parametrize("world,kind,fused,cut", [(2, "log", False, "pair"), (3, "log", False, "pair"),
-                                                  (2, "upper", False, "pair"), (2, "log", True, "pair"),
-                                                  (3, "log", True, "pair"), (3, "log", True, "space_end"),
-                                                  (3, "log", True, "space_start"), (2, "upper", True, "pair")])
-def test_sharded_small_frontend_huffman(world, kind, fused, cut):
+@pytest.mark.parametrize("world,kind,fused,cut,misalign", [(2, "log", False, "pair", -1), (3, "log", False, "pair", -1),
+                                                           (2, "upper", False, "pair", -1), (2, "log", True, "pair", -1),
+                                                           (3, "log", True, "pair", -1), (3, "log", True, "space_end", -1),
+                                                           (3, "log", True, "space_start", -1),
+                                                           (2, "upper", True, "pair", -1), (3, "log", True, "pair", 1)])
+def test_sharded_small_frontend_huffman(world, kind, fused, cut, misalign):
     """C5 orchestration (dist.ShardedSmall). Two stages: halo exchange, body per rank, global
     LITERAL decision, re-cut at 64*S, sharded Huffman. Fused (world > 1): each shard's one-pass
     encode at its global bit and symbol offsets, no re-cut (a LITERAL stream falls back to the
     two stages). Either way the gathered stream AND its sync index equal the oracle's
     single-stream Huffman encoding of the single-stream front-end output, and the ranks'
     decoded segments concatenate to the input. Cuts: on a pair's halves (' ' | letter), after a
-    ' ' that starts no pair, or on a ' ' that starts one (' ' + letter | ...)."""
+    ' ' that starts no pair, or on a ' ' that starts one (' ' + letter | ...). misalign: that
+    rank's shard is a view one byte into a buffer (the fused kernels need 16-B granules: the rank
+    encodes an aligned copy and stays in step with the others' collectives)."""
     from oracle import oracle as orc
     S, n_ary = 64, 16
     total = 64 * S * 4 * world + 777
@@ -145,7 +153,7 @@ def test_sharded_small_frontend_huffman(world, kind, fused, cut):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_small_worker, args=(r, world, port, cuts, kind, n_ary, S, q, fused))
+    procs = [ctx.Process(target=_small_worker, args=(r, world, port, cuts, kind, n_ary, S, q, fused, misalign))
              for r in range(world)]
     for p in procs:
         p.start()
