@@ -123,10 +123,13 @@ enum {
                                      SGPR-list resolve (k_nyb_resolve_c); 1 the one-pass
                                      single-wave k_nyb_adec; 2 tokens + r2's VGPR-list resolve;
                                      3 tokens + the plain-code resolve (k_nyb_resolve_s) (A/B) */
-    DC_OPT_PACK_BLOCK = 8,        /* 2: the wave-per-range pack (k_huff_pack_w) instead of the
-                                     workgroup-per-block one (k_huff_pack); 3: the same at 4 codes
-                                     a lane; A/B builds only (-DDC_AB_KERNELS; 0.386 vs 0.380 ms
-                                     on 1 GiB C2): a product build accepts 0 alone */
+    DC_OPT_PACK_BLOCK = 8,        /* A/B builds only (-DDC_AB_KERNELS): a product build accepts 0
+                                     alone. 2: the wave-per-range pack (k_huff_pack_w) instead of
+                                     the workgroup-per-block one (k_huff_pack); 3: the same at 4
+                                     codes a lane (0.386 vs 0.380 ms on 1 GiB C2); r6 (all slower,
+                                     DESIGN.md 'Round 6'): 4 the block by LDS-DMA, 5 half-block
+                                     stages, 6 one table read per byte (fold), 7 the next block's
+                                     loads issued as pass B frees each piece */
     DC_OPT_NYB_WTILE_OFF = 9      /* 1: the static nybble encode and the nybble decode write each
                                      4096-element tile with a workgroup (k_fsm_write) instead of a
                                      wave (k_nyb_enc_wtile / k_nyb_dec_wtile) */
