@@ -418,6 +418,7 @@ struct TblLds {   // k_huff_table's LDS (also carved from k_hist_blocks' counter
     uint32_t code[256];
     uint32_t nb[256];
     int k, mn, mx, maxbits, bad;
+    int aff_lo;   // fixed8: the byte whose code is 0
     uint64_t red[4];
 };
 static_assert(sizeof(TblLds) <= 256 * 64 * sizeof(uint32_t), "k_hist_blocks' last workgroup builds the table in its counters' LDS");
@@ -863,8 +864,19 @@ static __device__ void huff_table_body(TblLds &S, const uint64_t *__restrict__ f
     // pack and decode become byte maps (k_huff_pack / k_huff_decode8 fast paths)
     const int fixed_ok = __syncthreads_and(s_nb[t] == 0u || s_nb[t] == 8u);
     const int fixed_any = __syncthreads_or(s_nb[t] == 8u);
+    // affine: the codes of one length count up from 0 in byte order (canonical), so they are
+    // byte - lo exactly when the coded bytes are one run lo .. lo + count - 1
+    if (t == 0) S.aff_lo = -1;
+    const int ncoded = __syncthreads_count(s_nb[t] == 8u);
+    if (s_nb[t] == 8u && s_code[t] == 0u) S.aff_lo = t;
+    __syncthreads();
+    const int aff_lo = S.aff_lo;
+    const int affine = __syncthreads_and(s_nb[t] != 8u || (aff_lo >= 0 && s_code[t] == (uint32_t)(t - aff_lo)));
     if (t == 0) {
         T->fixed8 = (fixed_ok && fixed_any) ? 1 : 0;
+        T->fixed8_affine = (fixed_ok && fixed_any && affine) ? 1 : 0;
+        T->fixed8_lo = aff_lo;
+        T->fixed8_count = ncoded;
         T->n_ary = nary;
         T->w = w;
         T->max_symbol_value = M;
@@ -1444,7 +1456,8 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
     __syncthreads();
     if (T->fixed8 && vec_out && (bit_base & 127) == 0) {
         // every code 8 bits: stream byte bit_base / 8 + i = code(in[i]) (bit_base % 128 == 0: the
-        // stream's first byte is out's first byte, 16-B aligned); the plan is 8 bits per byte
+        // stream's first byte is out's first byte, 16-B aligned); the plan is 8 bits per byte.
+        // (A byte without a code is the plan's error, found from the histogram before the pack.)
         uint8_t *const ob = reinterpret_cast<uint8_t *>(out);
         for (uint64_t b = bx; b < nblocks; b += gstride) {
             const uint64_t blk_start = b * (uint64_t)DC_BLOCK_BYTES;
@@ -1454,6 +1467,9 @@ __global__ __launch_bounds__(256) void k_huff_pack(const uint8_t *__restrict__ i
 #pragma unroll
                 for (int k = 0; k < PACK_PIECES; ++k)
                     v[k] = LD_PACK(reinterpret_cast<const uint4 *>(in + blk_start + (uint64_t)k * PACK_TILE + (uint64_t)t * 16));
+                // (the affine map, code = byte - lo, is one subtraction per dword here, and measured
+                // slower than these lookups: 0.444 vs 0.358 ms per GiB of C3,
+                // profiles/r6r_fixed8_affine_ab.log; only the decoder uses it)
 #pragma unroll
                 for (int k = 0; k < PACK_PIECES; ++k) {
                     uint32_t w4[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
@@ -2446,6 +2462,13 @@ struct Dec8Lds {
 };
 
 static __device__ __forceinline__ uint32_t brev8(uint32_t v) { return __builtin_bitreverse32(__builtin_bswap32(v)); }
+// max of the two 16-bit halves separately (v_pk_max_u16)
+static __device__ __forceinline__ uint32_t pk_max_u16(uint32_t a, uint32_t b)
+{
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    const u16x2 r = __builtin_elementwise_max(__builtin_bit_cast(u16x2, a), __builtin_bit_cast(u16x2, b));
+    return __builtin_bit_cast(uint32_t, r);
+}
 
 
 // exact slow decode of the code at the start of an LSB-first 64-bit window (lo, hi):
@@ -2860,27 +2883,65 @@ __global__ __launch_bounds__(NW * 64) void k_huff_decode8(const uint32_t *__rest
         const uint8_t *const ib = reinterpret_cast<const uint8_t *>(in);
         const uint64_t nthr = (uint64_t)gridDim.x * NW * 64, me = (uint64_t)blockIdx.x * NW * 64 + tt;
         uint32_t bad = 0;
-        for (uint64_t g = me; g < n / 16; g += nthr) {
-            const uint4 v = LD_DEC(reinterpret_cast<const uint4 *>(ib + 16 * g));
-            uint32_t w4[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const uint32_t x = w4[q];
-                const uint32_t a = inv[x & 255u], b2 = inv[(x >> 8) & 255u], c2 = inv[(x >> 16) & 255u], d2 = inv[x >> 24];
-                bad |= (a | b2 | c2 | d2) & 0x100u;
-                w4[q] = (a & 255u) | ((b2 & 255u) << 8) | ((c2 & 255u) << 16) | ((d2 & 255u) << 24);
-            }
-            uint4 *const o4 = reinterpret_cast<uint4 *>(out + 16 * g);   // streaming stores, as d8_out
+        // affine (dc_dtable.fixed8_affine): symbol = code + lo for codes 0 .. count - 1; a code past
+        // them (the dummy leaves' codes) is a stream error: the largest code byte, kept per 16-bit
+        // lane by v_pk_max_u16 on the even and the odd bytes, is checked once at the end
+        const bool aff = T->fixed8_affine != 0;
+        const uint32_t lo4 = (uint32_t)(T->fixed8_lo & 255) * 0x01010101u;
+        uint32_t cmax = 0;
+        // 4 granules a thread per round, their loads issued together: one workgroup of NW waves
+        // per CU (the decoder's launch) keeps too few loads in flight with one
+        const uint64_t ng = n / 16;
+        auto put = [&](uint64_t g, const uint32_t (&w4)[4]) {   // streaming stores, as d8_out
+            uint4 *const o4 = reinterpret_cast<uint4 *>(out + 16 * g);
             __builtin_nontemporal_store(w4[0], &o4->x);
             __builtin_nontemporal_store(w4[1], &o4->y);
             __builtin_nontemporal_store(w4[2], &o4->z);
             __builtin_nontemporal_store(w4[3], &o4->w);
+        };
+        for (uint64_t g0 = me; g0 < ng; g0 += 4 * nthr) {
+            uint4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint64_t g = g0 + (uint64_t)u * nthr;
+                v[u] = g < ng ? LD_DEC(reinterpret_cast<const uint4 *>(ib + 16 * g)) : make_uint4(0u, 0u, 0u, 0u);
+            }
+            if (aff) {   // no byte carries: a valid code + lo is a byte
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    uint32_t w4[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        cmax = pk_max_u16(cmax, w4[q] & 0x00FF00FFu);
+                        cmax = pk_max_u16(cmax, (w4[q] >> 8) & 0x00FF00FFu);
+                        w4[q] += lo4;
+                    }
+                    const uint64_t g = g0 + (uint64_t)u * nthr;
+                    if (g < ng) put(g, w4);
+                }
+            } else {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    uint32_t w4[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const uint32_t x = w4[q];
+                        const uint32_t a = inv[x & 255u], b2 = inv[(x >> 8) & 255u], c2 = inv[(x >> 16) & 255u], d2 = inv[x >> 24];
+                        bad |= (a | b2 | c2 | d2) & 0x100u;
+                        w4[q] = (a & 255u) | ((b2 & 255u) << 8) | ((c2 & 255u) << 16) | ((d2 & 255u) << 24);
+                    }
+                    const uint64_t g = g0 + (uint64_t)u * nthr;
+                    if (g < ng) put(g, w4);
+                }
+            }
         }
         for (uint64_t i = (n & ~15ull) + me; i < n; i += nthr) {
             const uint32_t a = inv[ib[i]];
             bad |= a & 0x100u;
             out[i] = (uint8_t)a;
         }
+        const uint32_t cm = max(cmax & 0xFFFFu, cmax >> 16);
+        if (aff && cm >= (uint32_t)T->fixed8_count) bad = 1;
         if (bad) atomicOr(err, 1);
         const uint32_t ngr = (uint32_t)(((n + S - 1) / S + DC_SYNC_GROUP - 1) / DC_SYNC_GROUP);
         for (uint64_t g = me; g < ngr; g += nthr) fix_mask[g] = 0ull;

@@ -72,7 +72,10 @@ typedef struct dc_dtable {
     uint16_t dlut2[DC_LUT2_CAP];
     int32_t dlut2_k, dec_ready;   /* dec_ready: lut/dlut/dlut2/dlut14/dlut15 are current */
     int32_t fixed8;               /* every byte's code is 8 bits (or absent): pack and decode are byte maps */
-    int32_t pad_[3];
+    /* fixed8 with the coded bytes one contiguous range: code = byte - fixed8_lo for the
+     * fixed8_count bytes fixed8_lo.., so the maps are byte-wise subtractions (flat or random
+     * bytes: n = 2 on all 256 values codes every byte as itself) */
+    int32_t fixed8_affine, fixed8_lo, fixed8_count;
     /* dlut14: next 14 bits -> bits | sym << 8 for codes of <= 14 bits; bits 0: longer, sym =
      * the escape id of its 12-bit prefix (as dlut); 16-B aligned for vector copies */
     uint16_t dlut14[1 << DC_LUT14_BITS];

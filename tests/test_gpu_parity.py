@@ -230,22 +230,36 @@ def test_pack_into_dirty_words(torch_cuda, codec, bit_base, kind):
     assert (got[end:] == 0xFF).all(), (kind, bit_base)
 
 
+# alphabets whose codes are all 8 bits (flat counts): C3's bytes 1..255 (255 symbols + 1 dummy
+# fill a depth-2 16-ary tree), a run 10..250 (241 + 15 dummies), 241 bytes with gaps (no run:
+# the LDS byte map), and bytes 0..254 at n = 2 (+ the one dummy of n = 2: every byte coded as
+# itself; all 256 would give 257 leaves and 9-bit codes)
+FIXED8_ALPHABETS = {"c3": (np.arange(1, 256), 16, 1), "run": (np.arange(10, 251), 16, 10),
+                    "gaps": (np.setdiff1d(np.arange(256), np.arange(3, 256, 17)), 16, None),
+                    "n2": (np.arange(0, 255), 2, 0)}
+
+
+@pytest.mark.parametrize("alpha", list(FIXED8_ALPHABETS))
 @pytest.mark.parametrize("bit_base", [0, 128 * 3, 8, 32])
-def test_fixed8_byte_map_paths(torch_cuda, codec, bit_base):
-    """n = 16 on flat bytes: every code is 8 bits (dc_dtable.fixed8), so pack and decode run
-    as byte maps when the stream starts on a 128-bit boundary (bit_base 0, 384), and the
-    general kernels otherwise (8, 32); both bit-exact vs the oracle, ragged ends included."""
+def test_fixed8_byte_map_paths(torch_cuda, codec, bit_base, alpha):
+    """Every code 8 bits (dc_dtable.fixed8): pack and decode run as byte maps when the stream
+    starts on a 128-bit boundary (bit_base 0, 384), and the general kernels otherwise (8, 32);
+    both bit-exact vs the oracle, ragged ends included. When the coded bytes are one run
+    (fixed8_affine) the maps are byte-wise subtractions, and a code past the run in the stream
+    (a dummy leaf's) is reported as a stream error like the LDS map's missing entry."""
     torch = torch_cuda
+    syms, n_ary, lo = FIXED8_ALPHABETS[alpha]
     rng = np.random.default_rng(bit_base + 7)
     for n in (1 << 20, (1 << 20) + 12_345, 100_003):
-        # C3's alphabet (bytes 1..255, flat): 255 symbols + 1 dummy fill a depth-2 16-ary tree
-        x = rng.permutation(np.resize(np.arange(1, 256, dtype=np.uint8), n))
-        L, el, ev, code, nb, mx = _oracle_encode(x, 16)
-        assert set(np.unique(nb[:256])) <= {0, 8}
+        x = rng.permutation(np.resize(syms.astype(np.uint8), n))
+        L, el, ev, code, nb, mx = _oracle_encode(x, n_ary)
+        assert set(np.unique(nb[:256])) == {0, 8}
+        if lo is not None:   # the codes are byte - lo (what the affine map computes)
+            assert all(int(code[s]) == int(s) - lo for s in syms)
         S = 64
         payload, bits, idx = orc.huff_pack(x, code, nb, bit_base=bit_base, sync_syms=S)
         xt = torch.from_numpy(x).cuda()
-        enc = codec.encode(xt, n_ary=16, sync_syms=S, bit_base=bit_base)
+        enc = codec.encode(xt, n_ary=n_ary, sync_syms=S, bit_base=bit_base)
         assert enc["bits"] == bits == 8 * n
         got = enc["words"].cpu().numpy().view(np.uint8)
         off = (bit_base >> 3) - ((bit_base >> 5) << 2)
@@ -258,6 +272,12 @@ def test_fixed8_byte_map_paths(torch_cuda, codec, bit_base):
         assert codec.decode_status() == 0 and np.array_equal(out.cpu().numpy(), x), (n, bit_base)
         if bit_base % 128 == 0:   # the byte map redoes nothing (the general decoder redoes the ragged tail)
             assert codec.decode_redo_count() == 0
+        if alpha == "c3" and bit_base == 0 and n == 100_003:
+            # code 255 (the dummy leaf's) in the middle of the stream: an error, not a byte
+            wb = enc["words"].view(torch.uint8)
+            wb[n // 2] = 255
+            codec.decode_into(enc, out)
+            assert codec.decode_status() != 0
 
 
 @pytest.mark.parametrize("case", ["unaligned-out", "long-halves"])
